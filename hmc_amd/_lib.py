@@ -1,0 +1,81 @@
+"""ctypes binding of libhmc_amd.so (C-ABI declared in include/hmc_amd.h).
+
+The library is built in-tree by `__graft_entry__.build()` (or `make -C
+hmc_amd/csrc`).  There is no fallback: if the shared object is missing or does
+not load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhmc_amd.so")
+
+HMC_OK = 0
+ERRORS = {-1: "EARG", -2: "EHIP", -3: "EIO", -4: "EUNSUPPORTED", -5: "ENOPATTERN", -6: "ERCCL", -7: "ENOMEM"}
+
+
+class HMCError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"hmc_amd error {code} ({ERRORS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+class IterLog(C.Structure):
+    _fields_ = [("log_likelihood", C.c_double), ("t_estep_s", C.c_double), ("t_mstep_s", C.c_double),
+                ("r_e", C.c_uint64), ("r_m", C.c_uint64), ("n_patterns", C.c_int), ("n_samples", C.c_int)]
+
+
+_lib = None
+
+# (name, restype, argtypes)
+_P = C.POINTER
+_vp, _i, _d, _u64, _cp = C.c_void_p, C.c_int, C.c_double, C.c_uint64, C.c_char_p
+_SIGS = [
+    ("hmc_version", _cp, []),
+    ("hmc_ctx_create", _i, [_i, _P(_vp)]),
+    ("hmc_rccl_unique_id", _i, [_vp]),
+    ("hmc_ctx_create_dist", _i, [_i, _i, _i, _vp, _P(_vp)]),
+    ("hmc_ctx_destroy", None, [_vp]),
+    ("hmc_ctx_error", _cp, [_vp]),
+    ("hmc_set_params", _i, [_vp, _d, _d, _i, _i, _i]),
+    ("hmc_load_phase", _i, [_vp, _cp]),
+    ("hmc_load_genotypes", _i, [_vp, _i, _i, _P(C.c_int32), _cp]),
+    ("hmc_panel_info", _i, [_vp, _P(_i), _P(_i), _P(_i)]),
+    ("hmc_allele_table", _i, [_vp, _P(C.c_int32), _P(C.c_int32), _P(_d)]),
+    ("hmc_find_patterns", _i, [_vp, _P(_i), _P(_u64)]),
+    ("hmc_model_info", _i, [_vp, _P(_i), _P(_i)]),
+    ("hmc_get_patterns", _i, [_vp, _P(C.c_int32), _P(C.c_int32), _P(_d), _P(_d), _P(_d), _P(C.c_int32),
+                              _P(C.c_int32), _i]),
+    ("hmc_set_patterns", _i, [_vp, _i, _P(C.c_int32), _P(C.c_int32), _P(_d), _P(_d), _P(C.c_int32),
+                              _P(C.c_int32)]),
+    ("hmc_resolve_all", _i, [_vp, _P(_d), _P(_i), _P(_u64)]),
+    ("hmc_get_estep", _i, [_vp, _P(_d), _P(C.c_int32), _P(C.c_int32), _P(_d), _P(_d), _P(_d)]),
+    ("hmc_get_samples", _i, [_vp, _P(C.c_int32), _P(_d), _P(_d)]),
+    ("hmc_get_resolutions", _i, [_vp, _P(C.c_int32)]),
+    ("hmc_run", _i, [_vp, _i, _P(IterLog), _i, _P(_i), _P(_d), _P(_u64), _P(_i)]),
+    ("hmc_get_best_resolutions", _i, [_vp, _P(C.c_int32)]),
+    ("hmc_write_phase", _i, [_vp, _cp]),
+    ("hmc_set_tuning", _i, [_vp, _i, _u64, _i]),
+    ("hmc_last_timings", _i, [_vp, _P(_d), _P(_d), _P(_d)]),
+    ("hmc_test_nth_element", None, [_P(_d), _P(C.c_uint32), _i, _i]),
+    ("hmc_test_sort_small", None, [_P(_d), _P(C.c_uint32), _i]),
+]
+
+EXPORTED = [s[0] for s in _SIGS]
+
+
+def lib():
+    """Load libhmc_amd.so; raises if it is absent (no CPU fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is not built; run __graft_entry__.build() or make -C hmc_amd/csrc")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in _SIGS:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib

@@ -1,0 +1,1202 @@
+// api.cpp — host runtime of libhmc_amd.so: the C-ABI of include/hmc_amd.h,
+// the HaploModel EM driver, GenoData construction and PHASE I/O.
+//
+// Roles kept from the reference (drop-in seams):
+//   GenoData::checkAlleleSymbol   GenoData.cpp:78-118        -> Panel::build_tables
+//   HaploFile::readGenoData       HaploFile.cpp:54-118       -> read_phase
+//   HaploFile::writeGenoData      HaploFile.cpp:120-153      -> hmc_write_phase
+//   PatternManager::findPatternByFreq + initialize            -> Ctx::mine (mstep.hip)
+//   HaploModel::resolveAll        HaploModel.cpp:79-115      -> Ctx::estep (estep.hip)
+//   HaploModel::run               HaploModel.cpp:117-155     -> Ctx::run
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/hmc_amd.h"
+#include "hmc_internal.hpp"
+#include "mstep.hpp"
+#include "select.hpp"
+
+namespace hmc {
+
+// ------------------------------------------------------------- utilities --
+template <class T>
+struct DevBuf {
+  T *p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t ensure(size_t m) {  // contents not preserved
+    if (m <= n && p) return hipSuccess;
+    release();
+    hipError_t e = hipMalloc((void **)&p, std::max<size_t>(m, 1) * sizeof(T));
+    if (e != hipSuccess) { p = nullptr; return e; }
+    n = std::max<size_t>(m, 1);
+    return hipSuccess;
+  }
+  hipError_t grow_keep(size_t m, size_t used, hipStream_t st) {  // preserve the first `used` elements
+    if (m <= n && p) return hipSuccess;
+    size_t cap = std::max<size_t>(m, n + n / 2);
+    T *q = nullptr;
+    hipError_t e = hipMalloc((void **)&q, cap * sizeof(T));
+    if (e != hipSuccess) return e;
+    if (p && used) {
+      e = hipMemcpyAsync(q, p, used * sizeof(T), hipMemcpyDeviceToDevice, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      if (e != hipSuccess) { (void)hipFree(q); return e; }
+    }
+    release();
+    p = q;
+    n = cap;
+    return hipSuccess;
+  }
+};
+
+struct Err {
+  int code;
+};
+
+// ----------------------------------------------------------------- panel --
+struct Panel {
+  int N = 0, L = 0, amax = 0;
+  std::vector<int32_t> al;  // [N][2][L] symbols, -1 missing
+  std::string types;
+  std::vector<std::vector<std::pair<int32_t, double>>> sym;  // per locus (symbol, frequency), ascending
+  std::vector<uint8_t> idx;                                  // [N][2][L] allele index, 0xFF missing
+
+  // GenoData::checkAlleleSymbol (GenoData.cpp:78-118): distinct non-missing
+  // symbols sorted by value; frequency = count / non-missing count.
+  bool build_tables(std::string &err) {
+    sym.assign(L, {});
+    idx.assign((size_t)N * 2 * L, MISSING);
+    amax = 0;
+    for (int k = 0; k < L; ++k) {
+      std::map<int32_t, double> cnt;
+      double tot = 0.0;
+      for (int i = 0; i < N; ++i)
+        for (int h = 0; h < 2; ++h) {
+          const int32_t a = al[((size_t)i * 2 + h) * L + k];
+          if (a >= 0) {
+            cnt[a] += 1.0;
+            tot += 1.0;
+          }
+        }
+      for (auto &kv : cnt) sym[k].push_back({kv.first, kv.second / tot});
+      if ((int)sym[k].size() > A_MAX) {
+        err = "locus " + std::to_string(k) + " has more than 32 alleles";
+        return false;
+      }
+      amax = std::max(amax, (int)sym[k].size());
+      for (int i = 0; i < N; ++i)
+        for (int h = 0; h < 2; ++h) {
+          const int32_t a = al[((size_t)i * 2 + h) * L + k];
+          if (a < 0) continue;
+          int j = 0;
+          while (sym[k][j].first != a) ++j;
+          idx[((size_t)i * 2 + h) * L + k] = (uint8_t)j;
+        }
+    }
+    amax = std::max(amax, 1);
+    return true;
+  }
+  int32_t symbol(int k, uint8_t j) const { return j == MISSING ? -1 : sym[k][j].first; }
+  int index_of(int k, int32_t a) const {
+    for (size_t j = 0; j < sym[k].size(); ++j)
+      if (sym[k][j].first == a) return (int)j;
+    return -1;
+  }
+};
+
+// HaploFile::readGenoData (HaploFile.cpp:54-118) with AlleleSequence::read
+// (Allele.cpp:55-153): ids on, `P` positions line optional, per-locus type.
+static bool read_phase(const char *path, Panel &pn, std::string &err) {
+  FILE *fp = fopen(path, "r");
+  if (!fp) { err = std::string("Can not open file ") + path + "!"; return false; }
+  auto fail = [&](const char *m) { fclose(fp); err = m; return false; };
+  int n = 0, l = 0;
+  if (fscanf(fp, "%d\n", &n) != 1 || fscanf(fp, "%d\n", &l) != 1 || n <= 0 || l <= 0) return fail("Invalid file type!");
+  pn.N = n;
+  pn.L = l;
+  pn.al.assign((size_t)n * 2 * l, -1);
+  std::vector<char> line((size_t)l * 32 + 4096);
+  const char *D = " \t\r\n";
+  if (!fgets(line.data(), (int)line.size(), fp)) return fail("Truncated file!");
+  char *s = line.data() + strspn(line.data(), D);
+  if (s[0] == 'P') {
+    if (!fgets(line.data(), (int)line.size(), fp)) return fail("Truncated file!");
+    s = line.data() + strspn(line.data(), D);
+  }
+  pn.types.assign(l, 'M');
+  for (int k = 0; k < l; ++k) {
+    pn.types[k] = s[0];
+    if (*s) ++s;
+    s += strspn(s, D);
+  }
+  for (int i = 0; i < n; ++i) {
+    if (!fgets(line.data(), (int)line.size(), fp)) return fail("Truncated file!");  // id line
+    for (int h = 0; h < 2; ++h) {
+      if (!fgets(line.data(), (int)line.size(), fp)) return fail("Truncated file!");
+      char *b = line.data();
+      for (int k = 0; k < l; ++k) {
+        b += strspn(b, D);
+        int32_t a;
+        if (pn.types[k] == 'S') {
+          a = (b[0] == '-' || b[0] == '?' || b[0] == 0) ? -1 : (int32_t)(unsigned char)b[0];
+          if (*b) ++b;
+        } else {
+          if (b[0] == '-' || b[0] == '?') a = -1;
+          else {
+            int v = atoi(b);
+            a = v > 0 ? v : -1;
+          }
+          b += strcspn(b, D);
+        }
+        pn.al[((size_t)i * 2 + h) * l + k] = a;
+      }
+    }
+  }
+  fclose(fp);
+  return pn.build_tables(err);
+}
+
+// ---------------------------------------------------------------- context --
+struct Ctx {
+  int device = 0, rank = 0, world = 1;
+  hipStream_t st = nullptr;
+  ncclComm_t comm = nullptr;
+  std::string err;
+  // parameters (HaploModel.h:15-26 with the CLI defaults of HMC.cpp:35-47)
+  double min_freq_abs = 1.5, min_freq = -1.0;
+  int min_len = 1, max_len = 30, sample_size = 10;
+  // tuning
+  int fcap = 2048, waves = 0;
+  uint64_t trace_bytes = 0;
+
+  Panel pan;
+  bool have_panel = false;
+  int i0 = 0, i1 = 0;  // this rank's individuals
+
+  // device panel
+  DevBuf<uchar2> d_geno_im, d_geno_lm;
+  DevBuf<uint8_t> d_anum, d_npos, d_pos_allele, d_rank_of;
+  DevBuf<double> d_afreq;
+  DevBuf<int32_t> d_r_child_base;
+  std::vector<uint8_t> h_npos, h_anum;
+
+  // model
+  int P = 0, head_len = 1;
+  bool have_model = false;
+  DevBuf<int32_t> t_start, t_len, t_node;
+  DevBuf<double> t_freq, t_prefix, t_tp;
+  DevBuf<uint8_t> t_last;
+  DevBuf<uint32_t> t_succ, d_head_ids, d_head_pat0;
+  int n_head = 0;
+
+  // mining state
+  DevBuf<int32_t> n_parent, n_start, n_child_base, n_link;
+  DevBuf<uint8_t> n_allele, n_flags;
+  DevBuf<double> n_freq, n_prefix, n_tp, n_sum;
+  DevBuf<uint32_t> n_cnt, n_size, n_pos;
+  DevBuf<unsigned long long> n_list_off;
+  size_t node_cap = 0;
+  DevBuf<uint32_t> l_idx[2];
+  DevBuf<double> l_val[2];
+  DevBuf<unsigned long long> s_ext, s_lscan, d_totals, d_rm;
+  DevBuf<int32_t> s_child, s_cscan;
+  DevBuf<char> s_tmp;
+  DevBuf<uint32_t> d_rsize, d_rpos;
+
+  // samples (HaploData) and E-step buffers
+  int H = 0;
+  double total_weight = 0.0;
+  bool have_samples = false;
+  DevBuf<uint8_t> d_rows, d_samp_lm, d_res;
+  DevBuf<double> d_w;
+  DevBuf<char> d_scratch;
+  DevBuf<uint32_t> d_trace;
+  DevBuf<unsigned long long> d_trace_cursor, d_loc_off, d_re;
+  DevBuf<double> d_total, d_prior, d_post, d_weight;
+  DevBuf<int32_t> d_ncand, d_status, d_sbase;
+  DevBuf<uint32_t> d_cstate, d_cidx, d_maxst;
+  std::vector<double> h_total;
+  std::vector<int32_t> h_ncand, h_status, h_sbase;
+  std::vector<unsigned long long> h_re;
+  bool have_estep = false;
+  std::vector<uint8_t> best_res;  // [n][2][L] accepted resolutions (allele index)
+  bool have_best = false;
+
+  // timings
+  hipEvent_t ev[6] = {};
+  double ms_fwd = 0, ms_tb = 0, ms_m = 0;
+
+  int fail(int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    err = buf;
+    return code;
+  }
+  int hipfail(hipError_t e, const char *where) {
+    if (e == hipErrorOutOfMemory) return fail(HMC_ENOMEM, "%s: %s", where, hipGetErrorString(e));
+    return fail(HMC_EHIP, "%s: %s", where, hipGetErrorString(e));
+  }
+
+  int nloc() const { return i1 - i0; }
+  int S() const { return sample_size > 1 ? sample_size : 1; }  // HaploBuilder.cpp:44
+
+  // ---------------------------------------------------------- collectives --
+  int allreduce_sum(double *dptr, size_t n) {
+    if (world == 1 || n == 0) return HMC_OK;
+    ncclResult_t r = ncclAllReduce(dptr, dptr, n, ncclDouble, ncclSum, comm, st);
+    if (r != ncclSuccess) return fail(HMC_ERCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+    return HMC_OK;
+  }
+  int allreduce_host(double *h, size_t n) {  // small host vectors
+    if (world == 1 || n == 0) return HMC_OK;
+    DevBuf<double> tmp;
+    hipError_t e = tmp.ensure(n);
+    if (e) return hipfail(e, "allreduce_host");
+    if ((e = hipMemcpyAsync(tmp.p, h, n * 8, hipMemcpyHostToDevice, st))) return hipfail(e, "allreduce_host");
+    int rc = allreduce_sum(tmp.p, n);
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(h, tmp.p, n * 8, hipMemcpyDeviceToHost, st))) return hipfail(e, "allreduce_host");
+    if ((e = hipStreamSynchronize(st))) return hipfail(e, "allreduce_host");
+    return HMC_OK;
+  }
+
+  // ---------------------------------------------------------------- panel --
+  int upload_panel() {
+    const int N = pan.N, L = pan.L, A = pan.amax;
+    i0 = (int)((long long)N * rank / world);
+    i1 = (int)((long long)N * (rank + 1) / world);
+    std::vector<uchar2> im((size_t)N * L), lm((size_t)L * N);
+    for (int i = 0; i < N; ++i)
+      for (int k = 0; k < L; ++k) {
+        uchar2 g = make_uchar2(pan.idx[((size_t)i * 2) * L + k], pan.idx[((size_t)i * 2 + 1) * L + k]);
+        im[(size_t)i * L + k] = g;
+        lm[(size_t)k * N + i] = g;
+      }
+    h_anum.assign(L + 1, 0);
+    h_npos.assign(L + 1, 0);
+    std::vector<double> af((size_t)L * A, 0.0);
+    std::vector<uint8_t> pa((size_t)L * A, 0xFF), rk((size_t)L * A, 0xFF);
+    std::vector<int32_t> rcb(L + 1, 0);
+    int tot = 0;
+    for (int k = 0; k < L; ++k) {
+      h_anum[k] = (uint8_t)pan.sym[k].size();
+      for (size_t j = 0; j < pan.sym[k].size(); ++j) {
+        af[(size_t)k * A + j] = pan.sym[k][j].second;
+        if (pan.sym[k][j].second > 0) {
+          pa[(size_t)k * A + h_npos[k]] = (uint8_t)j;
+          rk[(size_t)k * A + j] = h_npos[k];
+          h_npos[k]++;
+        }
+      }
+      rcb[k] = tot;
+      tot += h_npos[k];
+    }
+    rcb[L] = tot;
+    hipError_t e;
+#define UP(buf, vec)                                                                              \
+  if ((e = buf.ensure(vec.size())) ||                                                             \
+      (e = hipMemcpyAsync(buf.p, vec.data(), vec.size() * sizeof(vec[0]), hipMemcpyHostToDevice, st))) \
+    return hipfail(e, "upload_panel");
+    UP(d_geno_im, im);
+    UP(d_geno_lm, lm);
+    UP(d_anum, h_anum);
+    UP(d_npos, h_npos);
+    UP(d_afreq, af);
+    UP(d_pos_allele, pa);
+    UP(d_rank_of, rk);
+    UP(d_r_child_base, rcb);
+#undef UP
+    if ((e = hipStreamSynchronize(st))) return hipfail(e, "upload_panel");
+    have_panel = true;
+    have_model = have_samples = have_estep = have_best = false;
+    P = 0;
+    H = 0;
+    return HMC_OK;
+  }
+
+  DevPanel dev_panel() const {
+    DevPanel d;
+    d.N = pan.N;
+    d.L = pan.L;
+    d.amax = pan.amax;
+    d.geno_im = d_geno_im.p;
+    d.geno_lm = d_geno_lm.p;
+    d.anum = d_anum.p;
+    d.afreq = d_afreq.p;
+    return d;
+  }
+
+  // --------------------------------------------------------------- mining --
+  int grow_nodes(size_t need, size_t used) {
+    if (need <= node_cap) return HMC_OK;
+    size_t cap = std::max<size_t>(need, node_cap + node_cap / 2);
+    hipError_t e;
+#define G(b) if ((e = b.grow_keep(cap, used, st))) return hipfail(e, "grow_nodes");
+    G(n_parent) G(n_start) G(n_child_base) G(n_link) G(n_allele) G(n_flags) G(n_freq) G(n_prefix) G(n_tp) G(n_sum)
+    G(n_cnt) G(n_size) G(n_pos) G(n_list_off)
+#undef G
+    node_cap = cap;
+    return HMC_OK;
+  }
+
+  MineArgs mine_args(bool genotype) const {
+    MineArgs a;
+    a.L = pan.L;
+    a.amax = pan.amax;
+    a.genotype = genotype;
+    if (genotype) {
+      a.n_items = nloc();
+      a.item_base = i0;
+      a.item_stride = pan.N;
+    } else {
+      a.n_items = H;
+      a.item_base = 0;
+      a.item_stride = H;
+    }
+    a.geno_lm = d_geno_lm.p;
+    a.samp_lm = d_samp_lm.p;
+    a.w = d_w.p;
+    a.afreq = d_afreq.p;
+    a.anum = d_anum.p;
+    a.npos = d_npos.p;
+    a.pos_allele = d_pos_allele.p;
+    a.rank_of = d_rank_of.p;
+    a.parent = n_parent.p;
+    a.start = n_start.p;
+    a.allele = n_allele.p;
+    a.flags = n_flags.p;
+    a.freq = n_freq.p;
+    a.prefix = n_prefix.p;
+    a.tp = n_tp.p;
+    a.sum = n_sum.p;
+    a.cnt = n_cnt.p;
+    a.size = n_size.p;
+    a.pos = n_pos.p;
+    a.child_base = n_child_base.p;
+    a.link = n_link.p;
+    a.list_off = n_list_off.p;
+    a.r_child_base = d_r_child_base.p;
+    a.rm = d_rm.p;
+    return a;
+  }
+
+  double current_min_freq() {  // HaploModel::findPatterns (HaploModel.cpp:52-56)
+    if (min_freq_abs > 0) min_freq = min_freq_abs / (2.0 * pan.N);
+    return min_freq;
+  }
+
+  int mine(int *P_out, uint64_t *rm_out) {
+    if (!have_panel) return fail(HMC_EARG, "no panel loaded");
+    const bool genotype = !have_samples;
+    const int L = pan.L;
+    hipError_t e;
+    hipEventRecord(ev[4], st);
+    // PatternManager::findPatternByFreq argument normalisation (PatternManager.cpp:29-32)
+    int mxl = max_len <= 0 ? L : max_len;
+    int mnl = std::max(min_len, 1);
+    mxl = std::max(mxl, mnl);
+    const double mf = current_min_freq();
+    if ((e = d_rm.ensure(1)) || (e = d_totals.ensure(2)) || (e = hipMemsetAsync(d_rm.p, 0, 8, st)))
+      return hipfail(e, "mine");
+    std::vector<int> lbeg{0, 0}, lend{0, 0};  // per level node ranges (index = level)
+    int n1 = 0;
+    for (int k = 0; k < L; ++k) n1 += h_npos[k];
+    int rc = grow_nodes(std::max(n1, 1), 0);
+    if (rc) return rc;
+    lbeg[1] = 0;
+    lend[1] = n1;
+    int level = 1, pbeg = 0, pend = L;  // level-1 parents are the L roots
+    int cur = 0;                        // list buffer holding the parents' lists
+    while (true) {
+      const int cb = lbeg[level], ce = lend[level], nlev = ce - cb;
+      MineArgs a = mine_args(genotype);
+      a.denom = genotype ? (double)pan.N : total_weight;
+      a.min_freq = mf;
+      a.min_len = mnl;
+      a.max_len = mxl;
+      a.lin_idx = level == 1 ? nullptr : l_idx[cur].p;
+      a.lin_val = level == 1 ? nullptr : l_val[cur].p;
+      if ((e = launch_mine_count(a, level, pbeg, pend, st))) return hipfail(e, "mine_count");
+      if ((rc = allreduce_sum(n_sum.p + cb, nlev))) return rc;
+      if ((e = s_ext.ensure(nlev)) || (e = s_lscan.ensure(nlev)) || (e = s_child.ensure(nlev)) ||
+          (e = s_cscan.ensure(nlev)))
+        return hipfail(e, "mine");
+      const size_t tmpb = mine_scan_tmp_bytes(nlev);
+      if ((e = s_tmp.ensure(tmpb))) return hipfail(e, "mine");
+      if ((e = launch_mine_finalize(a, level, cb, ce, s_ext.p, s_child.p, st))) return hipfail(e, "mine_finalize");
+      if ((e = launch_mine_offsets(a, cb, ce, s_ext.p, s_child.p, s_lscan.p, s_cscan.p, ce, s_tmp.p, s_tmp.n, d_totals.p,
+                                   st)))
+        return hipfail(e, "mine_offsets");
+      unsigned long long tot[2];
+      if ((e = hipMemcpyAsync(tot, d_totals.p, 16, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+        return hipfail(e, "mine");
+      const size_t list_total = tot[0];
+      const int nnext = (int)tot[1];
+      const int nxt = cur ^ 1;
+      if (list_total > 0) {
+        if ((e = l_idx[nxt].ensure(list_total))) return hipfail(e, "mine lists");
+        if (genotype && (e = l_val[nxt].ensure(list_total))) return hipfail(e, "mine lists");
+        a.lout_idx = l_idx[nxt].p;
+        a.lout_val = genotype ? l_val[nxt].p : nullptr;
+        if ((e = launch_mine_scatter(a, level, pbeg, pend, st))) return hipfail(e, "mine_scatter");
+      }
+      cur = nxt;
+      if (nnext == 0) break;
+      pbeg = cb;
+      pend = ce;
+      ++level;
+      lbeg.push_back(ce);
+      lend.push_back(ce + nnext);
+      if ((rc = grow_nodes((size_t)ce + nnext, ce))) return rc;
+    }
+    const int maxlev = level;
+    const int ntot = lend[maxlev];
+    // DFS pre-order ids from subtree sizes
+    MineArgs a = mine_args(genotype);
+    for (int lv = maxlev; lv >= 1; --lv)
+      if ((e = launch_mine_size(a, lv, lbeg[lv], lend[lv], st))) return hipfail(e, "mine_size");
+    if ((e = d_rsize.ensure(L)) || (e = d_rpos.ensure(L))) return hipfail(e, "mine");
+    if ((e = launch_mine_root_size(a, d_rsize.p, st))) return hipfail(e, "mine_root_size");
+    std::vector<uint32_t> rsize(L), rpos(L);
+    if ((e = hipMemcpyAsync(rsize.data(), d_rsize.p, (size_t)L * 4, hipMemcpyDeviceToHost, st)) ||
+        (e = hipStreamSynchronize(st)))
+      return hipfail(e, "mine");
+    uint64_t acc = 0;
+    for (int s = L - 1; s >= 0; --s) {  // roots popped from the back: start L-1 first
+      rpos[s] = (uint32_t)acc;
+      acc += rsize[s];
+    }
+    if (acc >= 0xFFFFFFFFull) return fail(HMC_EUNSUPPORTED, "too many patterns (%llu)", (unsigned long long)acc);
+    P = (int)acc;
+    if ((e = hipMemcpyAsync(d_rpos.p, rpos.data(), (size_t)L * 4, hipMemcpyHostToDevice, st)))
+      return hipfail(e, "mine");
+    if ((e = launch_mine_pos(a, 1, 0, L, d_rpos.p, st))) return hipfail(e, "mine_pos");
+    for (int lv = 2; lv <= maxlev; ++lv)
+      if ((e = launch_mine_pos(a, lv, lbeg[lv - 1], lend[lv - 1], d_rpos.p, st))) return hipfail(e, "mine_pos");
+    if ((rc = alloc_table(P))) return rc;
+    PatternTable t = table();
+    for (int lv = 1; lv <= maxlev; ++lv)
+      if ((e = launch_mine_emit(a, lv, lbeg[lv], lend[lv], t, st))) return hipfail(e, "mine_emit");
+    if ((e = launch_mine_succ(a, t, P, st))) return hipfail(e, "mine_succ");
+    head_len = mnl;
+    if ((rc = build_heads_from_nodes(a))) return rc;
+    unsigned long long rm = 0;
+    if ((e = hipMemcpyAsync(&rm, d_rm.p, 8, hipMemcpyDeviceToHost, st))) return hipfail(e, "mine");
+    hipEventRecord(ev[5], st);
+    if ((e = hipStreamSynchronize(st))) return hipfail(e, "mine");
+    float ms = 0;
+    hipEventElapsedTime(&ms, ev[4], ev[5]);
+    ms_m = ms;
+    have_model = true;
+    (void)ntot;
+    if (P_out) *P_out = P;
+    if (rm_out) *rm_out = rm;
+    return HMC_OK;
+  }
+
+  int alloc_table(int np) {
+    hipError_t e;
+    const size_t n = std::max(np, 1);
+    if ((e = t_start.ensure(n)) || (e = t_len.ensure(n)) || (e = t_node.ensure(n)) || (e = t_freq.ensure(n)) ||
+        (e = t_prefix.ensure(n)) || (e = t_tp.ensure(n)) || (e = t_last.ensure(n)) ||
+        (e = t_succ.ensure(n * pan.amax)))
+      return hipfail(e, "alloc_table");
+    return HMC_OK;
+  }
+  PatternTable table() const {
+    PatternTable t;
+    t.start = t_start.p;
+    t.len = t_len.p;
+    t.node = t_node.p;
+    t.freq = t_freq.p;
+    t.prefix = t_prefix.p;
+    t.tp = t_tp.p;
+    t.last = t_last.p;
+    t.succ = t_succ.p;
+    return t;
+  }
+
+  // Head list (PatternManager.cpp:304-306) and the locus-0 lookup used by
+  // initHeadList's findLongestMatchPattern(head_len, ...) for head_len == 1.
+  int set_heads(const std::vector<std::pair<uint32_t, uint8_t>> &heads /* (id, allele at 0) */) {
+    std::vector<uint32_t> ids, pat0(pan.amax + 1, NONE);
+    for (auto &h : heads) {
+      ids.push_back(h.first);
+      pat0[h.second] = h.first;
+    }
+    std::sort(ids.begin(), ids.end());
+    for (int x = 0; x < pan.amax; ++x)
+      if (pat0[x] != NONE) { pat0[pan.amax] = pat0[x]; break; }
+    n_head = (int)ids.size();
+    hipError_t e;
+    if ((e = d_head_ids.ensure(std::max<size_t>(ids.size(), 1))) || (e = d_head_pat0.ensure(pat0.size())))
+      return hipfail(e, "set_heads");
+    if (!ids.empty() &&
+        (e = hipMemcpyAsync(d_head_ids.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st)))
+      return hipfail(e, "set_heads");
+    if ((e = hipMemcpyAsync(d_head_pat0.p, pat0.data(), pat0.size() * 4, hipMemcpyHostToDevice, st)) ||
+        (e = hipStreamSynchronize(st)))
+      return hipfail(e, "set_heads");
+    return HMC_OK;
+  }
+
+  int build_heads_from_nodes(const MineArgs &) {
+    std::vector<std::pair<uint32_t, uint8_t>> heads;
+    if (head_len == 1 && pan.L > 0) {
+      const int n0 = h_npos[0];
+      std::vector<int32_t> rcb(1);
+      hipError_t e;
+      std::vector<uint8_t> fl(n0), alle(n0);
+      std::vector<uint32_t> pos(n0);
+      if ((e = hipMemcpyAsync(rcb.data(), d_r_child_base.p, 4, hipMemcpyDeviceToHost, st)) ||
+          (e = hipStreamSynchronize(st)))
+        return hipfail(e, "heads");
+      if (n0 > 0) {
+        if ((e = hipMemcpyAsync(fl.data(), n_flags.p + rcb[0], n0, hipMemcpyDeviceToHost, st)) ||
+            (e = hipMemcpyAsync(alle.data(), n_allele.p + rcb[0], n0, hipMemcpyDeviceToHost, st)) ||
+            (e = hipMemcpyAsync(pos.data(), n_pos.p + rcb[0], (size_t)n0 * 4, hipMemcpyDeviceToHost, st)) ||
+            (e = hipStreamSynchronize(st)))
+          return hipfail(e, "heads");
+      }
+      for (int k = 0; k < n0; ++k)
+        if (fl[k] & NODE_ACC) heads.push_back({pos[k], alle[k]});
+    }
+    return set_heads(heads);
+  }
+
+  // ---------------------------------------------------------------- E-step --
+  int estep(double *ll_out, int *H_out, uint64_t *re_out) {
+    if (!have_model) return fail(HMC_EARG, "no pattern model");
+    if (head_len != 1) return fail(HMC_EUNSUPPORTED, "GPU E-step implements min_pattern_len == 1 only");
+    const int L = pan.L, S = this->S(), n = nloc();
+    if (S > S_MAX) return fail(HMC_EUNSUPPORTED, "sample_size > %d", S_MAX);
+    hipError_t e;
+    int dev_cu = 256;
+    hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, device);
+    int G = waves > 0 ? waves : dev_cu * 8;
+    G = std::max(1, std::min(G, n));
+    if ((e = d_total.ensure(n)) || (e = d_ncand.ensure(n)) || (e = d_status.ensure(n)) || (e = d_re.ensure(n)) ||
+        (e = d_sbase.ensure(n)) || (e = d_prior.ensure((size_t)n * S_MAX)) || (e = d_post.ensure((size_t)n * S_MAX)) ||
+        (e = d_weight.ensure((size_t)n * S_MAX)) || (e = d_cstate.ensure((size_t)n * S_MAX)) ||
+        (e = d_cidx.ensure((size_t)n * S_MAX)) || (e = d_rows.ensure((size_t)2 * S * n * L)) ||
+        (e = d_w.ensure((size_t)2 * S * n)) || (e = d_trace_cursor.ensure(1)) || (e = d_maxst.ensure(1)))
+      return hipfail(e, "estep alloc");
+    // trace store budget
+    size_t freeb = 0, totb = 0;
+    hipMemGetInfo(&freeb, &totb);
+    uint64_t tb = trace_bytes ? trace_bytes : (uint64_t)(freeb * 0.35);
+    tb = std::max<uint64_t>(tb, 1ull << 20);
+    if (d_trace.n * 4 < tb / 2 || d_trace.n * 4 > tb * 2) {
+      d_trace.release();
+      if ((e = d_trace.ensure(tb / 4))) return hipfail(e, "trace alloc");
+    }
+    h_total.assign(n, 0.0);
+    h_ncand.assign(n, 0);
+    h_status.assign(n, 0);
+    h_sbase.assign(n, 0);
+    h_re.assign(n, 0);
+    hipMemsetAsync(d_maxst.p, 0, 4, st);
+    int Hacc = 0;
+    int b = 0, batch = n;
+    ms_fwd = ms_tb = 0;
+    while (b < n) {
+      const int bn = std::min(batch, n - b);
+      const int hcap = next_pow2(2 * fcap);
+      const size_t per = estep_scratch_bytes(fcap, hcap, S);
+      const int grid = std::min(G, bn);
+      if ((e = d_scratch.ensure(per * grid))) {
+        if (e == hipErrorOutOfMemory && fcap > 256) { fcap /= 2; continue; }
+        return hipfail(e, "estep scratch");
+      }
+      if ((e = d_loc_off.ensure((size_t)bn * (L + 1)))) return hipfail(e, "estep loc_off");
+      if ((e = hipMemsetAsync(d_trace_cursor.p, 0, 8, st))) return hipfail(e, "estep");
+      EstepArgs a;
+      a.pan = dev_panel();
+      a.mod = dev_model();
+      a.S = S;
+      a.indiv_begin = i0 + b;
+      a.indiv_end = i0 + b + bn;
+      a.scratch = d_scratch.p;
+      a.scratch_stride = per;
+      a.fcap = fcap;
+      a.hcap = hcap;
+      a.trace = d_trace.p;
+      a.trace_cap = d_trace.n;
+      a.trace_cursor = d_trace_cursor.p;
+      a.loc_off = d_loc_off.p;
+      a.total = d_total.p + b;
+      a.ncand = d_ncand.p + b;
+      a.status = d_status.p + b;
+      a.cand_state = d_cstate.p + (size_t)b * S_MAX;
+      a.cand_idx = d_cidx.p + (size_t)b * S_MAX;
+      a.prior = d_prior.p + (size_t)b * S_MAX;
+      a.posterior = d_post.p + (size_t)b * S_MAX;
+      a.weight = d_weight.p + (size_t)b * S_MAX;
+      a.re_count = d_re.p + b;
+      a.max_states = d_maxst.p;
+      hipEventRecord(ev[0], st);
+      if ((e = launch_estep(a, grid, st))) return hipfail(e, "estep_forward launch");
+      hipEventRecord(ev[1], st);
+      if ((e = hipMemcpyAsync(h_status.data() + b, d_status.p + b, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
+          (e = hipMemcpyAsync(h_ncand.data() + b, d_ncand.p + b, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
+          (e = hipStreamSynchronize(st)))
+        return hipfail(e, "estep_forward");
+      float ms = 0;
+      hipEventElapsedTime(&ms, ev[0], ev[1]);
+      ms_fwd += ms;
+      bool ovf_trace = false, ovf_front = false;
+      for (int i = b; i < b + bn; ++i) {
+        if (h_status[i] == EST_OVERFLOW_TRACE) ovf_trace = true;
+        if (h_status[i] == EST_OVERFLOW_FRONTIER) ovf_front = true;
+        if (h_status[i] == EST_NO_HEAD_PATTERN) return fail(HMC_ENOPATTERN, "Can not find matching pattern!");
+      }
+      if (ovf_front) {
+        if (fcap >= 65535) return fail(HMC_EUNSUPPORTED, "frontier exceeds 65535 states");
+        fcap = std::min(65535, fcap * 2);
+        continue;
+      }
+      if (ovf_trace) {
+        if (bn == 1) return fail(HMC_ENOMEM, "trace store too small for one individual");
+        batch = std::max(1, bn / 2);
+        continue;
+      }
+      // sample rows of this batch (HaploModel.cpp:105-106: candidates in order, h0 then h1)
+      for (int i = b; i < b + bn; ++i) {
+        h_sbase[i] = Hacc;
+        Hacc += 2 * h_ncand[i];
+      }
+      if ((e = hipMemcpyAsync(d_sbase.p + b, h_sbase.data() + b, (size_t)bn * 4, hipMemcpyHostToDevice, st)))
+        return hipfail(e, "estep");
+      TracebackArgs t;
+      t.L = L;
+      t.S = S;
+      t.head_len = head_len;
+      t.nbatch = bn;
+      t.trace = d_trace.p;
+      t.loc_off = d_loc_off.p;
+      t.ncand = d_ncand.p + b;
+      t.cand_state = d_cstate.p + (size_t)b * S_MAX;
+      t.cand_idx = d_cidx.p + (size_t)b * S_MAX;
+      t.weight = d_weight.p + (size_t)b * S_MAX;
+      t.sample_base = d_sbase.p + b;
+      t.rows = d_rows.p;
+      t.w_out = d_w.p;
+      hipEventRecord(ev[2], st);
+      if ((e = launch_traceback(t, 0, st))) return hipfail(e, "traceback");
+      hipEventRecord(ev[3], st);
+      if ((e = hipStreamSynchronize(st))) return hipfail(e, "traceback");
+      hipEventElapsedTime(&ms, ev[2], ev[3]);
+      ms_tb += ms;
+      b += bn;
+    }
+    H = Hacc;
+    if ((e = d_samp_lm.ensure((size_t)std::max(H, 1) * L))) return hipfail(e, "samples");
+    if ((e = launch_transpose_u8(d_rows.p, d_samp_lm.p, H, L, H, 0, st))) return hipfail(e, "transpose");
+    if ((e = hipMemcpyAsync(h_total.data(), d_total.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
+        (e = hipMemcpyAsync(h_re.data(), d_re.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)))
+      return hipfail(e, "estep");
+    std::vector<double> w(H);
+    if (H && (e = hipMemcpyAsync(w.data(), d_w.p, (size_t)H * 8, hipMemcpyDeviceToHost, st))) return hipfail(e, "estep");
+    if ((e = hipStreamSynchronize(st))) return hipfail(e, "estep");
+    // ll += log(genotype probability) in individual order (HaploModel.cpp:110)
+    double ll = 0.0;
+    for (int i = 0; i < n; ++i) ll += log(h_total[i]);
+    // HaploData::checkTotalWeight (HaploData.cpp:120-126)
+    double tw = 0.0;
+    for (int h = 0; h < H; ++h) tw += w[h];
+    double red[2] = {ll, tw};
+    int rc = allreduce_host(red, 2);
+    if (rc) return rc;
+    ll = red[0];
+    total_weight = red[1];
+    uint64_t re = 0;
+    for (int i = 0; i < n; ++i) re += h_re[i];
+    have_samples = true;
+    have_estep = true;
+    if (ll_out) *ll_out = ll;
+    if (H_out) *H_out = H;
+    if (re_out) *re_out = re;
+    return HMC_OK;
+  }
+
+  static int next_pow2(int x) {
+    int p = 1;
+    while (p < x) p <<= 1;
+    return p;
+  }
+
+  DevModel dev_model() const {
+    DevModel m;
+    m.P = P;
+    m.succ = t_succ.p;
+    m.tp = t_tp.p;
+    m.freq = t_freq.p;
+    m.last = t_last.p;
+    m.n_head = n_head;
+    m.head_len = head_len;
+    m.head_ids = d_head_ids.p;
+    m.head_pat0 = d_head_pat0.p;
+    return m;
+  }
+
+  // selected pairs of the last E-step, allele indices [n][2][L]
+  int resolutions_idx(std::vector<uint8_t> &out) {
+    if (!have_estep) return fail(HMC_EARG, "no E-step has run");
+    const int n = nloc(), L = pan.L;
+    hipError_t e;
+    if ((e = d_res.ensure((size_t)n * 2 * L))) return hipfail(e, "resolutions");
+    if ((e = launch_gather_resolutions(d_rows.p, L, d_sbase.p, d_ncand.p, d_geno_im.p, i0, n, d_res.p, st)))
+      return hipfail(e, "resolutions");
+    out.resize((size_t)n * 2 * L);
+    if ((e = hipMemcpyAsync(out.data(), d_res.p, out.size(), hipMemcpyDeviceToHost, st)) ||
+        (e = hipStreamSynchronize(st)))
+      return hipfail(e, "resolutions");
+    return HMC_OK;
+  }
+
+  void to_symbols(const std::vector<uint8_t> &idx, int32_t *out) const {
+    const int n = nloc(), L = pan.L;
+    for (int i = 0; i < n; ++i)
+      for (int h = 0; h < 2; ++h)
+        for (int k = 0; k < L; ++k) {
+          const size_t o = ((size_t)i * 2 + h) * L + k;
+          out[o] = pan.symbol(k, idx[o]);
+        }
+  }
+
+  // ------------------------------------------------------------------ run --
+  int run(int max_iter, hmc_iter_log *log, int cap, int *iters, double *t_m0, uint64_t *rm0, int *np0) {
+    using clk = std::chrono::steady_clock;
+    have_samples = false;  // HaploModel::build -> setGenoData clears samples (HaploBuilder.cpp:19-23)
+    auto t0 = clk::now();
+    int np = 0;
+    uint64_t rm = 0;
+    int rc = mine(&np, &rm);
+    if (rc) return rc;
+    if (t_m0) *t_m0 = std::chrono::duration<double>(clk::now() - t0).count();
+    if (rm0) *rm0 = rm;
+    if (np0) *np0 = np;
+    // resolutions = unphased (HaploModel.cpp:127)
+    const int n = nloc(), L = pan.L;
+    best_res.assign((size_t)n * 2 * L, 0);
+    for (int i = 0; i < n; ++i)
+      for (int h = 0; h < 2; ++h)
+        for (int k = 0; k < L; ++k)
+          best_res[((size_t)i * 2 + h) * L + k] = pan.idx[((size_t)(i0 + i) * 2 + h) * L + k];
+    have_best = true;
+    double old_ll = -DBL_MAX;
+    int it = 0;
+    for (it = 1; it <= max_iter; ++it) {
+      auto t1 = clk::now();
+      double ll = 0;
+      int Hs = 0;
+      uint64_t re = 0;
+      if ((rc = estep(&ll, &Hs, &re))) return rc;
+      const double te = std::chrono::duration<double>(clk::now() - t1).count();
+      if (ll >= old_ll) {
+        if ((rc = resolutions_idx(best_res))) return rc;
+      }
+      hmc_iter_log rec{};
+      rec.log_likelihood = ll;
+      rec.t_estep_s = te;
+      rec.r_e = re;
+      rec.n_samples = Hs;
+      rec.n_patterns = P;
+      const bool go = it < max_iter && ll >= old_ll && (old_ll - ll) / old_ll > 0.0001;  // HaploModel.cpp:139
+      if (go) {
+        auto t2 = clk::now();
+        if ((rc = mine(&np, &rm))) return rc;
+        rec.t_mstep_s = std::chrono::duration<double>(clk::now() - t2).count();
+        rec.r_m = rm;
+        rec.n_patterns = np;
+        old_ll = ll;
+      }
+      if (log && it - 1 < cap) log[it - 1] = rec;
+      if (!go) break;
+    }
+    if (iters) *iters = std::min(it, max_iter);
+    return HMC_OK;
+  }
+};
+
+}  // namespace hmc
+
+using hmc::Ctx;
+
+struct hmc_ctx {
+  Ctx c;
+};
+
+// ===================================================================== C-ABI
+extern "C" {
+
+const char *hmc_version(void) { return "hmc_amd 0.1 (gfx950)"; }
+
+static int ctx_init(hmc_ctx *h, int device) {
+  hipError_t e = hipSetDevice(device);
+  if (e) return h->c.hipfail(e, "hipSetDevice");
+  h->c.device = device;
+  if ((e = hipStreamCreateWithFlags(&h->c.st, hipStreamNonBlocking))) return h->c.hipfail(e, "hipStreamCreate");
+  for (auto &ev : h->c.ev)
+    if ((e = hipEventCreate(&ev))) return h->c.hipfail(e, "hipEventCreate");
+  return HMC_OK;
+}
+
+int hmc_ctx_create(int device, hmc_ctx **out) {
+  if (!out) return HMC_EARG;
+  hmc_ctx *h = new hmc_ctx;
+  int rc = ctx_init(h, device);
+  *out = h;  // returned even on failure so the caller can read hmc_ctx_error
+  return rc;
+}
+
+int hmc_rccl_unique_id(void *out128) {
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return HMC_ERCCL;
+  memcpy(out128, &id, sizeof id);
+  return HMC_OK;
+}
+
+int hmc_ctx_create_dist(int device, int rank, int world, const void *unique_id, hmc_ctx **out) {
+  if (!out || world < 1 || rank < 0 || rank >= world) return HMC_EARG;
+  hmc_ctx *h = new hmc_ctx;
+  *out = h;
+  int rc = ctx_init(h, device);
+  if (rc) return rc;
+  h->c.rank = rank;
+  h->c.world = world;
+  if (world > 1) {
+    ncclUniqueId id;
+    memcpy(&id, unique_id, sizeof id);
+    ncclResult_t r = ncclCommInitRank(&h->c.comm, world, id, rank);
+    if (r != ncclSuccess) return h->c.fail(HMC_ERCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  }
+  return HMC_OK;
+}
+
+void hmc_ctx_destroy(hmc_ctx *h) {
+  if (!h) return;
+  if (h->c.comm) ncclCommDestroy(h->c.comm);
+  for (auto &ev : h->c.ev)
+    if (ev) hipEventDestroy(ev);
+  if (h->c.st) hipStreamDestroy(h->c.st);
+  delete h;
+}
+
+const char *hmc_ctx_error(const hmc_ctx *h) { return h ? h->c.err.c_str() : "null context"; }
+
+int hmc_set_params(hmc_ctx *h, double min_freq_abs, double min_freq, int min_len, int max_len, int sample_size) {
+  if (!h) return HMC_EARG;
+  h->c.min_freq_abs = min_freq_abs;
+  h->c.min_freq = min_freq;
+  h->c.min_len = min_len;
+  h->c.max_len = max_len;
+  h->c.sample_size = sample_size;
+  return HMC_OK;
+}
+
+int hmc_set_tuning(hmc_ctx *h, int frontier_cap, uint64_t trace_bytes, int waves) {
+  if (!h) return HMC_EARG;
+  if (frontier_cap > 0) h->c.fcap = std::min(frontier_cap, 65535);
+  h->c.trace_bytes = trace_bytes;
+  h->c.waves = waves;
+  return HMC_OK;
+}
+
+int hmc_load_phase(hmc_ctx *h, const char *path) {
+  if (!h || !path) return HMC_EARG;
+  hmc::Panel p;
+  std::string err;
+  if (!hmc::read_phase(path, p, err)) return h->c.fail(HMC_EIO, "%s", err.c_str());
+  h->c.pan = std::move(p);
+  return h->c.upload_panel();
+}
+
+int hmc_load_genotypes(hmc_ctx *h, int N, int L, const int32_t *alleles, const char *types) {
+  if (!h || N <= 0 || L <= 0 || !alleles) return HMC_EARG;
+  hmc::Panel p;
+  p.N = N;
+  p.L = L;
+  p.al.assign(alleles, alleles + (size_t)N * 2 * L);
+  p.types = types ? std::string(types, strnlen(types, (size_t)L)) : std::string(L, 'S');
+  if ((int)p.types.size() < L) p.types.resize(L, 'S');
+  std::string err;
+  if (!p.build_tables(err)) return h->c.fail(HMC_EUNSUPPORTED, "%s", err.c_str());
+  h->c.pan = std::move(p);
+  return h->c.upload_panel();
+}
+
+int hmc_panel_info(const hmc_ctx *h, int *N, int *L, int *amax) {
+  if (!h || !h->c.have_panel) return HMC_EARG;
+  if (N) *N = h->c.pan.N;
+  if (L) *L = h->c.pan.L;
+  if (amax) *amax = h->c.pan.amax;
+  return HMC_OK;
+}
+
+int hmc_allele_table(const hmc_ctx *h, int32_t *num, int32_t *sym, double *freq) {
+  if (!h || !h->c.have_panel) return HMC_EARG;
+  const auto &p = h->c.pan;
+  for (int k = 0; k < p.L; ++k) {
+    if (num) num[k] = (int32_t)p.sym[k].size();
+    for (int j = 0; j < p.amax; ++j) {
+      const bool ok = j < (int)p.sym[k].size();
+      if (sym) sym[(size_t)k * p.amax + j] = ok ? p.sym[k][j].first : -1;
+      if (freq) freq[(size_t)k * p.amax + j] = ok ? p.sym[k][j].second : 0.0;
+    }
+  }
+  return HMC_OK;
+}
+
+int hmc_find_patterns(hmc_ctx *h, int *n_patterns, uint64_t *r_m) {
+  if (!h) return HMC_EARG;
+  return h->c.mine(n_patterns, r_m);
+}
+
+int hmc_model_info(const hmc_ctx *h, int *n_patterns, int *head_len) {
+  if (!h || !h->c.have_model) return HMC_EARG;
+  if (n_patterns) *n_patterns = h->c.P;
+  if (head_len) *head_len = h->c.head_len;
+  return HMC_OK;
+}
+
+int hmc_get_patterns(hmc_ctx *h, int32_t *start, int32_t *len, double *freq, double *prefix, double *tp,
+                     int32_t *succ, int32_t *alleles, int maxlen) {
+  if (!h || !h->c.have_model) return HMC_EARG;
+  Ctx &c = h->c;
+  const int P = c.P, A = c.pan.amax;
+  std::vector<int32_t> st(P), ln(P), node(P);
+  std::vector<uint8_t> last(P);
+  hipError_t e;
+  if ((e = hipMemcpyAsync(st.data(), c.t_start.p, (size_t)P * 4, hipMemcpyDeviceToHost, c.st)) ||
+      (e = hipMemcpyAsync(ln.data(), c.t_len.p, (size_t)P * 4, hipMemcpyDeviceToHost, c.st)) ||
+      (freq && (e = hipMemcpyAsync(freq, c.t_freq.p, (size_t)P * 8, hipMemcpyDeviceToHost, c.st))) ||
+      (prefix && (e = hipMemcpyAsync(prefix, c.t_prefix.p, (size_t)P * 8, hipMemcpyDeviceToHost, c.st))) ||
+      (tp && (e = hipMemcpyAsync(tp, c.t_tp.p, (size_t)P * 8, hipMemcpyDeviceToHost, c.st))) ||
+      (e = hipMemcpyAsync(last.data(), c.t_last.p, (size_t)P, hipMemcpyDeviceToHost, c.st)) ||
+      (e = hipStreamSynchronize(c.st)))
+    return c.hipfail(e, "get_patterns");
+  if (start) memcpy(start, st.data(), (size_t)P * 4);
+  if (len) memcpy(len, ln.data(), (size_t)P * 4);
+  if (succ) {
+    std::vector<uint32_t> s((size_t)P * A);
+    if ((e = hipMemcpyAsync(s.data(), c.t_succ.p, s.size() * 4, hipMemcpyDeviceToHost, c.st)) ||
+        (e = hipStreamSynchronize(c.st)))
+      return c.hipfail(e, "get_patterns");
+    for (size_t i = 0; i < s.size(); ++i) succ[i] = s[i] == hmc::NONE ? -1 : (int32_t)s[i];
+  }
+  if (alleles && maxlen > 0) {
+    // Rebuild allele strings from the candidate tree (parent chain) when the
+    // table came from the miner; else only the last allele is known.
+    std::vector<int32_t> par;
+    std::vector<uint8_t> al;
+    bool tree = c.node_cap > 0;
+    if (tree) {
+      if ((e = hipMemcpyAsync(node.data(), c.t_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, c.st)) ||
+          (e = hipStreamSynchronize(c.st)))
+        return c.hipfail(e, "get_patterns");
+      int nmax = 0;
+      for (int i = 0; i < P; ++i) nmax = std::max(nmax, node[i] + 1);
+      par.resize(nmax);
+      al.resize(nmax);
+      if (nmax && ((e = hipMemcpyAsync(par.data(), c.n_parent.p, (size_t)nmax * 4, hipMemcpyDeviceToHost, c.st)) ||
+                   (e = hipMemcpyAsync(al.data(), c.n_allele.p, (size_t)nmax, hipMemcpyDeviceToHost, c.st)) ||
+                   (e = hipStreamSynchronize(c.st))))
+        return c.hipfail(e, "get_patterns");
+    }
+    for (int i = 0; i < P; ++i) {
+      int32_t *row = alleles + (size_t)i * maxlen;
+      for (int k = 0; k < maxlen; ++k) row[k] = -1;
+      if (tree) {
+        int32_t v = node[i];
+        for (int k = ln[i] - 1; k >= 0 && v >= 0; --k) {
+          if (k < maxlen) row[k] = c.pan.symbol(st[i] + k, al[v]);
+          v = par[v];
+        }
+      } else if (ln[i] - 1 < maxlen && ln[i] > 0) {
+        row[ln[i] - 1] = c.pan.symbol(st[i] + ln[i] - 1, last[i]);
+      }
+    }
+  }
+  return HMC_OK;
+}
+
+int hmc_set_patterns(hmc_ctx *h, int P, const int32_t *start, const int32_t *len, const double *freq, const double *tp,
+                     const int32_t *succ, const int32_t *last_symbol) {
+  if (!h || !h->c.have_panel || P <= 0) return HMC_EARG;
+  Ctx &c = h->c;
+  const int A = c.pan.amax;
+  int rc = c.alloc_table(P);
+  if (rc) return rc;
+  std::vector<uint8_t> last(P);
+  std::vector<uint32_t> s((size_t)P * A);
+  std::vector<int32_t> node(P, -1);
+  std::vector<std::pair<uint32_t, uint8_t>> heads;
+  int hl = std::max(c.min_len, 1);
+  for (int i = 0; i < P; ++i) {
+    const int k = start[i] + len[i] - 1;
+    const int j = c.pan.index_of(k, last_symbol[i]);
+    if (j < 0) return c.fail(HMC_EARG, "pattern %d: allele not in locus table", i);
+    last[i] = (uint8_t)j;
+    for (int a = 0; a < A; ++a) s[(size_t)i * A + a] = succ[(size_t)i * A + a] < 0 ? hmc::NONE : (uint32_t)succ[(size_t)i * A + a];
+    if (start[i] == 0 && len[i] == hl) heads.push_back({(uint32_t)i, (uint8_t)j});
+  }
+  hipError_t e;
+  if ((e = hipMemcpyAsync(c.t_start.p, start, (size_t)P * 4, hipMemcpyHostToDevice, c.st)) ||
+      (e = hipMemcpyAsync(c.t_len.p, len, (size_t)P * 4, hipMemcpyHostToDevice, c.st)) ||
+      (e = hipMemcpyAsync(c.t_node.p, node.data(), (size_t)P * 4, hipMemcpyHostToDevice, c.st)) ||
+      (e = hipMemcpyAsync(c.t_freq.p, freq, (size_t)P * 8, hipMemcpyHostToDevice, c.st)) ||
+      (e = hipMemcpyAsync(c.t_prefix.p, freq, (size_t)P * 8, hipMemcpyHostToDevice, c.st)) ||
+      (e = hipMemcpyAsync(c.t_tp.p, tp, (size_t)P * 8, hipMemcpyHostToDevice, c.st)) ||
+      (e = hipMemcpyAsync(c.t_last.p, last.data(), (size_t)P, hipMemcpyHostToDevice, c.st)) ||
+      (e = hipMemcpyAsync(c.t_succ.p, s.data(), s.size() * 4, hipMemcpyHostToDevice, c.st)) ||
+      (e = hipStreamSynchronize(c.st)))
+    return c.hipfail(e, "set_patterns");
+  c.P = P;
+  c.head_len = hl;
+  c.node_cap = 0;  // allele strings are not known for an injected table
+  rc = c.set_heads(heads);
+  if (rc) return rc;
+  c.have_model = true;
+  return HMC_OK;
+}
+
+int hmc_resolve_all(hmc_ctx *h, double *ll, int *n_samples, uint64_t *r_e) {
+  if (!h) return HMC_EARG;
+  return h->c.estep(ll, n_samples, r_e);
+}
+
+int hmc_get_estep(hmc_ctx *h, double *total, int32_t *ncand, int32_t *status, double *prior, double *posterior,
+                  double *weight) {
+  if (!h || !h->c.have_estep) return HMC_EARG;
+  Ctx &c = h->c;
+  const int n = c.nloc(), S = c.S();
+  if (total) memcpy(total, c.h_total.data(), (size_t)n * 8);
+  if (ncand) memcpy(ncand, c.h_ncand.data(), (size_t)n * 4);
+  if (status) memcpy(status, c.h_status.data(), (size_t)n * 4);
+  std::vector<double> buf((size_t)n * hmc::S_MAX);
+  hipError_t e;
+  double *outs[3] = {prior, posterior, weight};
+  double *srcs[3] = {c.d_prior.p, c.d_post.p, c.d_weight.p};
+  for (int q = 0; q < 3; ++q) {
+    if (!outs[q]) continue;
+    if ((e = hipMemcpyAsync(buf.data(), srcs[q], buf.size() * 8, hipMemcpyDeviceToHost, c.st)) ||
+        (e = hipStreamSynchronize(c.st)))
+      return c.hipfail(e, "get_estep");
+    for (int i = 0; i < n; ++i)
+      for (int k = 0; k < S; ++k)
+        outs[q][(size_t)i * S + k] = k < c.h_ncand[i] ? buf[(size_t)i * hmc::S_MAX + k] : 0.0;
+  }
+  return HMC_OK;
+}
+
+int hmc_get_samples(hmc_ctx *h, int32_t *alleles, double *weights, double *total_weight) {
+  if (!h || !h->c.have_estep) return HMC_EARG;
+  Ctx &c = h->c;
+  const int H = c.H, L = c.pan.L;
+  hipError_t e;
+  if (alleles && H) {
+    std::vector<uint8_t> rows((size_t)H * L);
+    if ((e = hipMemcpyAsync(rows.data(), c.d_rows.p, rows.size(), hipMemcpyDeviceToHost, c.st)) ||
+        (e = hipStreamSynchronize(c.st)))
+      return c.hipfail(e, "get_samples");
+    for (int s = 0; s < H; ++s)
+      for (int k = 0; k < L; ++k) alleles[(size_t)s * L + k] = c.pan.symbol(k, rows[(size_t)s * L + k]);
+  }
+  if (weights && H) {
+    if ((e = hipMemcpyAsync(weights, c.d_w.p, (size_t)H * 8, hipMemcpyDeviceToHost, c.st)) ||
+        (e = hipStreamSynchronize(c.st)))
+      return c.hipfail(e, "get_samples");
+  }
+  if (total_weight) *total_weight = c.total_weight;
+  return HMC_OK;
+}
+
+int hmc_get_resolutions(hmc_ctx *h, int32_t *out) {
+  if (!h || !out) return HMC_EARG;
+  std::vector<uint8_t> idx;
+  int rc = h->c.resolutions_idx(idx);
+  if (rc) return rc;
+  h->c.to_symbols(idx, out);
+  return HMC_OK;
+}
+
+int hmc_run(hmc_ctx *h, int max_iteration, hmc_iter_log *log, int log_cap, int *iterations, double *t_m0_s,
+            uint64_t *r_m0, int *n_patterns0) {
+  if (!h) return HMC_EARG;
+  return h->c.run(max_iteration, log, log_cap, iterations, t_m0_s, r_m0, n_patterns0);
+}
+
+int hmc_get_best_resolutions(hmc_ctx *h, int32_t *out) {
+  if (!h || !out || !h->c.have_best) return HMC_EARG;
+  h->c.to_symbols(h->c.best_res, out);
+  return HMC_OK;
+}
+
+int hmc_write_phase(hmc_ctx *h, const char *path) {
+  if (!h || !path || !h->c.have_best || h->c.world != 1) return HMC_EARG;
+  Ctx &c = h->c;
+  FILE *fp = fopen(path, "w");
+  if (!fp) return c.fail(HMC_EIO, "Can not open file %s!", path);
+  const int N = c.pan.N, L = c.pan.L;
+  fprintf(fp, "%d\n%d\nP", N, L);
+  for (int k = 0; k < L; ++k) fprintf(fp, " %d", k * 1000);  // Constant::average_marker_distance
+  fprintf(fp, "\n%s\n", c.pan.types.c_str());
+  for (int i = 0; i < N; ++i) {
+    fprintf(fp, "#%d\n", i + 1);
+    for (int hh = 0; hh < 2; ++hh) {
+      for (int k = 0; k < L; ++k) {
+        const int32_t a = c.pan.symbol(k, c.best_res[((size_t)i * 2 + hh) * L + k]);
+        if (c.pan.types[k] == 'S') fprintf(fp, "%c ", a < 0 ? '?' : (char)a);
+        else fprintf(fp, "%d ", a);
+      }
+      fprintf(fp, "\n");
+    }
+  }
+  fclose(fp);
+  return HMC_OK;
+}
+
+int hmc_last_timings(const hmc_ctx *h, double *f, double *t, double *m) {
+  if (!h) return HMC_EARG;
+  if (f) *f = h->c.ms_fwd;
+  if (t) *t = h->c.ms_tb;
+  if (m) *m = h->c.ms_m;
+  return HMC_OK;
+}
+
+void hmc_test_nth_element(double *lik, uint32_t *tag, int n, int nth) {
+  hmc::LinkList v{lik, tag, 1};
+  hmc::nth_element_greater(v, n, nth);
+}
+
+void hmc_test_sort_small(double *lik, uint32_t *tag, int n) {
+  hmc::LinkList v{lik, tag, 1};
+  hmc::sort_greater_small(v, n);
+}
+
+}  // extern "C"

@@ -1,0 +1,111 @@
+// hmc_internal.hpp — device-side data layout shared by the HIP kernels and the
+// host runtime of libhmc_amd.  Nothing here crosses the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace hmc {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint8_t MISSING = 0xFF;
+constexpr int S_MAX = 16;    // sample_size limit (std::sort == insertion sort up to 16)
+constexpr int A_MAX = 32;    // alleles per locus limit
+constexpr int WAVE = 64;
+
+// Link metadata word (one k-best entry, HaploPairLink HaploPair.h:14-28):
+//   bits 0-15 predecessor state, 16-23 index in the predecessor's list,
+//   bit 24 reversed, bit 25 homozygous, bit 26 head (link == NULL).
+__host__ __device__ inline uint32_t meta_pack(uint32_t pred, uint32_t idx, bool rev, bool homo, bool head) {
+  return (pred & 0xFFFFu) | ((idx & 0xFFu) << 16) | (rev ? 1u << 24 : 0u) | (homo ? 1u << 25 : 0u) |
+         (head ? 1u << 26 : 0u);
+}
+__host__ __device__ inline uint32_t meta_pred(uint32_t m) { return m & 0xFFFFu; }
+__host__ __device__ inline uint32_t meta_idx(uint32_t m) { return (m >> 16) & 0xFFu; }
+__host__ __device__ inline bool meta_rev(uint32_t m) { return (m >> 24) & 1u; }
+__host__ __device__ inline bool meta_homo(uint32_t m) { return (m >> 25) & 1u; }
+__host__ __device__ inline bool meta_head(uint32_t m) { return (m >> 26) & 1u; }
+
+// Per-state trace header word: last allele of pattern a / b, link count.
+__host__ __device__ inline uint32_t hdr_pack(uint32_t al_a, uint32_t al_b, uint32_t n) {
+  return (al_a & 0xFFu) | ((al_b & 0xFFu) << 8) | ((n & 0xFFu) << 16);
+}
+
+// E-step status codes written per individual.
+enum EStatus : int32_t {
+  EST_OK = 0,
+  EST_UNRESOLVED = 1,          // dead frontier (HaploBuilder.cpp:80-81)
+  EST_OVERFLOW_FRONTIER = -1,  // more states than the per-wave capacity
+  EST_OVERFLOW_TRACE = -2,     // trace buffer exhausted
+  EST_NO_HEAD_PATTERN = -3,    // "Can not find matching pattern!" (HaploBuilder.cpp:215-217)
+};
+
+// Panel resident in HBM.
+struct DevPanel {
+  int N = 0, L = 0, amax = 0;
+  uchar2 *geno_im = nullptr;   // [N][L] (allele index of haplotype 0, 1), 0xFF missing
+  uchar2 *geno_lm = nullptr;   // [L][N] same, locus-major (genotype-branch mining)
+  uint8_t *anum = nullptr;     // [L]
+  double *afreq = nullptr;     // [L][amax]
+};
+
+// Pattern model resident in HBM (PatternManager after initialize()).
+struct DevModel {
+  int P = 0;
+  uint32_t *succ = nullptr;    // [P][amax]
+  double *tp = nullptr;        // [P]
+  double *freq = nullptr;      // [P]
+  uint8_t *last = nullptr;     // [P] last allele index
+  int n_head = 0, head_len = 1;
+  uint32_t *head_ids = nullptr;   // [n_head], id order
+  uint32_t *head_pat0 = nullptr;  // [amax+1] pattern id of (locus 0, allele x); [amax] = missing allele
+};
+
+struct EstepArgs {
+  DevPanel pan;
+  DevModel mod;
+  int S;
+  int indiv_begin, indiv_end;  // batch [begin, end)
+  // per-wave scratch
+  char *scratch;
+  size_t scratch_stride;
+  int fcap, hcap;
+  // trace store
+  uint32_t *trace;
+  unsigned long long trace_cap;     // words
+  unsigned long long *trace_cursor; // bump allocator
+  unsigned long long *loc_off;      // [batch][L+1] word offsets
+  // per-individual outputs (indexed by individual - indiv_begin)
+  double *total;
+  int32_t *ncand;
+  int32_t *status;
+  uint32_t *cand_state;  // [batch][S_MAX]
+  uint32_t *cand_idx;    // [batch][S_MAX]
+  double *prior;         // [batch][S_MAX]
+  double *posterior;     // [batch][S_MAX]
+  double *weight;        // [batch][S_MAX]
+  unsigned long long *re_count;  // [batch]
+  unsigned int *max_states;      // [1] running maximum frontier size
+};
+
+struct TracebackArgs {
+  int L, S, head_len, nbatch;
+  const uint32_t *trace;
+  const unsigned long long *loc_off;
+  const int32_t *ncand;
+  const uint32_t *cand_state, *cand_idx;
+  const double *weight;
+  const int32_t *sample_base;  // [batch] first sample row of each individual
+  uint8_t *rows;               // [H][L] sample-major haplotypes (allele index)
+  double *w_out;               // [H]
+};
+
+size_t estep_scratch_bytes(int fcap, int hcap, int S);
+hipError_t launch_estep(const EstepArgs &a, int grid, hipStream_t st);
+hipError_t launch_traceback(const TracebackArgs &a, int total_cands, hipStream_t st);
+hipError_t launch_transpose_u8(const uint8_t *in, uint8_t *out, int rows, int cols, int ld_out, int col0,
+                               hipStream_t st);
+hipError_t launch_gather_resolutions(const uint8_t *rows, int L, const int32_t *sbase, const int32_t *ncand,
+                                     const uchar2 *geno_im, int i0, int n, uint8_t *out, hipStream_t st);
+hipError_t launch_scan_i32(const int32_t *in, int32_t *out_excl, int n, int mul, int32_t *total, hipStream_t st);
+
+}  // namespace hmc

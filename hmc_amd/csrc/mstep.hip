@@ -1,0 +1,441 @@
+// mstep.hip — pattern mining (M-step) of the HaploModel EM on CDNA4 (gfx950).
+//
+// Restates PatternManager::findPatternByFreq (PatternManager.cpp:27-42), its
+// DFS candidate search searchPattern (:100-144), the frequency scans
+// checkFrequency / checkFrequencyWithExtension / getMatchingFrequency
+// (:146-291) and initialize (:293-318: ids, head list, successors through the
+// BackwardPatternTree, PatternTree.cpp:50-72,98-134).
+//
+// The reference grows the candidate tree depth-first with an explicit stack.
+// Here the same tree is grown breadth-first, one pattern length per step, so
+// that every candidate of a level is scanned in parallel:
+//   mine_count    one wavefront per extendable parent streams the parent's
+//                 matching list (sample or individual indices, in ascending
+//                 order, exactly the MatchingState the reference passes down)
+//                 and produces every child's weighted sum.  The sum of each
+//                 child is accumulated strictly in list order (a single
+//                 dependent add chain per child, lane k owns child k) so the
+//                 frequencies are bit-identical to the reference's sequential
+//                 `total_freq += ...` loops.
+//   mine_finalize frequency, prefix frequency, transition probability and the
+//                 accept / extend rules of searchPattern.
+//   mine_scatter  stable partition of the parent list into the children's
+//                 lists (ballot + prefix popcount), for extended children only.
+// After the last level the DFS pre-order of the reference (start L-1 first,
+// then descending allele index; PatternManager.cpp:94-97,112-113) is rebuilt
+// from subtree sizes (bottom-up) and positions (top-down): position = pattern
+// id.  Successors are found by walking suffix links (link(v) = v without its
+// first allele) from the longest suffix down, which visits exactly the
+// candidates the backward trie walk of findLongestMatchPattern would test.
+#include <hipcub/hipcub.hpp>
+
+#include "hmc_internal.hpp"
+#include "mstep.hpp"
+
+namespace hmc {
+
+namespace {
+
+__device__ inline int32_t root_code(int k) { return -(k + 2); }
+__device__ inline bool is_root(int32_t u) { return u <= -2; }
+__device__ inline int root_start(int32_t u) { return -u - 2; }
+
+// One matching-list entry's contribution to child allele `al` at locus e.
+struct EntryView {
+  bool in;
+  uint32_t item;
+  double v;    // genotype branch: product carried from the parent
+  uchar2 g;    // genotype branch: both alleles at e
+  uint8_t h;   // sample branch: allele at e
+  double w;    // sample branch: weight
+};
+
+__device__ inline EntryView load_entry(const MineArgs &a, bool root, const uint32_t *lidx, const double *lval,
+                                       int i, int n, int e) {
+  EntryView x;
+  x.in = i < n;
+  x.item = x.in ? (root ? (uint32_t)(a.item_base + i) : lidx[i]) : 0u;
+  x.v = 1.0;
+  x.w = 0.0;
+  x.h = 0xFE;
+  x.g = make_uchar2(0xFE, 0xFE);
+  if (x.in) {
+    if (a.genotype) {
+      if (!root) x.v = lval[i];
+      x.g = a.geno_lm[(size_t)e * a.item_stride + x.item];
+    } else {
+      x.h = a.samp_lm[(size_t)e * a.item_stride + x.item];
+      x.w = a.w[x.item];
+    }
+  }
+  return x;
+}
+
+// getMatchingFrequency (PatternManager.cpp:267-291) for one allele, times the
+// carried product (checkFrequencyWithExtension :243-248); sample branch
+// (:252-263) contributes the haplotype weight.
+__device__ inline bool contribution(const MineArgs &a, const EntryView &x, int e, uint8_t al, double &c) {
+  if (!x.in) { c = 0.0; return false; }
+  if (a.genotype) {
+    const bool m0 = x.g.x == MISSING, m1 = x.g.y == MISSING;
+    if (!(m0 || m1 || x.g.x == al || x.g.y == al)) { c = 0.0; return false; }
+    const double af = a.afreq[(size_t)e * a.amax + al];
+    const double x0 = m0 ? af : (x.g.x == al ? 1.0 : 0.0);
+    const double x1 = m1 ? af : (x.g.y == al ? 1.0 : 0.0);
+    const double f = (0.0 + x0) + x1;
+    const double t = 1.0 * (0.5 * f);
+    c = x.v * t;
+    return true;
+  }
+  if (x.h != al) { c = 0.0; return false; }
+  c = x.w;
+  return true;
+}
+
+struct ParentView {
+  bool ok;
+  int start, e, n, cb, nc;
+  double pfreq;
+  const uint32_t *lidx;
+  const double *lval;
+};
+
+__device__ inline ParentView parent_view(const MineArgs &a, int level, int pidx) {
+  ParentView p;
+  p.ok = true;
+  p.lidx = nullptr;
+  p.lval = nullptr;
+  if (level == 1) {
+    p.start = pidx;
+    p.e = pidx;
+    p.n = a.n_items;
+    p.cb = a.r_child_base[pidx];
+    p.pfreq = 1.0;  // HaploPattern ctor: empty pattern has frequency 1 (HaploPattern.h:86)
+  } else {
+    if (!(a.flags[pidx] & NODE_EXT)) { p.ok = false; return p; }
+    p.start = a.start[pidx];
+    p.e = p.start + level - 1;
+    p.n = (int)a.cnt[pidx];
+    p.cb = a.child_base[pidx];
+    p.pfreq = a.freq[pidx];
+    p.lidx = a.lin_idx + a.list_off[pidx];
+    if (a.genotype) p.lval = a.lin_val + a.list_off[pidx];
+  }
+  p.nc = a.npos[p.e];
+  return p;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg, int pend) {
+  extern __shared__ double cbuf[];  // [nc][65]
+  const int lane = threadIdx.x;
+  const int pidx = pbeg + blockIdx.x;
+  if (pidx >= pend) return;
+  const ParentView p = parent_view(a, level, pidx);
+  if (!p.ok) return;
+  const uint8_t *ca = a.pos_allele + (size_t)p.e * a.amax;
+  double sum = 0.0;
+  uint32_t cnt = 0;
+  for (int base = 0; base < p.n; base += WAVE) {
+    const EntryView x = load_entry(a, level == 1, p.lidx, p.lval, base + lane, p.n, p.e);
+    for (int k = 0; k < p.nc; ++k) {
+      double c;
+      const bool m = contribution(a, x, p.e, ca[k], c);
+      cbuf[k * 65 + lane] = c;  // non-matching entries add +0.0: an exact no-op on a sum >= +0
+      const uint64_t b = __ballot(m);
+      if (lane == k) cnt += (uint32_t)__popcll(b);
+    }
+    __syncthreads();
+    if (lane < p.nc) {
+      double s = sum;
+      const double *row = cbuf + lane * 65;
+#pragma unroll 16
+      for (int j = 0; j < WAVE; ++j) s = s + row[j];
+      sum = s;
+    }
+    __syncthreads();
+  }
+  if (lane < p.nc) {
+    const int c = p.cb + lane;
+    const uint8_t al = ca[lane];
+    a.sum[c] = sum;
+    a.cnt[c] = cnt;
+    a.start[c] = p.start;
+    a.allele[c] = al;
+    a.prefix[c] = p.pfreq;
+    a.parent[c] = level == 1 ? root_code(p.start) : pidx;
+    // suffix link: node for this pattern without its first allele
+    int32_t lk;
+    if (level == 1) {
+      lk = root_code(p.start + 1);
+    } else {
+      const int32_t lp = a.link[pidx];
+      const uint8_t rk = a.rank_of[(size_t)p.e * a.amax + al];
+      if (lp == -1 || rk == 0xFF) lk = -1;
+      else if (is_root(lp)) lk = a.r_child_base[root_start(lp)] + rk;
+      else lk = (a.flags[lp] & NODE_EXT) ? a.child_base[lp] + rk : -1;
+    }
+    a.link[c] = lk;
+  }
+  if (lane == 0) atomicAdd(a.rm, (unsigned long long)p.n * (unsigned long long)p.nc);
+}
+
+// searchPattern's rules (PatternManager.cpp:110-133) for the nodes [b, e) of one level.
+__global__ void mine_finalize(MineArgs a, int level, int b, int e, unsigned long long *ext_list,
+                              int32_t *next_children) {
+  const int c = b + blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= e) return;
+  const double freq = a.sum[c] / a.denom;
+  const double pre = a.prefix[c];
+  double tp = pre > 0 ? freq / pre : freq;
+  tp = tp < 1.0 ? tp : 1.0;  // HaploPattern::setTransitionProb (HaploPattern.h:47)
+  a.freq[c] = freq;
+  a.tp[c] = tp;
+  const int st = a.start[c];
+  const bool acc = (freq >= a.min_freq || level <= a.min_len) && level > 0 && level >= a.min_len;
+  const bool ext = (freq >= a.min_freq || level < a.min_len) && (st + level < a.L) && (level < a.max_len);
+  a.flags[c] = (acc ? NODE_ACC : 0) | (ext ? NODE_EXT : 0);
+  ext_list[c - b] = ext ? a.cnt[c] : 0ull;
+  next_children[c - b] = ext ? (int32_t)a.npos[st + level] : 0;
+}
+
+__global__ void mine_apply_offsets(MineArgs a, int b, int e, const unsigned long long *list_scan,
+                                   const int32_t *child_scan, int next_base) {
+  const int c = b + blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= e) return;
+  const bool ext = a.flags[c] & NODE_EXT;
+  a.list_off[c] = ext ? list_scan[c - b] : 0ull;
+  a.child_base[c] = ext ? next_base + child_scan[c - b] : -1;
+}
+
+__global__ void scan_totals(const unsigned long long *ls, const unsigned long long *lv, const int32_t *cs,
+                            const int32_t *cv, int n, unsigned long long *out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    out[0] = n ? ls[n - 1] + lv[n - 1] : 0ull;
+    out[1] = n ? (unsigned long long)(cs[n - 1] + cv[n - 1]) : 0ull;
+  }
+}
+
+__global__ __launch_bounds__(64) void mine_scatter(MineArgs a, int level, int pbeg, int pend) {
+  __shared__ uint32_t run[A_MAX];
+  const int lane = threadIdx.x;
+  const int pidx = pbeg + blockIdx.x;
+  if (pidx >= pend) return;
+  const ParentView p = parent_view(a, level, pidx);
+  if (!p.ok) return;
+  const uint8_t *ca = a.pos_allele + (size_t)p.e * a.amax;
+  if (lane < A_MAX) run[lane] = 0;
+  bool any = false;
+  for (int k = 0; k < p.nc; ++k) any |= (a.flags[p.cb + k] & NODE_EXT) != 0;
+  __syncthreads();
+  if (!any) return;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (int base = 0; base < p.n; base += WAVE) {
+    const EntryView x = load_entry(a, level == 1, p.lidx, p.lval, base + lane, p.n, p.e);
+    for (int k = 0; k < p.nc; ++k) {
+      const int c = p.cb + k;
+      if (!(a.flags[c] & NODE_EXT)) continue;
+      double v;
+      const bool m = contribution(a, x, p.e, ca[k], v);
+      const uint64_t b = __ballot(m);
+      if (m) {
+        const unsigned long long at = a.list_off[c] + run[k] + (uint32_t)__popcll(b & lt);
+        a.lout_idx[at] = x.item;
+        if (a.genotype) a.lout_val[at] = v;
+      }
+      __syncthreads();
+      if (lane == 0) run[k] += (uint32_t)__popcll(b);
+      __syncthreads();
+    }
+  }
+}
+
+// ---- DFS order ------------------------------------------------------------
+__global__ void mine_size(MineArgs a, int level, int b, int e) {
+  const int c = b + blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= e) return;
+  uint32_t s = (a.flags[c] & NODE_ACC) ? 1u : 0u;
+  if (a.flags[c] & NODE_EXT) {
+    const int cb = a.child_base[c];
+    const int nc = a.npos[a.start[c] + level];
+    for (int k = 0; k < nc; ++k) s += a.size[cb + k];
+  }
+  a.size[c] = s;
+}
+
+__global__ void mine_root_size(MineArgs a, uint32_t *rsize) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.L) return;
+  uint32_t t = 0;
+  const int cb = a.r_child_base[s];
+  for (int k = 0; k < a.npos[s]; ++k) t += a.size[cb + k];
+  rsize[s] = t;
+}
+
+// Pre-order positions: parent first, then children in descending allele order.
+__global__ void mine_pos(MineArgs a, int level, int pbeg, int pend, const uint32_t *rpos) {
+  const int pidx = pbeg + blockIdx.x * blockDim.x + threadIdx.x;
+  if (pidx >= pend) return;
+  uint32_t running;
+  int cb, nc;
+  if (level == 1) {
+    running = rpos[pidx];
+    cb = a.r_child_base[pidx];
+    nc = a.npos[pidx];
+  } else {
+    if (!(a.flags[pidx] & NODE_EXT)) return;
+    running = a.pos[pidx] + ((a.flags[pidx] & NODE_ACC) ? 1u : 0u);
+    cb = a.child_base[pidx];
+    nc = a.npos[a.start[pidx] + level - 1];
+  }
+  for (int k = nc - 1; k >= 0; --k) {
+    a.pos[cb + k] = running;
+    running += a.size[cb + k];
+  }
+}
+
+__global__ void mine_emit(MineArgs a, int level, int b, int e, PatternTable t) {
+  const int c = b + blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= e) return;
+  if (!(a.flags[c] & NODE_ACC)) return;
+  const uint32_t id = a.pos[c];
+  t.start[id] = a.start[c];
+  t.len[id] = level;
+  t.freq[id] = a.freq[c];
+  t.prefix[id] = a.prefix[c];
+  t.tp[id] = a.tp[c];
+  t.last[id] = a.allele[c];
+  t.node[id] = c;
+}
+
+// successor[j] = longest stored suffix of (pattern + allele j) (PatternManager.cpp:308-317).
+__global__ void mine_succ(MineArgs a, PatternTable t, int P) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long long)P * a.amax) return;
+  const int id = (int)(gid / a.amax), j = (int)(gid % a.amax);
+  const int e = t.start[id] + t.len[id];
+  uint32_t res = NONE;
+  if (e < a.L && j < a.anum[e]) {
+    const uint8_t rk = a.rank_of[(size_t)e * a.amax + j];
+    int32_t u = t.node[id];
+    int depth = 0;  // number of leading alleles dropped so far
+    while (true) {
+      if (is_root(u)) {
+        if (rk != 0xFF) {
+          const int c = a.r_child_base[root_start(u)] + rk;
+          if (a.flags[c] & NODE_ACC) res = a.pos[c];
+        }
+        break;
+      }
+      if (u == -1) {
+        // Chain broken: the suffix dropped `depth` alleles is no candidate.
+        // Navigate the shorter suffixes from their roots (rare; exact walk).
+        const int vs = t.start[id];
+        uint8_t al[256];
+        int32_t w = t.node[id];
+        const int L0 = t.len[id];
+        for (int q = L0 - 1; q >= 0 && L0 <= 256; --q) {
+          al[q] = a.allele[w];
+          w = a.parent[w];
+        }
+        for (int d = depth + 1; d <= L0 && res == NONE; ++d) {
+          const int ks = vs + d;  // suffix start
+          int32_t nd = root_code(ks);
+          bool ok = true;
+          for (int q = d; q < L0 && ok; ++q) {
+            const int loc = vs + q;
+            const uint8_t r = a.rank_of[(size_t)loc * a.amax + al[q]];
+            if (r == 0xFF) { ok = false; break; }
+            if (is_root(nd)) nd = a.r_child_base[root_start(nd)] + r;
+            else if (a.flags[nd] & NODE_EXT) nd = a.child_base[nd] + r;
+            else ok = false;
+          }
+          if (!ok || rk == 0xFF) continue;
+          int c;
+          if (is_root(nd)) c = a.r_child_base[root_start(nd)] + rk;
+          else if (a.flags[nd] & NODE_EXT) c = a.child_base[nd] + rk;
+          else continue;
+          if (a.flags[c] & NODE_ACC) res = a.pos[c];
+        }
+        break;
+      }
+      if ((a.flags[u] & NODE_EXT) && rk != 0xFF) {
+        const int c = a.child_base[u] + rk;
+        if (a.flags[c] & NODE_ACC) { res = a.pos[c]; break; }
+      }
+      u = a.link[u];
+      ++depth;
+    }
+  }
+  t.succ[gid] = res;
+}
+
+// ---- host-side launch helpers -----------------------------------------------
+hipError_t launch_mine_count(const MineArgs &a, int level, int pbeg, int pend, hipStream_t st) {
+  if (pend <= pbeg) return hipSuccess;
+  const size_t lds = (size_t)a.amax * 65 * 8;
+  hipLaunchKernelGGL(mine_count, dim3(pend - pbeg), dim3(WAVE), lds, st, a, level, pbeg, pend);
+  return hipGetLastError();
+}
+hipError_t launch_mine_finalize(const MineArgs &a, int level, int b, int e, unsigned long long *ext_list,
+                                int32_t *next_children, hipStream_t st) {
+  if (e <= b) return hipSuccess;
+  hipLaunchKernelGGL(mine_finalize, dim3((e - b + 255) / 256), dim3(256), 0, st, a, level, b, e, ext_list, next_children);
+  return hipGetLastError();
+}
+hipError_t launch_mine_offsets(const MineArgs &a, int b, int e, unsigned long long *ext_list, int32_t *next_children,
+                               unsigned long long *list_scan, int32_t *child_scan, int next_base, void *tmp,
+                               size_t tmp_bytes, unsigned long long *totals, hipStream_t st) {
+  const int n = e - b;
+  if (n <= 0) return hipSuccess;
+  size_t need = tmp_bytes;
+  hipError_t err = hipcub::DeviceScan::ExclusiveSum(tmp, need, ext_list, list_scan, n, st);
+  if (err != hipSuccess) return err;
+  need = tmp_bytes;
+  err = hipcub::DeviceScan::ExclusiveSum(tmp, need, next_children, child_scan, n, st);
+  if (err != hipSuccess) return err;
+  hipLaunchKernelGGL(mine_apply_offsets, dim3((n + 255) / 256), dim3(256), 0, st, a, b, e, list_scan, child_scan,
+                     next_base);
+  hipLaunchKernelGGL(scan_totals, dim3(1), dim3(1), 0, st, list_scan, ext_list, child_scan, next_children, n, totals);
+  return hipGetLastError();
+}
+size_t mine_scan_tmp_bytes(int n) {
+  size_t a = 0, b = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, a, (unsigned long long *)nullptr, (unsigned long long *)nullptr, n);
+  hipcub::DeviceScan::ExclusiveSum(nullptr, b, (int32_t *)nullptr, (int32_t *)nullptr, n);
+  return a > b ? a : b;
+}
+hipError_t launch_mine_scatter(const MineArgs &a, int level, int pbeg, int pend, hipStream_t st) {
+  if (pend <= pbeg) return hipSuccess;
+  hipLaunchKernelGGL(mine_scatter, dim3(pend - pbeg), dim3(WAVE), 0, st, a, level, pbeg, pend);
+  return hipGetLastError();
+}
+hipError_t launch_mine_size(const MineArgs &a, int level, int b, int e, hipStream_t st) {
+  if (e <= b) return hipSuccess;
+  hipLaunchKernelGGL(mine_size, dim3((e - b + 255) / 256), dim3(256), 0, st, a, level, b, e);
+  return hipGetLastError();
+}
+hipError_t launch_mine_root_size(const MineArgs &a, uint32_t *rsize, hipStream_t st) {
+  hipLaunchKernelGGL(mine_root_size, dim3((a.L + 255) / 256), dim3(256), 0, st, a, rsize);
+  return hipGetLastError();
+}
+hipError_t launch_mine_pos(const MineArgs &a, int level, int pbeg, int pend, const uint32_t *rpos, hipStream_t st) {
+  if (pend <= pbeg) return hipSuccess;
+  hipLaunchKernelGGL(mine_pos, dim3((pend - pbeg + 255) / 256), dim3(256), 0, st, a, level, pbeg, pend, rpos);
+  return hipGetLastError();
+}
+hipError_t launch_mine_emit(const MineArgs &a, int level, int b, int e, const PatternTable &t, hipStream_t st) {
+  if (e <= b) return hipSuccess;
+  hipLaunchKernelGGL(mine_emit, dim3((e - b + 255) / 256), dim3(256), 0, st, a, level, b, e, t);
+  return hipGetLastError();
+}
+hipError_t launch_mine_succ(const MineArgs &a, const PatternTable &t, int P, hipStream_t st) {
+  const long long n = (long long)P * a.amax;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mine_succ, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, t, P);
+  return hipGetLastError();
+}
+
+}  // namespace hmc

@@ -1,0 +1,180 @@
+// select.hpp — k-best selection with libstdc++ (GCC 11) tie semantics.
+//
+// The reference keeps the k best HaploPairLinks with
+//   std::nth_element(v.begin(), v.begin()+k-1, v.end(), greater<HaploPairLink>())
+// (HaploPair.cpp:86, HaploBuilder.cpp:101) and orders the final list with
+//   std::sort(..., greater<HaploPairLink>())            (HaploBuilder.cpp:105).
+// The comparator looks at the likelihood only (HaploPair.h:44-52), so WHICH of
+// several equal-likelihood links survive is decided by the element permutation
+// the library algorithm performs.  Bit-exact parity of the selected haplotype
+// pair therefore needs the same algorithm, step for step: introselect with a
+// median-of-three pivot and an unguarded Hoare partition, heap-select fallback
+// at depth 2*lg(n), and a final insertion sort (for n <= 16 std::sort is just
+// the insertion sort).  This header restates that algorithm over an abstract
+// "list" so one body serves device code (lists striped across a wavefront in
+// LDS) and host code (plain arrays, used by the CPU-side tests).
+#pragma once
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#define HMC_HD __host__ __device__ __forceinline__
+#else
+#define HMC_HD inline
+#endif
+
+namespace hmc {
+
+// A list view: element k lives at lik[k*stride], meta[k*stride].
+struct LinkList {
+  double *lik;
+  uint32_t *meta;
+  int stride;
+  HMC_HD double l(int k) const { return lik[k * stride]; }
+  HMC_HD uint32_t m(int k) const { return meta[k * stride]; }
+  HMC_HD void set(int k, double x, uint32_t y) const {
+    lik[k * stride] = x;
+    meta[k * stride] = y;
+  }
+  HMC_HD void copy(int dst, int src) const { set(dst, l(src), m(src)); }
+  HMC_HD void swap(int a, int b) const {
+    double x = l(a);
+    uint32_t y = m(a);
+    copy(a, b);
+    set(b, x, y);
+  }
+  // comp(a, b) == greater<HaploPairLink>()(v[a], v[b])
+  HMC_HD bool gt(int a, int b) const { return l(a) > l(b); }
+};
+
+HMC_HD int lg2_floor(int n) { return 31 - __builtin_clz((unsigned)n); }
+
+// std::__move_median_to_first (stl_algo.h:79-102)
+HMC_HD void move_median_to_first(const LinkList &v, int result, int a, int b, int c) {
+  if (v.gt(a, b)) {
+    if (v.gt(b, c)) v.swap(result, b);
+    else if (v.gt(a, c)) v.swap(result, c);
+    else v.swap(result, a);
+  } else if (v.gt(a, c)) v.swap(result, a);
+  else if (v.gt(b, c)) v.swap(result, c);
+  else v.swap(result, b);
+}
+
+// std::__unguarded_partition (stl_algo.h:1878-1896); pivot value stays at `pivot`.
+HMC_HD int unguarded_partition(const LinkList &v, int first, int last, int pivot) {
+  while (true) {
+    while (v.gt(first, pivot)) ++first;
+    --last;
+    while (v.gt(pivot, last)) --last;
+    if (!(first < last)) return first;
+    v.swap(first, last);
+    ++first;
+  }
+}
+
+// std::__unguarded_partition_pivot (stl_algo.h:1900-1907)
+HMC_HD int unguarded_partition_pivot(const LinkList &v, int first, int last) {
+  int mid = first + (last - first) / 2;
+  move_median_to_first(v, first, first + 1, mid, last - 1);
+  return unguarded_partition(v, first + 1, last, first);
+}
+
+// std::__insertion_sort + __unguarded_linear_insert (stl_algo.h:1799-1849)
+HMC_HD void insertion_sort(const LinkList &v, int first, int last) {
+  if (first == last) return;
+  for (int i = first + 1; i != last; ++i) {
+    double x = v.l(i);
+    uint32_t y = v.m(i);
+    if (x > v.l(first)) {
+      for (int k = i; k > first; --k) v.copy(k, k - 1);
+      v.set(first, x, y);
+    } else {
+      int hole = i, next = i - 1;
+      while (x > v.l(next)) {
+        v.copy(hole, next);
+        hole = next;
+        --next;
+      }
+      v.set(hole, x, y);
+    }
+  }
+}
+
+// std::__push_heap with a value comparator (stl_heap.h:134-149)
+HMC_HD void push_heap(const LinkList &v, int first, int hole, int top, double x, uint32_t y) {
+  int parent = (hole - 1) / 2;
+  while (hole > top && v.l(first + parent) > x) {
+    v.copy(first + hole, first + parent);
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  v.set(first + hole, x, y);
+}
+
+// std::__adjust_heap (stl_heap.h:223-250)
+HMC_HD void adjust_heap(const LinkList &v, int first, int hole, int len, double x, uint32_t y) {
+  const int top = hole;
+  int second = hole;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    if (v.gt(first + second, first + (second - 1))) second--;
+    v.copy(first + hole, first + second);
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    v.copy(first + hole, first + (second - 1));
+    hole = second - 1;
+  }
+  push_heap(v, first, hole, top, x, y);
+}
+
+// std::__make_heap (stl_heap.h:339-360)
+HMC_HD void make_heap(const LinkList &v, int first, int last) {
+  int len = last - first;
+  if (len < 2) return;
+  int parent = (len - 2) / 2;
+  while (true) {
+    double x = v.l(first + parent);
+    uint32_t y = v.m(first + parent);
+    adjust_heap(v, first, parent, len, x, y);
+    if (parent == 0) return;
+    parent--;
+  }
+}
+
+// std::__heap_select with std::__pop_heap (stl_algo.h:1642-1651, stl_heap.h:253-266)
+HMC_HD void heap_select(const LinkList &v, int first, int middle, int last) {
+  make_heap(v, first, middle);
+  for (int i = middle; i < last; ++i) {
+    if (v.gt(i, first)) {
+      double x = v.l(i);
+      uint32_t y = v.m(i);
+      v.copy(i, first);
+      adjust_heap(v, first, 0, middle - first, x, y);
+    }
+  }
+}
+
+// std::nth_element(first, first+nth, first+n, greater) (stl_algo.h:1964-1986, 4794-4812)
+HMC_HD void nth_element_greater(const LinkList &v, int n, int nth) {
+  if (n == 0 || nth == n) return;
+  int first = 0, last = n, depth = lg2_floor(n) * 2;
+  while (last - first > 3) {
+    if (depth == 0) {
+      heap_select(v, first, nth + 1, last);
+      v.swap(first, nth);
+      return;
+    }
+    --depth;
+    int cut = unguarded_partition_pivot(v, first, last);
+    if (cut <= nth) first = cut;
+    else last = cut;
+  }
+  insertion_sort(v, first, last);
+}
+
+// std::sort(first, first+n, greater) for n <= 16 (stl_algo.h:1925-1958):
+// __introsort_loop is a no-op below _S_threshold, leaving __insertion_sort.
+HMC_HD void sort_greater_small(const LinkList &v, int n) { insertion_sort(v, 0, n); }
+
+}  // namespace hmc

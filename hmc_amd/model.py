@@ -1,0 +1,227 @@
+"""Python mirror of the reference's HaploModel interface over libhmc_amd.so.
+
+Names, parameters and defaults follow HaploModel (HaploModel.h:15-33) and the
+HMC command line (HMC.cpp:35-47):
+
+    m = HaploModel()
+    m.sample_size = 10; m.max_iteration = 50
+    resolutions = m.run(genos)            # HaploModel::run (HaploModel.cpp:117-155)
+
+Lower-level seams (used by the parity tests) mirror the reference's internal
+calls: find_patterns() = PatternManager::findPatternByFreq + initialize,
+resolve_all() = HaploModel::resolveAll.  Every call goes through the C-ABI of
+include/hmc_amd.h; errors the reference reports with Logger::error + exit(1)
+raise HMCError here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+
+import numpy as np
+
+from ._lib import HMCError, IterLog, lib
+
+_P = C.POINTER
+
+
+def _p(a: np.ndarray, t):
+    return a.ctypes.data_as(_P(t))
+
+
+@dataclasses.dataclass
+class GenoData:
+    """Genotype panel: alleles[N][2][L] allele symbols (-1 missing), per-locus types."""
+
+    alleles: np.ndarray
+    types: str
+
+    @property
+    def genotype_num(self) -> int:
+        return self.alleles.shape[0]
+
+    @property
+    def genotype_len(self) -> int:
+        return self.alleles.shape[2]
+
+    @classmethod
+    def from_panel(cls, panel) -> "GenoData":
+        return cls(np.ascontiguousarray(panel.alleles, dtype=np.int32), panel.types)
+
+
+class HaploModel:
+    """HaploModel (model "MV", sampling EM) on one MI355X, or one rank of a sharded run."""
+
+    def __init__(self, device: int = 0, rank: int = 0, world: int = 1, unique_id: bytes | None = None):
+        L = lib()
+        h = C.c_void_p()
+        if world > 1:
+            uid = C.create_string_buffer(unique_id, 128)
+            rc = L.hmc_ctx_create_dist(device, rank, world, C.cast(uid, C.c_void_p), C.byref(h))
+        else:
+            rc = L.hmc_ctx_create(device, C.byref(h))
+        self._h = h
+        self.rank, self.world = rank, world
+        if rc:
+            msg = L.hmc_ctx_error(h).decode() if h else ""
+            self.close()
+            raise HMCError(rc, msg)
+        # HaploModel public fields (HaploModel.h:15-26) with the CLI defaults (HMC.cpp:35-47)
+        self.min_freq = -1.0
+        self.min_freq_abs = 1.5
+        self.min_pattern_len = 1
+        self.max_pattern_len = 30
+        self.sample_size = 10
+        self.max_iteration = 1
+        self.N = self.L = self.amax = 0
+        self.iterations = 0
+        self.log: list[dict] = []
+
+    # ------------------------------------------------------------------ util
+    def _check(self, rc: int):
+        if rc:
+            raise HMCError(rc, lib().hmc_ctx_error(self._h).decode())
+
+    def _push_params(self):
+        self._check(lib().hmc_set_params(self._h, float(self.min_freq_abs), float(self.min_freq),
+                                         int(self.min_pattern_len), int(self.max_pattern_len),
+                                         int(self.sample_size)))
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib().hmc_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        rc = lib().hmc_rccl_unique_id(C.cast(buf, C.c_void_p))
+        if rc:
+            raise HMCError(rc, "ncclGetUniqueId failed")
+        return buf.raw
+
+    def set_tuning(self, frontier_cap: int = 0, trace_bytes: int = 0, waves: int = 0):
+        self._check(lib().hmc_set_tuning(self._h, frontier_cap, trace_bytes, waves))
+
+    # ----------------------------------------------------------------- panel
+    def load(self, genos: GenoData):
+        a = np.ascontiguousarray(genos.alleles, dtype=np.int32)
+        N, _, L = a.shape
+        self._check(lib().hmc_load_genotypes(self._h, N, L, _p(a, C.c_int32), genos.types.encode()))
+        self._info()
+
+    def load_phase(self, path: str):
+        self._check(lib().hmc_load_phase(self._h, path.encode()))
+        self._info()
+
+    def _info(self):
+        n, l, a = C.c_int(), C.c_int(), C.c_int()
+        self._check(lib().hmc_panel_info(self._h, C.byref(n), C.byref(l), C.byref(a)))
+        self.N, self.L, self.amax = n.value, l.value, a.value
+        self.i0 = self.N * self.rank // self.world
+        self.i1 = self.N * (self.rank + 1) // self.world
+
+    def allele_table(self):
+        num = np.zeros(self.L, np.int32)
+        sym = np.zeros((self.L, self.amax), np.int32)
+        fr = np.zeros((self.L, self.amax), np.float64)
+        self._check(lib().hmc_allele_table(self._h, _p(num, C.c_int32), _p(sym, C.c_int32), _p(fr, C.c_double)))
+        return num, sym, fr
+
+    # ---------------------------------------------------------------- M-step
+    def find_patterns(self) -> tuple[int, int]:
+        """PatternManager::findPatternByFreq + initialize; returns (patterns, R_M)."""
+        self._push_params()
+        n, rm = C.c_int(), C.c_uint64()
+        self._check(lib().hmc_find_patterns(self._h, C.byref(n), C.byref(rm)))
+        return n.value, rm.value
+
+    def patterns(self, maxlen: int | None = None) -> dict:
+        P, hl = C.c_int(), C.c_int()
+        self._check(lib().hmc_model_info(self._h, C.byref(P), C.byref(hl)))
+        P = P.value
+        A = self.amax
+        ml = min(maxlen or self.L, self.L)
+        out = dict(start=np.zeros(P, np.int32), len=np.zeros(P, np.int32), freq=np.zeros(P),
+                   prefix=np.zeros(P), tp=np.zeros(P), succ=np.zeros((P, A), np.int32),
+                   alleles=np.zeros((P, ml), np.int32))
+        self._check(lib().hmc_get_patterns(
+            self._h, _p(out["start"], C.c_int32), _p(out["len"], C.c_int32), _p(out["freq"], C.c_double),
+            _p(out["prefix"], C.c_double), _p(out["tp"], C.c_double), _p(out["succ"], C.c_int32),
+            _p(out["alleles"], C.c_int32), ml))
+        return out
+
+    def set_patterns(self, start, length, freq, tp, succ, last_symbol):
+        self._push_params()
+        start = np.ascontiguousarray(start, np.int32)
+        length = np.ascontiguousarray(length, np.int32)
+        freq = np.ascontiguousarray(freq, np.float64)
+        tp = np.ascontiguousarray(tp, np.float64)
+        succ = np.ascontiguousarray(succ, np.int32)
+        last = np.ascontiguousarray(last_symbol, np.int32)
+        self._check(lib().hmc_set_patterns(self._h, len(start), _p(start, C.c_int32), _p(length, C.c_int32),
+                                           _p(freq, C.c_double), _p(tp, C.c_double), _p(succ, C.c_int32),
+                                           _p(last, C.c_int32)))
+
+    # ---------------------------------------------------------------- E-step
+    def resolve_all(self) -> tuple[float, int, int]:
+        """HaploModel::resolveAll; returns (log-likelihood, samples, R_E)."""
+        self._push_params()
+        ll, H, re = C.c_double(), C.c_int(), C.c_uint64()
+        self._check(lib().hmc_resolve_all(self._h, C.byref(ll), C.byref(H), C.byref(re)))
+        return ll.value, H.value, re.value
+
+    def estep_results(self) -> dict:
+        n = self.i1 - self.i0
+        S = max(1, self.sample_size)
+        out = dict(total=np.zeros(n), ncand=np.zeros(n, np.int32), status=np.zeros(n, np.int32),
+                   prior=np.zeros((n, S)), posterior=np.zeros((n, S)), weight=np.zeros((n, S)))
+        self._check(lib().hmc_get_estep(self._h, _p(out["total"], C.c_double), _p(out["ncand"], C.c_int32),
+                                        _p(out["status"], C.c_int32), _p(out["prior"], C.c_double),
+                                        _p(out["posterior"], C.c_double), _p(out["weight"], C.c_double)))
+        return out
+
+    def samples(self, H: int):
+        al = np.zeros((H, self.L), np.int32)
+        w = np.zeros(H)
+        tw = C.c_double()
+        self._check(lib().hmc_get_samples(self._h, _p(al, C.c_int32), _p(w, C.c_double), C.byref(tw)))
+        return al, w, tw.value
+
+    def resolutions(self) -> np.ndarray:
+        out = np.zeros((self.i1 - self.i0, 2, self.L), np.int32)
+        self._check(lib().hmc_get_resolutions(self._h, _p(out, C.c_int32)))
+        return out
+
+    def timings(self) -> dict:
+        f, t, m = C.c_double(), C.c_double(), C.c_double()
+        self._check(lib().hmc_last_timings(self._h, C.byref(f), C.byref(t), C.byref(m)))
+        return dict(estep_forward_ms=f.value, estep_traceback_ms=t.value, mstep_ms=m.value)
+
+    # ------------------------------------------------------------ whole EM
+    def run(self, genos: GenoData | None = None) -> np.ndarray:
+        """HaploModel::run: M0, then E/M iterations until the LL stops improving."""
+        if genos is not None:
+            self.load(genos)
+        self._push_params()
+        cap = max(1, int(self.max_iteration))
+        logs = (IterLog * cap)()
+        it, tm0, rm0, np0 = C.c_int(), C.c_double(), C.c_uint64(), C.c_int()
+        self._check(lib().hmc_run(self._h, int(self.max_iteration), logs, cap, C.byref(it), C.byref(tm0),
+                                  C.byref(rm0), C.byref(np0)))
+        self.iterations = it.value
+        self.m0 = dict(t_s=tm0.value, r_m=rm0.value, n_patterns=np0.value)
+        self.log = [dict(ll=l.log_likelihood, t_e=l.t_estep_s, t_m=l.t_mstep_s, r_e=l.r_e, r_m=l.r_m,
+                         n_patterns=l.n_patterns, n_samples=l.n_samples) for l in logs[:it.value]]
+        out = np.zeros((self.i1 - self.i0, 2, self.L), np.int32)
+        self._check(lib().hmc_get_best_resolutions(self._h, _p(out, C.c_int32)))
+        return out
+
+    def write_phase(self, path: str):
+        self._check(lib().hmc_write_phase(self._h, path.encode()))

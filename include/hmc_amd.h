@@ -1,0 +1,141 @@
+/* hmc_amd.h — C-ABI of libhmc_amd.so, the MI355X-native HaploModel EM.
+ *
+ * The reference (Wu-Lab/HMC v0.9.1) has no plugin or FFI surface: its hot path
+ * is the C++ class seam HaploModel::run -> HaploBuilder::resolve /
+ * PatternManager::findPatternByFreq inside one binary.  Each entry point below
+ * replaces one of those seams; the citation names the reference interface it
+ * stands in for.  Conventions:
+ *   - plain pointers and sizes, no C++ or torch types;
+ *   - host buffers are caller-owned, device buffers are owned by the context;
+ *   - every function returns 0 (HMC_OK) or a negative HMC_E* code; the text of
+ *     the last failure is available from hmc_ctx_error().  The reference's
+ *     fatal errors (Logger::error + exit(1)) become return codes here;
+ *   - allele symbols are the reference's Allele values (the ASCII code for SNP
+ *     'S' loci, the integer for microsatellite 'M' loci), -1 = missing;
+ *   - one host thread per context.
+ */
+#ifndef HMC_AMD_H
+#define HMC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HMC_OK 0
+#define HMC_EARG -1         /* invalid argument / call order */
+#define HMC_EHIP -2         /* HIP runtime failure */
+#define HMC_EIO -3          /* file could not be read or written */
+#define HMC_EUNSUPPORTED -4 /* parameter outside what the GPU path implements */
+#define HMC_ENOPATTERN -5   /* "Can not find matching pattern!" (HaploBuilder.cpp:215-217) */
+#define HMC_ERCCL -6        /* RCCL failure */
+#define HMC_ENOMEM -7       /* device memory exhausted */
+
+typedef struct hmc_ctx hmc_ctx;
+
+/* ---- context ---------------------------------------------------------- */
+/* One context per GPU.  Replaces constructing HaploModel (HaploModel.h:29). */
+int hmc_ctx_create(int device, hmc_ctx **out);
+/* Multi-GPU: one process per GPU; `unique_id` = 128 bytes from
+ * hmc_rccl_unique_id() on rank 0, broadcast by the caller.  Individuals are
+ * sharded in contiguous blocks; the M-step all-reduces per-level sums. */
+int hmc_rccl_unique_id(void *out128);
+int hmc_ctx_create_dist(int device, int rank, int world, const void *unique_id, hmc_ctx **out);
+void hmc_ctx_destroy(hmc_ctx *ctx);
+const char *hmc_ctx_error(const hmc_ctx *ctx);
+
+/* HaploModel public parameters (HaploModel.h:15-26; CLI defaults HMC.cpp:35-47).
+ * min_freq_abs > 0 overrides min_freq exactly as HaploModel::findPatterns does
+ * (HaploModel.cpp:54-56). */
+int hmc_set_params(hmc_ctx *ctx, double min_freq_abs, double min_freq, int min_pattern_len, int max_pattern_len,
+                   int sample_size);
+
+/* ---- panel (GenoData / HaploFile) --------------------------------------- */
+/* HaploFile::readGenoData for the PHASE format (HaploFile.cpp:54-118). */
+int hmc_load_phase(hmc_ctx *ctx, const char *path);
+/* Same panel from memory: alleles[N][2][L] symbols, types[L] ('S' or 'M').
+ * Runs GenoData::checkAlleleSymbol (GenoData.cpp:78-118) and uploads. */
+int hmc_load_genotypes(hmc_ctx *ctx, int N, int L, const int32_t *alleles, const char *types);
+int hmc_panel_info(const hmc_ctx *ctx, int *N, int *L, int *max_alleles);
+/* Per-locus allele tables: num[L], sym[L][max_alleles], freq[L][max_alleles]
+ * (GenoData::allele_num / allele_symbol / allele_frequency, GenoData.h:43-49). */
+int hmc_allele_table(const hmc_ctx *ctx, int32_t *num, int32_t *sym, double *freq);
+
+/* ---- M-step: PatternManager::findPatternByFreq (PatternManager.cpp:27-42) --
+ * Mines from the genotypes while no E-step samples exist (M0), from the
+ * weighted samples afterwards, then runs initialize() (ids, head list,
+ * successors).  *n_patterns = patterns found; *r_m = candidate x item scan
+ * steps (SURVEY.md §8d R_M, local to this rank). */
+int hmc_find_patterns(hmc_ctx *ctx, int *n_patterns, uint64_t *r_m);
+int hmc_model_info(const hmc_ctx *ctx, int *n_patterns, int *head_len);
+/* Pattern table in id order (HaploPattern.h:16-98).  succ[P][max_alleles]
+ * holds pattern ids (-1 = none); alleles[P][maxlen] symbols (-1 padding).
+ * Any output pointer may be NULL. */
+int hmc_get_patterns(hmc_ctx *ctx, int32_t *start, int32_t *len, double *freq, double *prefix, double *tp,
+                     int32_t *succ, int32_t *alleles, int maxlen);
+/* Install an externally built pattern table (test seam: lets the E-step be
+ * checked against another implementation's M-step output).  last_symbol[P] is
+ * the pattern's last allele; succ as above. */
+int hmc_set_patterns(hmc_ctx *ctx, int P, const int32_t *start, const int32_t *len, const double *freq,
+                     const double *tp, const int32_t *succ, const int32_t *last_symbol);
+
+/* ---- E-step: HaploModel::resolveAll (HaploModel.cpp:79-115) ------------
+ * Resolves every individual of this rank's shard with HaploBuilder::resolve
+ * (HaploBuilder.cpp:35-126), keeps the weighted samples on the device for the
+ * next M-step, and returns the log-likelihood (all ranks), the number of
+ * samples (this rank) and R_E (retained k-best links, this rank). */
+int hmc_resolve_all(hmc_ctx *ctx, double *log_likelihood, int *n_samples, uint64_t *r_e);
+/* Per individual of the shard: genotype probability (total forward
+ * likelihood), number of candidates, status (0 ok, 1 unresolved), and per
+ * candidate [n][sample_size] prior / posterior / sample weight. */
+int hmc_get_estep(hmc_ctx *ctx, double *total, int32_t *ncand, int32_t *status, double *prior, double *posterior,
+                  double *weight);
+/* HaploData samples of this rank: alleles[H][L] symbols, weights[H]. */
+int hmc_get_samples(hmc_ctx *ctx, int32_t *alleles, double *weights, double *total_weight);
+/* Selected pair per individual of the last E-step ([n][2][L] symbols;
+ * unresolved individuals keep the input genotype, HaploBuilder.cpp:117-124). */
+int hmc_get_resolutions(hmc_ctx *ctx, int32_t *out);
+
+/* ---- whole EM: HaploModel::run (HaploModel.cpp:117-155) ------------------ */
+typedef struct hmc_iter_log {
+  double log_likelihood;
+  double t_estep_s, t_mstep_s; /* wall time of E_k and of M_k (0 if no M-step) */
+  uint64_t r_e, r_m;
+  int n_patterns;              /* patterns after M_k */
+  int n_samples;
+} hmc_iter_log;
+/* Runs M0 + up to max_iteration EM iterations with the reference's
+ * convergence rule.  log[] receives up to log_cap iterations; *iterations the
+ * number run; *t_m0_s, *r_m0, *n_patterns0 describe M0. */
+int hmc_run(hmc_ctx *ctx, int max_iteration, hmc_iter_log *log, int log_cap, int *iterations, double *t_m0_s,
+            uint64_t *r_m0, int *n_patterns0);
+/* Accepted resolutions of the last hmc_run ([n][2][L] symbols). */
+int hmc_get_best_resolutions(hmc_ctx *ctx, int32_t *out);
+/* HaploFile::writeGenoData (HaploFile.cpp:120-153) of the accepted
+ * resolutions (single-rank contexts). */
+int hmc_write_phase(hmc_ctx *ctx, const char *path);
+
+/* ---- tuning -------------------------------------------------------------- */
+/* frontier_cap: states per locus per wave before a batch is re-run with a
+ * larger capacity; trace_bytes: trace-store budget (0 = automatic);
+ * waves: resident E-step waves (0 = automatic). */
+int hmc_set_tuning(hmc_ctx *ctx, int frontier_cap, uint64_t trace_bytes, int waves);
+/* Device time (ms, HIP events on the context stream) of the last E-step
+ * forward kernel, traceback and whole M-step. */
+int hmc_last_timings(const hmc_ctx *ctx, double *estep_forward_ms, double *estep_traceback_ms, double *mstep_ms);
+
+/* ---- CPU-side test hooks (no GPU needed) --------------------------------- */
+/* The libstdc++-exact selection used by the E-step kernel (select.hpp), run on
+ * host arrays: nth_element(v, v+nth, v+n, greater) and sort(v, v+n, greater)
+ * of (lik, tag) records ordered by lik. */
+void hmc_test_nth_element(double *lik, uint32_t *tag, int n, int nth);
+void hmc_test_sort_small(double *lik, uint32_t *tag, int n);
+/* Library version string. */
+const char *hmc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HMC_AMD_H */

@@ -1,0 +1,926 @@
+// ============================================================================
+// hmc_oracle.cpp — TEST INFRASTRUCTURE ONLY (never shipped, never measured as
+// the product).  Only tests/, __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg may load liboracle.so.
+//
+// A single-threaded CPU restatement of Wu-Lab/HMC's HaploModel EM loop (model
+// "MV", sampling EM), written from a reading of /root/reference.  Each routine
+// cites the reference file:line it restates.
+//
+// PARITY UNPINNED: the reference cannot be built in this image without
+// stand-ins for Boost (boost/pool, tr1::shared_ptr, program_options are absent),
+// which the build rules forbid, and the reference ships no tests, fixtures or
+// golden vectors.  This restatement is therefore pinned only by hand-derived
+// known-answer tests (tests/test_oracle.py) and by its own frozen regression
+// vectors (tests/golden/).  See DESIGN.md §Oracle.
+//
+// Tie semantics: the reference selects k-best links with std::nth_element and
+// std::sort (HaploPair.cpp:86, HaploBuilder.cpp:101,105).  This file calls the
+// same libstdc++ (GCC 11.4) algorithms on the same element sequences, so its
+// tie order is the one a g++-11 build of the reference would produce.
+// ============================================================================
+#include <algorithm>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace ora {
+
+// ---------------------------------------------------------------- alleles --
+// Allele.h:11-36 — an int, negative = missing; isMatch treats missing as a
+// wildcard, operator== treats two missings as equal.
+static inline bool missing(int a) { return a < 0; }
+static inline bool amatch(int a, int b) { return a < 0 || b < 0 || a == b; }
+static inline bool aeq(int a, int b) { return a == b || (a < 0 && b < 0); }
+
+// --------------------------------------------------------------- genodata --
+struct Geno {
+  int N = 0, L = 0;
+  std::vector<int> al;  // [N][2][L] allele symbols
+  std::string types;    // per-locus type char ('S' SNP, 'M' microsatellite)
+  std::vector<std::vector<std::pair<int, double>>> sym;  // per locus (symbol, freq)
+
+  int at(int i, int h, int k) const { return al[((size_t)i * 2 + h) * L + k]; }
+  int num(int k) const { return (int)sym[k].size(); }
+  int symbol(int k, int j) const { return sym[k][j].first; }
+  double afreq(int k, int j) const { return sym[k][j].second; }
+  int maxnum() const {
+    int m = 0;
+    for (int k = 0; k < L; ++k) m = std::max(m, num(k));
+    return m;
+  }
+  // GenoData.cpp:27-44 — linear search with Allele operator==.
+  int index(int k, int a) const {
+    for (int j = 0; j < num(k); ++j)
+      if (aeq(a, sym[k][j].first)) return j;
+    return -1;
+  }
+  // Genotype.h:115-133
+  bool isMissing(int i, int k) const { return missing(at(i, 0, k)) && missing(at(i, 1, k)); }
+  bool hasMissing(int i, int k) const { return missing(at(i, 0, k)) || missing(at(i, 1, k)); }
+  bool hasAllele(int i, int k, int a) const { return aeq(at(i, 0, k), a) || aeq(at(i, 1, k), a); }
+  bool isHet(int i, int k) const { return !amatch(at(i, 0, k), at(i, 1, k)); }
+  bool gmatch(int i, int k, int a) const { return amatch(at(i, 0, k), a) || amatch(at(i, 1, k), a); }
+
+  // GenoData.cpp:78-118 — distinct non-missing symbols in first-seen order,
+  // sorted by value, frequency = count / non-missing count (weights are 1.0).
+  void checkAlleleSymbol() {
+    sym.assign(L, {});
+    for (int i = 0; i < N; ++i)
+      for (int h = 0; h < 2; ++h)
+        for (int k = 0; k < L; ++k) {
+          int a = at(i, h, k);
+          if (!missing(a) && index(k, a) < 0) sym[k].push_back({a, 0.0});
+        }
+    for (int k = 0; k < L; ++k) std::sort(sym[k].begin(), sym[k].end());
+    std::vector<double> tot(L, 0.0);
+    for (int i = 0; i < N; ++i)
+      for (int h = 0; h < 2; ++h)
+        for (int k = 0; k < L; ++k) {
+          int a = at(i, h, k);
+          if (!missing(a)) {
+            sym[k][index(k, a)].second += 1.0;
+            tot[k] += 1.0;
+          }
+        }
+    for (int k = 0; k < L; ++k)
+      for (auto &p : sym[k]) p.second /= tot[k];
+  }
+};
+
+// ------------------------------------------------------------ PHASE input --
+// HaploFile.cpp:54-118 (m_has_id = true, HaploFile.h:44-53) and
+// Allele.cpp:55-153 (readAllele / AlleleSequence::read with types).
+static const char *DELIM = " \t\r\n";
+static char *read_allele(char type, char *buf, int &a) {
+  buf += strspn(buf, DELIM);
+  if (type == 'S') {
+    a = (buf[0] == '-' || buf[0] == '?') ? -1 : (int)(unsigned char)buf[0];
+    if (buf[0]) buf++;
+  } else {
+    if (buf[0] == '-' || buf[0] == '?') a = -1;
+    else {
+      int v = atoi(buf);
+      a = v > 0 ? v : -1;
+    }
+    buf += strcspn(buf, DELIM);
+  }
+  return buf;
+}
+
+static bool read_phase(const char *path, Geno &g, std::string &err) {
+  FILE *fp = fopen(path, "r");
+  if (!fp) { err = "Can not open file"; return false; }
+  int n = 0, l = 0;
+  if (fscanf(fp, "%d\n", &n) != 1 || fscanf(fp, "%d\n", &l) != 1 || n <= 0 || l <= 0) {
+    fclose(fp);
+    err = "Invalid file type!";
+    return false;
+  }
+  g.N = n;
+  g.L = l;
+  g.al.assign((size_t)n * 2 * l, -1);
+  std::vector<char> line(std::max<size_t>(409600, (size_t)l * 64 + 1024));
+  if (!fgets(line.data(), (int)line.size(), fp)) { fclose(fp); err = "truncated"; return false; }
+  char *s = line.data() + strspn(line.data(), DELIM);
+  if (s[0] == 'P') {
+    if (!fgets(line.data(), (int)line.size(), fp)) { fclose(fp); err = "truncated"; return false; }
+    s = line.data() + strspn(line.data(), DELIM);
+  }
+  g.types.assign(l, 'M');
+  for (int k = 0; k < l; ++k) {
+    g.types[k] = s[0];
+    if (s[0]) s++;
+    s += strspn(s, DELIM);
+  }
+  for (int i = 0; i < n; ++i) {
+    for (int r = 0; r < 3; ++r) {
+      if (!fgets(line.data(), (int)line.size(), fp)) { fclose(fp); err = "truncated"; return false; }
+      if (r == 0) continue;  // id line
+      char *b = line.data();
+      for (int k = 0; k < l; ++k) {
+        int a;
+        b = read_allele(g.types[k], b, a);
+        g.al[((size_t)i * 2 + (r - 1)) * l + k] = a;
+      }
+    }
+  }
+  fclose(fp);
+  g.checkAlleleSymbol();
+  return true;
+}
+
+// ---------------------------------------------------------------- pattern --
+// HaploPattern.h:16-98.  Alleles are symbols; end is exclusive.
+struct Pat {
+  int start = 0, end = 0;
+  std::vector<int> al;
+  unsigned id = 0;
+  double freq = 1.0, prefix = 1.0, tp = 1.0;  // HaploPattern.h:86-88 defaults
+  std::vector<int> succ;                     // successor pattern index or -1
+  int len() const { return (int)al.size(); }
+  void setTp(double p) { tp = p < 1.0 ? p : 1.0; }  // HaploPattern.h:47
+};
+
+// ----------------------------------------------------- BackwardPatternTree --
+// PatternTree.cpp:15-72,98-134, Tree.h:12-99: one trie per end locus, walked
+// from the last allele backwards.  Node data = pattern index (or -1).
+struct BTree {
+  struct Node { std::vector<int> ch; int data = -1; };
+  const Geno *g = nullptr;
+  std::vector<Node> nodes;
+  std::vector<int> root;  // per end locus 0..L
+  int width = 0;
+
+  int newNode() { nodes.push_back(Node{std::vector<int>(width, -1), -1}); return (int)nodes.size() - 1; }
+  void init(const Geno &gd) {
+    g = &gd;
+    width = gd.maxnum();
+    nodes.clear();
+    root.assign(gd.L + 1, -1);
+    for (int e = 0; e <= gd.L; ++e) root[e] = newNode();
+  }
+  int addChild(int n, int i) {
+    if (nodes[n].ch[i] < 0) { int c = newNode(); nodes[n].ch[i] = c; }
+    return nodes[n].ch[i];
+  }
+  // PatternTree.cpp:24-48
+  void add(const std::vector<Pat> &P, int pi) { addRec(root[P[pi].end], P, pi, P[pi].len()); }
+  void addRec(int n, const std::vector<Pat> &P, int pi, int len) {
+    const Pat &p = P[pi];
+    int locus = p.start + len - 1;
+    int a = p.al[len - 1];
+    int i = missing(a) ? -1 : g->index(locus, a);
+    if (i < 0) {
+      for (int j = 0; j < g->num(locus); ++j) {
+        if (len == 1) nodes[addChild(n, j)].data = pi;
+        else addRec(addChild(n, j), P, pi, len - 1);
+      }
+    } else {
+      if (len == 1) nodes[addChild(n, i)].data = pi;
+      else addRec(addChild(n, i), P, pi, len - 1);
+    }
+  }
+  // PatternTree.cpp:62-72 (AlleleSequence overload)
+  int longest(const std::vector<Pat> &P, int end, const std::vector<int> &as, int as_start) const {
+    int aslen = (int)as.size();
+    if (end <= as_start || end > as_start + aslen) return -1;
+    int maxl = end - as_start;
+    return walk(P, root[end], as, end - 1, maxl - 1, maxl);
+  }
+  // PatternTree.cpp:98-134
+  int walk(const std::vector<Pat> &P, int n, const std::vector<int> &as, int lg, int ll, int len) const {
+    int result = nodes[n].data;
+    auto consider = [&](int c) {
+      int tmp = len > 1 ? walk(P, c, as, lg - 1, ll - 1, len - 1) : nodes[c].data;
+      if (result < 0 || (tmp >= 0 && P[tmp].len() > P[result].len())) result = tmp;
+    };
+    if (missing(as[ll])) {
+      for (int i = 0; i < g->num(lg); ++i)
+        if (nodes[n].ch[i] >= 0) consider(nodes[n].ch[i]);
+    } else {
+      int i = g->index(lg, as[ll]);
+      if (i >= 0 && nodes[n].ch[i] >= 0) consider(nodes[n].ch[i]);
+    }
+    return result;
+  }
+};
+
+// --------------------------------------------------------------- E-step --
+// HaploPair.h:14-52 — a k-best link.  pred = -1 marks a head pair.
+struct Link {
+  int pred;
+  int index;
+  bool rev;
+  bool homo;
+  double lik;
+};
+struct GreaterLik {  // std::greater<HaploPairLink> via HaploPair.h:49-52
+  bool operator()(const Link &a, const Link &b) const { return a.lik > b.lik; }
+};
+
+// HaploPair.h:55-100 — an unordered pattern pair (canonical: id_a <= id_b).
+struct Pair {
+  int pa, pb;
+  int alA, alB;  // last alleles of the two patterns
+  double tp, fwd;
+  std::vector<Link> links;
+};
+
+struct Sample {  // one weighted haplotype of HaploData (HaploData.h:57-65)
+  std::vector<int> al;
+  double w;
+};
+
+struct Candidate {  // one entry of res_list (HaploBuilder.cpp:105-114)
+  std::vector<int> h0, h1;
+  double prior, posterior, gp;
+};
+
+struct Params {
+  double min_freq_abs = 1.5;  // HMC.cpp:37
+  double min_freq = -1;       // HaploModel.cpp:10
+  int min_len = 1;            // HMC.cpp:39
+  int max_len = 30;           // HMC.cpp:40
+  int sample_size = 10;       // HMC.cpp:43
+  int max_iter = 1;           // HMC.cpp:46
+};
+
+struct Timing { double m0 = 0, e = 0, m = 0; };
+
+struct Model {
+  Geno g;       // the input panel (true phase kept for HaploComp)
+  Params prm;
+  std::vector<Pat> P;
+  BTree tree;
+  std::vector<int> head_list;
+  std::vector<int> minlen, maxlen;
+  double min_freq = 0;
+  // samples (HaploData)
+  std::vector<Sample> samples;
+  double total_weight = 0;
+  // last E-step results
+  std::vector<std::vector<Candidate>> res;  // per individual
+  std::vector<double> gp;                   // genotype probability per individual
+  std::vector<std::vector<int>> resolution; // per individual: [2][L]
+  std::vector<std::vector<int>> best_res;   // accepted resolutions (HaploModel.cpp:132)
+  // counters
+  uint64_t R_E = 0, R_M = 0;
+  // EM log
+  std::vector<double> ll_log;
+  std::vector<uint64_t> re_log, rm_log;
+  std::vector<int> npat_log;
+  std::vector<double> t_e_log, t_m_log;
+  double t_m0 = 0;
+  int iterations = 0;
+
+  // ------------------------------------------------------------ mining ----
+  struct Cand {
+    Pat p;
+    std::vector<std::pair<int, double>> st;  // MatchingState (PatternManager.h:19)
+  };
+
+  int head_len() const { return minlen[0]; }
+
+  // PatternManager.cpp:349-373
+  double matchFreq(int i, const int *pa, int start, int len) const {
+    double tot = 1.0;
+    for (int k = 0; k < len; ++k) {
+      if (missing(pa[k])) continue;
+      double f = 0;
+      for (int h = 0; h < 2; ++h) {
+        int b = g.at(i, h, start + k);
+        if (missing(b)) f += g.afreq(start + k, g.index(start + k, pa[k]));
+        else if (aeq(b, pa[k])) f += 1.0;
+      }
+      tot *= 0.5 * f;
+    }
+    return tot;
+  }
+  bool genoMatch(int i, const Pat &p, int start, int len) const {  // Genotype.cpp:79-96
+    int s2 = start - p.start;
+    if (start + len > g.L || s2 + len > p.len()) return false;
+    for (int k = 0; k < len; ++k)
+      if (!g.gmatch(i, start + k, p.al[s2 + k])) return false;
+    return true;
+  }
+  bool hapMatch(const Sample &h, const Pat &p, int start, int len) const {  // Allele.cpp:11-28
+    int s2 = start - p.start;
+    if (start + len > (int)h.al.size() || s2 + len > p.len()) return false;
+    for (int k = 0; k < len; ++k)
+      if (!amatch(h.al[start + k], p.al[s2 + k])) return false;
+    return true;
+  }
+
+  // PatternManager.cpp:146-193 (phased branches are dead: Genotype.cpp:40)
+  void checkFrequency(Pat &p, std::vector<std::pair<int, double>> &ms) {
+    ms.clear();
+    if (p.len() == 0) { p.freq = 1.0; return; }
+    double tot = 0;
+    if (samples.empty()) {
+      for (int i = 0; i < g.N; ++i) {
+        ++R_M;
+        if (genoMatch(i, p, p.start, p.len())) {
+          double f = matchFreq(i, p.al.data(), p.start, p.len());
+          tot += f;
+          ms.push_back({i, f});
+        }
+      }
+      p.freq = tot / g.N;
+    } else {
+      for (int i = 0; i < (int)samples.size(); ++i) {
+        ++R_M;
+        if (hapMatch(samples[i], p, p.start, p.len())) {
+          tot += samples[i].w;
+          ms.push_back({i, 0.0});
+        }
+      }
+      p.freq = tot / total_weight;
+    }
+  }
+  // PatternManager.cpp:195-265
+  void checkFreqExt(Pat &p, std::vector<std::pair<int, double>> &ms,
+                    const std::vector<std::pair<int, double>> &oms, int start) {
+    if (p.len() == 0 || oms.empty()) { checkFrequency(p, ms); return; }
+    ms.clear();
+    double tot = 0;
+    if (samples.empty()) {
+      for (auto &e : oms) {
+        ++R_M;
+        if (genoMatch(e.first, p, start, 1)) {
+          double f = e.second * matchFreq(e.first, &p.al[start - p.start], start, 1);
+          tot += f;
+          ms.push_back({e.first, f});
+        }
+      }
+      p.freq = tot / g.N;
+    } else {
+      for (auto &e : oms) {
+        ++R_M;
+        if (hapMatch(samples[e.first], p, start, 1)) {
+          tot += samples[e.first].w;
+          ms.push_back({e.first, 0.0});
+        }
+      }
+      p.freq = tot / total_weight;
+    }
+  }
+
+  // PatternManager.cpp:27-42, 90-144 — DFS mining; output order = DFS pre-order.
+  void findPatternByFreq(double mf, int mnl, int mxl) {
+    int L = g.L;
+    mxl = mxl <= 0 ? L : mxl;
+    mnl = std::max(mnl, 1);
+    mxl = std::max(mxl, mnl);
+    minlen.resize(L, mnl);  // vector::resize keeps old values (PatternManager.cpp:33-34)
+    maxlen.resize(L, mxl);
+    P.clear();
+    std::vector<Cand *> stack;
+    for (int s = 0; s < L; ++s) {  // generateCandidates (:90-98)
+      Cand *c = new Cand;
+      c->p.start = c->p.end = s;
+      stack.push_back(c);
+    }
+    min_freq = mf;
+    while (!stack.empty()) {  // searchPattern (:100-144)
+      Cand *pc = stack.back();
+      stack.pop_back();
+      const Pat &hp = pc->p;
+      if (hp.freq >= min_freq || hp.len() < minlen[hp.start]) {
+        if (hp.end < L && hp.len() < maxlen[hp.start]) {
+          for (int i = 0; i < g.num(hp.end); ++i) {
+            if (g.afreq(hp.end, i) > 0) {
+              Cand *nc = new Cand;
+              nc->p.start = hp.start;
+              nc->p.end = hp.end + 1;
+              nc->p.al = hp.al;
+              nc->p.al.push_back(g.symbol(hp.end, i));
+              nc->p.freq = hp.freq;
+              checkFreqExt(nc->p, nc->st, pc->st, hp.end);
+              nc->p.prefix = hp.freq;
+              if (nc->p.prefix > 0) nc->p.setTp(nc->p.freq / nc->p.prefix);
+              else nc->p.setTp(nc->p.freq);
+              stack.push_back(nc);
+            }
+          }
+        }
+      }
+      if (hp.freq >= min_freq || hp.len() <= minlen[hp.start]) {
+        if (hp.len() > 0 && hp.len() >= minlen[hp.start]) P.push_back(pc->p);
+      }
+      delete pc;
+    }
+    initialize();
+  }
+
+  // PatternManager.cpp:293-318
+  void initialize() {
+    tree.init(g);
+    head_list.clear();
+    int n = (int)P.size();
+    for (int i = 0; i < n; ++i) {
+      P[i].id = i;
+      tree.add(P, i);
+      if (P[i].start == 0 && P[i].len() == head_len()) head_list.push_back(i);
+    }
+    std::vector<int> tmp;
+    for (int i = 0; i < n; ++i) {
+      Pat &p = P[i];
+      p.succ.clear();
+      if (p.end < g.L) {
+        tmp = p.al;
+        tmp.push_back(-1);
+        for (int j = 0; j < g.num(p.end); ++j) {
+          tmp.back() = g.symbol(p.end, j);
+          int s = tree.longest(P, p.end + 1, tmp, p.start);
+          p.succ.resize(j + 1);
+          p.succ[j] = s;
+        }
+      }
+    }
+  }
+
+  // HaploModel.cpp:52-63
+  void findPatterns() {
+    if (prm.min_freq_abs > 0) prm.min_freq = prm.min_freq_abs / (2.0 * g.N);
+    findPatternByFreq(prm.min_freq, prm.min_len, prm.max_len);
+  }
+
+  // ------------------------------------------------------------ E-step ----
+  std::vector<std::vector<Pair>> hp;  // m_haplopairs
+  int S = 1;
+
+  int succOf(int pi, int a, int locus) const {  // HaploPattern.h:36-37
+    int j = g.index(locus, a);
+    const Pat &p = P[pi];
+    return (j >= 0 && j < (int)p.succ.size()) ? p.succ[j] : -1;
+  }
+
+  // HaploPair.cpp:14-33 — head constructor.
+  Pair headPair(int a, int b) {
+    Pair x;
+    x.pa = a; x.pb = b;
+    x.alA = P[a].al.back(); x.alB = P[b].al.back();
+    x.fwd = x.tp = P[a].freq * P[b].freq;
+    bool homo = (P[a].id == P[b].id);
+    if (!homo) x.fwd *= 2.0;
+    x.links.push_back(Link{-1, 0, false, homo, x.tp});
+    return x;
+  }
+
+  // HaploBuilder.cpp:153-224 (head_len general).
+  void initHeadList(int gi, std::unordered_map<uint64_t, int> &best) {
+    int hl = head_len();
+    for (int head : head_list) {
+      const Pat &H = P[head];
+      if (!genoMatch(gi, H, H.start, H.len())) continue;
+      std::vector<std::vector<int>> last(1), next;
+      for (int j = 0; j < hl; ++j) {
+        next.clear();
+        if (g.isMissing(gi, j) || (g.hasMissing(gi, j) && g.hasAllele(gi, j, H.al[j]))) {
+          for (auto &as : last)
+            for (int k = 0; k < g.num(j); ++k)
+              if (g.afreq(j, k) > 0) { next.push_back(as); next.back().push_back(g.symbol(j, k)); }
+        } else if (g.isHet(gi, j)) {
+          for (auto &as : last) {
+            next.push_back(as);
+            next.back().push_back(aeq(H.al[j], g.at(gi, 0, j)) ? g.at(gi, 1, j) : g.at(gi, 0, j));
+          }
+        } else {
+          for (auto &as : last) { next.push_back(as); next.back().push_back(g.at(gi, 0, j)); }
+        }
+        last.swap(next);
+      }
+      for (auto &as : last) {
+        int q = tree.longest(P, hl, as, 0);
+        if (q >= 0 && P[q].start == 0) {
+          if (P[q].id >= H.id) {
+            hp[hl].push_back(headPair(head, q));
+            best[((uint64_t)P[head].id << 32) | P[q].id] = (int)hp[hl].size();
+          }
+        } else {
+          fprintf(stderr, "Can not find matching pattern!\n");
+          exit(1);
+        }
+      }
+    }
+  }
+
+  // HaploBuilder.cpp:246-261 + HaploPair.cpp:35-89
+  void addPair(int locus, int predIdx, int a, int b, std::unordered_map<uint64_t, int> &best) {
+    const Pair &pred = hp[locus][predIdx];
+    bool rev = false;
+    if (P[a].id > P[b].id) { rev = true; std::swap(a, b); }
+    uint64_t key = ((uint64_t)P[a].id << 32) | P[b].id;
+    auto it = best.find(key);
+    std::vector<Pair> &nxt = hp[locus + 1];
+    if (it == best.end()) {
+      Pair x;  // extension constructor HaploPair.cpp:35-61
+      x.pa = a; x.pb = b;
+      x.alA = P[a].al.back(); x.alB = P[b].al.back();
+      x.tp = P[a].tp * P[b].tp;
+      x.fwd = pred.fwd * x.tp;
+      x.links = pred.links;
+      for (int i = 0; i < (int)x.links.size(); ++i) {
+        x.links[i].pred = predIdx;
+        x.links[i].index = i;
+        x.links[i].rev = rev;
+        x.links[i].lik *= x.tp;
+      }
+      if (!aeq(x.alA, x.alB))
+        for (auto &l : x.links)
+          if (l.homo) { if (rev) l.lik = 0; l.homo = false; }
+      nxt.push_back(std::move(x));
+      best[key] = (int)nxt.size();
+    } else {
+      Pair &x = nxt[it->second - 1];  // HaploPair::add, HaploPair.cpp:63-89
+      x.fwd += pred.fwd * x.tp;
+      int k = (int)x.links.size();
+      int n = (int)pred.links.size();
+      x.links.insert(x.links.end(), pred.links.begin(), pred.links.end());
+      for (int i = k; i < k + n; ++i) {
+        x.links[i].pred = predIdx;
+        x.links[i].index = i - k;
+        x.links[i].rev = rev;
+        x.links[i].lik *= x.tp;
+      }
+      if (!aeq(x.alA, x.alB))
+        for (int i = k; i < k + n; ++i)
+          if (x.links[i].homo) { if (rev) x.links[i].lik = 0; x.links[i].homo = false; }
+      if ((int)x.links.size() > S) {
+        std::nth_element(x.links.begin(), x.links.begin() + S - 1, x.links.end(), GreaterLik());
+        x.links.resize(S);
+      }
+    }
+  }
+
+  // HaploBuilder.cpp:226-244
+  void extendAll(int locus, int a1, int a2, std::unordered_map<uint64_t, int> &best) {
+    int n = (int)hp[locus].size();
+    for (int s = 0; s < n; ++s) {
+      for (int o = 0; o < (aeq(a1, a2) ? 1 : 2); ++o) {
+        int x = o ? a2 : a1, y = o ? a1 : a2;
+        const Pair &q = hp[locus][s];
+        if (q.fwd <= 0) continue;
+        int sa = succOf(q.pa, x, P[q.pa].end);
+        int sb = succOf(q.pb, y, P[q.pb].end);
+        if (sa >= 0 && sb >= 0) addPair(locus, s, sa, sb, best);
+      }
+    }
+  }
+
+  // HaploPair.cpp:91-124
+  void traceback(int locus, int state, int index, std::vector<int> &h0, std::vector<int> &h1) const {
+    std::vector<int> *gh[2] = {&h0, &h1};
+    h0.assign(g.L, -1);
+    h1.assign(g.L, -1);
+    int a = 0, b = 1;
+    int i = g.L - 1;
+    int lc = locus, st = state;
+    while (true) {
+      const Pair &x = hp[lc][st];
+      if (index < (int)x.links.size() && x.links[index].pred >= 0) {
+        (*gh[a])[i] = P[x.pa].al[i - P[x.pa].start];
+        (*gh[b])[i] = P[x.pb].al[i - P[x.pb].start];
+        if (x.links[index].rev) std::swap(a, b);
+        int nst = x.links[index].pred;
+        index = x.links[index].index;
+        st = nst;
+        --lc;
+        --i;
+      } else {
+        const Pat &pa = P[x.pa], &pb = P[x.pb];
+        for (int k = 0; k < i + 1 - pa.start; ++k) (*gh[a])[pa.start + k] = pa.al[k];
+        for (int k = 0; k < i + 1 - pb.start; ++k) (*gh[b])[pb.start + k] = pb.al[k];
+        break;
+      }
+    }
+  }
+
+  // HaploBuilder.cpp:35-126 — returns coverage.
+  double resolve(int gi, std::vector<Candidate> &out, std::vector<int> &resol, double &gprob) {
+    int L = g.L, hl = head_len();
+    S = prm.sample_size > 1 ? prm.sample_size : 1;
+    hp.assign(L + 1, {});
+    std::vector<std::unordered_map<uint64_t, int>> best(L + 1);
+    initHeadList(gi, best[hl]);
+    for (int i = hl; i < L; ++i) {
+      std::unordered_map<uint64_t, int> &bm = best[i + 1];
+      if (g.isMissing(gi, i)) {
+        for (int j = 0; j < g.num(i); ++j)
+          if (g.afreq(i, j) > 0)
+            for (int k = j; k < g.num(i); ++k)
+              if (g.afreq(i, k) > 0) extendAll(i, g.symbol(i, j), g.symbol(i, k), bm);
+      } else if (missing(g.at(gi, 0, i))) {
+        for (int j = 0; j < g.num(i); ++j)
+          if (g.afreq(i, j) > 0) extendAll(i, g.symbol(i, j), g.at(gi, 1, i), bm);
+      } else if (missing(g.at(gi, 1, i))) {
+        for (int j = 0; j < g.num(i); ++j)
+          if (g.afreq(i, j) > 0) extendAll(i, g.symbol(i, j), g.at(gi, 0, i), bm);
+      } else {
+        extendAll(i, g.at(gi, 0, i), g.at(gi, 1, i), bm);
+      }
+      if (hp[i + 1].empty()) break;
+    }
+    for (int i = hl; i <= L; ++i)
+      for (auto &x : hp[i]) R_E += x.links.size();
+    out.clear();
+    double coverage = 0;
+    if (!hp[L].empty()) {
+      double total = 0;
+      std::vector<Link> rl;
+      for (int s = 0; s < (int)hp[L].size(); ++s) {
+        const Pair &x = hp[L][s];
+        total += x.fwd;
+        int k = (int)rl.size(), n = (int)x.links.size();
+        rl.insert(rl.end(), x.links.begin(), x.links.end());
+        for (int i = k; i < k + n; ++i) {
+          rl[i].pred = s;
+          rl[i].index = i - k;
+          if (!rl[i].homo) rl[i].lik *= 2.0;
+        }
+        if ((int)rl.size() > S) {
+          std::nth_element(rl.begin(), rl.begin() + S - 1, rl.end(), GreaterLik());
+          rl.resize(S);
+        }
+      }
+      std::sort(rl.begin(), rl.end(), GreaterLik());
+      for (auto &l : rl) {
+        Candidate c;
+        traceback(L, l.pred, l.index, c.h0, c.h1);
+        const Link &own = hp[L][l.pred].links[l.index];
+        c.prior = own.homo ? own.lik : own.lik * 2.0;  // HaploPair.cpp:97-102
+        c.posterior = c.prior / total;
+        c.gp = total;
+        coverage += c.posterior;
+        out.push_back(std::move(c));
+      }
+      resol.assign(2 * L, 0);
+      std::copy(out[0].h0.begin(), out[0].h0.end(), resol.begin());
+      std::copy(out[0].h1.begin(), out[0].h1.end(), resol.begin() + L);
+      gprob = total;
+    } else {  // HaploBuilder.cpp:117-124
+      resol.assign(2 * L, 0);
+      for (int k = 0; k < L; ++k) { resol[k] = g.at(gi, 0, k); resol[L + k] = g.at(gi, 1, k); }
+      gprob = 0;
+    }
+    return coverage;
+  }
+
+  // HaploModel.cpp:79-115
+  double resolveAll() {
+    samples.clear();
+    res.assign(g.N, {});
+    gp.assign(g.N, 0.0);
+    resolution.assign(g.N, {});
+    double ll = 0;
+    for (int i = 0; i < g.N; ++i) {
+      double cov = resolve(i, res[i], resolution[i], gp[i]);
+      for (auto &c : res[i]) {
+        double w = c.posterior / cov;
+        samples.push_back(Sample{c.h0, w});
+        samples.push_back(Sample{c.h1, w});
+      }
+      ll += log(gp[i]);
+    }
+    total_weight = 0;  // HaploData.cpp:120-126
+    for (auto &s : samples) total_weight += s.w;
+    hp.clear();
+    return ll;
+  }
+
+  // HaploModel.cpp:117-155 (MV, sampling EM).
+  void run() {
+    using clk = std::chrono::steady_clock;
+    samples.clear();
+    auto t0 = clk::now();
+    findPatterns();  // M0 on genotypes
+    t_m0 = std::chrono::duration<double>(clk::now() - t0).count();
+    npat_log.assign(1, (int)P.size());
+    rm_log.assign(1, R_M);
+    best_res.assign(g.N, {});
+    for (int i = 0; i < g.N; ++i) {
+      best_res[i].assign(2 * g.L, 0);
+      for (int k = 0; k < g.L; ++k) { best_res[i][k] = g.at(i, 0, k); best_res[i][g.L + k] = g.at(i, 1, k); }
+    }
+    ll_log.clear(); re_log.clear(); t_e_log.clear(); t_m_log.clear();
+    double old_ll = -DBL_MAX;
+    iterations = 0;
+    for (int it = 1; it <= prm.max_iter; ++it) {
+      uint64_t re0 = R_E;
+      auto t1 = clk::now();
+      double ll = resolveAll();
+      t_e_log.push_back(std::chrono::duration<double>(clk::now() - t1).count());
+      re_log.push_back(R_E - re0);
+      ll_log.push_back(ll);
+      iterations = it;
+      if (ll >= old_ll) best_res = resolution;
+      if (it < prm.max_iter && ll >= old_ll && (old_ll - ll) / old_ll > 0.0001) {
+        uint64_t rm0 = R_M;
+        auto t2 = clk::now();
+        findPatterns();
+        t_m_log.push_back(std::chrono::duration<double>(clk::now() - t2).count());
+        rm_log.push_back(R_M - rm0);
+        npat_log.push_back((int)P.size());
+        old_ll = ll;
+      } else {
+        break;
+      }
+    }
+  }
+};
+
+}  // namespace ora
+
+// ============================================================== C API ======
+using ora::Model;
+extern "C" {
+
+void *ora_create(int N, int L, const int *alleles, const char *types) {
+  Model *m = new Model;
+  m->g.N = N;
+  m->g.L = L;
+  m->g.al.assign(alleles, alleles + (size_t)N * 2 * L);
+  m->g.types = types ? std::string(types) : std::string(L, 'S');
+  m->g.checkAlleleSymbol();
+  return m;
+}
+
+void *ora_create_from_phase(const char *path) {
+  Model *m = new Model;
+  std::string err;
+  if (!ora::read_phase(path, m->g, err)) {
+    fprintf(stderr, "oracle: %s (%s)\n", err.c_str(), path);
+    delete m;
+    return nullptr;
+  }
+  return m;
+}
+
+void ora_destroy(void *h) { delete (Model *)h; }
+
+void ora_set_params(void *h, double min_freq_abs, int min_len, int max_len, int sample_size, int max_iter) {
+  Model *m = (Model *)h;
+  m->prm.min_freq_abs = min_freq_abs;
+  m->prm.min_len = min_len;
+  m->prm.max_len = max_len;
+  m->prm.sample_size = sample_size;
+  m->prm.max_iter = max_iter;
+}
+
+void ora_dims(void *h, int *N, int *L, int *amax) {
+  Model *m = (Model *)h;
+  *N = m->g.N;
+  *L = m->g.L;
+  *amax = m->g.maxnum();
+}
+// allele tables: num[L], sym[L][amax], freq[L][amax]
+void ora_allele_table(void *h, int amax, int *num, int *sym, double *freq) {
+  Model *m = (Model *)h;
+  for (int k = 0; k < m->g.L; ++k) {
+    num[k] = m->g.num(k);
+    for (int j = 0; j < amax; ++j) {
+      sym[k * amax + j] = j < m->g.num(k) ? m->g.symbol(k, j) : -1;
+      freq[k * amax + j] = j < m->g.num(k) ? m->g.afreq(k, j) : 0.0;
+    }
+  }
+}
+void ora_genotypes(void *h, int *out) {
+  Model *m = (Model *)h;
+  std::copy(m->g.al.begin(), m->g.al.end(), out);
+}
+
+// M-step: findPatterns() (genotype branch while no samples exist).
+int ora_find_patterns(void *h) {
+  Model *m = (Model *)h;
+  m->findPatterns();
+  return (int)m->P.size();
+}
+int ora_pattern_count(void *h) { return (int)((Model *)h)->P.size(); }
+int ora_head_len(void *h) { return ((Model *)h)->head_len(); }
+// pattern table in id order; succ is [P][amax] pattern ids, -1 = none;
+// alleles is [P][maxlen] symbols padded with -1.
+void ora_patterns(void *h, int amax, int maxlen, int *start, int *len, double *freq, double *prefix,
+                  double *tp, int *succ, int *alleles) {
+  Model *m = (Model *)h;
+  for (size_t i = 0; i < m->P.size(); ++i) {
+    const ora::Pat &p = m->P[i];
+    start[i] = p.start;
+    len[i] = p.len();
+    freq[i] = p.freq;
+    prefix[i] = p.prefix;
+    tp[i] = p.tp;
+    for (int j = 0; j < amax; ++j) succ[i * amax + j] = j < (int)p.succ.size() ? p.succ[j] : -1;
+    if (alleles)
+      for (int k = 0; k < maxlen; ++k) alleles[i * maxlen + k] = k < p.len() ? p.al[k] : -1;
+  }
+}
+
+// E-step: resolveAll(); returns the log-likelihood.
+double ora_resolve_all(void *h) { return ((Model *)h)->resolveAll(); }
+int ora_sample_count(void *h) { return (int)((Model *)h)->samples.size(); }
+double ora_total_weight(void *h) { return ((Model *)h)->total_weight; }
+void ora_samples(void *h, int *al /*[H][L]*/, double *w) {
+  Model *m = (Model *)h;
+  int L = m->g.L;
+  for (size_t s = 0; s < m->samples.size(); ++s) {
+    std::copy(m->samples[s].al.begin(), m->samples[s].al.end(), al + s * L);
+    w[s] = m->samples[s].w;
+  }
+}
+// per individual: number of candidates, genotype probability (total)
+void ora_estep_summary(void *h, int *ncand, double *gprob) {
+  Model *m = (Model *)h;
+  for (int i = 0; i < m->g.N; ++i) {
+    ncand[i] = (int)m->res[i].size();
+    gprob[i] = m->gp[i];
+  }
+}
+// candidate c of individual i: haplotypes [2][L], prior, posterior
+int ora_candidate(void *h, int i, int c, int *hap, double *prior, double *posterior) {
+  Model *m = (Model *)h;
+  if (i < 0 || i >= m->g.N || c < 0 || c >= (int)m->res[i].size()) return -1;
+  const ora::Candidate &x = m->res[i][c];
+  std::copy(x.h0.begin(), x.h0.end(), hap);
+  std::copy(x.h1.begin(), x.h1.end(), hap + m->g.L);
+  *prior = x.prior;
+  *posterior = x.posterior;
+  return 0;
+}
+// resolution (selected pair) per individual from the last E-step: [N][2][L]
+void ora_resolutions(void *h, int *out) {
+  Model *m = (Model *)h;
+  for (int i = 0; i < m->g.N; ++i) std::copy(m->resolution[i].begin(), m->resolution[i].end(), out + (size_t)i * 2 * m->g.L);
+}
+void ora_counters(void *h, uint64_t *re, uint64_t *rm) {
+  *re = ((Model *)h)->R_E;
+  *rm = ((Model *)h)->R_M;
+}
+void ora_reset_counters(void *h) { ((Model *)h)->R_E = ((Model *)h)->R_M = 0; }
+
+// Whole EM (HaploModel::run).  Returns iterations run.
+int ora_run(void *h) {
+  Model *m = (Model *)h;
+  m->R_E = m->R_M = 0;
+  m->run();
+  return m->iterations;
+}
+// per-iteration logs; arrays sized >= iterations (npat, rm: iterations + 1 entries: M0 first)
+void ora_run_log(void *h, double *ll, uint64_t *re, uint64_t *rm, int *npat, double *t_e, double *t_m,
+                 double *t_m0) {
+  Model *m = (Model *)h;
+  for (size_t i = 0; i < m->ll_log.size(); ++i) { ll[i] = m->ll_log[i]; re[i] = m->re_log[i]; t_e[i] = m->t_e_log[i]; }
+  for (size_t i = 0; i < m->rm_log.size(); ++i) rm[i] = m->rm_log[i];
+  for (size_t i = 0; i < m->npat_log.size(); ++i) npat[i] = m->npat_log[i];
+  for (size_t i = 0; i < m->t_m_log.size(); ++i) t_m[i] = m->t_m_log[i];
+  *t_m0 = m->t_m0;
+}
+// accepted resolutions after run(): [N][2][L]
+void ora_best_resolutions(void *h, int *out) {
+  Model *m = (Model *)h;
+  for (int i = 0; i < m->g.N; ++i) std::copy(m->best_res[i].begin(), m->best_res[i].end(), out + (size_t)i * 2 * m->g.L);
+}
+
+// Exposes std::nth_element / std::sort on (lik, tag) records so that tests can
+// check the product's libstdc++-exact selection replica against the real thing.
+void ora_std_nth_element(double *lik, int *tag, int n, int nth) {
+  std::vector<ora::Link> v(n);
+  for (int i = 0; i < n; ++i) v[i] = ora::Link{tag[i], 0, false, false, lik[i]};
+  std::nth_element(v.begin(), v.begin() + nth, v.end(), ora::GreaterLik());
+  for (int i = 0; i < n; ++i) { lik[i] = v[i].lik; tag[i] = v[i].pred; }
+}
+void ora_std_sort(double *lik, int *tag, int n) {
+  std::vector<ora::Link> v(n);
+  for (int i = 0; i < n; ++i) v[i] = ora::Link{tag[i], 0, false, false, lik[i]};
+  std::sort(v.begin(), v.end(), ora::GreaterLik());
+  for (int i = 0; i < n; ++i) { lik[i] = v[i].lik; tag[i] = v[i].pred; }
+}
+
+}  // extern "C"

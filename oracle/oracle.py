@@ -1,0 +1,206 @@
+"""ctypes binding of the CPU restatement (liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, never by the product package hmc_amd.
+Parity unpinned (see hmc_oracle.cpp header and DESIGN.md §Oracle).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    src = os.path.join(_HERE, "hmc_oracle.cpp")
+    if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
+    return _LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(_LIB)
+        vp, i, d, u64 = C.c_void_p, C.c_int, C.c_double, C.c_uint64
+        P = C.POINTER
+        L.ora_create.restype = vp
+        L.ora_create.argtypes = [i, i, P(i), C.c_char_p]
+        L.ora_create_from_phase.restype = vp
+        L.ora_create_from_phase.argtypes = [C.c_char_p]
+        L.ora_destroy.argtypes = [vp]
+        L.ora_set_params.argtypes = [vp, d, i, i, i, i]
+        L.ora_dims.argtypes = [vp, P(i), P(i), P(i)]
+        L.ora_allele_table.argtypes = [vp, i, P(i), P(i), P(d)]
+        L.ora_genotypes.argtypes = [vp, P(i)]
+        L.ora_find_patterns.restype = i
+        L.ora_find_patterns.argtypes = [vp]
+        L.ora_pattern_count.restype = i
+        L.ora_pattern_count.argtypes = [vp]
+        L.ora_head_len.restype = i
+        L.ora_head_len.argtypes = [vp]
+        L.ora_patterns.argtypes = [vp, i, i, P(i), P(i), P(d), P(d), P(d), P(i), P(i)]
+        L.ora_resolve_all.restype = d
+        L.ora_resolve_all.argtypes = [vp]
+        L.ora_sample_count.restype = i
+        L.ora_sample_count.argtypes = [vp]
+        L.ora_total_weight.restype = d
+        L.ora_total_weight.argtypes = [vp]
+        L.ora_samples.argtypes = [vp, P(i), P(d)]
+        L.ora_estep_summary.argtypes = [vp, P(i), P(d)]
+        L.ora_candidate.restype = i
+        L.ora_candidate.argtypes = [vp, i, i, P(i), P(d), P(d)]
+        L.ora_resolutions.argtypes = [vp, P(i)]
+        L.ora_counters.argtypes = [vp, P(u64), P(u64)]
+        L.ora_reset_counters.argtypes = [vp]
+        L.ora_run.restype = i
+        L.ora_run.argtypes = [vp]
+        L.ora_run_log.argtypes = [vp, P(d), P(u64), P(u64), P(i), P(d), P(d), P(d)]
+        L.ora_best_resolutions.argtypes = [vp, P(i)]
+        L.ora_std_nth_element.argtypes = [P(d), P(i), i, i]
+        L.ora_std_sort.argtypes = [P(d), P(i), i]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+class Oracle:
+    """Single-threaded CPU restatement of HaploModel (MV, sampling EM)."""
+
+    def __init__(self, alleles: np.ndarray | None = None, types: str | None = None,
+                 phase_path: str | None = None, min_freq_abs=1.5, min_len=1, max_len=30,
+                 sample_size=10, max_iter=1):
+        L = lib()
+        if phase_path is not None:
+            self.h = L.ora_create_from_phase(phase_path.encode())
+            if not self.h:
+                raise IOError(phase_path)
+        else:
+            a = np.ascontiguousarray(alleles, dtype=np.int32)
+            N, _, Lc = a.shape
+            self.h = L.ora_create(N, Lc, _p(a, C.c_int), (types or "S" * Lc).encode())
+        self.set_params(min_freq_abs, min_len, max_len, sample_size, max_iter)
+        n, l, am = C.c_int(), C.c_int(), C.c_int()
+        L.ora_dims(self.h, C.byref(n), C.byref(l), C.byref(am))
+        self.N, self.L, self.amax = n.value, l.value, am.value
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.ora_destroy(self.h)
+            self.h = None
+
+    def set_params(self, min_freq_abs=1.5, min_len=1, max_len=30, sample_size=10, max_iter=1):
+        self.max_len = max_len if max_len > 0 else 0
+        lib().ora_set_params(self.h, min_freq_abs, min_len, max_len, sample_size, max_iter)
+
+    def allele_table(self):
+        num = np.zeros(self.L, np.int32)
+        sym = np.zeros((self.L, self.amax), np.int32)
+        fr = np.zeros((self.L, self.amax), np.float64)
+        lib().ora_allele_table(self.h, self.amax, _p(num, C.c_int), _p(sym, C.c_int), _p(fr, C.c_double))
+        return num, sym, fr
+
+    def genotypes(self):
+        out = np.zeros((self.N, 2, self.L), np.int32)
+        lib().ora_genotypes(self.h, _p(out, C.c_int))
+        return out
+
+    def find_patterns(self) -> int:
+        return lib().ora_find_patterns(self.h)
+
+    def head_len(self) -> int:
+        return lib().ora_head_len(self.h)
+
+    def patterns(self, maxlen: int | None = None) -> dict:
+        P = lib().ora_pattern_count(self.h)
+        A = self.amax
+        start = np.zeros(P, np.int32)
+        ln = np.zeros(P, np.int32)
+        fr = np.zeros(P, np.float64)
+        pre = np.zeros(P, np.float64)
+        tp = np.zeros(P, np.float64)
+        succ = np.zeros((P, A), np.int32)
+        ml = maxlen or max(1, self.L)
+        ml = min(ml, self.L)
+        al = np.zeros((P, ml), np.int32)
+        lib().ora_patterns(self.h, A, ml, _p(start, C.c_int), _p(ln, C.c_int), _p(fr, C.c_double),
+                           _p(pre, C.c_double), _p(tp, C.c_double), _p(succ, C.c_int), _p(al, C.c_int))
+        return dict(start=start, len=ln, freq=fr, prefix=pre, tp=tp, succ=succ, alleles=al)
+
+    def resolve_all(self) -> float:
+        return lib().ora_resolve_all(self.h)
+
+    def samples(self):
+        H = lib().ora_sample_count(self.h)
+        al = np.zeros((H, self.L), np.int32)
+        w = np.zeros(H, np.float64)
+        lib().ora_samples(self.h, _p(al, C.c_int), _p(w, C.c_double))
+        return al, w, lib().ora_total_weight(self.h)
+
+    def estep_summary(self):
+        nc = np.zeros(self.N, np.int32)
+        gp = np.zeros(self.N, np.float64)
+        lib().ora_estep_summary(self.h, _p(nc, C.c_int), _p(gp, C.c_double))
+        return nc, gp
+
+    def candidate(self, i: int, c: int):
+        hap = np.zeros((2, self.L), np.int32)
+        pr, po = C.c_double(), C.c_double()
+        rc = lib().ora_candidate(self.h, i, c, _p(hap, C.c_int), C.byref(pr), C.byref(po))
+        if rc:
+            raise IndexError((i, c))
+        return hap, pr.value, po.value
+
+    def resolutions(self):
+        out = np.zeros((self.N, 2, self.L), np.int32)
+        lib().ora_resolutions(self.h, _p(out, C.c_int))
+        return out
+
+    def counters(self):
+        re, rm = C.c_uint64(), C.c_uint64()
+        lib().ora_counters(self.h, C.byref(re), C.byref(rm))
+        return re.value, rm.value
+
+    def reset_counters(self):
+        lib().ora_reset_counters(self.h)
+
+    def run(self) -> dict:
+        it = lib().ora_run(self.h)
+        ll = np.zeros(it, np.float64)
+        re = np.zeros(it, np.uint64)
+        rm = np.zeros(it + 1, np.uint64)
+        npat = np.zeros(it + 1, np.int32)
+        te = np.zeros(it, np.float64)
+        tm = np.zeros(it, np.float64)
+        tm0 = C.c_double()
+        lib().ora_run_log(self.h, _p(ll, C.c_double), _p(re, C.c_uint64), _p(rm, C.c_uint64),
+                          _p(npat, C.c_int), _p(te, C.c_double), _p(tm, C.c_double), C.byref(tm0))
+        best = np.zeros((self.N, 2, self.L), np.int32)
+        lib().ora_best_resolutions(self.h, _p(best, C.c_int))
+        n_m = max(0, it - 1) if len(ll) and np.isfinite(ll).all() else max(0, it - 1)
+        return dict(iterations=it, ll=ll, R_E=re, R_M=rm, n_patterns=npat, t_e=te, t_m=tm,
+                    t_m0=tm0.value, resolutions=best, n_m=n_m)
+
+
+def std_nth_element(lik: np.ndarray, tag: np.ndarray, nth: int):
+    lik = np.ascontiguousarray(lik, np.float64).copy()
+    tag = np.ascontiguousarray(tag, np.int32).copy()
+    lib().ora_std_nth_element(_p(lik, C.c_double), _p(tag, C.c_int), len(lik), nth)
+    return lik, tag
+
+
+def std_sort(lik: np.ndarray, tag: np.ndarray):
+    lik = np.ascontiguousarray(lik, np.float64).copy()
+    tag = np.ascontiguousarray(tag, np.int32).copy()
+    lib().ora_std_sort(_p(lik, C.c_double), _p(tag, C.c_int), len(lik))
+    return lik, tag
