@@ -54,6 +54,7 @@ _SIGS = [
     ("hmc_get_estep", _i, [_vp, _P(_d), _P(C.c_int32), _P(C.c_int32), _P(_d), _P(_d), _P(_d)]),
     ("hmc_get_samples", _i, [_vp, _P(C.c_int32), _P(_d), _P(_d)]),
     ("hmc_get_resolutions", _i, [_vp, _P(C.c_int32)]),
+    ("hmc_clear_samples", _i, [_vp]),
     ("hmc_run", _i, [_vp, _i, _P(IterLog), _i, _P(_i), _P(_d), _P(_u64), _P(_i)]),
     ("hmc_get_best_resolutions", _i, [_vp, _P(C.c_int32)]),
     ("hmc_write_phase", _i, [_vp, _cp]),

@@ -605,14 +605,16 @@ struct Ctx {
         (e = d_cidx.ensure((size_t)n * S_MAX)) || (e = d_rows.ensure((size_t)2 * S * n * L)) ||
         (e = d_w.ensure((size_t)2 * S * n)) || (e = d_trace_cursor.ensure(1)) || (e = d_maxst.ensure(1)))
       return hipfail(e, "estep alloc");
-    // trace store budget
+    // trace store: start from an estimate (96 states of 1+S words per
+    // individual-locus), grow up to the budget on overflow, then split batches
     size_t freeb = 0, totb = 0;
     hipMemGetInfo(&freeb, &totb);
-    uint64_t tb = trace_bytes ? trace_bytes : (uint64_t)(freeb * 0.35);
-    tb = std::max<uint64_t>(tb, 1ull << 20);
-    if (d_trace.n * 4 < tb / 2 || d_trace.n * 4 > tb * 2) {
+    const uint64_t cap_bytes =
+        std::max<uint64_t>(trace_bytes ? trace_bytes : (uint64_t)((freeb + d_trace.n * 4) * 0.35), 1ull << 20);
+    const uint64_t want = std::min<uint64_t>(cap_bytes, std::max<uint64_t>((uint64_t)n * L * (1 + S) * 4 * 96, 64ull << 20));
+    if (d_trace.n * 4 < want) {
       d_trace.release();
-      if ((e = d_trace.ensure(tb / 4))) return hipfail(e, "trace alloc");
+      if ((e = d_trace.ensure(want / 4))) return hipfail(e, "trace alloc");
     }
     h_total.assign(n, 0.0);
     h_ncand.assign(n, 0);
@@ -680,6 +682,12 @@ struct Ctx {
         continue;
       }
       if (ovf_trace) {
+        if (d_trace.n * 4 < cap_bytes) {  // grow the store before splitting the batch
+          const uint64_t nb = std::min<uint64_t>(cap_bytes, d_trace.n * 4 * 4);
+          d_trace.release();
+          if ((e = d_trace.ensure(nb / 4))) return hipfail(e, "trace alloc");
+          continue;
+        }
         if (bn == 1) return fail(HMC_ENOMEM, "trace store too small for one individual");
         batch = std::max(1, bn / 2);
         continue;
@@ -1149,6 +1157,13 @@ int hmc_run(hmc_ctx *h, int max_iteration, hmc_iter_log *log, int log_cap, int *
             uint64_t *r_m0, int *n_patterns0) {
   if (!h) return HMC_EARG;
   return h->c.run(max_iteration, log, log_cap, iterations, t_m0_s, r_m0, n_patterns0);
+}
+
+int hmc_clear_samples(hmc_ctx *h) {
+  if (!h) return HMC_EARG;
+  h->c.have_samples = false;
+  h->c.H = 0;
+  return HMC_OK;
 }
 
 int hmc_get_best_resolutions(hmc_ctx *h, int32_t *out) {

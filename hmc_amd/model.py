@@ -194,6 +194,9 @@ class HaploModel:
         self._check(lib().hmc_get_samples(self._h, _p(al, C.c_int32), _p(w, C.c_double), C.byref(tw)))
         return al, w, tw.value
 
+    def clear_samples(self):
+        self._check(lib().hmc_clear_samples(self._h))
+
     def resolutions(self) -> np.ndarray:
         out = np.zeros((self.i1 - self.i0, 2, self.L), np.int32)
         self._check(lib().hmc_get_resolutions(self._h, _p(out, C.c_int32)))

@@ -94,6 +94,9 @@ int hmc_get_estep(hmc_ctx *ctx, double *total, int32_t *ncand, int32_t *status, 
                   double *weight);
 /* HaploData samples of this rank: alleles[H][L] symbols, weights[H]. */
 int hmc_get_samples(hmc_ctx *ctx, int32_t *alleles, double *weights, double *total_weight);
+/* Drop the samples so the next hmc_find_patterns mines the genotypes again
+ * (HaploBuilder::setGenoData clears m_samples, HaploBuilder.cpp:19-23). */
+int hmc_clear_samples(hmc_ctx *ctx);
 /* Selected pair per individual of the last E-step ([n][2][L] symbols;
  * unresolved individuals keep the input genotype, HaploBuilder.cpp:117-124). */
 int hmc_get_resolutions(hmc_ctx *ctx, int32_t *out);

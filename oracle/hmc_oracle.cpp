@@ -923,4 +923,67 @@ void ora_std_sort(double *lik, int *tag, int n) {
   for (int i = 0; i < n; ++i) { lik[i] = v[i].lik; tag[i] = v[i].pred; }
 }
 
+// ---- seams used by bench.py's cpu_baseline leg ------------------------------
+// Install a pattern table (id order) and run initialize()'s tree build; the
+// given successors are kept (they come from a parity-checked M-step).
+int ora_set_patterns(void *h, int P, const int *start, const int *len, const int *alleles, int maxlen,
+                     const double *freq, const double *prefix, const double *tp, const int *succ, int amax) {
+  Model *m = (Model *)h;
+  m->P.assign(P, ora::Pat{});
+  for (int i = 0; i < P; ++i) {
+    ora::Pat &p = m->P[i];
+    p.start = start[i];
+    p.end = start[i] + len[i];
+    p.al.assign(alleles + (size_t)i * maxlen, alleles + (size_t)i * maxlen + len[i]);
+    p.freq = freq[i];
+    p.prefix = prefix[i];
+    p.tp = tp[i];
+    p.id = i;
+    if (p.end < m->g.L) {
+      p.succ.assign(succ + (size_t)i * amax, succ + (size_t)i * amax + m->g.num(p.end));
+    }
+  }
+  if (m->minlen.empty()) {
+    m->minlen.assign(m->g.L, std::max(m->prm.min_len, 1));
+    m->maxlen.assign(m->g.L, m->prm.max_len <= 0 ? m->g.L : m->prm.max_len);
+  }
+  m->tree.init(m->g);
+  m->head_list.clear();
+  for (int i = 0; i < P; ++i) {
+    m->tree.add(m->P, i);
+    if (m->P[i].start == 0 && m->P[i].len() == m->head_len()) m->head_list.push_back(i);
+  }
+  return 0;
+}
+// Time HaploBuilder::resolve over individuals [i0, i1) (results discarded).
+double ora_time_resolve_range(void *h, int i0, int i1) {
+  Model *m = (Model *)h;
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<ora::Candidate> out;
+  std::vector<int> resol;
+  double gp;
+  for (int i = i0; i < i1; ++i) m->resolve(i, out, resol, gp);
+  m->hp.clear();
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+// Install HaploData samples ([H][L] symbols, weights) and total_weight.
+void ora_set_samples(void *h, int H, const int *al, const double *w) {
+  Model *m = (Model *)h;
+  int L = m->g.L;
+  m->samples.assign(H, ora::Sample{});
+  m->total_weight = 0;
+  for (int s = 0; s < H; ++s) {
+    m->samples[s].al.assign(al + (size_t)s * L, al + (size_t)s * L + L);
+    m->samples[s].w = w[s];
+    m->total_weight += w[s];
+  }
+}
+// Time findPatterns() (sample branch when samples are installed).
+double ora_time_find_patterns(void *h) {
+  Model *m = (Model *)h;
+  auto t0 = std::chrono::steady_clock::now();
+  m->findPatterns();
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 }  // extern "C"

@@ -66,6 +66,13 @@ def lib():
         L.ora_best_resolutions.argtypes = [vp, P(i)]
         L.ora_std_nth_element.argtypes = [P(d), P(i), i, i]
         L.ora_std_sort.argtypes = [P(d), P(i), i]
+        L.ora_set_patterns.restype = i
+        L.ora_set_patterns.argtypes = [vp, i, P(i), P(i), P(i), i, P(d), P(d), P(d), P(i), i]
+        L.ora_time_resolve_range.restype = d
+        L.ora_time_resolve_range.argtypes = [vp, i, i]
+        L.ora_set_samples.argtypes = [vp, i, P(i), P(d)]
+        L.ora_time_find_patterns.restype = d
+        L.ora_time_find_patterns.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -136,6 +143,27 @@ class Oracle:
         lib().ora_patterns(self.h, A, ml, _p(start, C.c_int), _p(ln, C.c_int), _p(fr, C.c_double),
                            _p(pre, C.c_double), _p(tp, C.c_double), _p(succ, C.c_int), _p(al, C.c_int))
         return dict(start=start, len=ln, freq=fr, prefix=pre, tp=tp, succ=succ, alleles=al)
+
+    def set_patterns(self, pt: dict):
+        al = np.ascontiguousarray(pt["alleles"], np.int32)
+        succ = np.ascontiguousarray(pt["succ"], np.int32)
+        P = len(pt["start"])
+        a = lambda x, t: np.ascontiguousarray(x, t)
+        lib().ora_set_patterns(self.h, P, _p(a(pt["start"], np.int32), C.c_int), _p(a(pt["len"], np.int32), C.c_int),
+                               _p(al, C.c_int), al.shape[1], _p(a(pt["freq"], np.float64), C.c_double),
+                               _p(a(pt["prefix"], np.float64), C.c_double), _p(a(pt["tp"], np.float64), C.c_double),
+                               _p(succ, C.c_int), succ.shape[1])
+
+    def time_resolve_range(self, i0: int, i1: int) -> float:
+        return lib().ora_time_resolve_range(self.h, i0, i1)
+
+    def set_samples(self, al: np.ndarray, w: np.ndarray):
+        al = np.ascontiguousarray(al, np.int32)
+        w = np.ascontiguousarray(w, np.float64)
+        lib().ora_set_samples(self.h, al.shape[0], _p(al, C.c_int), _p(w, C.c_double))
+
+    def time_find_patterns(self) -> float:
+        return lib().ora_time_find_patterns(self.h)
 
     def resolve_all(self) -> float:
         return lib().ora_resolve_all(self.h)
