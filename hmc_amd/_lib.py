@@ -27,6 +27,8 @@ class IterLog(C.Structure):
                 ("r_e", C.c_uint64), ("r_m", C.c_uint64), ("n_patterns", C.c_int), ("n_samples", C.c_int)]
 
 
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_size_t, C.c_void_p)
+
 _lib = None
 
 # (name, restype, argtypes)
@@ -37,6 +39,7 @@ _SIGS = [
     ("hmc_ctx_create", _i, [_i, _P(_vp)]),
     ("hmc_rccl_unique_id", _i, [_vp]),
     ("hmc_ctx_create_dist", _i, [_i, _i, _i, _vp, _P(_vp)]),
+    ("hmc_ctx_create_hostcoll", _i, [_i, _i, _i, ALLREDUCE_FN, _vp, _P(_vp)]),
     ("hmc_ctx_destroy", None, [_vp]),
     ("hmc_ctx_error", _cp, [_vp]),
     ("hmc_set_params", _i, [_vp, _d, _d, _i, _i, _i]),

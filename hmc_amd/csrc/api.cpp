@@ -182,6 +182,8 @@ struct Ctx {
   int device = 0, rank = 0, world = 1;
   hipStream_t st = nullptr;
   ncclComm_t comm = nullptr;
+  hmc_allreduce_fn host_fn = nullptr;  // host-callback collective (tests, gloo)
+  void *host_user = nullptr;
   std::string err;
   // parameters (HaploModel.h:15-26 with the CLI defaults of HMC.cpp:35-47)
   double min_freq_abs = 1.5, min_freq = -1.0;
@@ -267,12 +269,22 @@ struct Ctx {
   // ---------------------------------------------------------- collectives --
   int allreduce_sum(double *dptr, size_t n) {
     if (world == 1 || n == 0) return HMC_OK;
+    if (host_fn) {
+      std::vector<double> h(n);
+      hipError_t e;
+      if ((e = hipMemcpyAsync(h.data(), dptr, n * 8, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+        return hipfail(e, "allreduce");
+      if (host_fn(h.data(), n, host_user) != 0) return fail(HMC_ERCCL, "host all-reduce callback failed");
+      if ((e = hipMemcpyAsync(dptr, h.data(), n * 8, hipMemcpyHostToDevice, st))) return hipfail(e, "allreduce");
+      return HMC_OK;
+    }
     ncclResult_t r = ncclAllReduce(dptr, dptr, n, ncclDouble, ncclSum, comm, st);
     if (r != ncclSuccess) return fail(HMC_ERCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
     return HMC_OK;
   }
   int allreduce_host(double *h, size_t n) {  // small host vectors
     if (world == 1 || n == 0) return HMC_OK;
+    if (host_fn) return host_fn(h, n, host_user) == 0 ? HMC_OK : fail(HMC_ERCCL, "host all-reduce callback failed");
     DevBuf<double> tmp;
     hipError_t e = tmp.ensure(n);
     if (e) return hipfail(e, "allreduce_host");
@@ -903,6 +915,19 @@ int hmc_ctx_create_dist(int device, int rank, int world, const void *unique_id, 
     ncclResult_t r = ncclCommInitRank(&h->c.comm, world, id, rank);
     if (r != ncclSuccess) return h->c.fail(HMC_ERCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
   }
+  return HMC_OK;
+}
+
+int hmc_ctx_create_hostcoll(int device, int rank, int world, hmc_allreduce_fn fn, void *user, hmc_ctx **out) {
+  if (!out || world < 1 || rank < 0 || rank >= world || (world > 1 && !fn)) return HMC_EARG;
+  hmc_ctx *h = new hmc_ctx;
+  *out = h;
+  int rc = ctx_init(h, device);
+  if (rc) return rc;
+  h->c.rank = rank;
+  h->c.world = world;
+  h->c.host_fn = fn;
+  h->c.host_user = user;
   return HMC_OK;
 }
 

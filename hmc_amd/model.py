@@ -20,7 +20,7 @@ import dataclasses
 
 import numpy as np
 
-from ._lib import HMCError, IterLog, lib
+from ._lib import ALLREDUCE_FN, HMCError, IterLog, lib
 
 _P = C.POINTER
 
@@ -52,10 +52,26 @@ class GenoData:
 class HaploModel:
     """HaploModel (model "MV", sampling EM) on one MI355X, or one rank of a sharded run."""
 
-    def __init__(self, device: int = 0, rank: int = 0, world: int = 1, unique_id: bytes | None = None):
+    def __init__(self, device: int = 0, rank: int = 0, world: int = 1, unique_id: bytes | None = None,
+                 host_allreduce=None):
+        """world > 1 shards individuals over ranks.  The M-step collective is
+        RCCL (unique_id from HaploModel.unique_id() on rank 0), or, when
+        `host_allreduce(np.ndarray)` is given, that callable, which must sum the
+        float64 array across ranks in place (e.g. torch.distributed gloo)."""
         L = lib()
         h = C.c_void_p()
-        if world > 1:
+        self._cb = None
+        if host_allreduce is not None:
+            def _cb(buf, n, _user):
+                try:
+                    arr = np.ctypeslib.as_array(buf, shape=(n,))
+                    host_allreduce(arr)
+                    return 0
+                except Exception:  # noqa: BLE001 — reported to the library as failure
+                    return 1
+            self._cb = ALLREDUCE_FN(_cb)
+            rc = L.hmc_ctx_create_hostcoll(device, rank, world, self._cb, None, C.byref(h))
+        elif world > 1:
             uid = C.create_string_buffer(unique_id, 128)
             rc = L.hmc_ctx_create_dist(device, rank, world, C.cast(uid, C.c_void_p), C.byref(h))
         else:

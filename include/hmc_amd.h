@@ -43,6 +43,11 @@ int hmc_ctx_create(int device, hmc_ctx **out);
  * sharded in contiguous blocks; the M-step all-reduces per-level sums. */
 int hmc_rccl_unique_id(void *out128);
 int hmc_ctx_create_dist(int device, int rank, int world, const void *unique_id, hmc_ctx **out);
+/* Same sharding with a caller-supplied collective instead of RCCL: fn must
+ * sum `n` doubles element-wise across ranks in place and return 0.  Lets
+ * several ranks share one GPU (tests) or run over any host transport. */
+typedef int (*hmc_allreduce_fn)(double *buf, size_t n, void *user);
+int hmc_ctx_create_hostcoll(int device, int rank, int world, hmc_allreduce_fn fn, void *user, hmc_ctx **out);
 void hmc_ctx_destroy(hmc_ctx *ctx);
 const char *hmc_ctx_error(const hmc_ctx *ctx);
 

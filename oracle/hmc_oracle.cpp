@@ -986,4 +986,28 @@ double ora_time_find_patterns(void *h) {
   return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// HaploModel::resolveAll restricted to individuals [i0, i1) (the shard one
+// rank of the sharded E-step owns); samples/results cover only that range.
+double ora_resolve_range(void *h, int i0, int i1) {
+  Model *m = (Model *)h;
+  m->samples.clear();
+  m->res.assign(m->g.N, {});
+  m->gp.assign(m->g.N, 0.0);
+  m->resolution.assign(m->g.N, {});
+  double ll = 0;
+  for (int i = i0; i < i1; ++i) {
+    double cov = m->resolve(i, m->res[i], m->resolution[i], m->gp[i]);
+    for (auto &c : m->res[i]) {
+      double w = c.posterior / cov;
+      m->samples.push_back(ora::Sample{c.h0, w});
+      m->samples.push_back(ora::Sample{c.h1, w});
+    }
+    ll += log(m->gp[i]);
+  }
+  m->total_weight = 0;
+  for (auto &x : m->samples) m->total_weight += x.w;
+  m->hp.clear();
+  return ll;
+}
+
 }  // extern "C"

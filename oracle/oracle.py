@@ -73,6 +73,8 @@ def lib():
         L.ora_set_samples.argtypes = [vp, i, P(i), P(d)]
         L.ora_time_find_patterns.restype = d
         L.ora_time_find_patterns.argtypes = [vp]
+        L.ora_resolve_range.restype = d
+        L.ora_resolve_range.argtypes = [vp, i, i]
         _lib = L
     return _lib
 
@@ -164,6 +166,9 @@ class Oracle:
 
     def time_find_patterns(self) -> float:
         return lib().ora_time_find_patterns(self.h)
+
+    def resolve_range(self, i0: int, i1: int) -> float:
+        return lib().ora_resolve_range(self.h, i0, i1)
 
     def resolve_all(self) -> float:
         return lib().ora_resolve_all(self.h)

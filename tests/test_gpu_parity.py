@@ -1,0 +1,331 @@
+"""GPU parity: the gfx950 path (libhmc_amd.so, called through its C-ABI) against
+the CPU restatement on the same seeded panels.  Bar: bit-exact for every
+integer, allele and index output and for every double (likelihoods, weights,
+frequencies, transition probabilities) — the kernels keep the reference's
+operation order (tolerance 0 everywhere on one GPU)."""
+import hashlib
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import hmc_amd
+from hmc_amd import synth
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+PANELS = {
+    "cfg1": dict(N=10, L=20, A=2, missing=0.0, seed=1),
+    "n60": dict(N=60, L=40, A=2, missing=0.0, seed=2),
+    "a4": dict(N=100, L=100, A=4, missing=0.0, seed=3),
+    "miss2": dict(N=100, L=100, A=2, missing=0.02, seed=4),
+    "a3miss5": dict(N=80, L=60, A=3, missing=0.05, seed=5),
+    "a8": dict(N=60, L=50, A=8, missing=0.01, seed=6),
+    "n300": dict(N=300, L=200, A=2, missing=0.0, seed=7),
+}
+
+
+def panel(name):
+    c = PANELS[name]
+    return synth.founder_mosaic(c["N"], c["L"], A=c["A"], missing=c["missing"], seed=c["seed"])
+
+
+def gpu_model(p, S=10, **kw):
+    m = hmc_amd.HaploModel()
+    m.sample_size = S
+    for k, v in kw.items():
+        setattr(m, k, v)
+    m.load(hmc_amd.GenoData.from_panel(p))
+    return m
+
+
+def last_symbols(pt):
+    return np.array([pt["alleles"][i, pt["len"][i] - 1] for i in range(len(pt["len"]))], np.int32)
+
+
+def assert_tables_equal(g, o):
+    assert len(g["start"]) == len(o["start"])
+    for k in ("start", "len", "freq", "prefix", "tp", "succ", "alleles"):
+        assert np.array_equal(g[k], o[k]), k
+
+
+def assert_estep_equal(m, o, ll_g, ll_o, H, re_g):
+    re_o, _ = o.counters()
+    assert ll_g == ll_o
+    assert re_g == re_o
+    nc, gp = o.estep_summary()
+    er = m.estep_results()
+    assert np.array_equal(er["ncand"], nc)
+    assert np.array_equal(er["total"], gp)
+    al_o, w_o, tw_o = o.samples()
+    al_g, w_g, tw_g = m.samples(H)
+    assert np.array_equal(al_g, al_o) and np.array_equal(w_g, w_o) and tw_g == tw_o
+    for i in range(o.N):
+        for c in range(nc[i]):
+            _, pr, po = o.candidate(i, c)
+            assert er["prior"][i, c] == pr and er["posterior"][i, c] == po
+    assert np.array_equal(m.resolutions(), o.resolutions())
+
+
+@pytest.mark.parametrize("name", sorted(PANELS))
+@pytest.mark.parametrize("S", [10])
+def test_estep_on_reference_model(oracle_mod, name, S):
+    """E-step kernels fed the restatement's M0 table == HaploModel::resolveAll."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=S)
+    o.find_patterns()
+    pt = o.patterns()
+    m = gpu_model(p, S)
+    m.set_patterns(pt["start"], pt["len"], pt["freq"], pt["tp"], pt["succ"], last_symbols(pt))
+    ll_g, H, re_g = m.resolve_all()
+    o.reset_counters()
+    ll_o = o.resolve_all()
+    assert_estep_equal(m, o, ll_g, ll_o, H, re_g)
+
+
+@pytest.mark.parametrize("S", [1, 2, 5, 16])
+def test_estep_sample_sizes(oracle_mod, S):
+    p = panel("miss2")
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=S)
+    o.find_patterns()
+    pt = o.patterns()
+    m = gpu_model(p, S)
+    m.set_patterns(pt["start"], pt["len"], pt["freq"], pt["tp"], pt["succ"], last_symbols(pt))
+    ll_g, H, re_g = m.resolve_all()
+    o.reset_counters()
+    assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
+
+
+@pytest.mark.parametrize("name", sorted(PANELS))
+def test_mine_genotypes_and_samples(oracle_mod, name):
+    """M0 (genotype branch) and M1 (sample branch) pattern tables, bit-exact."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
+    o.find_patterns()
+    _, rm0_o = o.counters()
+    m = gpu_model(p)
+    P0, rm0 = m.find_patterns()
+    assert P0 == len(o.patterns()["start"]) and rm0 == rm0_o
+    assert_tables_equal(m.patterns(), o.patterns())
+    ll_g, H, _ = m.resolve_all()
+    ll_o = o.resolve_all()
+    assert ll_g == ll_o
+    o.reset_counters()
+    P1, rm1 = m.find_patterns()
+    o.find_patterns()
+    _, rm1_o = o.counters()
+    assert rm1 == rm1_o
+    assert_tables_equal(m.patterns(), o.patterns())
+
+
+@pytest.mark.parametrize("name", ["cfg1", "n60", "a4", "miss2", "a3miss5", "a8"])
+def test_full_em(oracle_mod, name):
+    """HaploModel::run: iteration count, per-iteration LL / R_E / R_M / pattern
+    counts and the accepted haplotype pair of every individual."""
+    p = panel(name)
+    m = gpu_model(p, max_iteration=30)
+    res = m.run()
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10, max_iter=30)
+    r = o.run()
+    assert m.iterations == r["iterations"]
+    assert [x["ll"] for x in m.log] == r["ll"].tolist()
+    assert [x["r_e"] for x in m.log] == r["R_E"].tolist()
+    assert m.m0["r_m"] == r["R_M"][0] and m.m0["n_patterns"] == r["n_patterns"][0]
+    for k in range(r["iterations"] - 1):
+        assert m.log[k]["r_m"] == r["R_M"][k + 1]
+        assert m.log[k]["n_patterns"] == r["n_patterns"][k + 1]
+    assert np.array_equal(res, r["resolutions"])
+
+
+@pytest.mark.parametrize("gname", ["cfg1", "miss_a3", "snp_miss", "s3"])
+def test_against_golden_fixtures(gname):
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    import make_golden
+
+    c = make_golden.CASES[gname]
+    g = np.load(os.path.join(HERE, "golden", f"{gname}.npz"))
+    p = synth.founder_mosaic(c["N"], c["L"], A=c["A"], missing=c["missing"], seed=c["seed"])
+    assert np.array_equal(p.alleles, g["alleles"])
+    m = gpu_model(p, c["S"])
+    m.find_patterns()
+    pt = m.patterns(maxlen=g["m0_alleles"].shape[1])
+    for k in ("start", "len", "freq", "prefix", "tp", "succ", "alleles"):
+        assert np.array_equal(pt[k], g["m0_" + k]), k
+    ll, H, _ = m.resolve_all()
+    assert ll == g["e1_ll"][0]
+    er = m.estep_results()
+    assert np.array_equal(er["ncand"], g["e1_ncand"]) and np.array_equal(er["total"], g["e1_total"])
+    al, w, tw = m.samples(H)
+    assert np.array_equal(al, g["e1_samples"]) and np.array_equal(w, g["e1_w"]) and tw == g["e1_tw"][0]
+    m2 = gpu_model(p, c["S"], max_iteration=20)
+    res = m2.run()
+    assert m2.iterations == g["em_iterations"][0]
+    assert np.array_equal(np.array([x["ll"] for x in m2.log]), g["em_ll"])
+    assert np.array_equal(res, g["em_resolutions"])
+
+
+def test_phase_file_io(tmp_path, oracle_mod):
+    p = panel("a3miss5")
+    f = tmp_path / "in.phase"
+    synth.write_phase(p, str(f))
+    m = hmc_amd.HaploModel()
+    m.max_iteration = 10
+    m.load_phase(str(f))  # HaploFile::readGenoData
+    res = m.run()
+    m2 = gpu_model(p, max_iteration=10)
+    assert np.array_equal(res, m2.run())
+    out = tmp_path / "out.phase"
+    m.write_phase(str(out))  # HaploFile::writeGenoData
+    back = synth.read_phase(str(out))
+    assert np.array_equal(back.alleles, res)
+
+
+def test_edge_cases(oracle_mod):
+    """L = 1, monomorphic loci, an all-missing locus and individual, missing at
+    locus 0 (initHeadList's missing-complement branch)."""
+    rng = np.random.default_rng(9)
+    base = synth.founder_mosaic(30, 12, A=3, missing=0.0, seed=9).alleles.copy()
+    base[:, :, 3] = ord("2")        # monomorphic locus
+    base[:, :, 5] = -1              # all missing at one locus
+    base[4, :, :] = -1              # one individual entirely missing
+    base[7, 0, 0] = -1              # one missing allele at locus 0
+    base[8, :, 0] = -1              # both missing at locus 0
+    cases = [base, base[:, :, :1].copy(), base[:5, :, 2:4].copy()]
+    for a in cases:
+        o = oracle_mod.Oracle(a, "S" * a.shape[2], sample_size=10, max_iter=10)
+        r = o.run()
+        m = hmc_amd.HaploModel()
+        m.max_iteration = 10
+        res = m.run(hmc_amd.GenoData(a, "S" * a.shape[2]))
+        assert m.iterations == r["iterations"]
+        assert [x["ll"] for x in m.log] == r["ll"].tolist()
+        assert np.array_equal(res, r["resolutions"])
+
+
+def test_underflow_unresolved(oracle_mod):
+    """Raw double products underflow on long i.i.d. panels; those individuals
+    are unresolved (HaploBuilder.cpp:117-124), LL = -inf and the EM stops —
+    both implementations must agree on all of it."""
+    rng = np.random.default_rng(5)
+    a = (rng.integers(0, 2, (6, 2, 2500)) + ord("1")).astype(np.int32)
+    o = oracle_mod.Oracle(a, "S" * 2500, sample_size=4, max_iter=3)
+    r = o.run()
+    m = hmc_amd.HaploModel()
+    m.sample_size = 4
+    m.max_iteration = 3
+    res = m.run(hmc_amd.GenoData(a, "S" * 2500))
+    assert [x["ll"] for x in m.log] == r["ll"].tolist()
+    assert np.isneginf(r["ll"][0])
+    assert np.array_equal(res, r["resolutions"])
+
+
+def _digest_patterns(pt):
+    h = hashlib.sha256()
+    for k in ("start", "len", "freq", "prefix", "tp", "succ"):
+        h.update(np.ascontiguousarray(pt[k]).tobytes())
+    return h.hexdigest()
+
+
+def test_cfg2_full_size_against_oracle_digest():
+    """BASELINE configs[1] (1000 x 500) at full size: per-iteration LL,
+    pattern counts, R_E, R_M and SHA-256 of the M0 table and of the accepted
+    resolutions equal the restatement's (tests/golden/cfg2_digest.json)."""
+    d = json.load(open(os.path.join(HERE, "golden", "cfg2_digest.json")))
+    p = synth.config_panel(2)
+    m = gpu_model(p)
+    m.find_patterns()
+    assert _digest_patterns(m.patterns(maxlen=1)) == d["m0_patterns_sha256"]
+    m2 = gpu_model(p, max_iteration=50)
+    res = m2.run()
+    assert m2.iterations == d["iterations"]
+    assert [float(x["ll"]).hex() for x in m2.log] == d["ll_hex"]
+    assert [x["r_e"] for x in m2.log] == d["R_E"]
+    assert m2.m0["r_m"] == d["R_M"][0] and m2.m0["n_patterns"] == d["n_patterns"][0]
+    for k in range(d["iterations"] - 1):
+        assert m2.log[k]["r_m"] == d["R_M"][k + 1]
+        assert m2.log[k]["n_patterns"] == d["n_patterns"][k + 1]
+    assert hashlib.sha256(np.ascontiguousarray(res, np.int32).tobytes()).hexdigest() == d["resolutions_sha256"]
+
+
+def test_cfg2_properties():
+    """Size-independent properties at full size: samples are phasings of the
+    genotypes, weights of each individual sum to 1, priors are sorted, successors
+    are suffixes, frequencies in (0, 1], tp <= 1, and the run is deterministic."""
+    p = synth.config_panel(2)
+    m = gpu_model(p)
+    m.find_patterns()
+    ll, H, _ = m.resolve_all()
+    er = m.estep_results()
+    al, w, tw = m.samples(H)
+    g = p.alleles
+    base = 0
+    for i in range(p.N):
+        n = er["ncand"][i]
+        assert n > 0
+        assert np.all(np.diff(er["prior"][i, :n]) <= 0)
+        assert abs(er["weight"][i, :n].sum() - 1.0) < 1e-12
+        for c in range(n):
+            h0, h1 = al[base + 2 * c], al[base + 2 * c + 1]
+            ok = ((h0 == g[i, 0]) & (h1 == g[i, 1])) | ((h0 == g[i, 1]) & (h1 == g[i, 0]))
+            assert ok.all()
+        base += 2 * n
+    assert base == H and abs(tw - 2 * p.N) < 1e-9  # two haplotypes per individual, weights sum to 1 each
+    P, _ = m.find_patterns()
+    pt = m.patterns()
+    num, sym, _ = m.allele_table()
+    assert np.all(pt["freq"] > 0) and np.all(pt["freq"] <= 1) and np.all(pt["tp"] <= 1)
+    rng = np.random.default_rng(0)
+    for i in rng.choice(P, 2000, replace=False):
+        e = pt["start"][i] + pt["len"][i]
+        if e >= p.L:
+            continue
+        for j in range(num[e]):
+            s = pt["succ"][i, j]
+            if s < 0:
+                continue
+            ext = np.append(pt["alleles"][i, :pt["len"][i]], sym[e, j])
+            assert pt["start"][s] + pt["len"][s] == e + 1
+            assert np.array_equal(pt["alleles"][s, :pt["len"][s]], ext[len(ext) - pt["len"][s]:])
+    m3 = gpu_model(p)
+    m3.find_patterns()
+    assert m3.resolve_all()[0] == ll
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_two_ranks_one_gpu_host_collective(oracle_mod, tmp_path):
+    """The sharded multi-rank path (individual shards, per-level all-reduce of
+    candidate sums, all-reduced LL / total weight) with 2 ranks on one GPU and a
+    gloo host collective.  Sums are reassociated across ranks, so frequencies
+    agree to 1e-12 relative; LL and resolutions are compared to the restatement."""
+    script = os.path.join(HERE, "_two_rank_worker.py")
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
+    procs = [subprocess.Popen([sys.executable, script, str(r), str(tmp_path)], env=dict(env, RANK=str(r)))
+             for r in range(2)]
+    for pr in procs:
+        assert pr.wait(timeout=300) == 0
+    p = panel("a3miss5")
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10, max_iter=10)
+    r = o.run()
+    outs = [np.load(tmp_path / f"rank{k}.npz") for k in range(2)]
+    ll = outs[0]["ll"]
+    assert np.array_equal(ll, outs[1]["ll"])  # every rank sees the same all-reduced LL
+    assert len(ll) == r["iterations"]
+    assert np.allclose(ll, r["ll"], rtol=1e-10, atol=0)
+    res = np.concatenate([outs[0]["res"], outs[1]["res"]])
+    same = np.mean(np.all(res == r["resolutions"], axis=(1, 2)))
+    assert same >= 0.97, same
+    assert np.array_equal(outs[0]["m0_freq"], outs[1]["m0_freq"])
