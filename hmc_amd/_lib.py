@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhmc_amd.so")
+LIB_PATH = os.environ.get("HMC_AMD_LIB") or os.path.join(_HERE, "libhmc_amd.so")
 
 HMC_OK = 0
 ERRORS = {-1: "EARG", -2: "EHIP", -3: "EIO", -4: "EUNSUPPORTED", -5: "ENOPATTERN", -6: "ERCCL", -7: "ENOMEM"}
@@ -55,6 +55,8 @@ _SIGS = [
                               _P(C.c_int32)]),
     ("hmc_resolve_all", _i, [_vp, _P(_d), _P(_i), _P(_u64)]),
     ("hmc_get_estep", _i, [_vp, _P(_d), _P(C.c_int32), _P(C.c_int32), _P(_d), _P(_d), _P(_d)]),
+    ("hmc_get_estep_stats", _i, [_vp, _P(C.c_int32)]),
+    ("hmc_get_stamps", _i, [_vp, _P(C.c_uint64)]),
     ("hmc_get_samples", _i, [_vp, _P(C.c_int32), _P(_d), _P(_d)]),
     ("hmc_get_resolutions", _i, [_vp, _P(C.c_int32)]),
     ("hmc_clear_samples", _i, [_vp]),
@@ -65,6 +67,9 @@ _SIGS = [
     ("hmc_last_timings", _i, [_vp, _P(_d), _P(_d), _P(_d)]),
     ("hmc_test_nth_element", None, [_P(_d), _P(C.c_uint32), _i, _i]),
     ("hmc_test_sort_small", None, [_P(_d), _P(C.c_uint32), _i]),
+    ("hmc_test_nth_element_masks", None, [_P(_d), _P(C.c_uint32), _i, _i]),
+    ("hmc_test_coop_nth_element", _i, [_i, _P(_d), _P(C.c_uint32), _P(C.c_int32), _P(C.c_int32), _P(C.c_int32),
+                                       _i, _i, _i]),
 ]
 
 EXPORTED = [s[0] for s in _SIGS]

@@ -190,6 +190,7 @@ struct Ctx {
   int min_len = 1, max_len = 30, sample_size = 10;
   // tuning
   int fcap = 2048, waves = 0;
+  int lds_waves_per_cu = 2;  // E-step waves sharing one CU's 160 KiB LDS
   uint64_t trace_bytes = 0;
 
   Panel pan;
@@ -236,8 +237,9 @@ struct Ctx {
   DevBuf<uint32_t> d_trace;
   DevBuf<unsigned long long> d_trace_cursor, d_loc_off, d_re;
   DevBuf<double> d_total, d_prior, d_post, d_weight;
-  DevBuf<int32_t> d_ncand, d_status, d_sbase;
+  DevBuf<int32_t> d_ncand, d_status, d_sbase, d_fmax;
   DevBuf<uint32_t> d_cstate, d_cidx, d_maxst;
+  DevBuf<unsigned long long> d_stamps;
   std::vector<double> h_total;
   std::vector<int32_t> h_ncand, h_status, h_sbase;
   std::vector<unsigned long long> h_re;
@@ -615,7 +617,8 @@ struct Ctx {
         (e = d_sbase.ensure(n)) || (e = d_prior.ensure((size_t)n * S_MAX)) || (e = d_post.ensure((size_t)n * S_MAX)) ||
         (e = d_weight.ensure((size_t)n * S_MAX)) || (e = d_cstate.ensure((size_t)n * S_MAX)) ||
         (e = d_cidx.ensure((size_t)n * S_MAX)) || (e = d_rows.ensure((size_t)2 * S * n * L)) ||
-        (e = d_w.ensure((size_t)2 * S * n)) || (e = d_trace_cursor.ensure(1)) || (e = d_maxst.ensure(1)))
+        (e = d_w.ensure((size_t)2 * S * n)) || (e = d_trace_cursor.ensure(1)) || (e = d_maxst.ensure(1)) ||
+        (e = d_fmax.ensure(n)))
       return hipfail(e, "estep alloc");
     // trace store: start from an estimate (96 states of 1+S words per
     // individual-locus), grow up to the budget on overflow, then split batches
@@ -634,6 +637,7 @@ struct Ctx {
     h_sbase.assign(n, 0);
     h_re.assign(n, 0);
     hipMemsetAsync(d_maxst.p, 0, 4, st);
+    if ((e = d_stamps.ensure(20)) || (e = hipMemsetAsync(d_stamps.p, 0, 20 * 8, st))) return hipfail(e, "stamps");
     int Hacc = 0;
     int b = 0, batch = n;
     ms_fwd = ms_tb = 0;
@@ -658,6 +662,7 @@ struct Ctx {
       a.scratch_stride = per;
       a.fcap = fcap;
       a.hcap = hcap;
+      lds_tier(S, a.lds_fc, a.lds_hc);
       a.trace = d_trace.p;
       a.trace_cap = d_trace.n;
       a.trace_cursor = d_trace_cursor.p;
@@ -672,6 +677,8 @@ struct Ctx {
       a.weight = d_weight.p + (size_t)b * S_MAX;
       a.re_count = d_re.p + b;
       a.max_states = d_maxst.p;
+      a.fmax = d_fmax.p + b;
+      a.stamps = d_stamps.p;
       hipEventRecord(ev[0], st);
       if ((e = launch_estep(a, grid, st))) return hipfail(e, "estep_forward launch");
       hipEventRecord(ev[1], st);
@@ -761,6 +768,17 @@ struct Ctx {
     if (H_out) *H_out = H;
     if (re_out) *re_out = re;
     return HMC_OK;
+  }
+
+  // Largest LDS frontier tier that fits lds_waves_per_cu waves per CU.
+  void lds_tier(int S, int &fc, int &hc) const {
+    const int budget = 160 * 1024 / std::max(1, lds_waves_per_cu) - 256;
+    fc = 0;
+    hc = 64;
+    for (int f = 4096; f >= 0; f -= 16) {
+      const int h = next_pow2(std::max(64, 2 * f));
+      if ((int)estep_lds_bytes(S, f, h) <= budget) { fc = f; hc = h; return; }
+    }
   }
 
   static int next_pow2(int x) {
@@ -954,6 +972,7 @@ int hmc_set_params(hmc_ctx *h, double min_freq_abs, double min_freq, int min_len
 
 int hmc_set_tuning(hmc_ctx *h, int frontier_cap, uint64_t trace_bytes, int waves) {
   if (!h) return HMC_EARG;
+  if (waves < 0) { h->c.lds_waves_per_cu = -waves; waves = 0; }  // negative: E-step waves per CU (LDS split)
   if (frontier_cap > 0) h->c.fcap = std::min(frontier_cap, 65535);
   h->c.trace_bytes = trace_bytes;
   h->c.waves = waves;
@@ -1147,6 +1166,24 @@ int hmc_get_estep(hmc_ctx *h, double *total, int32_t *ncand, int32_t *status, do
   return HMC_OK;
 }
 
+int hmc_get_estep_stats(hmc_ctx *h, int32_t *fmax) {
+  if (!h || !h->c.have_estep || !fmax) return HMC_EARG;
+  hipError_t e;
+  if ((e = hipMemcpyAsync(fmax, h->c.d_fmax.p, (size_t)h->c.nloc() * 4, hipMemcpyDeviceToHost, h->c.st)) ||
+      (e = hipStreamSynchronize(h->c.st)))
+    return h->c.hipfail(e, "get_estep_stats");
+  return HMC_OK;
+}
+
+int hmc_get_stamps(hmc_ctx *h, uint64_t *out12) {
+  if (!h || !out12 || !h->c.d_stamps.p) return HMC_EARG;
+  hipError_t e;
+  if ((e = hipMemcpyAsync(out12, h->c.d_stamps.p, 20 * 8, hipMemcpyDeviceToHost, h->c.st)) ||
+      (e = hipStreamSynchronize(h->c.st)))
+    return h->c.hipfail(e, "get_stamps");
+  return HMC_OK;
+}
+
 int hmc_get_samples(hmc_ctx *h, int32_t *alleles, double *weights, double *total_weight) {
   if (!h || !h->c.have_estep) return HMC_EARG;
   Ctx &c = h->c;
@@ -1232,6 +1269,38 @@ int hmc_last_timings(const hmc_ctx *h, double *f, double *t, double *m) {
 void hmc_test_nth_element(double *lik, uint32_t *tag, int n, int nth) {
   hmc::LinkList v{lik, tag, 1};
   hmc::nth_element_greater(v, n, nth);
+}
+
+int hmc_test_coop_nth_element(int device, double *lik, uint32_t *tag, const int32_t *off, const int32_t *n,
+                              const int32_t *nth, int count, int total, int seg_width) {
+  if (hipSetDevice(device) != hipSuccess) return HMC_EHIP;
+  if (seg_width < 2 || seg_width > 32) return HMC_EARG;
+  for (int j = 0; j < count; ++j)
+    if (n[j] < 0 || n[j] > seg_width || nth[j] < 0 || nth[j] > n[j] || off[j] < 0 || off[j] + n[j] > total)
+      return HMC_EARG;
+  hmc::DevBuf<double> dl;
+  hmc::DevBuf<uint32_t> dt;
+  hmc::DevBuf<int32_t> doff, dn, dnth;
+  hipError_t e;
+  if ((e = dl.ensure(total)) || (e = dt.ensure(total)) || (e = doff.ensure(count)) || (e = dn.ensure(count)) ||
+      (e = dnth.ensure(count)))
+    return HMC_EHIP;
+  if ((e = hipMemcpy(dl.p, lik, (size_t)total * 8, hipMemcpyHostToDevice)) ||
+      (e = hipMemcpy(dt.p, tag, (size_t)total * 4, hipMemcpyHostToDevice)) ||
+      (e = hipMemcpy(doff.p, off, (size_t)count * 4, hipMemcpyHostToDevice)) ||
+      (e = hipMemcpy(dn.p, n, (size_t)count * 4, hipMemcpyHostToDevice)) ||
+      (e = hipMemcpy(dnth.p, nth, (size_t)count * 4, hipMemcpyHostToDevice)))
+    return HMC_EHIP;
+  if ((e = hmc::launch_test_coop_nth(dl.p, dt.p, doff.p, dn.p, dnth.p, count, seg_width, nullptr))) return HMC_EHIP;
+  if ((e = hipMemcpy(lik, dl.p, (size_t)total * 8, hipMemcpyDeviceToHost)) ||
+      (e = hipMemcpy(tag, dt.p, (size_t)total * 4, hipMemcpyDeviceToHost)))
+    return HMC_EHIP;
+  return HMC_OK;
+}
+
+void hmc_test_nth_element_masks(double *lik, uint32_t *tag, int n, int nth) {
+  hmc::LinkList v{lik, tag, 1};
+  hmc::nth_element_greater_masks(v, n, nth, n);
 }
 
 void hmc_test_sort_small(double *lik, uint32_t *tag, int n) {

@@ -29,6 +29,7 @@
 // -ffp-contract=off so `fwd += fwd_pred * tp` is not fused into an FMA.
 #include "hmc_internal.hpp"
 #include "select.hpp"
+#include "coop_select.hpp"
 
 namespace hmc {
 
@@ -37,49 +38,115 @@ namespace {
 constexpr unsigned long long KEY_EMPTY = ~0ull;
 constexpr unsigned long long TRACE_CHUNK = 1ull << 16;  // words per bump allocation
 constexpr int NP_MAX = A_MAX * (A_MAX + 1) / 2;          // allele pairs at a fully missing locus
-
-struct Front {
-  double *fwd;
-  uint32_t *lo, *hi, *nl, *slot_of;
-  double *lik;     // [fcap][S]
-  uint32_t *meta;  // [fcap][S]
-};
-
-struct WaveScratch {
-  Front f[2];
-  unsigned long long *hkey;
-  uint32_t *hcnt, *hstate;
-};
+constexpr int PROBE_LDS = 16;                            // LDS probes before a key goes to the HBM table
 
 __host__ __device__ inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// HBM-tier arrays of one frontier (states fc .. fcap-1 of the wave).
+struct FrontG {
+  double *fwd, *lik;
+  uint32_t *lo, *hi, *nl, *slot, *meta;
+};
 
 __host__ __device__ inline size_t front_bytes(int fcap, int S) {
   return al256((size_t)fcap * 8) + 4 * al256((size_t)fcap * 4) + al256((size_t)fcap * S * 8) +
          al256((size_t)fcap * S * 4);
 }
 
-__device__ inline Front carve_front(char *&p, int fcap, int S) {
-  Front f;
+__device__ inline FrontG carve_front(char *&p, int fcap, int S) {
+  FrontG f;
   f.fwd = (double *)p; p += al256((size_t)fcap * 8);
   f.lo = (uint32_t *)p; p += al256((size_t)fcap * 4);
   f.hi = (uint32_t *)p; p += al256((size_t)fcap * 4);
   f.nl = (uint32_t *)p; p += al256((size_t)fcap * 4);
-  f.slot_of = (uint32_t *)p; p += al256((size_t)fcap * 4);
+  f.slot = (uint32_t *)p; p += al256((size_t)fcap * 4);
   f.lik = (double *)p; p += al256((size_t)fcap * S * 8);
   f.meta = (uint32_t *)p; p += al256((size_t)fcap * S * 4);
   return f;
 }
 
-__device__ inline WaveScratch carve(char *base, int fcap, int hcap, int S) {
-  WaveScratch w;
-  char *p = base;
-  w.f[0] = carve_front(p, fcap, S);
-  w.f[1] = carve_front(p, fcap, S);
-  w.hkey = (unsigned long long *)p; p += al256((size_t)hcap * 8);
-  w.hcnt = (uint32_t *)p; p += al256((size_t)hcap * 4);
-  w.hstate = (uint32_t *)p;
-  return w;
+// A frontier (m_haplopairs[i]): states [0, fc) live in LDS, states >= fc in
+// the wave's HBM scratch.  Every accessor branches on the tier so both sides
+// compile to native ds_* / global_* instructions.
+struct Front {
+  int fc, S;
+  int o_fwd, o_lo, o_hi, o_nl, o_slot, o_lik, o_meta;  // LDS byte offsets
+  FrontG g;
+};
+
+struct Lds {
+  unsigned char *base;
+  __device__ double *d(int off) const { return (double *)(base + off); }
+  __device__ uint32_t *u(int off) const { return (uint32_t *)(base + off); }
+};
+
+// Accessors select a flat pointer into the state's tier instead of branching,
+// so lanes whose states sit in different tiers stay converged and a list's S
+// loads issue back to back.
+#define FR_SCALAR(NAME, T, ARR, OFF)                                                  \
+  __device__ inline T *NAME##_ptr(const Lds &l, const Front &F, int t) {              \
+    return t < F.fc ? (T *)(l.base + F.OFF) + t : F.g.ARR + (t - F.fc);               \
+  }                                                                                   \
+  __device__ inline T get_##NAME(const Lds &l, const Front &F, int t) { return *NAME##_ptr(l, F, t); } \
+  __device__ inline void set_##NAME(const Lds &l, const Front &F, int t, T v) { *NAME##_ptr(l, F, t) = v; }
+FR_SCALAR(fwd, double, fwd, o_fwd)
+FR_SCALAR(lo, uint32_t, lo, o_lo)
+FR_SCALAR(hi, uint32_t, hi, o_hi)
+FR_SCALAR(nl, uint32_t, nl, o_nl)
+FR_SCALAR(slot, uint32_t, slot, o_slot)
+#undef FR_SCALAR
+
+__device__ inline double *lik_ptr(const Lds &l, const Front &F, int t) {
+  return t < F.fc ? (double *)(l.base + F.o_lik) + t * F.S : F.g.lik + (size_t)(t - F.fc) * F.S;
 }
+__device__ inline uint32_t *meta_ptr(const Lds &l, const Front &F, int t) {
+  return t < F.fc ? (uint32_t *)(l.base + F.o_meta) + t * F.S : F.g.meta + (size_t)(t - F.fc) * F.S;
+}
+__device__ inline double get_lik(const Lds &l, const Front &F, int t, int k) { return lik_ptr(l, F, t)[k]; }
+__device__ inline uint32_t get_meta(const Lds &l, const Front &F, int t, int k) { return meta_ptr(l, F, t)[k]; }
+__device__ inline void set_link(const Lds &l, const Front &F, int t, int k, double x, uint32_t m) {
+  lik_ptr(l, F, t)[k] = x;
+  meta_ptr(l, F, t)[k] = m;
+}
+
+// One state's k-best list held in registers (static indices only).
+struct RegList {
+  double v[S_MAX];
+  uint32_t m[S_MAX];
+};
+// Load the first S links of a list; slots >= nl hold stale values the callers ignore.
+__device__ inline void load_list(RegList &r, const double *pl, const uint32_t *pm, int S) {
+#pragma unroll
+  for (int k = 0; k < S_MAX; ++k)
+    if (k < S) {
+      r.v[k] = pl[k];
+      r.m[k] = pm[k];
+    }
+}
+// Links of predecessor state s as they enter a successor: the extension
+// constructor / add transformation (HaploPair.cpp:35-61, 63-80).
+__device__ inline void extend_links(RegList &r, int S, uint32_t s, double tpv, bool rev, bool differ) {
+#pragma unroll
+  for (int k = 0; k < S_MAX; ++k)
+    if (k < S) {
+      double lk = r.v[k] * tpv;
+      bool homo = meta_homo(r.m[k]);
+      if (differ && homo) {
+        if (rev) lk = 0.0;
+        homo = false;
+      }
+      r.v[k] = lk;
+      r.m[k] = meta_pack(s, (uint32_t)k, rev, homo, false);
+    }
+}
+
+// Key table replacing m_best_pair: slot ids < hc are LDS slots, >= hc HBM slots.
+struct Keys {
+  int hc, o_key, o_cnt, o_state, o_lanes;  // LDS tier
+  unsigned long long *gkey, *glanes;        // HBM tier
+  uint32_t *gcnt, *gstate;
+  uint32_t gmask;
+};
 
 __device__ inline uint32_t key_hash(uint32_t lo, uint32_t hi) {
   uint32_t h = lo * 0x9E3779B1u ^ (hi + 0x7F4A7C15u) * 0x85EBCA77u;
@@ -87,6 +154,62 @@ __device__ inline uint32_t key_hash(uint32_t lo, uint32_t hi) {
   h *= 0x2C1B3C6Du;
   h ^= h >> 13;
   return h;
+}
+
+// Insert-or-find: a key lands in the first free or matching slot of its LDS
+// probe sequence (at most PROBE_LDS slots), else in the HBM table.  Slots never
+// empty during a locus, so every lane holding the same key ends in one slot.
+__device__ inline uint32_t key_slot(const Lds &l, const Keys &K, unsigned long long key, uint32_t h0) {
+  unsigned long long *lk = (unsigned long long *)(l.base + K.o_key);
+  uint32_t h = h0 & (uint32_t)(K.hc - 1);
+  for (int p = 0; p < PROBE_LDS; ++p) {
+    const unsigned long long prev = atomicCAS(&lk[h], KEY_EMPTY, key);
+    if (prev == KEY_EMPTY || prev == key) return h;
+    h = (h + 1) & (uint32_t)(K.hc - 1);
+  }
+  uint32_t g = (h0 * 0x9E3779B1u) & K.gmask;
+  while (true) {
+    const unsigned long long prev = atomicCAS(&K.gkey[g], KEY_EMPTY, key);
+    if (prev == KEY_EMPTY || prev == key) return (uint32_t)K.hc + g;
+    g = (g + 1) & K.gmask;
+  }
+}
+__device__ inline uint32_t slot_cnt(const Lds &l, const Keys &K, uint32_t s) {
+  return s < (uint32_t)K.hc ? ((uint32_t *)(l.base + K.o_cnt))[s] : K.gcnt[s - K.hc];
+}
+__device__ inline void set_slot_cnt(const Lds &l, const Keys &K, uint32_t s, uint32_t v) {
+  if (s < (uint32_t)K.hc) ((uint32_t *)(l.base + K.o_cnt))[s] = v;
+  else K.gcnt[s - K.hc] = v;
+}
+__device__ inline uint32_t slot_state(const Lds &l, const Keys &K, uint32_t s) {
+  return s < (uint32_t)K.hc ? ((uint32_t *)(l.base + K.o_state))[s] : K.gstate[s - K.hc];
+}
+__device__ inline void set_slot_state(const Lds &l, const Keys &K, uint32_t s, uint32_t v) {
+  if (s < (uint32_t)K.hc) ((uint32_t *)(l.base + K.o_state))[s] = v;
+  else K.gstate[s - K.hc] = v;
+}
+// Lanes of the current chunk holding each key, as a 64-bit mask (OR is
+// order-free, so the grouping needs no serial ballot loop).
+__device__ inline void slot_or_lanes(const Lds &l, const Keys &K, uint32_t s, unsigned long long bit) {
+  if (s < (uint32_t)K.hc) atomicOr(&((unsigned long long *)(l.base + K.o_lanes))[s], bit);
+  else atomicOr(&K.glanes[s - K.hc], bit);
+}
+__device__ inline unsigned long long slot_lanes(const Lds &l, const Keys &K, uint32_t s) {
+  return s < (uint32_t)K.hc ? ((unsigned long long *)(l.base + K.o_lanes))[s]
+                            : __hip_atomic_load(&K.glanes[s - K.hc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void clear_slot_lanes(const Lds &l, const Keys &K, uint32_t s) {
+  if (s < (uint32_t)K.hc) ((unsigned long long *)(l.base + K.o_lanes))[s] = 0ull;
+  else atomicExch(&K.glanes[s - K.hc], 0ull);
+}
+__device__ inline void clear_slot(const Lds &l, const Keys &K, uint32_t s) {
+  if (s < (uint32_t)K.hc) {
+    ((unsigned long long *)(l.base + K.o_key))[s] = KEY_EMPTY;
+    ((uint32_t *)(l.base + K.o_cnt))[s] = 0;
+  } else {
+    K.gkey[s - K.hc] = KEY_EMPTY;
+    K.gcnt[s - K.hc] = 0;
+  }
 }
 
 __device__ inline uint64_t lanemask_lt() { return (1ull << threadIdx.x) - 1ull; }
@@ -107,48 +230,184 @@ __device__ inline unsigned long long trace_alloc(const EstepArgs &a, unsigned lo
   return off;
 }
 
-// Stream the finished k-best lists of one locus into the trace store.
-__device__ inline bool write_trace(const EstepArgs &a, const Front &F, int Fn, int locus, int bi,
+// Stream the finished k-best lists of one locus into the trace store:
+// [Fn][Fn headers][Fn x S link words].
+__device__ inline bool write_trace(const EstepArgs &a, const Lds &l, const Front &F, int Fn, int locus, int bi,
                                    unsigned long long &cur, unsigned long long &end) {
-  const int S = a.S, rec = 1 + S;
-  unsigned long long words = (unsigned long long)Fn * rec;
-  unsigned long long off = trace_alloc(a, cur, end, words);
+  const int S = a.S;
+  const unsigned long long words = 1ull + (unsigned long long)Fn * (1 + S);
+  const unsigned long long off = trace_alloc(a, cur, end, words);
   if (off + words > a.trace_cap) return false;
-  for (unsigned long long w = threadIdx.x; w < words; w += WAVE) {
-    uint32_t t = (uint32_t)(w / rec), k = (uint32_t)(w % rec);
-    uint32_t v;
-    if (k == 0) v = hdr_pack(a.mod.last[F.lo[t]], a.mod.last[F.hi[t]], F.nl[t]);
-    else v = (k - 1 < F.nl[t]) ? F.meta[(size_t)t * S + k - 1] : 0u;
-    a.trace[off + w] = v;
+  uint32_t *hdr = a.trace + off + 1;
+  uint32_t *lnk = hdr + Fn;
+  for (int t = threadIdx.x; t < Fn; t += WAVE)
+    hdr[t] = hdr_pack(a.mod.last[get_lo(l, F, t)], a.mod.last[get_hi(l, F, t)], get_nl(l, F, t));
+  const int nw = Fn * S;
+  constexpr int U = 4;
+  for (int w0 = 0; w0 < nw; w0 += U * WAVE) {
+    uint32_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int w = w0 + u * WAVE + (int)threadIdx.x;
+      const int t = w < nw ? w / S : 0, k = w - t * S;
+      const uint32_t n = get_nl(l, F, t), m = get_meta(l, F, t, w < nw ? k : 0);
+      v[u] = (uint32_t)k < n ? m : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int w = w0 + u * WAVE + (int)threadIdx.x;
+      if (w < nw) lnk[w] = v[u];
+    }
   }
-  if (threadIdx.x == 0) a.loc_off[(size_t)bi * (a.pan.L + 1) + locus] = off;
+  if (threadIdx.x == 0) {
+    a.trace[off] = (uint32_t)Fn;
+    a.loc_off[(size_t)bi * (a.pan.L + 1) + locus] = off;
+  }
   return true;
 }
 
 }  // namespace
 
 size_t estep_scratch_bytes(int fcap, int hcap, int S) {
-  return al256(2 * front_bytes(fcap, S) + al256((size_t)hcap * 8) + al256((size_t)hcap * 4) +
+  return al256(2 * front_bytes(fcap, S) + 2 * al256((size_t)hcap * 8) + al256((size_t)hcap * 4) +
                al256((size_t)hcap * 4));
 }
 
+// One add handed to a selection segment.
+struct AddPar {
+  double tpv;
+  uint32_t st, s;
+  uint32_t k0ns;   // k0 | ns << 8 | rev << 16 | differ << 17
+  uint32_t pad;
+};
+
+// LDS carve of one wave: [selection scratch] [add parameters] [allele pairs] [key
+// table hc x (key, cnt, state)] [frontier A] [frontier B], each frontier fc x
+// (fwd, lo, hi, nl, slot, lik[S], meta[S]).
+struct LdsPlan {
+  int o_lpos, o_rpos, o_slik, o_smeta, o_par, o_pairs, o_key, o_cnt, o_state, o_lanes, o_front[2][7], bytes;
+};
+
+__host__ __device__ inline LdsPlan lds_plan(int S, int fc, int hc) {
+  LdsPlan p;
+  int o = 0;
+  auto take = [&](int bytes) { int r = o; o += (bytes + 15) & ~15; return r; };
+  p.o_lpos = take(WAVE * 4);
+  p.o_rpos = take(WAVE * 4);
+  p.o_slik = take(WAVE * 8);
+  p.o_smeta = take(WAVE * 4);
+  p.o_par = take(WAVE / 2 * (int)sizeof(AddPar));
+  p.o_pairs = take((NP_MAX + 2) * 4 + 3 * NP_MAX);
+  p.o_key = take(hc * 8);
+  p.o_cnt = take(hc * 4);
+  p.o_state = take(hc * 4);
+  p.o_lanes = take(hc * 8);
+  for (int f = 0; f < 2; ++f) {
+    p.o_front[f][0] = take(fc * 8);       // fwd
+    p.o_front[f][1] = take(fc * 4);       // lo
+    p.o_front[f][2] = take(fc * 4);       // hi
+    p.o_front[f][3] = take(fc * 4);       // nl
+    p.o_front[f][4] = take(fc * 4);       // slot
+    p.o_front[f][5] = take(fc * S * 8);   // lik
+    p.o_front[f][6] = take(fc * S * 4);   // meta
+  }
+  p.bytes = o;
+  return p;
+}
+
+size_t estep_lds_bytes(int S, int fc, int hc) { return (size_t)lds_plan(S, fc, hc).bytes; }
+
+// Diagnostic build only (-DHMC_STAMPS): per-phase shader-clock shares.  Each
+// stamp drains the wave's memory counters so a phase is charged with the
+// latency of the loads it issued.  The product build compiles these out.
+#ifdef HMC_STAMPS
+#define STAMP_DECL unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_acc[20] = {};
+#define STAMP(k)                                              \
+  do {                                                        \
+    __builtin_amdgcn_s_waitcnt(0);                            \
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += t1 - st_t0;                                  \
+    st_t0 = t1;                                               \
+  } while (0)
+// Per-lane shares inside divergent code (summed over lanes): 14, 15, 17-19.
+#define DIAG_T0 \
+  __builtin_amdgcn_s_waitcnt(0);                     \
+  unsigned long long dg0 = __builtin_amdgcn_s_memtime();
+#define DIAG(k)                                               \
+  do {                                                        \
+    __builtin_amdgcn_s_waitcnt(0);                            \
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += t1 - dg0;                                    \
+    dg0 = t1;                                                 \
+  } while (0)
+#define STAMP_FLUSH                                                                       \
+  if (a.stamps)                                                                           \
+    for (int k = 0; k < 20; ++k) {                                                        \
+      const bool per_lane = k == 14 || k == 15 || k >= 17;                                \
+      if (per_lane || threadIdx.x == 0) atomicAdd(&a.stamps[k], st_acc[k]);               \
+    }
+#else
+#define DIAG_T0
+#define DIAG(k) do { } while (0)
+#define STAMP_DECL
+#define STAMP(k) do { } while (0)
+#define STAMP_FLUSH
+#endif
+
 __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
+  STAMP_DECL
   const int S = a.S, L = a.pan.L, amax = a.pan.amax;
   const int lane = threadIdx.x;
-  double *wl = (double *)smem;                               // [2S][64]
-  uint32_t *wm = (uint32_t *)(smem + (size_t)2 * S * WAVE * 8);  // [2S][64]
-  int *pr_off = (int *)(smem + (size_t)2 * S * WAVE * 12);   // [NP_MAX+2]; [NP_MAX+1] = npairs
+  const LdsPlan plan = lds_plan(S, a.lds_fc, a.lds_hc);
+  const Lds l{smem};
+  int *pr_off = (int *)(smem + plan.o_pairs);  // [NP_MAX+2]; [NP_MAX+1] = npairs
   uint8_t *pr_x = (uint8_t *)(pr_off + NP_MAX + 2);
   uint8_t *pr_y = pr_x + NP_MAX;
   uint8_t *pr_o = pr_y + NP_MAX;
-  const LinkList W{wl + lane, wm + lane, WAVE};
+  const SegScratch ss{(int *)(smem + plan.o_lpos), (int *)(smem + plan.o_rpos), (double *)(smem + plan.o_slik),
+                      (uint32_t *)(smem + plan.o_smeta)};
+  AddPar *par = (AddPar *)(smem + plan.o_par);
+  const Seg sg = make_seg(2 * S);
+  const int G = WAVE / (2 * S);
+  const LinkList W{ss.slik, ss.smeta, 1};  // final selection (lane 0)
 
-  WaveScratch ws = carve(a.scratch + (size_t)blockIdx.x * a.scratch_stride, a.fcap, a.hcap, S);
-  const uint32_t hmask = (uint32_t)a.hcap - 1u;
+  char *sp = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
+  Front FA, FB;
+  FA.g = carve_front(sp, a.fcap, S);
+  FB.g = carve_front(sp, a.fcap, S);
+  Keys K;
+  K.gkey = (unsigned long long *)sp; sp += al256((size_t)a.hcap * 8);
+  K.glanes = (unsigned long long *)sp; sp += al256((size_t)a.hcap * 8);
+  K.gcnt = (uint32_t *)sp; sp += al256((size_t)a.hcap * 4);
+  K.gstate = (uint32_t *)sp;
+  K.gmask = (uint32_t)a.hcap - 1u;
+  K.hc = a.lds_hc;
+  K.o_key = plan.o_key;
+  K.o_cnt = plan.o_cnt;
+  K.o_state = plan.o_state;
+  K.o_lanes = plan.o_lanes;
+  Front *FF[2] = {&FA, &FB};
+  for (int f = 0; f < 2; ++f) {
+    FF[f]->fc = a.lds_fc;
+    FF[f]->S = S;
+    FF[f]->o_fwd = plan.o_front[f][0];
+    FF[f]->o_lo = plan.o_front[f][1];
+    FF[f]->o_hi = plan.o_front[f][2];
+    FF[f]->o_nl = plan.o_front[f][3];
+    FF[f]->o_slot = plan.o_front[f][4];
+    FF[f]->o_lik = plan.o_front[f][5];
+    FF[f]->o_meta = plan.o_front[f][6];
+  }
   for (int h = lane; h < a.hcap; h += WAVE) {
-    ws.hkey[h] = KEY_EMPTY;
-    ws.hcnt[h] = 0;
+    K.gkey[h] = KEY_EMPTY;
+    K.gcnt[h] = 0;
+    K.glanes[h] = 0ull;
+  }
+  for (int h = lane; h < K.hc; h += WAVE) {
+    ((unsigned long long *)(smem + K.o_key))[h] = KEY_EMPTY;
+    ((uint32_t *)(smem + K.o_cnt))[h] = 0;
+    ((unsigned long long *)(smem + K.o_lanes))[h] = 0ull;
   }
   unsigned long long tcur = 0, tend = 0;
   __syncthreads();
@@ -159,7 +418,8 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
     const int hl = a.mod.head_len;
     int status = EST_OK;
     unsigned long long re = 0;
-    Front X = ws.f[0], Y = ws.f[1];
+    int fbig = 0;
+    Front X = FA, Y = FB;
 
     // ---- initHeadList (HaploBuilder.cpp:153-224), head_len == 1 ---------
     int Fp = 0;
@@ -179,7 +439,7 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
         } else if (!m0 && !m1 && g0.x != g0.y) {
           xs[nx++] = (ah == g0.x) ? g0.y : g0.x;
         } else {
-          xs[nx++] = g0.x;  // may be missing: resolved below like findLongestMatchPattern
+          xs[nx++] = g0.x;  // may be missing: resolved like findLongestMatchPattern
         }
         for (int k = 0; k < nx; ++k) {
           uint32_t q = xs[k] == MISSING ? a.mod.head_pat0[amax] : a.mod.head_pat0[xs[k]];
@@ -188,12 +448,11 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
           if (Fp >= a.fcap) { status = EST_OVERFLOW_FRONTIER; break; }
           const double tpv = a.mod.freq[head] * a.mod.freq[q];  // HaploPair.cpp:27-32
           const bool homo = (q == head);
-          X.fwd[Fp] = homo ? tpv : tpv * 2.0;
-          X.lo[Fp] = head;
-          X.hi[Fp] = q;
-          X.nl[Fp] = 1;
-          X.lik[(size_t)Fp * S] = tpv;
-          X.meta[(size_t)Fp * S] = meta_pack(0, 0, false, homo, true);
+          set_fwd(l, X, Fp, homo ? tpv : tpv * 2.0);
+          set_lo(l, X, Fp, head);
+          set_hi(l, X, Fp, q);
+          set_nl(l, X, Fp, 1);
+          set_link(l, X, Fp, 0, tpv, meta_pack(0, 0, false, homo, true));
           ++Fp;
         }
         if (status != EST_OK) break;
@@ -203,13 +462,14 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
     status = __shfl(status, 0);
     __syncthreads();
     if (status == EST_OK) {
-      if (!write_trace(a, X, Fp, hl, bi, tcur, tend)) status = EST_OVERFLOW_TRACE;
-      for (int t = lane; t < Fp; t += WAVE) re += X.nl[t];
+      if (!write_trace(a, l, X, Fp, hl, bi, tcur, tend)) status = EST_OVERFLOW_TRACE;
+      for (int t = lane; t < Fp; t += WAVE) re += get_nl(l, X, t);
     }
 
     // ---- forward over loci (HaploBuilder.cpp:47-82) -----------------------
     for (int i = hl; i < L && status == EST_OK; ++i) {
       if (Fp == 0) { status = EST_UNRESOLVED; break; }
+      STAMP(0);
       const uchar2 gg = g[i];
       if (lane == 0) {  // allele-pair list in extendAll call order
         const double *af = a.pan.afreq + (size_t)i * amax;
@@ -245,7 +505,8 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
         bool valid = c < C;
         uint32_t s = 0, lo = 0, hi = 0, slot = 0;
         bool rev = false;
-        double fwd_s = 0.0;
+        double fwd_s = 0.0, tpv = 0.0;
+        bool differ = false;
         if (valid) {
           int p = 0;
           while (p + 1 < npairs && c >= pr_off[p + 1]) ++p;
@@ -254,151 +515,221 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
           s = pr_o[p] == 2 ? (uint32_t)(local >> 1) : (uint32_t)local;
           const uint32_t x = o ? pr_y[p] : pr_x[p];
           const uint32_t y = o ? pr_x[p] : pr_y[p];
-          fwd_s = X.fwd[s];
+          fwd_s = get_fwd(l, X, s);
           valid = fwd_s > 0.0;  // extend(): forward_likelihood() <= 0 -> skip
+          STAMP(1);
           if (valid) {
-            const uint32_t sa = a.mod.succ[(size_t)X.lo[s] * amax + x];
-            const uint32_t sb = a.mod.succ[(size_t)X.hi[s] * amax + y];
+            const uint32_t sa = a.mod.succ[(size_t)get_lo(l, X, s) * amax + x];
+            const uint32_t sb = a.mod.succ[(size_t)get_hi(l, X, s) * amax + y];
+            STAMP(2);
             valid = sa != NONE && sb != NONE;
             rev = sa > sb;  // addHaploPair: id_a > id_b -> swap, reversed
             lo = rev ? sb : sa;
             hi = rev ? sa : sb;
+            if (valid) {  // issue the pattern gathers early; consumed after the key work
+              tpv = a.mod.tp[lo] * a.mod.tp[hi];
+              differ = a.mod.last[lo] != a.mod.last[hi];
+            }
           }
         }
-        if (valid) {
-          const unsigned long long key = ((unsigned long long)lo << 32) | hi;
-          uint32_t h = key_hash(lo, hi) & hmask;
-          while (true) {
-            unsigned long long prev = atomicCAS(&ws.hkey[h], KEY_EMPTY, key);
-            if (prev == KEY_EMPTY || prev == key) break;
-            h = (h + 1) & hmask;
-          }
-          slot = h;
-        }
-        // group lanes by key, in lane (= reference) order
-        int li = 0, gsz = 0;
-        uint64_t rem = __ballot(valid);
-        while (rem) {
-          const int leader = __ffsll((long long)rem) - 1;
-          const uint32_t lslot = (uint32_t)__builtin_amdgcn_readlane((int)slot, leader);
-          const bool mine = valid && slot == lslot;
-          const uint64_t grp = __ballot(mine);
-          if (mine) {
-            li = __popcll(grp & lanemask_lt());
-            gsz = __popcll(grp);
-          }
-          rem &= ~grp;
-        }
-        const uint32_t cnt0 = valid ? ws.hcnt[slot] : 0u;
+        STAMP(3);
+        if (valid) slot = key_slot(l, K, ((unsigned long long)lo << 32) | hi, key_hash(lo, hi));
+        STAMP(4);
+        // group lanes by key: rank of each lane among the chunk's lanes with its key
+        if (valid) slot_or_lanes(l, K, slot, 1ull << lane);
+        __syncthreads();
+        const uint64_t gm = valid ? slot_lanes(l, K, slot) : 0ull;
+        const int li = __popcll(gm & lanemask_lt());
+        const int gsz = __popcll(gm);
+        __syncthreads();
+        if (valid && li == 0) clear_slot_lanes(l, K, slot);
+        STAMP(5);
+        const uint32_t cnt0 = valid ? slot_cnt(l, K, slot) : 0u;
         const bool is_new = valid && cnt0 == 0 && li == 0;
         const uint64_t nm = __ballot(is_new);
         if (Fn + __popcll(nm) > a.fcap) { status = EST_OVERFLOW_FRONTIER; break; }
         uint32_t st = 0;
         if (is_new) {
           st = (uint32_t)(Fn + __popcll(nm & lanemask_lt()));
-          ws.hstate[slot] = st;
-          Y.slot_of[st] = slot;
+          set_slot_state(l, K, slot, st);
+          set_slot(l, Y, (int)st, slot);
         }
         Fn += __popcll(nm);
-        if (valid && li == 0) ws.hcnt[slot] = cnt0 + (uint32_t)gsz;
+        if (valid && li == 0) set_slot_cnt(l, K, slot, cnt0 + (uint32_t)gsz);
         __syncthreads();
-        if (valid && !is_new) st = ws.hstate[slot];
+        if (valid && !is_new) st = slot_state(l, K, slot);
         const uint32_t rank = cnt0 + (uint32_t)li;
+        STAMP(6);
 
-        for (int r = 0; __ballot(valid && li == r) != 0; ++r) {
-          if (valid && li == r) {
-            const double tpv = a.mod.tp[lo] * a.mod.tp[hi];
-            const bool differ = a.mod.last[lo] != a.mod.last[hi];
-            const uint32_t ns = X.nl[s];
-            const double *pl = X.lik + (size_t)s * S;
-            const uint32_t *pm = X.meta + (size_t)s * S;
-            double *yl = Y.lik + (size_t)st * S;
-            uint32_t *ym = Y.meta + (size_t)st * S;
-            if (rank == 0) {  // extension constructor, HaploPair.cpp:35-61
-              Y.fwd[st] = fwd_s * tpv;
-              Y.lo[st] = lo;
-              Y.hi[st] = hi;
-              Y.nl[st] = ns;
-              for (uint32_t k = 0; k < ns; ++k) {
-                double lk = pl[k] * tpv;
-                bool homo = meta_homo(pm[k]);
-                if (differ && homo) {
-                  if (rev) lk = 0.0;
-                  homo = false;
-                }
-                yl[k] = lk;
-                ym[k] = meta_pack(s, k, rev, homo, false);
-              }
-            } else {  // HaploPair::add, HaploPair.cpp:63-89
-              const double inc = fwd_s * tpv;
-              Y.fwd[st] = Y.fwd[st] + inc;
-              const int k0 = (int)Y.nl[st];
-              for (int k = 0; k < k0; ++k) W.set(k, yl[k], ym[k]);
-              for (uint32_t k = 0; k < ns; ++k) {
-                double lk = pl[k] * tpv;
-                bool homo = meta_homo(pm[k]);
-                if (differ && homo) {
-                  if (rev) lk = 0.0;
-                  homo = false;
-                }
-                W.set(k0 + (int)k, lk, meta_pack(s, k, rev, homo, false));
-              }
-              int n = k0 + (int)ns;
-              if (n > S) {
-                nth_element_greater(W, n, S - 1);
-                n = S;
-              }
-              for (int k = 0; k < n; ++k) {
-                yl[k] = W.l(k);
-                ym[k] = W.m(k);
-              }
-              Y.nl[st] = (uint32_t)n;
+        // first contribution of a key: extension constructor (HaploPair.cpp:35-61), lane-parallel
+        if (valid && rank == 0) {
+          const uint32_t ns = get_nl(l, X, s);
+          RegList r;
+          load_list(r, lik_ptr(l, X, s), meta_ptr(l, X, s), S);
+          extend_links(r, S, s, tpv, rev, differ);
+          set_fwd(l, Y, st, fwd_s * tpv);
+          set_lo(l, Y, st, lo);
+          set_hi(l, Y, st, hi);
+          set_nl(l, Y, st, ns);
+          double *yl = lik_ptr(l, Y, st);
+          uint32_t *ym = meta_ptr(l, Y, st);
+#pragma unroll
+          for (int k = 0; k < S_MAX; ++k)
+            if (k < S && (uint32_t)k < ns) {
+              yl[k] = r.v[k];
+              ym[k] = r.m[k];
             }
-          }
-          __syncthreads();
         }
+        __syncthreads();
+        // later contributions: HaploPair::add (HaploPair.cpp:63-89).  Round r
+        // applies every lane whose key rank inside the chunk is r, so distinct
+        // keys merge in parallel and each key sees its adds in reference order.
+        // The lane appends into its private LDS column and keeps the S best
+        // with the mask-partition nth_element (select.hpp).
+        int rounds = (valid && rank != 0) ? li + 1 : 0;
+        for (int o = 32; o > 0; o >>= 1) { const int t = __shfl_xor(rounds, o); rounds = t > rounds ? t : rounds; }
+#ifdef HMC_STAMPS
+        st_acc[10] += __popcll(__ballot(valid && rank != 0));
+        st_acc[11] += rounds;
+#endif
+        for (int r = 0; r < rounds; ++r) {
+          STAMP(7);
+          STAMP(12);
+          bool sel = false;
+          uint32_t k0 = 0, ns = 0;
+          if (valid && rank != 0 && li == r) {
+            DIAG_T0
+            k0 = get_nl(l, Y, st);
+            ns = get_nl(l, X, s);
+            set_fwd(l, Y, st, get_fwd(l, Y, st) + fwd_s * tpv);
+            if (k0 + ns <= (uint32_t)S) {  // room left: append, no selection
+              RegList x;
+              load_list(x, lik_ptr(l, X, s), meta_ptr(l, X, s), S);
+              extend_links(x, S, s, tpv, rev, differ);
+              double *yl = lik_ptr(l, Y, st);
+              uint32_t *ym = meta_ptr(l, Y, st);
+#pragma unroll
+              for (int q = 0; q < S_MAX; ++q)
+                if (q < S && (uint32_t)q < ns) {
+                  yl[k0 + q] = x.v[q];
+                  ym[k0 + q] = x.m[q];
+                }
+              set_nl(l, Y, st, k0 + ns);
+            } else {
+              sel = true;
+            }
+            DIAG(14);
+#ifdef HMC_STAMPS
+            st_acc[17] += st < (uint32_t)a.lds_fc ? 1 : 0;
+            st_acc[18] += s < (uint32_t)a.lds_fc ? 1 : 0;
+#endif
+          }
+          // adds that overflow S: G at a time, one per selection segment
+          uint64_t selm = __ballot(sel);
+          while (selm) {
+            uint64_t take = 0;
+            for (int q = 0; q < G && selm; ++q) {
+              const uint64_t bit = selm & (~selm + 1ull);
+              take |= bit;
+              selm ^= bit;
+            }
+            if (sel && ((take >> lane) & 1ull)) {
+              AddPar &P = par[__popcll(take & lanemask_lt())];
+              P.tpv = tpv;
+              P.st = st;
+              P.s = s;
+              P.k0ns = k0 | ns << 8 | (rev ? 1u << 16 : 0u) | (differ ? 1u << 17 : 0u);
+            }
+            wave_lds_sync();
+            const int nseg = __popcll(take);
+            int n = 0;
+            double v = 0.0;
+            uint32_t m = 0, pst = 0;
+            if (sg.g < nseg) {
+              const AddPar P = par[sg.g];
+              const int pk0 = (int)(P.k0ns & 0xFF), pns = (int)((P.k0ns >> 8) & 0xFF);
+              pst = P.st;
+              n = pk0 + pns;
+              if (sg.k < n) {
+                const bool fromY = sg.k < pk0;
+                const int q = fromY ? sg.k : sg.k - pk0;
+                const double *pl = fromY ? lik_ptr(l, Y, (int)P.st) : lik_ptr(l, X, (int)P.s);
+                const uint32_t *pm = fromY ? meta_ptr(l, Y, (int)P.st) : meta_ptr(l, X, (int)P.s);
+                v = pl[q];
+                m = pm[q];
+                if (!fromY) {  // HaploPair::add transformation (HaploPair.cpp:63-80)
+                  bool homo = meta_homo(m);
+                  const bool prev = (P.k0ns >> 16) & 1u, pdiff = (P.k0ns >> 17) & 1u;
+                  v = v * P.tpv;
+                  if (pdiff && homo) {
+                    if (prev) v = 0.0;
+                    homo = false;
+                  }
+                  m = meta_pack(P.s, (uint32_t)q, prev, homo, false);
+                }
+              }
+            }
+            seg_nth_element(v, m, n, S - 1, sg, ss);
+            if (sg.g < nseg && sg.k < S) {
+              set_link(l, Y, (int)pst, sg.k, v, m);
+              if (sg.k == 0) set_nl(l, Y, (int)pst, (uint32_t)S);
+            }
+            wave_lds_sync();  // par[] is rewritten by the next batch
+          }
+          STAMP(13);
+          __syncthreads();
+          STAMP(16);
+        }
+        STAMP(7);
       }
       if (status != EST_OK) break;
       if (Fn == 0) { status = EST_UNRESOLVED; break; }
-      if (!write_trace(a, Y, Fn, i + 1, bi, tcur, tend)) { status = EST_OVERFLOW_TRACE; break; }
+      if (!write_trace(a, l, Y, Fn, i + 1, bi, tcur, tend)) { status = EST_OVERFLOW_TRACE; break; }
       for (int t = lane; t < Fn; t += WAVE) {
-        re += Y.nl[t];
-        const uint32_t sl = Y.slot_of[t];
-        ws.hkey[sl] = KEY_EMPTY;
-        ws.hcnt[sl] = 0;
+        re += get_nl(l, Y, t);
+        clear_slot(l, K, get_slot(l, Y, t));
       }
       if (lane == 0 && a.max_states) atomicMax(a.max_states, (unsigned)Fn);
+      fbig = Fn > fbig ? Fn : fbig;
       __syncthreads();
       Front T = X; X = Y; Y = T;
       Fp = Fn;
+      STAMP(8);
     }
     if (status == EST_OK && Fp == 0) status = EST_UNRESOLVED;
 
     // ---- final selection (HaploBuilder.cpp:87-116) ------------------------
-    if (status < 0) {  // aborted mid-locus: keys may be left in the table
+    if (status < 0) {  // aborted mid-locus: keys may be left in the tables
       for (int h = lane; h < a.hcap; h += WAVE) {
-        ws.hkey[h] = KEY_EMPTY;
-        ws.hcnt[h] = 0;
+        K.gkey[h] = KEY_EMPTY;
+        K.gcnt[h] = 0;
+        K.glanes[h] = 0ull;
+      }
+      for (int h = lane; h < K.hc; h += WAVE) {
+        ((unsigned long long *)(smem + K.o_key))[h] = KEY_EMPTY;
+        ((uint32_t *)(smem + K.o_cnt))[h] = 0;
+        ((unsigned long long *)(smem + K.o_lanes))[h] = 0ull;
       }
     }
     for (int o = 32; o > 0; o >>= 1) re += __shfl_xor(re, o);
     if (lane == 0) {
       a.re_count[bi] = re;
       a.status[bi] = status;
+      if (a.fmax) a.fmax[bi] = fbig > Fp ? fbig : Fp;
       int cnt = 0;
       double total = 0.0;
       if (status == EST_OK) {
         for (int t = 0; t < Fp; ++t) {
-          total += X.fwd[t];
-          const uint32_t n = X.nl[t];
+          total += get_fwd(l, X, t);
+          const uint32_t n = get_nl(l, X, t);
           for (uint32_t k = 0; k < n; ++k) {
-            double lk = X.lik[(size_t)t * S + k];
-            const bool homo = meta_homo(X.meta[(size_t)t * S + k]);
+            double lk = get_lik(l, X, t, k);
+            const bool homo = meta_homo(get_meta(l, X, t, k));
             if (!homo) lk *= 2.0;
             W.set(cnt++, lk, meta_pack((uint32_t)t, k, false, homo, false));
           }
           if (cnt > S) {
-            nth_element_greater(W, cnt, S - 1);
+            nth_element_greater_masks(W, cnt, S - 1, cnt);
             cnt = S;
           }
         }
@@ -407,7 +738,7 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
         for (int c = 0; c < cnt; ++c) {
           const uint32_t m = W.m(c);
           const uint32_t t = meta_pred(m), k = meta_idx(m);
-          const double own = X.lik[(size_t)t * S + k];
+          const double own = get_lik(l, X, (int)t, (int)k);
           const double prior = meta_homo(m) ? own : own * 2.0;  // HaploPair.cpp:97-102
           const double post = prior / total;
           coverage += post;
@@ -423,7 +754,9 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
       a.ncand[bi] = cnt;
     }
     __syncthreads();
+    STAMP(9);
   }
+  STAMP_FLUSH
 }
 
 // Traceback (HaploPair::getGenotype, HaploPair.cpp:91-124): 16 lanes per
@@ -433,7 +766,7 @@ __global__ __launch_bounds__(256) void estep_traceback(TracebackArgs a) {
   const int bi = blockIdx.x * 16 + threadIdx.x / 16;
   const int c = threadIdx.x % 16;
   if (bi >= a.nbatch || c >= a.ncand[bi]) return;
-  const int L = a.L, S = a.S, rec = 1 + S;
+  const int L = a.L, S = a.S;
   const size_t h0 = (size_t)a.sample_base[bi] + 2 * c;
   uint8_t *row[2] = {a.rows + h0 * L, a.rows + (h0 + 1) * L};
   const unsigned long long *lo = a.loc_off + (size_t)bi * (L + 1);
@@ -441,16 +774,17 @@ __global__ __launch_bounds__(256) void estep_traceback(TracebackArgs a) {
   uint32_t idx = a.cand_idx[(size_t)bi * S_MAX + c];
   int ra = 0, rb = 1;
   for (int j = L; j > a.head_len; --j) {
-    const uint32_t *r = a.trace + lo[j] + (size_t)st * rec;
-    const uint32_t hdr = r[0];
-    const uint32_t m = r[1 + idx];
+    const uint32_t *r = a.trace + lo[j];
+    const uint32_t F = r[0];
+    const uint32_t hdr = r[1 + st];
+    const uint32_t m = r[1 + F + (size_t)st * S + idx];
     row[ra][j - 1] = (uint8_t)(hdr & 0xFF);
     row[rb][j - 1] = (uint8_t)((hdr >> 8) & 0xFF);
     if (meta_rev(m)) { int t = ra; ra = rb; rb = t; }
     st = meta_pred(m);
     idx = meta_idx(m);
   }
-  const uint32_t hdr = a.trace[lo[a.head_len] + (size_t)st * rec];
+  const uint32_t hdr = a.trace[lo[a.head_len] + 1 + st];
   row[ra][a.head_len - 1] = (uint8_t)(hdr & 0xFF);
   row[rb][a.head_len - 1] = (uint8_t)((hdr >> 8) & 0xFF);
   const double w = a.weight[(size_t)bi * S_MAX + c];
@@ -528,10 +862,51 @@ hipError_t launch_gather_resolutions(const uint8_t *rows, int L, const int32_t *
   return hipGetLastError();
 }
 
+// Test kernel: segmented selection, 64/sw lists per wave; list j (offset
+// off[j], length n[j] <= sw) -> nth_element(nth[j]).
+__global__ __launch_bounds__(64) void test_seg_nth(double *lik, uint32_t *tag, const int *off, const int *n,
+                                                   const int *nth, int count, int sw) {
+  __shared__ int lpos[64], rpos[64];
+  __shared__ double slik[64];
+  __shared__ uint32_t smeta[64];
+  const Seg sg = make_seg(sw);
+  const int G = 64 / sw;
+  const int j = blockIdx.x * G + sg.g;
+  const bool mine = sg.mask != 0ull && j < count;
+  const int nj = mine ? n[j] : 0;
+  double v = 0.0;
+  uint32_t m = 0;
+  if (mine && sg.k < nj) {
+    v = lik[off[j] + sg.k];
+    m = tag[off[j] + sg.k];
+  }
+  const SegScratch ss{lpos, rpos, slik, smeta};
+  seg_nth_element(v, m, nj, mine ? nth[j] : 0, sg, ss);
+  if (mine && sg.k < nj) {
+    lik[off[j] + sg.k] = v;
+    tag[off[j] + sg.k] = m;
+  }
+}
+
+hipError_t launch_test_coop_nth(double *lik, uint32_t *tag, const int *off, const int *n, const int *nth, int count,
+                                int sw, hipStream_t st) {
+  if (sw < 2 || sw > 32) return hipErrorInvalidValue;
+  const int G = 64 / sw;
+  hipLaunchKernelGGL(test_seg_nth, dim3((count + G - 1) / G), dim3(WAVE), 0, st, lik, tag, off, n, nth, count, sw);
+  return hipGetLastError();
+}
+
 hipError_t launch_estep(const EstepArgs &a, int grid, hipStream_t st) {
-  if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > 65535 || (a.hcap & (a.hcap - 1)))
+  if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > 65535 || (a.hcap & (a.hcap - 1)) ||
+      a.lds_hc < 1 || (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0)
     return hipErrorInvalidValue;
-  const size_t lds = (size_t)2 * a.S * WAVE * 12 + (NP_MAX + 2) * 4 + 3 * NP_MAX;
+  const size_t lds = estep_lds_bytes(a.S, a.lds_fc, a.lds_hc);
+  static size_t lds_attr = 0;
+  if (lds > 65536 && lds > lds_attr) {
+    hipError_t e = hipFuncSetAttribute((const void *)estep_forward, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    lds_attr = lds;
+  }
   hipLaunchKernelGGL(estep_forward, dim3(grid), dim3(WAVE), lds, st, a);
   return hipGetLastError();
 }

@@ -68,7 +68,8 @@ struct EstepArgs {
   // per-wave scratch
   char *scratch;
   size_t scratch_stride;
-  int fcap, hcap;
+  int fcap, hcap;    // HBM tier capacities (states, key slots)
+  int lds_fc, lds_hc;  // LDS tier: states per frontier, key slots (power of two)
   // trace store
   uint32_t *trace;
   unsigned long long trace_cap;     // words
@@ -85,6 +86,8 @@ struct EstepArgs {
   double *weight;        // [batch][S_MAX]
   unsigned long long *re_count;  // [batch]
   unsigned int *max_states;      // [1] running maximum frontier size
+  int32_t *fmax;                 // [batch] largest frontier of each individual
+  unsigned long long *stamps;    // [12] diagnostic build: shader cycles per phase
 };
 
 struct TracebackArgs {
@@ -100,6 +103,8 @@ struct TracebackArgs {
 };
 
 size_t estep_scratch_bytes(int fcap, int hcap, int S);
+size_t estep_lds_bytes(int S, int fc, int hc);
+hipError_t launch_test_coop_nth(double *lik, uint32_t *tag, const int *off, const int *n, const int *nth, int count, int sw, hipStream_t st);
 hipError_t launch_estep(const EstepArgs &a, int grid, hipStream_t st);
 hipError_t launch_traceback(const TracebackArgs &a, int total_cands, hipStream_t st);
 hipError_t launch_transpose_u8(const uint8_t *in, uint8_t *out, int rows, int cols, int ld_out, int col0,

@@ -173,6 +173,69 @@ HMC_HD void nth_element_greater(const LinkList &v, int n, int nth) {
   insertion_sort(v, first, last);
 }
 
+// ---------------------------------------------------------------------------
+// Same algorithm, partition evaluated with stop masks (lists of <= 32).
+// std::__unguarded_partition with comp = greater and the pivot at `first`
+// stops its left scan at p in [first+1,last) with !(v[p] > pivot) and its
+// right scan at p in [first,last) with !(pivot > v[p]).  Pairing the k-th
+// left stop l_k with the k-th right stop r_k (counted from the right) on the
+// values the scans start from, the loop swaps l_k <-> r_k while l_k < r_k and
+// returns min(l_{K+1}, r_K) after K swaps: an element moved to the right half
+// came from a left stop (and vice versa), so a scan that runs into the
+// already-swapped region stops at once (see coop_select.hpp).  Reading the
+// range once and scanning masks replaces the pointer walk's dependent loads.
+HMC_HD uint32_t bit_lo(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
+HMC_HD uint32_t bit_hi(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
+
+// `span` >= last is the scan bound; on the device it is the same for every
+// lane (2S), so the reads of one partition issue back to back.
+HMC_HD int partition_pivot_masks(const LinkList &v, int first, int last, int span) {
+  const int a = first + 1, b = first + (last - first) / 2, c = last - 1;
+  const double va = v.l(a), vb = v.l(b), vc = v.l(c);
+  // the branch tree of move_median_to_first as selects
+  const int r = va > vb ? (vb > vc ? b : (va > vc ? c : a)) : (va > vc ? a : (vb > vc ? c : b));
+  v.swap(first, r);
+  const double pivot = v.l(first);
+  uint32_t Lm = 0, Rm = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll 4
+#endif
+  for (int k = 0; k < span; ++k) {
+    const double x = v.l(k);
+    const bool inr = k >= first && k < last;
+    Lm |= (uint32_t)(inr && k != first && !(x > pivot)) << k;
+    Rm |= (uint32_t)(inr && !(pivot > x)) << k;
+  }
+  int rlast = 64;
+  while (true) {
+    const int l = Lm ? (int)bit_lo(Lm) : 64;
+    const int rr = Rm ? (int)bit_hi(Rm) : -1;
+    if (!(l < rr)) return l < rlast ? l : rlast;
+    v.swap(l, rr);
+    Lm &= Lm - 1u;
+    Rm &= ~(1u << rr);
+    rlast = rr;
+  }
+}
+
+// nth_element_greater with the mask partition (n <= span <= 32).
+HMC_HD void nth_element_greater_masks(const LinkList &v, int n, int nth, int span) {
+  if (n == 0 || nth == n) return;
+  int first = 0, last = n, depth = lg2_floor(n) * 2;
+  while (last - first > 3) {
+    if (depth == 0) {
+      heap_select(v, first, nth + 1, last);
+      v.swap(first, nth);
+      return;
+    }
+    --depth;
+    const int cut = partition_pivot_masks(v, first, last, span);
+    if (cut <= nth) first = cut;
+    else last = cut;
+  }
+  insertion_sort(v, first, last);
+}
+
 // std::sort(first, first+n, greater) for n <= 16 (stl_algo.h:1925-1958):
 // __introsort_loop is a no-op below _S_threshold, leaving __insertion_sort.
 HMC_HD void sort_greater_small(const LinkList &v, int n) { insertion_sort(v, 0, n); }

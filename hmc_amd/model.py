@@ -203,6 +203,11 @@ class HaploModel:
                                         _p(out["posterior"], C.c_double), _p(out["weight"], C.c_double)))
         return out
 
+    def frontier_max(self) -> np.ndarray:
+        out = np.zeros(self.i1 - self.i0, np.int32)
+        self._check(lib().hmc_get_estep_stats(self._h, _p(out, C.c_int32)))
+        return out
+
     def samples(self, H: int):
         al = np.zeros((H, self.L), np.int32)
         w = np.zeros(H)

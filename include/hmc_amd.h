@@ -97,6 +97,12 @@ int hmc_resolve_all(hmc_ctx *ctx, double *log_likelihood, int *n_samples, uint64
  * candidate [n][sample_size] prior / posterior / sample weight. */
 int hmc_get_estep(hmc_ctx *ctx, double *total, int32_t *ncand, int32_t *status, double *prior, double *posterior,
                   double *weight);
+/* Largest number of HaploPair states any locus of each individual held in the
+ * last E-step (diagnostic). */
+int hmc_get_estep_stats(hmc_ctx *ctx, int32_t *fmax);
+/* Diagnostic build (libhmc_amd_diag.so) only: 20 shader-cycle / event
+ * counters of the E-step phases summed over waves; zeros in the product build. */
+int hmc_get_stamps(hmc_ctx *ctx, uint64_t *out20);
 /* HaploData samples of this rank: alleles[H][L] symbols, weights[H]. */
 int hmc_get_samples(hmc_ctx *ctx, int32_t *alleles, double *weights, double *total_weight);
 /* Drop the samples so the next hmc_find_patterns mines the genotypes again
@@ -140,6 +146,14 @@ int hmc_last_timings(const hmc_ctx *ctx, double *estep_forward_ms, double *estep
  * of (lik, tag) records ordered by lik. */
 void hmc_test_nth_element(double *lik, uint32_t *tag, int n, int nth);
 void hmc_test_sort_small(double *lik, uint32_t *tag, int n);
+/* The E-step's mask-partition formulation of the same nth_element (n <= 32). */
+void hmc_test_nth_element_masks(double *lik, uint32_t *tag, int n, int nth);
+/* GPU check of the segmented wave selection the E-step kernel uses
+ * (coop_select.hpp), 64/seg_width lists per wavefront: list b =
+ * lik/tag[off[b] .. off[b]+n[b]) (n[b] <= seg_width <= 32) gets
+ * nth_element(.., nth[b], greater) in place on `device`. */
+int hmc_test_coop_nth_element(int device, double *lik, uint32_t *tag, const int32_t *off, const int32_t *n,
+                              const int32_t *nth, int count, int total, int seg_width);
 /* Library version string. */
 const char *hmc_version(void);
 

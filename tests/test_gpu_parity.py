@@ -329,3 +329,51 @@ def test_two_ranks_one_gpu_host_collective(oracle_mod, tmp_path):
     same = np.mean(np.all(res == r["resolutions"], axis=(1, 2)))
     assert same >= 0.97, same
     assert np.array_equal(outs[0]["m0_freq"], outs[1]["m0_freq"])
+
+
+@pytest.mark.parametrize("sw", [32, 20, 8, 2])
+def test_segmented_nth_element_matches_libstdcxx(oracle_mod, sw):
+    """The segmented wave selection of the E-step kernel (coop_select.hpp),
+    64/sw lists per wavefront, permutes every list exactly like
+    std::nth_element (ties, NaN, sorted and organ-pipe inputs, n up to the
+    segment width; 32 = 2 x the largest sample size)."""
+    import ctypes as C
+
+    rng = np.random.default_rng(77 + sw)
+    liks, ns, nths = [], [], []
+    for n in list(range(1, sw + 1)) * 24:
+        kind = rng.integers(0, 6)
+        if kind == 0:
+            v = rng.random(n)
+        elif kind == 1:
+            v = rng.integers(0, 3, n).astype(np.float64)
+        elif kind == 2:
+            v = np.zeros(n)
+        elif kind == 3:
+            v = np.arange(n, dtype=np.float64)[:: (1 if rng.random() < 0.5 else -1)].copy()
+        elif kind == 4:
+            v = np.concatenate([np.arange(n // 2), np.arange(n - n // 2)[::-1]]).astype(np.float64)
+        else:
+            v = rng.integers(0, 4, n).astype(np.float64) * 1e-300
+            v[rng.integers(0, n)] = np.nan
+        liks.append(v)
+        ns.append(n)
+        nths.append(int(rng.integers(0, n + 1)))  # nth == n is a no-op in libstdc++
+    perm = rng.permutation(len(ns))  # mix lengths inside each wavefront
+    liks = [liks[i] for i in perm]
+    ns = [ns[i] for i in perm]
+    nths = [nths[i] for i in perm]
+    off = np.cumsum([0] + ns[:-1]).astype(np.int32)
+    lik = np.concatenate(liks)
+    tag = np.concatenate([np.arange(n, dtype=np.uint32) for n in ns])
+    l2, t2 = lik.copy(), tag.copy()
+    n_a, nth_a = np.array(ns, np.int32), np.array(nths, np.int32)
+    rc = hmc_amd.lib().hmc_test_coop_nth_element(
+        0, l2.ctypes.data_as(C.POINTER(C.c_double)), t2.ctypes.data_as(C.POINTER(C.c_uint32)),
+        off.ctypes.data_as(C.POINTER(C.c_int32)), n_a.ctypes.data_as(C.POINTER(C.c_int32)),
+        nth_a.ctypes.data_as(C.POINTER(C.c_int32)), len(ns), len(lik), sw)
+    assert rc == 0
+    for b, n in enumerate(ns):
+        o = off[b]
+        _, ref = oracle_mod.std_nth_element(lik[o:o + n], tag[o:o + n].astype(np.int32), nths[b])
+        assert np.array_equal(t2[o:o + n].astype(np.int32), ref), (n, nths[b], lik[o:o + n])

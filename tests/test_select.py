@@ -41,6 +41,22 @@ def test_nth_element_matches_libstdcxx(oracle_mod, n):
             assert np.array_equal(t1, t2), (n, nth, lik)
 
 
+@pytest.mark.parametrize("n", list(range(1, 33)))
+def test_mask_partition_nth_element_matches_libstdcxx(oracle_mod, n):
+    """The stop-mask formulation of the Hoare partition (select.hpp,
+    partition_pivot_masks) used by the E-step kernel gives the identical
+    permutation."""
+    L = hmc_amd.lib()
+    rng = np.random.default_rng(500 + n)
+    for rep in range(40):
+        for lik in _cases(rng, n):
+            nth = int(rng.integers(0, n))
+            tag = np.arange(n, dtype=np.int32)
+            _, t1 = _ours(L.hmc_test_nth_element_masks, lik, tag, nth)
+            _, t2 = oracle_mod.std_nth_element(lik, tag, nth)
+            assert np.array_equal(t1, t2), (n, nth, lik)
+
+
 @pytest.mark.parametrize("n", range(0, 17))
 def test_small_sort_matches_libstdcxx(oracle_mod, n):
     L = hmc_amd.lib()
