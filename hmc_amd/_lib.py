@@ -64,6 +64,7 @@ _SIGS = [
     ("hmc_get_best_resolutions", _i, [_vp, _P(C.c_int32)]),
     ("hmc_write_phase", _i, [_vp, _cp]),
     ("hmc_set_tuning", _i, [_vp, _i, _u64, _i]),
+    ("hmc_set_estep_shape", _i, [_vp, _i, _i]),
     ("hmc_last_timings", _i, [_vp, _P(_d), _P(_d), _P(_d)]),
     ("hmc_test_nth_element", None, [_P(_d), _P(C.c_uint32), _i, _i]),
     ("hmc_test_sort_small", None, [_P(_d), _P(C.c_uint32), _i]),

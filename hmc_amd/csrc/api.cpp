@@ -190,7 +190,8 @@ struct Ctx {
   int min_len = 1, max_len = 30, sample_size = 10;
   // tuning
   int fcap = 2048, waves = 0;
-  int lds_waves_per_cu = 2;  // E-step waves sharing one CU's 160 KiB LDS
+  int lds_waves_per_cu = 4;  // E-step individuals (blocks) sharing one CU's 160 KiB LDS
+  int estep_nw = 2;          // E-step waves per individual
   uint64_t trace_bytes = 0;
 
   Panel pan;
@@ -644,7 +645,7 @@ struct Ctx {
     while (b < n) {
       const int bn = std::min(batch, n - b);
       const int hcap = next_pow2(2 * fcap);
-      const size_t per = estep_scratch_bytes(fcap, hcap, S);
+      const size_t per = estep_scratch_bytes(fcap, hcap, S, estep_nw);
       const int grid = std::min(G, bn);
       if ((e = d_scratch.ensure(per * grid))) {
         if (e == hipErrorOutOfMemory && fcap > 256) { fcap /= 2; continue; }
@@ -679,8 +680,10 @@ struct Ctx {
       a.max_states = d_maxst.p;
       a.fmax = d_fmax.p + b;
       a.stamps = d_stamps.p;
+      a.diag_indiv = -1;
+      if (const char *di = getenv("HMC_DIAG_INDIV")) a.diag_indiv = atoi(di) - b;
       hipEventRecord(ev[0], st);
-      if ((e = launch_estep(a, grid, st))) return hipfail(e, "estep_forward launch");
+      if ((e = launch_estep(a, grid, estep_nw, st))) return hipfail(e, "estep_forward launch");
       hipEventRecord(ev[1], st);
       if ((e = hipMemcpyAsync(h_status.data() + b, d_status.p + b, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
           (e = hipMemcpyAsync(h_ncand.data() + b, d_ncand.p + b, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
@@ -777,7 +780,7 @@ struct Ctx {
     hc = 64;
     for (int f = 4096; f >= 0; f -= 16) {
       const int h = next_pow2(std::max(64, 2 * f));
-      if ((int)estep_lds_bytes(S, f, h) <= budget) { fc = f; hc = h; return; }
+      if ((int)estep_lds_bytes(S, f, h, estep_nw) <= budget) { fc = f; hc = h; return; }
     }
   }
 
@@ -976,6 +979,14 @@ int hmc_set_tuning(hmc_ctx *h, int frontier_cap, uint64_t trace_bytes, int waves
   if (frontier_cap > 0) h->c.fcap = std::min(frontier_cap, 65535);
   h->c.trace_bytes = trace_bytes;
   h->c.waves = waves;
+  return HMC_OK;
+}
+
+int hmc_set_estep_shape(hmc_ctx *h, int waves_per_individual, int individuals_per_cu) {
+  if (!h) return HMC_EARG;
+  if (waves_per_individual < 0 || waves_per_individual > 4 || individuals_per_cu < 0) return HMC_EARG;
+  if (waves_per_individual > 0) h->c.estep_nw = waves_per_individual;
+  if (individuals_per_cu > 0) h->c.lds_waves_per_cu = individuals_per_cu;
   return HMC_OK;
 }
 

@@ -59,119 +59,141 @@ struct Seg {
   int g;          // segment index (>= G: lane outside every segment)
   int base;       // first lane of the segment
   int k;          // element index inside the segment
+  int sw;         // segment width
   uint64_t mask;  // lanes of the segment
   uint64_t lt;    // lanes of the segment below this lane
+  uint32_t wm;    // segment-relative: all SW bits (0 outside every segment)
+  uint32_t ltk;   // segment-relative: bits below k
 };
+
+// A wave ballot seen from this lane's segment (bit k = element k).
+__device__ inline uint32_t seg_bits(uint64_t ballot, const Seg &sg) { return (uint32_t)(ballot >> sg.base) & sg.wm; }
 
 __device__ inline Seg make_seg(int SW) {
   Seg s;
-  const int lane = threadIdx.x;
+  const int lane = (int)(threadIdx.x & 63);
   const int G = 64 / SW;
   s.g = lane / SW;
   s.base = s.g * SW;
   s.k = lane - s.base;
+  s.sw = SW;
   const uint64_t w = SW >= 64 ? ~0ull : ((1ull << SW) - 1ull);
   s.mask = s.g < G ? (w << s.base) : 0ull;
   s.lt = s.mask & ((1ull << lane) - 1ull);
+  s.wm = s.g < G ? (SW >= 32 ? ~0u : ((1u << SW) - 1u)) : 0u;
+  s.ltk = (1u << s.k) - 1u;
   return s;
 }
 
+// Lowest set element of a segment-relative mask (64 if none).
+__device__ inline int seg_lowest(uint32_t bits) {
+  return bits ? __builtin_ctz(bits) : 64;
+}
+
 // LDS scratch of the segmented selection, one entry per lane (segment g uses
-// [base, base+SW)): left-stop and right-stop positions, and a spill list for
-// the heap-select path.
+// [base, base+SW)): left-stop and right-stop positions, a per-lane junk slot
+// pair that absorbs the writes of lanes that are not stops, and a spill list
+// for the heap-select path.
 struct SegScratch {
   int *lpos;      // [64]
   int *rpos;      // [64]
+  int *junk;      // [128]
   double *slik;   // [64]
   uint32_t *smeta;
 };
 
 // std::nth_element(v, v+nth, v+n, greater) on every segment's list (lane
 // g*SW+k holds element k; n, nth uniform inside a segment, n <= SW <= 32;
-// n == 0 marks an idle segment).  Whole-wave call.
+// n == 0 marks an idle segment).  Whole-wave call, branch-free per lane.
+// The lists live in the LDS slots slik/smeta (slot = lane) while the
+// partitions run: a partition costs two LDS round trips — one batch that
+// reads the median candidates together with every lane's own element, and the
+// stop pairing — after which each lane writes its element straight into its
+// partner's slot (a swap is an involution).
 __device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, const Seg &sg,
                                        const SegScratch &ss) {
-  const int lane = threadIdx.x;
+  const int lane = (int)(threadIdx.x & 63);
   int first = 0, last = n, depth = n > 0 ? lg2_floor(n) * 2 : 0;
-  bool act = n > 0 && nth != n && sg.mask != 0ull;
+  const bool act = n > 0 && nth != n && sg.mask != 0ull;
   bool heap = false;
+  double *sl = ss.slik + sg.base;
+  uint32_t *sm = ss.smeta + sg.base;
   int *lp = ss.lpos + sg.base, *rp = ss.rpos + sg.base;
+  int *jl = ss.junk + lane, *jr = ss.junk + 64 + lane;
+  const int kmax = sg.sw - 1;
+  ss.slik[lane] = v;
+  ss.smeta[lane] = m;
+  wave_lds_sync();
   while (true) {
-    if (act && last - first > 3 && depth == 0) heap = true;
+    heap = heap || (act && last - first > 3 && depth == 0);
     const bool part = act && !heap && last - first > 3;
     if (!__any(part)) break;
-    if (part) --depth;
+    depth -= part ? 1 : 0;
     // std::__move_median_to_first(first, first+1, mid, last-1) (stl_algo.h:79-102)
-    const int a = first + 1, b = first + (last - first) / 2, c = last - 1;
-    const double va = gat_f64(v, sg.base + a), vb = gat_f64(v, sg.base + b), vc = gat_f64(v, sg.base + c);
-    const double vf = gat_f64(v, sg.base + first);
-    const int r = va > vb ? (vb > vc ? b : (va > vc ? c : a)) : (va > vc ? a : (vb > vc ? c : b));
-    const double vr = r == a ? va : (r == b ? vb : vc);
-    const uint32_t mr = gat_u32(m, sg.base + r), mf = gat_u32(m, sg.base + first);
-    if (part) {
-      if (sg.k == first) { v = vr; m = mr; }
-      else if (sg.k == r) { v = vf; m = mf; }
-    }
-    const double pivot = vr;
+    const int a = first + 1, b = first + ((last - first) >> 1), c = last > 0 ? last - 1 : 0;
+    const double va = sl[a], vb = sl[b], vc = sl[c], vf = sl[first];
+    const uint32_t ma = sm[a], mb = sm[b], mc = sm[c], mf = sm[first];
+    v = ss.slik[lane];
+    m = ss.smeta[lane];
+    // which of a (0), b (1), c (2) is the median, as a table over the three
+    // comparisons (index ab*4 + bc*2 + ac) so it compiles to selects
+    const int idx = (va > vb ? 4 : 0) | (vb > vc ? 2 : 0) | (va > vc ? 1 : 0);
+    const int w = (22561 >> (2 * idx)) & 3;
+    const bool w0 = w == 0, w1 = w == 1;
+    const int r = w0 ? a : (w1 ? b : c);
+    const double pivot = w0 ? va : (w1 ? vb : vc);
+    const uint32_t mr = w0 ? ma : (w1 ? mb : mc);
+    const bool isf = part && sg.k == first, isr = part && sg.k == r;
+    const double v1 = isr ? vf : v;
+    const uint32_t m1 = isr ? mf : m;
+    v = isf ? pivot : v1;
+    m = isf ? mr : m1;
+    // stops, numbered inside the segment (left from the left, right from the right)
     const bool inr = part && sg.k >= first && sg.k < last;
-    const bool isL = inr && sg.k != first && !(v > pivot);
+    const bool isL = inr && !isf && !(v > pivot);
     const bool isR = inr && !(pivot > v);
-    const uint64_t Lw = __ballot(isL) & sg.mask, Rw = __ballot(isR) & sg.mask;
-    const int nL = __popcll(Lw), nR = __popcll(Rw);
-    const int kL = __popcll(Lw & sg.lt);
-    const int kR = nR - 1 - __popcll(Rw & sg.lt);
-    if (isL) lp[kL] = sg.k;
-    if (isR) rp[kR] = sg.k;
+    const uint32_t Lw = seg_bits(__ballot(isL), sg), Rw = seg_bits(__ballot(isR), sg);
+    const int nL = __popc(Lw), nR = __popc(Rw);
+    const int kL = __popc(Lw & sg.ltk);
+    const int kR = nR - 1 - __popc(Rw & sg.ltk);
+    *(isL ? lp + kL : jl) = sg.k;
+    *(isR ? rp + kR : jr) = sg.k;
     wave_lds_sync();
-    int partner = lane;
-    bool lswap = false;  // swapped in the left-stop role (a tie can be both stops)
-    if (isL && kL < nR) {
-      const int q = rp[kL];
-      if (sg.k < q) {
-        partner = sg.base + q;
-        lswap = true;
-      }
-    }
-    if (isR && kR < nL) {
-      const int q = lp[kR];
-      if (q < sg.k) partner = sg.base + q;
-    }
-    const int K = __popcll(__ballot(lswap) & sg.mask);
-    const int lK = K < nL ? lp[K] : 64;
-    const int rK = K >= 1 ? rp[K - 1] : 64;
+    const int qR = rp[kL < kmax ? kL : kmax];
+    const int qL = lp[kR < 0 ? 0 : (kR < kmax ? kR : kmax)];
+    // pair k swaps iff l_k < r_k; both roles are checked, a position swaps at most once
+    const bool lsw = isL && kL < nR && sg.k < qR;
+    const bool rsw = isR && kR < nL && qL < sg.k;
+    const int dest = lsw ? sg.base + qR : (rsw ? sg.base + qL : lane);
+    // cut = min(l_K, r_{K-1}): the first left stop that does not swap and the
+    // leftmost right stop that does
+    const int lK = seg_lowest(seg_bits(__ballot(isL && !lsw), sg));
+    const int rK = seg_lowest(seg_bits(__ballot(rsw), sg));
+    const int cut = lK < rK ? lK : rK;
+    ss.slik[dest] = v;
+    ss.smeta[dest] = m;
     wave_lds_sync();
-    const double nv = gat_f64(v, partner);
-    const uint32_t nm = gat_u32(m, partner);
-    if (part) {
-      v = nv;
-      m = nm;
-      const int cut = lK < rK ? lK : rK;
-      if (cut <= nth) first = cut;
-      else last = cut;
-    }
+    first = part && cut <= nth ? cut : first;
+    last = part && cut > nth ? cut : last;
   }
   // Depth limit reached (std::__heap_select + iter_swap, stl_algo.h:1973-1979):
-  // rare, so the segment spills to LDS and its first lane runs the sequential code.
+  // rare; the segment's first lane runs the sequential code on the slots.
   if (__any(heap)) {
-    double *sl = ss.slik + sg.base;
-    uint32_t *sm = ss.smeta + sg.base;
-    if (heap && sg.k < n) { sl[sg.k] = v; sm[sg.k] = m; }
-    wave_lds_sync();
     if (heap && sg.k == 0) {
-      const LinkList w{sl, sm, 1};
-      heap_select(w, first, nth + 1, last);
-      w.swap(first, nth);
+      const LinkList wl{sl, sm, 1};
+      heap_select(wl, first, nth + 1, last);
+      wl.swap(first, nth);
     }
-    wave_lds_sync();
-    if (heap && sg.k < n) { v = sl[sg.k]; m = sm[sg.k]; }
     wave_lds_sync();
   }
   // std::__insertion_sort of the <= 3 remaining elements (stl_algo.h:1819-1849)
   const bool ins = act && !heap && last - first > 1;
   if (__any(ins)) {
     const int len = last - first;
-    double x0 = gat_f64(v, sg.base + first), x1 = gat_f64(v, sg.base + first + 1), x2 = gat_f64(v, sg.base + first + 2);
-    uint32_t y0 = gat_u32(m, sg.base + first), y1 = gat_u32(m, sg.base + first + 1), y2 = gat_u32(m, sg.base + first + 2);
+    const int f0 = first < kmax ? first : kmax;
+    const int f1 = first + 1 < kmax ? first + 1 : kmax, f2 = first + 2 < kmax ? first + 2 : kmax;
+    double x0 = sl[f0], x1 = sl[f1], x2 = sl[f2];
+    uint32_t y0 = sm[f0], y1 = sm[f1], y2 = sm[f2];
     if (x1 > x0) {
       const double t = x1; x1 = x0; x0 = t;
       const uint32_t u = y1; y1 = y0; y0 = u;
@@ -185,13 +207,19 @@ __device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, c
         x2 = x1; y2 = y1; x1 = t; y1 = u;
       }
     }
-    if (ins) {
-      const int j = sg.k - first;
-      if (j == 0) { v = x0; m = y0; }
-      else if (j == 1) { v = x1; m = y1; }
-      else if (j == 2 && len > 2) { v = x2; m = y2; }
+    const int j = sg.k - first;
+    const bool mine = ins && (j == 0 || j == 1 || (j == 2 && len > 2));
+    const double xv = j == 0 ? x0 : (j == 1 ? x1 : x2);
+    const uint32_t yv = j == 0 ? y0 : (j == 1 ? y1 : y2);
+    wave_lds_sync();
+    if (mine) {
+      ss.slik[lane] = xv;
+      ss.smeta[lane] = yv;
     }
+    wave_lds_sync();
   }
+  v = ss.slik[lane];
+  m = ss.smeta[lane];
 }
 
 }  // namespace hmc

@@ -142,7 +142,7 @@ __device__ inline void extend_links(RegList &r, int S, uint32_t s, double tpv, b
 
 // Key table replacing m_best_pair: slot ids < hc are LDS slots, >= hc HBM slots.
 struct Keys {
-  int hc, o_key, o_cnt, o_state, o_lanes;  // LDS tier
+  int hc, nw, o_key, o_cnt, o_state, o_lanes;  // LDS tier (nw lane-mask words per slot)
   unsigned long long *gkey, *glanes;        // HBM tier
   uint32_t *gcnt, *gstate;
   uint32_t gmask;
@@ -188,19 +188,22 @@ __device__ inline void set_slot_state(const Lds &l, const Keys &K, uint32_t s, u
   if (s < (uint32_t)K.hc) ((uint32_t *)(l.base + K.o_state))[s] = v;
   else K.gstate[s - K.hc] = v;
 }
-// Lanes of the current chunk holding each key, as a 64-bit mask (OR is
-// order-free, so the grouping needs no serial ballot loop).
-__device__ inline void slot_or_lanes(const Lds &l, const Keys &K, uint32_t s, unsigned long long bit) {
-  if (s < (uint32_t)K.hc) atomicOr(&((unsigned long long *)(l.base + K.o_lanes))[s], bit);
-  else atomicOr(&K.glanes[s - K.hc], bit);
+// Threads of the current chunk holding each key: one 64-bit lane mask per
+// wave (OR is order-free, so the grouping needs no serial ballot loop).
+__device__ inline void slot_or_lanes(const Lds &l, const Keys &K, uint32_t s, int w, unsigned long long bit) {
+  if (s < (uint32_t)K.hc) atomicOr(&((unsigned long long *)(l.base + K.o_lanes))[s * K.nw + w], bit);
+  else atomicOr(&K.glanes[(size_t)(s - K.hc) * K.nw + w], bit);
 }
-__device__ inline unsigned long long slot_lanes(const Lds &l, const Keys &K, uint32_t s) {
-  return s < (uint32_t)K.hc ? ((unsigned long long *)(l.base + K.o_lanes))[s]
-                            : __hip_atomic_load(&K.glanes[s - K.hc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ inline unsigned long long slot_lanes(const Lds &l, const Keys &K, uint32_t s, int w) {
+  return s < (uint32_t)K.hc ? ((unsigned long long *)(l.base + K.o_lanes))[s * K.nw + w]
+                            : __hip_atomic_load(&K.glanes[(size_t)(s - K.hc) * K.nw + w], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ inline void clear_slot_lanes(const Lds &l, const Keys &K, uint32_t s) {
-  if (s < (uint32_t)K.hc) ((unsigned long long *)(l.base + K.o_lanes))[s] = 0ull;
-  else atomicExch(&K.glanes[s - K.hc], 0ull);
+  for (int w = 0; w < K.nw; ++w) {
+    if (s < (uint32_t)K.hc) ((unsigned long long *)(l.base + K.o_lanes))[s * K.nw + w] = 0ull;
+    else atomicExch(&K.glanes[(size_t)(s - K.hc) * K.nw + w], 0ull);
+  }
 }
 __device__ inline void clear_slot(const Lds &l, const Keys &K, uint32_t s) {
   if (s < (uint32_t)K.hc) {
@@ -212,16 +215,26 @@ __device__ inline void clear_slot(const Lds &l, const Keys &K, uint32_t s) {
   }
 }
 
-__device__ inline uint64_t lanemask_lt() { return (1ull << threadIdx.x) - 1ull; }
+__device__ inline int lane_id() { return (int)(threadIdx.x & (WAVE - 1)); }
+__device__ inline uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
-// Bump-allocate `words` contiguous trace words for this wave (lane-uniform).
-__device__ inline unsigned long long trace_alloc(const EstepArgs &a, unsigned long long &cur,
+// Block-wide scalars exchanged through LDS (a block = one individual, NW waves).
+struct BlockShared {
+  unsigned long long u[2];
+  int i[4];
+  int wcnt[4];   // per-wave counts (new states / selection adds)
+  int wmax[4];   // per-wave maxima
+};
+
+// Bump-allocate `words` contiguous trace words for this block (block-uniform call).
+__device__ inline unsigned long long trace_alloc(const EstepArgs &a, BlockShared *bs, unsigned long long &cur,
                                                  unsigned long long &end, unsigned long long words) {
   if (cur + words > end) {
     unsigned long long take = words > TRACE_CHUNK ? words : TRACE_CHUNK;
-    unsigned long long base = 0;
-    if (threadIdx.x == 0) base = atomicAdd(a.trace_cursor, take);
-    base = __shfl(base, 0);
+    if (threadIdx.x == 0) bs->u[0] = atomicAdd(a.trace_cursor, take);
+    __syncthreads();
+    const unsigned long long base = bs->u[0];
+    __syncthreads();
     cur = base;
     end = base + take;
   }
@@ -232,30 +245,30 @@ __device__ inline unsigned long long trace_alloc(const EstepArgs &a, unsigned lo
 
 // Stream the finished k-best lists of one locus into the trace store:
 // [Fn][Fn headers][Fn x S link words].
-__device__ inline bool write_trace(const EstepArgs &a, const Lds &l, const Front &F, int Fn, int locus, int bi,
-                                   unsigned long long &cur, unsigned long long &end) {
-  const int S = a.S;
+__device__ inline bool write_trace(const EstepArgs &a, const Lds &l, BlockShared *bs, const Front &F, int Fn,
+                                   int locus, int bi, unsigned long long &cur, unsigned long long &end) {
+  const int S = a.S, NT = (int)blockDim.x;
   const unsigned long long words = 1ull + (unsigned long long)Fn * (1 + S);
-  const unsigned long long off = trace_alloc(a, cur, end, words);
+  const unsigned long long off = trace_alloc(a, bs, cur, end, words);
   if (off + words > a.trace_cap) return false;
   uint32_t *hdr = a.trace + off + 1;
   uint32_t *lnk = hdr + Fn;
-  for (int t = threadIdx.x; t < Fn; t += WAVE)
+  for (int t = threadIdx.x; t < Fn; t += NT)
     hdr[t] = hdr_pack(a.mod.last[get_lo(l, F, t)], a.mod.last[get_hi(l, F, t)], get_nl(l, F, t));
   const int nw = Fn * S;
   constexpr int U = 4;
-  for (int w0 = 0; w0 < nw; w0 += U * WAVE) {
+  for (int w0 = 0; w0 < nw; w0 += U * NT) {
     uint32_t v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int w = w0 + u * WAVE + (int)threadIdx.x;
+      const int w = w0 + u * NT + (int)threadIdx.x;
       const int t = w < nw ? w / S : 0, k = w - t * S;
       const uint32_t n = get_nl(l, F, t), m = get_meta(l, F, t, w < nw ? k : 0);
       v[u] = (uint32_t)k < n ? m : 0u;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int w = w0 + u * WAVE + (int)threadIdx.x;
+      const int w = w0 + u * NT + (int)threadIdx.x;
       if (w < nw) lnk[w] = v[u];
     }
   }
@@ -268,9 +281,9 @@ __device__ inline bool write_trace(const EstepArgs &a, const Lds &l, const Front
 
 }  // namespace
 
-size_t estep_scratch_bytes(int fcap, int hcap, int S) {
-  return al256(2 * front_bytes(fcap, S) + 2 * al256((size_t)hcap * 8) + al256((size_t)hcap * 4) +
-               al256((size_t)hcap * 4));
+size_t estep_scratch_bytes(int fcap, int hcap, int S, int nw) {
+  return al256(2 * front_bytes(fcap, S) + al256((size_t)hcap * 8) + al256((size_t)hcap * 8 * nw) +
+               al256((size_t)hcap * 4) + al256((size_t)hcap * 4));
 }
 
 // One add handed to a selection segment.
@@ -281,27 +294,31 @@ struct AddPar {
   uint32_t pad;
 };
 
-// LDS carve of one wave: [selection scratch] [add parameters] [allele pairs] [key
-// table hc x (key, cnt, state)] [frontier A] [frontier B], each frontier fc x
-// (fwd, lo, hi, nl, slot, lik[S], meta[S]).
+// LDS carve of one block (nw waves, one individual): [per-wave selection
+// scratch] [add parameters] [block scalars] [allele pairs] [key table hc x
+// (key, cnt, state, nw lane masks)] [frontier A] [frontier B], each frontier
+// fc x (fwd, lo, hi, nl, slot, lik[S], meta[S]).
 struct LdsPlan {
-  int o_lpos, o_rpos, o_slik, o_smeta, o_par, o_pairs, o_key, o_cnt, o_state, o_lanes, o_front[2][7], bytes;
+  int o_lpos, o_rpos, o_junk, o_slik, o_smeta, o_par, o_bs, o_pairs, o_key, o_cnt, o_state, o_lanes, o_front[2][7],
+      bytes;
 };
 
-__host__ __device__ inline LdsPlan lds_plan(int S, int fc, int hc) {
+__host__ __device__ inline LdsPlan lds_plan(int S, int fc, int hc, int nw) {
   LdsPlan p;
   int o = 0;
   auto take = [&](int bytes) { int r = o; o += (bytes + 15) & ~15; return r; };
-  p.o_lpos = take(WAVE * 4);
-  p.o_rpos = take(WAVE * 4);
-  p.o_slik = take(WAVE * 8);
-  p.o_smeta = take(WAVE * 4);
-  p.o_par = take(WAVE / 2 * (int)sizeof(AddPar));
+  p.o_lpos = take(nw * WAVE * 4);
+  p.o_rpos = take(nw * WAVE * 4);
+  p.o_junk = take(nw * 2 * WAVE * 4);
+  p.o_slik = take(nw * WAVE * 8);
+  p.o_smeta = take(nw * WAVE * 4);
+  p.o_par = take(nw * WAVE * (int)sizeof(AddPar));
+  p.o_bs = take((int)sizeof(BlockShared));
   p.o_pairs = take((NP_MAX + 2) * 4 + 3 * NP_MAX);
   p.o_key = take(hc * 8);
   p.o_cnt = take(hc * 4);
   p.o_state = take(hc * 4);
-  p.o_lanes = take(hc * 8);
+  p.o_lanes = take(hc * 8 * nw);
   for (int f = 0; f < 2; ++f) {
     p.o_front[f][0] = take(fc * 8);       // fwd
     p.o_front[f][1] = take(fc * 4);       // lo
@@ -315,7 +332,7 @@ __host__ __device__ inline LdsPlan lds_plan(int S, int fc, int hc) {
   return p;
 }
 
-size_t estep_lds_bytes(int S, int fc, int hc) { return (size_t)lds_plan(S, fc, hc).bytes; }
+size_t estep_lds_bytes(int S, int fc, int hc, int nw) { return (size_t)lds_plan(S, fc, hc, nw).bytes; }
 
 // Diagnostic build only (-DHMC_STAMPS): per-phase shader-clock shares.  Each
 // stamp drains the wave's memory counters so a phase is charged with the
@@ -341,9 +358,9 @@ size_t estep_lds_bytes(int S, int fc, int hc) { return (size_t)lds_plan(S, fc, h
     dg0 = t1;                                                 \
   } while (0)
 #define STAMP_FLUSH                                                                       \
-  if (a.stamps)                                                                           \
+  if (a.stamps && (a.diag_indiv < 0 || a.diag_indiv == (int)blockIdx.x))                  \
     for (int k = 0; k < 20; ++k) {                                                        \
-      const bool per_lane = k == 14 || k == 15 || k >= 17;                                \
+      const bool per_lane = k == 14 || k == 17;                                \
       if (per_lane || threadIdx.x == 0) atomicAdd(&a.stamps[k], st_acc[k]);               \
     }
 #else
@@ -354,23 +371,27 @@ size_t estep_lds_bytes(int S, int fc, int hc) { return (size_t)lds_plan(S, fc, h
 #define STAMP_FLUSH
 #endif
 
-__global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void estep_forward(EstepArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   STAMP_DECL
   const int S = a.S, L = a.pan.L, amax = a.pan.amax;
-  const int lane = threadIdx.x;
-  const LdsPlan plan = lds_plan(S, a.lds_fc, a.lds_hc);
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;
+  const int NT = blockDim.x, NW = NT / WAVE;
+  const LdsPlan plan = lds_plan(S, a.lds_fc, a.lds_hc, NW);
   const Lds l{smem};
   int *pr_off = (int *)(smem + plan.o_pairs);  // [NP_MAX+2]; [NP_MAX+1] = npairs
   uint8_t *pr_x = (uint8_t *)(pr_off + NP_MAX + 2);
   uint8_t *pr_y = pr_x + NP_MAX;
   uint8_t *pr_o = pr_y + NP_MAX;
-  const SegScratch ss{(int *)(smem + plan.o_lpos), (int *)(smem + plan.o_rpos), (double *)(smem + plan.o_slik),
-                      (uint32_t *)(smem + plan.o_smeta)};
+  BlockShared *bs = (BlockShared *)(smem + plan.o_bs);
+  // this wave's selection scratch
+  const SegScratch ss{(int *)(smem + plan.o_lpos) + wv * WAVE, (int *)(smem + plan.o_rpos) + wv * WAVE,
+                      (int *)(smem + plan.o_junk) + wv * 2 * WAVE, (double *)(smem + plan.o_slik) + wv * WAVE,
+                      (uint32_t *)(smem + plan.o_smeta) + wv * WAVE};
   AddPar *par = (AddPar *)(smem + plan.o_par);
   const Seg sg = make_seg(2 * S);
   const int G = WAVE / (2 * S);
-  const LinkList W{ss.slik, ss.smeta, 1};  // final selection (lane 0)
+  const LinkList W{(double *)(smem + plan.o_slik), (uint32_t *)(smem + plan.o_smeta), 1};  // final selection
 
   char *sp = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
   Front FA, FB;
@@ -378,11 +399,12 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
   FB.g = carve_front(sp, a.fcap, S);
   Keys K;
   K.gkey = (unsigned long long *)sp; sp += al256((size_t)a.hcap * 8);
-  K.glanes = (unsigned long long *)sp; sp += al256((size_t)a.hcap * 8);
+  K.glanes = (unsigned long long *)sp; sp += al256((size_t)a.hcap * 8 * NW);
   K.gcnt = (uint32_t *)sp; sp += al256((size_t)a.hcap * 4);
   K.gstate = (uint32_t *)sp;
   K.gmask = (uint32_t)a.hcap - 1u;
   K.hc = a.lds_hc;
+  K.nw = NW;
   K.o_key = plan.o_key;
   K.o_cnt = plan.o_cnt;
   K.o_state = plan.o_state;
@@ -399,16 +421,19 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
     FF[f]->o_lik = plan.o_front[f][5];
     FF[f]->o_meta = plan.o_front[f][6];
   }
-  for (int h = lane; h < a.hcap; h += WAVE) {
-    K.gkey[h] = KEY_EMPTY;
-    K.gcnt[h] = 0;
-    K.glanes[h] = 0ull;
-  }
-  for (int h = lane; h < K.hc; h += WAVE) {
-    ((unsigned long long *)(smem + K.o_key))[h] = KEY_EMPTY;
-    ((uint32_t *)(smem + K.o_cnt))[h] = 0;
-    ((unsigned long long *)(smem + K.o_lanes))[h] = 0ull;
-  }
+  auto reset_tables = [&]() {
+    for (int h = tid; h < a.hcap; h += NT) {
+      K.gkey[h] = KEY_EMPTY;
+      K.gcnt[h] = 0;
+    }
+    for (int h = tid; h < a.hcap * NW; h += NT) K.glanes[h] = 0ull;
+    for (int h = tid; h < K.hc; h += NT) {
+      ((unsigned long long *)(smem + K.o_key))[h] = KEY_EMPTY;
+      ((uint32_t *)(smem + K.o_cnt))[h] = 0;
+    }
+    for (int h = tid; h < K.hc * NW; h += NT) ((unsigned long long *)(smem + K.o_lanes))[h] = 0ull;
+  };
+  reset_tables();
   unsigned long long tcur = 0, tend = 0;
   __syncthreads();
 
@@ -416,14 +441,17 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
     const int bi = gi - a.indiv_begin;
     const uchar2 *g = a.pan.geno_im + (size_t)gi * L;
     const int hl = a.mod.head_len;
+#ifdef HMC_STAMPS
+    const unsigned long long t_indiv = __builtin_amdgcn_s_memtime();
+#endif
     int status = EST_OK;
     unsigned long long re = 0;
     int fbig = 0;
     Front X = FA, Y = FB;
 
     // ---- initHeadList (HaploBuilder.cpp:153-224), head_len == 1 ---------
-    int Fp = 0;
-    if (lane == 0) {
+    if (tid == 0) {
+      int Fp0 = 0, st0 = EST_OK;
       const uchar2 g0 = g[0];
       const bool m0 = g0.x == MISSING, m1 = g0.y == MISSING;
       for (int hix = 0; hix < a.mod.n_head; ++hix) {
@@ -443,27 +471,30 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
         }
         for (int k = 0; k < nx; ++k) {
           uint32_t q = xs[k] == MISSING ? a.mod.head_pat0[amax] : a.mod.head_pat0[xs[k]];
-          if (q == NONE) { status = EST_NO_HEAD_PATTERN; break; }
+          if (q == NONE) { st0 = EST_NO_HEAD_PATTERN; break; }
           if (q < head) continue;  // hp->id() >= head->id()
-          if (Fp >= a.fcap) { status = EST_OVERFLOW_FRONTIER; break; }
+          if (Fp0 >= a.fcap) { st0 = EST_OVERFLOW_FRONTIER; break; }
           const double tpv = a.mod.freq[head] * a.mod.freq[q];  // HaploPair.cpp:27-32
           const bool homo = (q == head);
-          set_fwd(l, X, Fp, homo ? tpv : tpv * 2.0);
-          set_lo(l, X, Fp, head);
-          set_hi(l, X, Fp, q);
-          set_nl(l, X, Fp, 1);
-          set_link(l, X, Fp, 0, tpv, meta_pack(0, 0, false, homo, true));
-          ++Fp;
+          set_fwd(l, X, Fp0, homo ? tpv : tpv * 2.0);
+          set_lo(l, X, Fp0, head);
+          set_hi(l, X, Fp0, q);
+          set_nl(l, X, Fp0, 1);
+          set_link(l, X, Fp0, 0, tpv, meta_pack(0, 0, false, homo, true));
+          ++Fp0;
         }
-        if (status != EST_OK) break;
+        if (st0 != EST_OK) break;
       }
+      bs->i[0] = Fp0;
+      bs->i[1] = st0;
     }
-    Fp = __shfl(Fp, 0);
-    status = __shfl(status, 0);
+    __syncthreads();
+    int Fp = bs->i[0];
+    status = bs->i[1];
     __syncthreads();
     if (status == EST_OK) {
-      if (!write_trace(a, l, X, Fp, hl, bi, tcur, tend)) status = EST_OVERFLOW_TRACE;
-      for (int t = lane; t < Fp; t += WAVE) re += get_nl(l, X, t);
+      if (!write_trace(a, l, bs, X, Fp, hl, bi, tcur, tend)) status = EST_OVERFLOW_TRACE;
+      for (int t = tid; t < Fp; t += NT) re += get_nl(l, X, t);
     }
 
     // ---- forward over loci (HaploBuilder.cpp:47-82) -----------------------
@@ -471,7 +502,7 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
       if (Fp == 0) { status = EST_UNRESOLVED; break; }
       STAMP(0);
       const uchar2 gg = g[i];
-      if (lane == 0) {  // allele-pair list in extendAll call order
+      if (tid == 0) {  // allele-pair list in extendAll call order
         const double *af = a.pan.afreq + (size_t)i * amax;
         const int an = a.pan.anum[i];
         int np = 0;
@@ -500,8 +531,8 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
       const int C = pr_off[npairs];
       int Fn = 0;
 
-      for (int c0 = 0; c0 < C && status == EST_OK; c0 += WAVE) {
-        const int c = c0 + lane;
+      for (int c0 = 0; c0 < C && status == EST_OK; c0 += NT) {
+        const int c = c0 + tid;
         bool valid = c < C;
         uint32_t s = 0, lo = 0, hi = 0, slot = 0;
         bool rev = false;
@@ -535,33 +566,46 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
         STAMP(3);
         if (valid) slot = key_slot(l, K, ((unsigned long long)lo << 32) | hi, key_hash(lo, hi));
         STAMP(4);
-        // group lanes by key: rank of each lane among the chunk's lanes with its key
-        if (valid) slot_or_lanes(l, K, slot, 1ull << lane);
+        // group threads by key: rank of each contribution among the chunk's with its key
+        if (valid) slot_or_lanes(l, K, slot, wv, 1ull << lane);
         __syncthreads();
-        const uint64_t gm = valid ? slot_lanes(l, K, slot) : 0ull;
-        const int li = __popcll(gm & lanemask_lt());
-        const int gsz = __popcll(gm);
+        int li = 0, gsz = 0;
+        if (valid)
+          for (int w = 0; w < NW; ++w) {
+            const uint64_t gm = slot_lanes(l, K, slot, w);
+            gsz += __popcll(gm);
+            if (w < wv) li += __popcll(gm);
+            else if (w == wv) li += __popcll(gm & lanemask_lt());
+          }
         __syncthreads();
         if (valid && li == 0) clear_slot_lanes(l, K, slot);
         STAMP(5);
         const uint32_t cnt0 = valid ? slot_cnt(l, K, slot) : 0u;
         const bool is_new = valid && cnt0 == 0 && li == 0;
         const uint64_t nm = __ballot(is_new);
-        if (Fn + __popcll(nm) > a.fcap) { status = EST_OVERFLOW_FRONTIER; break; }
+        if (lane == 0) bs->wcnt[wv] = __popcll(nm);
+        __syncthreads();
+        int pre = 0, tot = 0;
+        for (int w = 0; w < NW; ++w) {
+          const int cw = bs->wcnt[w];
+          pre += w < wv ? cw : 0;
+          tot += cw;
+        }
+        if (Fn + tot > a.fcap) { status = EST_OVERFLOW_FRONTIER; break; }
         uint32_t st = 0;
         if (is_new) {
-          st = (uint32_t)(Fn + __popcll(nm & lanemask_lt()));
+          st = (uint32_t)(Fn + pre + __popcll(nm & lanemask_lt()));
           set_slot_state(l, K, slot, st);
           set_slot(l, Y, (int)st, slot);
         }
-        Fn += __popcll(nm);
+        Fn += tot;
         if (valid && li == 0) set_slot_cnt(l, K, slot, cnt0 + (uint32_t)gsz);
         __syncthreads();
         if (valid && !is_new) st = slot_state(l, K, slot);
         const uint32_t rank = cnt0 + (uint32_t)li;
         STAMP(6);
 
-        // first contribution of a key: extension constructor (HaploPair.cpp:35-61), lane-parallel
+        // first contribution of a key: extension constructor (HaploPair.cpp:35-61), thread-parallel
         if (valid && rank == 0) {
           const uint32_t ns = get_nl(l, X, s);
           RegList r;
@@ -580,21 +624,24 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
               ym[k] = r.m[k];
             }
         }
-        __syncthreads();
         // later contributions: HaploPair::add (HaploPair.cpp:63-89).  Round r
-        // applies every lane whose key rank inside the chunk is r, so distinct
-        // keys merge in parallel and each key sees its adds in reference order.
-        // The lane appends into its private LDS column and keeps the S best
-        // with the mask-partition nth_element (select.hpp).
+        // applies every contribution whose key rank inside the chunk is r, so
+        // distinct keys merge in parallel and each key sees its adds in
+        // reference order.  An add that still fits appends in place; adds that
+        // overflow S are packed 64/(2S) per selection step, the steps dealt to
+        // the block's waves, and keep the S best with the libstdc++-exact
+        // segmented nth_element (coop_select.hpp).
         int rounds = (valid && rank != 0) ? li + 1 : 0;
         for (int o = 32; o > 0; o >>= 1) { const int t = __shfl_xor(rounds, o); rounds = t > rounds ? t : rounds; }
+        if (lane == 0) bs->wmax[wv] = rounds;
+        __syncthreads();
+        for (int w = 0; w < NW; ++w) rounds = bs->wmax[w] > rounds ? bs->wmax[w] : rounds;
 #ifdef HMC_STAMPS
         st_acc[10] += __popcll(__ballot(valid && rank != 0));
         st_acc[11] += rounds;
 #endif
         for (int r = 0; r < rounds; ++r) {
           STAMP(7);
-          STAMP(12);
           bool sel = false;
           uint32_t k0 = 0, ns = 0;
           if (valid && rank != 0 && li == r) {
@@ -621,32 +668,35 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
             DIAG(14);
 #ifdef HMC_STAMPS
             st_acc[17] += st < (uint32_t)a.lds_fc ? 1 : 0;
-            st_acc[18] += s < (uint32_t)a.lds_fc ? 1 : 0;
 #endif
           }
-          // adds that overflow S: G at a time, one per selection segment
-          uint64_t selm = __ballot(sel);
-          while (selm) {
-            uint64_t take = 0;
-            for (int q = 0; q < G && selm; ++q) {
-              const uint64_t bit = selm & (~selm + 1ull);
-              take |= bit;
-              selm ^= bit;
-            }
-            if (sel && ((take >> lane) & 1ull)) {
-              AddPar &P = par[__popcll(take & lanemask_lt())];
-              P.tpv = tpv;
-              P.st = st;
-              P.s = s;
-              P.k0ns = k0 | ns << 8 | (rev ? 1u << 16 : 0u) | (differ ? 1u << 17 : 0u);
-            }
-            wave_lds_sync();
-            const int nseg = __popcll(take);
+          // number the overflowing adds across the block (chunk order)
+          const uint64_t selm = __ballot(sel);
+          if (lane == 0) bs->wcnt[wv] = __popcll(selm);
+          __syncthreads();
+          int spre = 0, nsel = 0;
+          for (int w = 0; w < NW; ++w) {
+            const int cw = bs->wcnt[w];
+            spre += w < wv ? cw : 0;
+            nsel += cw;
+          }
+          if (sel) {
+            AddPar &P = par[spre + __popcll(selm & lanemask_lt())];
+            P.tpv = tpv;
+            P.st = st;
+            P.s = s;
+            P.k0ns = k0 | ns << 8 | (rev ? 1u << 16 : 0u) | (differ ? 1u << 17 : 0u);
+          }
+          __syncthreads();
+          STAMP(13);
+          const int nbatch = (nsel + G - 1) / G;
+          for (int bt = wv; bt < nbatch; bt += NW) {
+            const int nseg = nsel - bt * G < G ? nsel - bt * G : G;
             int n = 0;
             double v = 0.0;
             uint32_t m = 0, pst = 0;
             if (sg.g < nseg) {
-              const AddPar P = par[sg.g];
+              const AddPar P = par[bt * G + sg.g];
               const int pk0 = (int)(P.k0ns & 0xFF), pns = (int)((P.k0ns >> 8) & 0xFF);
               pst = P.st;
               n = pk0 + pns;
@@ -669,14 +719,18 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
                 }
               }
             }
+            STAMP(15);
             seg_nth_element(v, m, n, S - 1, sg, ss);
+            STAMP(19);
+#ifdef HMC_STAMPS
+            st_acc[18] += 1;
+#endif
             if (sg.g < nseg && sg.k < S) {
               set_link(l, Y, (int)pst, sg.k, v, m);
               if (sg.k == 0) set_nl(l, Y, (int)pst, (uint32_t)S);
             }
-            wave_lds_sync();  // par[] is rewritten by the next batch
+            STAMP(12);
           }
-          STAMP(13);
           __syncthreads();
           STAMP(16);
         }
@@ -684,12 +738,12 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
       }
       if (status != EST_OK) break;
       if (Fn == 0) { status = EST_UNRESOLVED; break; }
-      if (!write_trace(a, l, Y, Fn, i + 1, bi, tcur, tend)) { status = EST_OVERFLOW_TRACE; break; }
-      for (int t = lane; t < Fn; t += WAVE) {
+      if (!write_trace(a, l, bs, Y, Fn, i + 1, bi, tcur, tend)) { status = EST_OVERFLOW_TRACE; break; }
+      for (int t = tid; t < Fn; t += NT) {
         re += get_nl(l, Y, t);
         clear_slot(l, K, get_slot(l, Y, t));
       }
-      if (lane == 0 && a.max_states) atomicMax(a.max_states, (unsigned)Fn);
+      if (tid == 0 && a.max_states) atomicMax(a.max_states, (unsigned)Fn);
       fbig = Fn > fbig ? Fn : fbig;
       __syncthreads();
       Front T = X; X = Y; Y = T;
@@ -700,22 +754,21 @@ __global__ __launch_bounds__(64) void estep_forward(EstepArgs a) {
 
     // ---- final selection (HaploBuilder.cpp:87-116) ------------------------
     if (status < 0) {  // aborted mid-locus: keys may be left in the tables
-      for (int h = lane; h < a.hcap; h += WAVE) {
-        K.gkey[h] = KEY_EMPTY;
-        K.gcnt[h] = 0;
-        K.glanes[h] = 0ull;
-      }
-      for (int h = lane; h < K.hc; h += WAVE) {
-        ((unsigned long long *)(smem + K.o_key))[h] = KEY_EMPTY;
-        ((uint32_t *)(smem + K.o_cnt))[h] = 0;
-        ((unsigned long long *)(smem + K.o_lanes))[h] = 0ull;
-      }
+      __syncthreads();
+      reset_tables();
     }
     for (int o = 32; o > 0; o >>= 1) re += __shfl_xor(re, o);
-    if (lane == 0) {
-      a.re_count[bi] = re;
+    if (tid == 0) bs->u[1] = 0ull;
+    __syncthreads();
+    if (lane == 0) atomicAdd(&bs->u[1], re);
+    __syncthreads();
+    if (tid == 0) {
+      a.re_count[bi] = bs->u[1];
       a.status[bi] = status;
       if (a.fmax) a.fmax[bi] = fbig > Fp ? fbig : Fp;
+#ifdef HMC_STAMPS  // diagnostic build: the slot carries the individual's shader time (kcycles)
+      if (a.fmax) a.fmax[bi] = (int32_t)((__builtin_amdgcn_s_memtime() - t_indiv) >> 10);
+#endif
       int cnt = 0;
       double total = 0.0;
       if (status == EST_OK) {
@@ -866,7 +919,7 @@ hipError_t launch_gather_resolutions(const uint8_t *rows, int L, const int32_t *
 // off[j], length n[j] <= sw) -> nth_element(nth[j]).
 __global__ __launch_bounds__(64) void test_seg_nth(double *lik, uint32_t *tag, const int *off, const int *n,
                                                    const int *nth, int count, int sw) {
-  __shared__ int lpos[64], rpos[64];
+  __shared__ int lpos[64], rpos[64], junk[128];
   __shared__ double slik[64];
   __shared__ uint32_t smeta[64];
   const Seg sg = make_seg(sw);
@@ -880,7 +933,7 @@ __global__ __launch_bounds__(64) void test_seg_nth(double *lik, uint32_t *tag, c
     v = lik[off[j] + sg.k];
     m = tag[off[j] + sg.k];
   }
-  const SegScratch ss{lpos, rpos, slik, smeta};
+  const SegScratch ss{lpos, rpos, junk, slik, smeta};
   seg_nth_element(v, m, nj, mine ? nth[j] : 0, sg, ss);
   if (mine && sg.k < nj) {
     lik[off[j] + sg.k] = v;
@@ -896,18 +949,18 @@ hipError_t launch_test_coop_nth(double *lik, uint32_t *tag, const int *off, cons
   return hipGetLastError();
 }
 
-hipError_t launch_estep(const EstepArgs &a, int grid, hipStream_t st) {
+hipError_t launch_estep(const EstepArgs &a, int grid, int nw, hipStream_t st) {
   if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > 65535 || (a.hcap & (a.hcap - 1)) ||
-      a.lds_hc < 1 || (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0)
+      a.lds_hc < 1 || (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || nw < 1 || nw > 4)
     return hipErrorInvalidValue;
-  const size_t lds = estep_lds_bytes(a.S, a.lds_fc, a.lds_hc);
+  const size_t lds = estep_lds_bytes(a.S, a.lds_fc, a.lds_hc, nw);
   static size_t lds_attr = 0;
   if (lds > 65536 && lds > lds_attr) {
     hipError_t e = hipFuncSetAttribute((const void *)estep_forward, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     lds_attr = lds;
   }
-  hipLaunchKernelGGL(estep_forward, dim3(grid), dim3(WAVE), lds, st, a);
+  hipLaunchKernelGGL(estep_forward, dim3(grid), dim3(WAVE * nw), lds, st, a);
   return hipGetLastError();
 }
 

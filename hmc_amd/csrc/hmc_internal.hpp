@@ -87,7 +87,8 @@ struct EstepArgs {
   unsigned long long *re_count;  // [batch]
   unsigned int *max_states;      // [1] running maximum frontier size
   int32_t *fmax;                 // [batch] largest frontier of each individual
-  unsigned long long *stamps;    // [12] diagnostic build: shader cycles per phase
+  unsigned long long *stamps;    // [20] diagnostic build: shader cycles per phase
+  int diag_indiv;                // diagnostic build: stamp only this batch index (-1: all)
 };
 
 struct TracebackArgs {
@@ -102,10 +103,10 @@ struct TracebackArgs {
   double *w_out;               // [H]
 };
 
-size_t estep_scratch_bytes(int fcap, int hcap, int S);
-size_t estep_lds_bytes(int S, int fc, int hc);
+size_t estep_scratch_bytes(int fcap, int hcap, int S, int nw);
+size_t estep_lds_bytes(int S, int fc, int hc, int nw);
 hipError_t launch_test_coop_nth(double *lik, uint32_t *tag, const int *off, const int *n, const int *nth, int count, int sw, hipStream_t st);
-hipError_t launch_estep(const EstepArgs &a, int grid, hipStream_t st);
+hipError_t launch_estep(const EstepArgs &a, int grid, int nw, hipStream_t st);
 hipError_t launch_traceback(const TracebackArgs &a, int total_cands, hipStream_t st);
 hipError_t launch_transpose_u8(const uint8_t *in, uint8_t *out, int rows, int cols, int ld_out, int col0,
                                hipStream_t st);

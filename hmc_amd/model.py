@@ -125,6 +125,10 @@ class HaploModel:
     def set_tuning(self, frontier_cap: int = 0, trace_bytes: int = 0, waves: int = 0):
         self._check(lib().hmc_set_tuning(self._h, frontier_cap, trace_bytes, waves))
 
+    def set_estep_shape(self, waves_per_individual: int = 0, individuals_per_cu: int = 0):
+        """E-step launch shape (results are identical for every shape)."""
+        self._check(lib().hmc_set_estep_shape(self._h, waves_per_individual, individuals_per_cu))
+
     # ----------------------------------------------------------------- panel
     def load(self, genos: GenoData):
         a = np.ascontiguousarray(genos.alleles, dtype=np.int32)

@@ -136,6 +136,10 @@ int hmc_write_phase(hmc_ctx *ctx, const char *path);
  * larger capacity; trace_bytes: trace-store budget (0 = automatic);
  * waves: resident E-step waves (0 = automatic). */
 int hmc_set_tuning(hmc_ctx *ctx, int frontier_cap, uint64_t trace_bytes, int waves);
+/* E-step launch shape: wavefronts cooperating on one individual (1..4,
+ * default 2) and individuals sharing one CU's LDS (default 4); 0 keeps the
+ * current value.  Results do not depend on the shape. */
+int hmc_set_estep_shape(hmc_ctx *ctx, int waves_per_individual, int individuals_per_cu);
 /* Device time (ms, HIP events on the context stream) of the last E-step
  * forward kernel, traceback and whole M-step. */
 int hmc_last_timings(const hmc_ctx *ctx, double *estep_forward_ms, double *estep_traceback_ms, double *mstep_ms);

@@ -331,6 +331,27 @@ def test_two_ranks_one_gpu_host_collective(oracle_mod, tmp_path):
     assert np.array_equal(outs[0]["m0_freq"], outs[1]["m0_freq"])
 
 
+@pytest.mark.parametrize("name", ["a3miss5", "cfg1"])
+def test_estep_shape_invariance(oracle_mod, name):
+    """1, 2 and 4 wavefronts per individual (and any LDS split) give the
+    identical E-step: same LL, resolutions, weights and link count."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
+    o.find_patterns()
+    pt = o.patterns()
+    ref = None
+    for nw, ipc in [(1, 4), (2, 4), (4, 2), (2, 1), (2, 16)]:
+        m = gpu_model(p, 10)
+        m.set_estep_shape(nw, ipc)
+        m.set_patterns(pt["start"], pt["len"], pt["freq"], pt["tp"], pt["succ"], last_symbols(pt))
+        ll, H, re = m.resolve_all()
+        er = m.estep_results()
+        got = (ll, H, re, m.resolutions().tobytes(), er["weight"].tobytes(), er["prior"].tobytes())
+        if ref is None:
+            ref = got
+        assert got == ref, (nw, ipc)
+
+
 @pytest.mark.parametrize("sw", [32, 20, 8, 2])
 def test_segmented_nth_element_matches_libstdcxx(oracle_mod, sw):
     """The segmented wave selection of the E-step kernel (coop_select.hpp),
