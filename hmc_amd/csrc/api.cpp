@@ -219,6 +219,7 @@ struct Ctx {
   DevBuf<uint8_t> n_allele, n_flags;
   DevBuf<double> n_freq, n_prefix, n_tp, n_sum;
   DevBuf<uint32_t> n_cnt, n_size, n_pos;
+  DevBuf<unsigned long long> d_mstamps;  // diagnostic build: mine_count phase cycles
   DevBuf<unsigned long long> n_list_off;
   size_t node_cap = 0;
   DevBuf<uint32_t> l_idx[2];
@@ -435,7 +436,7 @@ struct Ctx {
     int mnl = std::max(min_len, 1);
     mxl = std::max(mxl, mnl);
     const double mf = current_min_freq();
-    if ((e = d_rm.ensure(1)) || (e = d_totals.ensure(2)) || (e = hipMemsetAsync(d_rm.p, 0, 8, st)))
+    if ((e = d_rm.ensure(RM_SLOTS * 16)) || (e = d_totals.ensure(2)) || (e = hipMemsetAsync(d_rm.p, 0, RM_SLOTS * 16 * 8, st)))
       return hipfail(e, "mine");
     std::vector<int> lbeg{0, 0}, lend{0, 0};  // per level node ranges (index = level)
     int n1 = 0;
@@ -455,7 +456,57 @@ struct Ctx {
       a.max_len = mxl;
       a.lin_idx = level == 1 ? nullptr : l_idx[cur].p;
       a.lin_val = level == 1 ? nullptr : l_val[cur].p;
+      static const bool diag_mine = getenv("HMC_DIAG_MINE") != nullptr;
+      hipEvent_t dm0 = nullptr, dm1 = nullptr;
+      if (diag_mine) {
+        hipEventCreate(&dm0);
+        hipEventCreate(&dm1);
+        hipEventRecord(dm0, st);
+      }
+#ifdef HMC_STAMPS
+      if (diag_mine) {
+        d_mstamps.ensure((size_t)(pend - pbeg) * 8);
+        hipMemsetAsync(d_mstamps.p, 0, (size_t)(pend - pbeg) * 64, st);
+        a.stamps = d_mstamps.p;
+      }
+#endif
       if ((e = launch_mine_count(a, level, pbeg, pend, st))) return hipfail(e, "mine_count");
+      if (diag_mine) {  // per-level list statistics of the parents (diagnostic)
+        hipEventRecord(dm1, st);
+        hipStreamSynchronize(st);
+        float ms = 0;
+        hipEventElapsedTime(&ms, dm0, dm1);
+        size_t tot_n = 0, max_n = 0, npar = 0;
+        if (level == 1) {
+          npar = (size_t)L;
+          tot_n = (size_t)L * (size_t)a.n_items;
+          max_n = (size_t)a.n_items;
+        } else {
+          std::vector<uint32_t> hc((size_t)(pend - pbeg));
+          std::vector<uint8_t> hf((size_t)(pend - pbeg));
+          hipMemcpy(hc.data(), n_cnt.p + pbeg, hc.size() * 4, hipMemcpyDeviceToHost);
+          hipMemcpy(hf.data(), n_flags.p + pbeg, hf.size(), hipMemcpyDeviceToHost);
+          for (size_t q = 0; q < hc.size(); ++q)
+            if (hf[q] & 2) {
+              ++npar;
+              tot_n += hc[q];
+              max_n = std::max<size_t>(max_n, hc[q]);
+            }
+        }
+        fprintf(stderr, "mine level %2d: %7zu ext parents of %7d, entries %9zu, max list %7zu, mine_count %.3f ms\n",
+                level, npar, pend - pbeg, tot_n, max_n, ms);
+#ifdef HMC_STAMPS
+        unsigned long long hs[8] = {};
+        std::vector<unsigned long long> hv((size_t)(pend - pbeg) * 8);
+        hipMemcpy(hv.data(), d_mstamps.p, hv.size() * 8, hipMemcpyDeviceToHost);
+        for (size_t q = 0; q < hv.size(); ++q) hs[q % 8] += hv[q];
+        const double nwv = hs[5] ? (double)hs[5] : 1.0;
+        fprintf(stderr, "   per wave (cycles): view %.0f  loads %.0f  compact %.0f  sum %.0f  epilogue %.0f; waves %llu\n",
+                hs[0] / nwv, hs[1] / nwv, hs[2] / nwv, hs[3] / nwv, hs[4] / nwv, hs[5]);
+#endif
+        hipEventDestroy(dm0);
+        hipEventDestroy(dm1);
+      }
       if ((rc = allreduce_sum(n_sum.p + cb, nlev))) return rc;
       if ((e = s_ext.ensure(nlev)) || (e = s_lscan.ensure(nlev)) || (e = s_child.ensure(nlev)) ||
           (e = s_cscan.ensure(nlev)))
@@ -519,10 +570,13 @@ struct Ctx {
     if ((e = launch_mine_succ(a, t, P, st))) return hipfail(e, "mine_succ");
     head_len = mnl;
     if ((rc = build_heads_from_nodes(a))) return rc;
-    unsigned long long rm = 0;
-    if ((e = hipMemcpyAsync(&rm, d_rm.p, 8, hipMemcpyDeviceToHost, st))) return hipfail(e, "mine");
+    std::vector<unsigned long long> rm_slots((size_t)RM_SLOTS * 16);
+    if ((e = hipMemcpyAsync(rm_slots.data(), d_rm.p, rm_slots.size() * 8, hipMemcpyDeviceToHost, st)))
+      return hipfail(e, "mine");
     hipEventRecord(ev[5], st);
     if ((e = hipStreamSynchronize(st))) return hipfail(e, "mine");
+    unsigned long long rm = 0;
+    for (int k = 0; k < RM_SLOTS; ++k) rm += rm_slots[(size_t)k * 16];
     float ms = 0;
     hipEventElapsedTime(&ms, ev[4], ev[5]);
     ms_m = ms;

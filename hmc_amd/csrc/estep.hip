@@ -743,7 +743,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void e
         re += get_nl(l, Y, t);
         clear_slot(l, K, get_slot(l, Y, t));
       }
-      if (tid == 0 && a.max_states) atomicMax(a.max_states, (unsigned)Fn);
       fbig = Fn > fbig ? Fn : fbig;
       __syncthreads();
       Front T = X; X = Y; Y = T;
@@ -763,6 +762,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void e
     if (lane == 0) atomicAdd(&bs->u[1], re);
     __syncthreads();
     if (tid == 0) {
+      if (a.max_states) atomicMax(a.max_states, (unsigned)(fbig > Fp ? fbig : Fp));
       a.re_count[bi] = bs->u[1];
       a.status[bi] = status;
       if (a.fmax) a.fmax[bi] = fbig > Fp ? fbig : Fp;

@@ -128,38 +128,88 @@ __device__ inline ParentView parent_view(const MineArgs &a, int level, int pidx)
 }  // namespace
 
 // ---------------------------------------------------------------------------
+constexpr int CROW = WAVE + 18;  // LDS row stride (doubles): one chunk's contributions + batch padding
+
+#ifdef HMC_STAMPS
+#define MSTAMP(k)                                                \
+  do {                                                           \
+    __builtin_amdgcn_s_waitcnt(0);                               \
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();  \
+    ms_acc[k] += t1 - ms_t0;                                     \
+    ms_t0 = t1;                                                  \
+  } while (0)
+#else
+#define MSTAMP(k) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg, int pend) {
-  extern __shared__ double cbuf[];  // [nc][65]
-  const int lane = threadIdx.x;
+  extern __shared__ __align__(16) double cbuf[];  // [nc][CROW]
+  const int tid = threadIdx.x, lane = tid;
   const int pidx = pbeg + blockIdx.x;
   if (pidx >= pend) return;
+#ifdef HMC_STAMPS
+  unsigned long long ms_t0 = __builtin_amdgcn_s_memtime(), ms_acc[8] = {};
+#endif
   const ParentView p = parent_view(a, level, pidx);
+  MSTAMP(0);
   if (!p.ok) return;
   const uint8_t *ca = a.pos_allele + (size_t)p.e * a.amax;
+  const uint64_t lt = (1ull << lane) - 1ull;
   double sum = 0.0;
   uint32_t cnt = 0;
-  for (int base = 0; base < p.n; base += WAVE) {
-    const EntryView x = load_entry(a, level == 1, p.lidx, p.lval, base + lane, p.n, p.e);
-    for (int k = 0; k < p.nc; ++k) {
-      double c;
-      const bool m = contribution(a, x, p.e, ca[k], c);
-      cbuf[k * 65 + lane] = c;  // non-matching entries add +0.0: an exact no-op on a sum >= +0
-      const uint64_t b = __ballot(m);
-      if (lane == k) cnt += (uint32_t)__popcll(b);
+  constexpr int U = 4;  // chunks whose loads are in flight together
+  for (int base = 0; base < p.n; base += U * WAVE) {
+    EntryView xs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) xs[u] = load_entry(a, level == 1, p.lidx, p.lval, base + u * WAVE + lane, p.n, p.e);
+    MSTAMP(1);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (base + u * WAVE >= p.n) break;
+      const EntryView &x = xs[u];
+      // Each child's matching entries, compacted in list order.  Non-matching
+      // entries would add +0.0, an exact no-op on a sum >= +0, so skipping them
+      // leaves every child's add chain — and its rounding — unchanged.
+      // Rows are pre-filled with +0.0 so the summation below can run whole
+      // 16-value batches without predication (x + 0.0 == x exactly).
+      int mine = 0;
+      for (int k = 0; k < p.nc; ++k) {
+        double c;
+        const bool m = contribution(a, x, p.e, ca[k], c);
+        const uint64_t b = __ballot(m);
+        cbuf[k * CROW + lane] = 0.0;
+        if (lane < 16) cbuf[k * CROW + WAVE + lane] = 0.0;
+        if (m) cbuf[k * CROW + __popcll(b & lt)] = c;
+        if (lane == k) mine = __popcll(b);
+      }
+      __syncthreads();
+      MSTAMP(2);
+      if (lane < p.nc) {
+        cnt += (uint32_t)mine;
+        double s = sum;
+        const double2 *row = (const double2 *)(cbuf + lane * CROW);
+        // 16 values per batch: the reads issue together, the adds stay one
+        // ordered chain (the +0.0 padding past `mine` changes nothing)
+        for (int j = 0; j < mine; j += 16) {
+          double2 q[8];
+#pragma unroll
+          for (int v = 0; v < 8; ++v) q[v] = row[(j >> 1) + v];
+#pragma unroll
+          for (int v = 0; v < 8; ++v) {
+            s = s + q[v].x;
+            s = s + q[v].y;
+          }
+        }
+        sum = s;
+      }
+      __syncthreads();
+      MSTAMP(3);
     }
-    __syncthreads();
-    if (lane < p.nc) {
-      double s = sum;
-      const double *row = cbuf + lane * 65;
-#pragma unroll 16
-      for (int j = 0; j < WAVE; ++j) s = s + row[j];
-      sum = s;
-    }
-    __syncthreads();
   }
-  if (lane < p.nc) {
-    const int c = p.cb + lane;
-    const uint8_t al = ca[lane];
+  const int lane_c = tid;  // child lanes: threads 0..nc-1
+  if (lane_c < p.nc) {
+    const int c = p.cb + lane_c;
+    const uint8_t al = ca[lane_c];
     a.sum[c] = sum;
     a.cnt[c] = cnt;
     a.start[c] = p.start;
@@ -179,7 +229,18 @@ __global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg
     }
     a.link[c] = lk;
   }
-  if (lane == 0) atomicAdd(a.rm, (unsigned long long)p.n * (unsigned long long)p.nc);
+  // R_M: spread over RM_SLOTS counters a cache line apart (one shared counter
+  // serialises every wave of the level in a single L2 channel)
+  if (tid == 0) atomicAdd(&a.rm[(blockIdx.x % RM_SLOTS) * 16], (unsigned long long)p.n * (unsigned long long)p.nc);
+#ifdef HMC_STAMPS
+  MSTAMP(4);
+  if (tid == 0 && a.stamps) {  // one private slot per block: no contended atomics
+    unsigned long long *o = a.stamps + (size_t)blockIdx.x * 8;
+    for (int k = 0; k < 5; ++k) o[k] = ms_acc[k];
+    o[5] = 1ull;
+    o[6] = (unsigned long long)p.n;
+  }
+#endif
 }
 
 // searchPattern's rules (PatternManager.cpp:110-133) for the nodes [b, e) of one level.
@@ -219,35 +280,40 @@ __global__ void scan_totals(const unsigned long long *ls, const unsigned long lo
 }
 
 __global__ __launch_bounds__(64) void mine_scatter(MineArgs a, int level, int pbeg, int pend) {
-  __shared__ uint32_t run[A_MAX];
   const int lane = threadIdx.x;
   const int pidx = pbeg + blockIdx.x;
   if (pidx >= pend) return;
   const ParentView p = parent_view(a, level, pidx);
   if (!p.ok) return;
   const uint8_t *ca = a.pos_allele + (size_t)p.e * a.amax;
-  if (lane < A_MAX) run[lane] = 0;
   bool any = false;
   for (int k = 0; k < p.nc; ++k) any |= (a.flags[p.cb + k] & NODE_EXT) != 0;
-  __syncthreads();
   if (!any) return;
   const uint64_t lt = (1ull << lane) - 1ull;
-  for (int base = 0; base < p.n; base += WAVE) {
-    const EntryView x = load_entry(a, level == 1, p.lidx, p.lval, base + lane, p.n, p.e);
-    for (int k = 0; k < p.nc; ++k) {
-      const int c = p.cb + k;
-      if (!(a.flags[c] & NODE_EXT)) continue;
-      double v;
-      const bool m = contribution(a, x, p.e, ca[k], v);
-      const uint64_t b = __ballot(m);
-      if (m) {
-        const unsigned long long at = a.list_off[c] + run[k] + (uint32_t)__popcll(b & lt);
-        a.lout_idx[at] = x.item;
-        if (a.genotype) a.lout_val[at] = v;
+  uint32_t run = 0;  // lane k: entries already written to child k's list
+  constexpr int U = 4;  // chunks whose loads are in flight together
+  for (int base = 0; base < p.n; base += U * WAVE) {
+    EntryView xs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) xs[u] = load_entry(a, level == 1, p.lidx, p.lval, base + u * WAVE + lane, p.n, p.e);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (base + u * WAVE >= p.n) break;
+      const EntryView &x = xs[u];
+      for (int k = 0; k < p.nc; ++k) {
+        const int c = p.cb + k;
+        if (!(a.flags[c] & NODE_EXT)) continue;
+        double v;
+        const bool m = contribution(a, x, p.e, ca[k], v);
+        const uint64_t b = __ballot(m);
+        const uint32_t rk = (uint32_t)__builtin_amdgcn_readlane((int)run, k);
+        if (m) {
+          const unsigned long long at = a.list_off[c] + rk + (uint32_t)__popcll(b & lt);
+          a.lout_idx[at] = x.item;
+          if (a.genotype) a.lout_val[at] = v;
+        }
+        if (lane == k) run += (uint32_t)__popcll(b);
       }
-      __syncthreads();
-      if (lane == 0) run[k] += (uint32_t)__popcll(b);
-      __syncthreads();
     }
   }
 }
@@ -375,7 +441,14 @@ __global__ void mine_succ(MineArgs a, PatternTable t, int P) {
 // ---- host-side launch helpers -----------------------------------------------
 hipError_t launch_mine_count(const MineArgs &a, int level, int pbeg, int pend, hipStream_t st) {
   if (pend <= pbeg) return hipSuccess;
-  const size_t lds = (size_t)a.amax * 65 * 8;
+  const size_t lds = (size_t)a.amax * CROW * 8;
+  static size_t lds_attr = 0;
+  if (lds > 65536 - 1024 && lds > lds_attr) {  // many alleles: opt in to the CU's full LDS
+    hipError_t e = hipFuncSetAttribute((const void *)mine_count, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds + 1024);
+    if (e != hipSuccess) return e;
+    lds_attr = lds;
+  }
   hipLaunchKernelGGL(mine_count, dim3(pend - pbeg), dim3(WAVE), lds, st, a, level, pbeg, pend);
   return hipGetLastError();
 }

@@ -9,6 +9,8 @@ constexpr uint8_t NODE_EXT = 2;  // extended by one allele   (PatternManager.cpp
 
 // Candidate nodes of all levels live in flat arrays; roots (the empty pattern
 // at each start) are virtual and encoded as -(start + 2); -1 = none.
+constexpr int RM_SLOTS = 64;  // R_M counters, 16 words (128 B) apart
+
 struct MineArgs {
   int L = 0, amax = 0, n_items = 0;     // items scanned by the root lists (this rank)
   int item_base = 0, item_stride = 0;   // first root item; row stride of geno_lm / samp_lm
@@ -16,6 +18,7 @@ struct MineArgs {
   const uchar2 *geno_lm = nullptr;      // [L][N]
   const uint8_t *samp_lm = nullptr;     // [L][H]
   const double *w = nullptr;            // [H]
+  unsigned long long *stamps = nullptr; // diagnostic build: shader cycles per mine_count phase [8]
   const double *afreq = nullptr;        // [L][amax]
   const uint8_t *anum = nullptr;        // [L+1]
   const uint8_t *npos = nullptr;        // [L+1] alleles with frequency > 0
