@@ -191,7 +191,7 @@ struct Ctx {
   // tuning
   int fcap = 2048, waves = 0;
   int lds_waves_per_cu = 4;  // E-step individuals (blocks) sharing one CU's 160 KiB LDS
-  int estep_nw = 2;          // E-step waves per individual
+  int estep_nw = 3;          // E-step waves per individual
   uint64_t trace_bytes = 0;
 
   Panel pan;
@@ -244,6 +244,8 @@ struct Ctx {
   DevBuf<unsigned long long> d_stamps;
   std::vector<double> h_total;
   std::vector<int32_t> h_ncand, h_status, h_sbase;
+  std::vector<int32_t> h_cost, h_order;  // E-step scheduling: per-individual cost, block-visit order
+  DevBuf<int32_t> d_cost, d_order;
   std::vector<unsigned long long> h_re;
   bool have_estep = false;
   std::vector<uint8_t> best_res;  // [n][2][L] accepted resolutions (allele index)
@@ -713,6 +715,25 @@ struct Ctx {
       a.S = S;
       a.indiv_begin = i0 + b;
       a.indiv_end = i0 + b + bn;
+      // heaviest individuals first (cost of the previous E-step; before the
+      // first one, the number of heterozygous or missing loci)
+      if ((int)h_cost.size() != n) {
+        h_cost.assign(n, 0);
+        for (int i = 0; i < n; ++i)
+          for (int k = 0; k < L; ++k) {
+            const uint8_t x = pan.idx[((size_t)(i0 + i) * 2) * L + k], y = pan.idx[((size_t)(i0 + i) * 2 + 1) * L + k];
+            h_cost[i] += (x != y || x == MISSING) ? 1 : 0;
+          }
+      }
+      h_order.resize(bn);
+      for (int q = 0; q < bn; ++q) h_order[q] = q;
+      std::stable_sort(h_order.begin(), h_order.end(),
+                       [&](int x, int y) { return h_cost[b + x] > h_cost[b + y]; });
+      if ((e = d_order.ensure(bn)) || (e = d_cost.ensure(n)) ||
+          (e = hipMemcpyAsync(d_order.p, h_order.data(), (size_t)bn * 4, hipMemcpyHostToDevice, st)))
+        return hipfail(e, "estep order");
+      a.order = d_order.p;
+      a.cost = d_cost.p + b;
       a.scratch = d_scratch.p;
       a.scratch_stride = per;
       a.fcap = fcap;
@@ -801,7 +822,8 @@ struct Ctx {
     if ((e = d_samp_lm.ensure((size_t)std::max(H, 1) * L))) return hipfail(e, "samples");
     if ((e = launch_transpose_u8(d_rows.p, d_samp_lm.p, H, L, H, 0, st))) return hipfail(e, "transpose");
     if ((e = hipMemcpyAsync(h_total.data(), d_total.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
-        (e = hipMemcpyAsync(h_re.data(), d_re.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)))
+        (e = hipMemcpyAsync(h_re.data(), d_re.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
+        (e = hipMemcpyAsync(h_cost.data(), d_cost.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)))
       return hipfail(e, "estep");
     std::vector<double> w(H);
     if (H && (e = hipMemcpyAsync(w.data(), d_w.p, (size_t)H * 8, hipMemcpyDeviceToHost, st))) return hipfail(e, "estep");

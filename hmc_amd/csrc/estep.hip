@@ -109,35 +109,35 @@ __device__ inline void set_link(const Lds &l, const Front &F, int t, int k, doub
   meta_ptr(l, F, t)[k] = m;
 }
 
-// One state's k-best list held in registers (static indices only).
-struct RegList {
-  double v[S_MAX];
-  uint32_t m[S_MAX];
-};
-// Load the first S links of a list; slots >= nl hold stale values the callers ignore.
-__device__ inline void load_list(RegList &r, const double *pl, const uint32_t *pm, int S) {
+// Copy the first ns links of predecessor state s into a successor list at
+// position k0, transformed as by the extension constructor / add
+// (HaploPair.cpp:35-61, 63-80).  Groups of 8 links: the loads of a group
+// issue together, few registers stay live.
+__device__ inline void copy_extended(const double *xl, const uint32_t *xm, double *yl, uint32_t *ym, int k0, int ns,
+                                     uint32_t s, double tpv, bool rev, bool differ) {
+  constexpr int GRP = 8;
+  for (int k = 0; k < ns; k += GRP) {
+    double v[GRP];
+    uint32_t m[GRP];
 #pragma unroll
-  for (int k = 0; k < S_MAX; ++k)
-    if (k < S) {
-      r.v[k] = pl[k];
-      r.m[k] = pm[k];
-    }
-}
-// Links of predecessor state s as they enter a successor: the extension
-// constructor / add transformation (HaploPair.cpp:35-61, 63-80).
-__device__ inline void extend_links(RegList &r, int S, uint32_t s, double tpv, bool rev, bool differ) {
-#pragma unroll
-  for (int k = 0; k < S_MAX; ++k)
-    if (k < S) {
-      double lk = r.v[k] * tpv;
-      bool homo = meta_homo(r.m[k]);
-      if (differ && homo) {
-        if (rev) lk = 0.0;
-        homo = false;
+    for (int u = 0; u < GRP; ++u)
+      if (k + u < ns) {
+        v[u] = xl[k + u];
+        m[u] = xm[k + u];
       }
-      r.v[k] = lk;
-      r.m[k] = meta_pack(s, (uint32_t)k, rev, homo, false);
-    }
+#pragma unroll
+    for (int u = 0; u < GRP; ++u)
+      if (k + u < ns) {
+        double lk = v[u] * tpv;
+        bool homo = meta_homo(m[u]);
+        if (differ && homo) {
+          if (rev) lk = 0.0;
+          homo = false;
+        }
+        yl[k0 + k + u] = lk;
+        ym[k0 + k + u] = meta_pack(s, (uint32_t)(k + u), rev, homo, false);
+      }
+  }
 }
 
 // Key table replacing m_best_pair: slot ids < hc are LDS slots, >= hc HBM slots.
@@ -243,33 +243,52 @@ __device__ inline unsigned long long trace_alloc(const EstepArgs &a, BlockShared
   return off;
 }
 
-// Stream the finished k-best lists of one locus into the trace store:
-// [Fn][Fn headers][Fn x S link words].
+// Trace record of one locus at word `off`: [Fn][Fn headers][pad to an even
+// word][Fn x S link words]; this is the word index of the link block.
+__host__ __device__ inline unsigned long long trace_links(unsigned long long off, uint32_t F) {
+  return (off + 1 + F + 1) & ~1ull;
+}
+
+// Stream the finished k-best lists of one locus into the trace store.
 __device__ inline bool write_trace(const EstepArgs &a, const Lds &l, BlockShared *bs, const Front &F, int Fn,
                                    int locus, int bi, unsigned long long &cur, unsigned long long &end) {
   const int S = a.S, NT = (int)blockDim.x;
-  const unsigned long long words = 1ull + (unsigned long long)Fn * (1 + S);
+  // +1: the link block starts on an even word (8-byte aligned), see trace_links()
+  const unsigned long long words = 2ull + (unsigned long long)Fn * (1 + S);
   const unsigned long long off = trace_alloc(a, bs, cur, end, words);
   if (off + words > a.trace_cap) return false;
   uint32_t *hdr = a.trace + off + 1;
-  uint32_t *lnk = hdr + Fn;
+  uint32_t *lnk = a.trace + trace_links(off, (uint32_t)Fn);
   for (int t = threadIdx.x; t < Fn; t += NT)
     hdr[t] = hdr_pack(a.mod.last[get_lo(l, F, t)], a.mod.last[get_hi(l, F, t)], get_nl(l, F, t));
-  const int nw = Fn * S;
-  constexpr int U = 4;
-  for (int w0 = 0; w0 < nw; w0 += U * NT) {
-    uint32_t v[U];
+  // one thread per state: its S link words (zero past nl), all loads issued
+  // before the stores (the source may be LDS or HBM); 8-byte pairs for even S
+  if ((S & 1) == 0) {
+    for (int t = threadIdx.x; t < Fn; t += NT) {
+      const uint32_t n = get_nl(l, F, t);
+      const uint2 *pm = (const uint2 *)meta_ptr(l, F, t);
+      uint2 *dst = (uint2 *)(lnk + (size_t)t * S);
+      uint2 v[S_MAX / 2];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int w = w0 + u * NT + (int)threadIdx.x;
-      const int t = w < nw ? w / S : 0, k = w - t * S;
-      const uint32_t n = get_nl(l, F, t), m = get_meta(l, F, t, w < nw ? k : 0);
-      v[u] = (uint32_t)k < n ? m : 0u;
+      for (int k = 0; k < S_MAX / 2; ++k)
+        if (2 * k < S) v[k] = pm[k];
+#pragma unroll
+      for (int k = 0; k < S_MAX / 2; ++k)
+        if (2 * k < S)
+          dst[k] = make_uint2((uint32_t)(2 * k) < n ? v[k].x : 0u, (uint32_t)(2 * k + 1) < n ? v[k].y : 0u);
     }
+  } else {
+    for (int t = threadIdx.x; t < Fn; t += NT) {
+      const uint32_t n = get_nl(l, F, t);
+      const uint32_t *pm = meta_ptr(l, F, t);
+      uint32_t *dst = lnk + (size_t)t * S;
+      uint32_t v[S_MAX];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int w = w0 + u * NT + (int)threadIdx.x;
-      if (w < nw) lnk[w] = v[u];
+      for (int k = 0; k < S_MAX; ++k)
+        if (k < S) v[k] = pm[k];
+#pragma unroll
+      for (int k = 0; k < S_MAX; ++k)
+        if (k < S) dst[k] = (uint32_t)k < n ? v[k] : 0u;
     }
   }
   if (threadIdx.x == 0) {
@@ -371,7 +390,7 @@ size_t estep_lds_bytes(int S, int fc, int hc, int nw) { return (size_t)lds_plan(
 #define STAMP_FLUSH
 #endif
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void estep_forward(EstepArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void estep_forward(EstepArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   STAMP_DECL
   const int S = a.S, L = a.pan.L, amax = a.pan.amax;
@@ -437,13 +456,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void e
   unsigned long long tcur = 0, tend = 0;
   __syncthreads();
 
-  for (int gi = a.indiv_begin + blockIdx.x; gi < a.indiv_end; gi += gridDim.x) {
-    const int bi = gi - a.indiv_begin;
+  // Individuals in the host's visit order (heaviest first: blocks b, b+256,
+  // ... share a CU, so the heaviest ones land on distinct CUs).
+  const int nbatch = a.indiv_end - a.indiv_begin;
+  for (int q = blockIdx.x; q < nbatch; q += gridDim.x) {
+    const int bi = a.order ? a.order[q] : q;
+    const int gi = a.indiv_begin + bi;
     const uchar2 *g = a.pan.geno_im + (size_t)gi * L;
     const int hl = a.mod.head_len;
-#ifdef HMC_STAMPS
     const unsigned long long t_indiv = __builtin_amdgcn_s_memtime();
-#endif
     int status = EST_OK;
     unsigned long long re = 0;
     int fbig = 0;
@@ -608,21 +629,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void e
         // first contribution of a key: extension constructor (HaploPair.cpp:35-61), thread-parallel
         if (valid && rank == 0) {
           const uint32_t ns = get_nl(l, X, s);
-          RegList r;
-          load_list(r, lik_ptr(l, X, s), meta_ptr(l, X, s), S);
-          extend_links(r, S, s, tpv, rev, differ);
           set_fwd(l, Y, st, fwd_s * tpv);
           set_lo(l, Y, st, lo);
           set_hi(l, Y, st, hi);
           set_nl(l, Y, st, ns);
-          double *yl = lik_ptr(l, Y, st);
-          uint32_t *ym = meta_ptr(l, Y, st);
-#pragma unroll
-          for (int k = 0; k < S_MAX; ++k)
-            if (k < S && (uint32_t)k < ns) {
-              yl[k] = r.v[k];
-              ym[k] = r.m[k];
-            }
+          copy_extended(lik_ptr(l, X, s), meta_ptr(l, X, s), lik_ptr(l, Y, st), meta_ptr(l, Y, st), 0, (int)ns, s, tpv,
+                        rev, differ);
         }
         // later contributions: HaploPair::add (HaploPair.cpp:63-89).  Round r
         // applies every contribution whose key rank inside the chunk is r, so
@@ -650,17 +662,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void e
             ns = get_nl(l, X, s);
             set_fwd(l, Y, st, get_fwd(l, Y, st) + fwd_s * tpv);
             if (k0 + ns <= (uint32_t)S) {  // room left: append, no selection
-              RegList x;
-              load_list(x, lik_ptr(l, X, s), meta_ptr(l, X, s), S);
-              extend_links(x, S, s, tpv, rev, differ);
-              double *yl = lik_ptr(l, Y, st);
-              uint32_t *ym = meta_ptr(l, Y, st);
-#pragma unroll
-              for (int q = 0; q < S_MAX; ++q)
-                if (q < S && (uint32_t)q < ns) {
-                  yl[k0 + q] = x.v[q];
-                  ym[k0 + q] = x.m[q];
-                }
+              copy_extended(lik_ptr(l, X, s), meta_ptr(l, X, s), lik_ptr(l, Y, st), meta_ptr(l, Y, st), (int)k0, (int)ns,
+                            s, tpv, rev, differ);
               set_nl(l, Y, st, k0 + ns);
             } else {
               sel = true;
@@ -762,6 +765,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void e
     if (lane == 0) atomicAdd(&bs->u[1], re);
     __syncthreads();
     if (tid == 0) {
+      if (a.cost) a.cost[bi] = (int32_t)((__builtin_amdgcn_s_memtime() - t_indiv) >> 10);
       if (a.max_states) atomicMax(a.max_states, (unsigned)(fbig > Fp ? fbig : Fp));
       a.re_count[bi] = bs->u[1];
       a.status[bi] = status;
@@ -830,7 +834,7 @@ __global__ __launch_bounds__(256) void estep_traceback(TracebackArgs a) {
     const uint32_t *r = a.trace + lo[j];
     const uint32_t F = r[0];
     const uint32_t hdr = r[1 + st];
-    const uint32_t m = r[1 + F + (size_t)st * S + idx];
+    const uint32_t m = a.trace[trace_links(lo[j], F) + (size_t)st * S + idx];
     row[ra][j - 1] = (uint8_t)(hdr & 0xFF);
     row[rb][j - 1] = (uint8_t)((hdr >> 8) & 0xFF);
     if (meta_rev(m)) { int t = ra; ra = rb; rb = t; }

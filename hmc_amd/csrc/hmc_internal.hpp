@@ -87,6 +87,8 @@ struct EstepArgs {
   unsigned long long *re_count;  // [batch]
   unsigned int *max_states;      // [1] running maximum frontier size
   int32_t *fmax;                 // [batch] largest frontier of each individual
+  const int32_t *order;          // [batch] individuals in block-visit order (nullptr: natural order)
+  int32_t *cost;                 // [batch] shader kcycles spent per individual (scheduling hint)
   unsigned long long *stamps;    // [20] diagnostic build: shader cycles per phase
   int diag_indiv;                // diagnostic build: stamp only this batch index (-1: all)
 };

@@ -286,11 +286,12 @@ __global__ __launch_bounds__(64) void mine_scatter(MineArgs a, int level, int pb
   const ParentView p = parent_view(a, level, pidx);
   if (!p.ok) return;
   const uint8_t *ca = a.pos_allele + (size_t)p.e * a.amax;
-  bool any = false;
-  for (int k = 0; k < p.nc; ++k) any |= (a.flags[p.cb + k] & NODE_EXT) != 0;
-  if (!any) return;
+  // lane k carries child k: extended?, list offset, entries written so far
+  const bool ext = lane < p.nc && (a.flags[p.cb + lane] & NODE_EXT);
+  const uint64_t extm = __ballot(ext);
+  if (!extm) return;
+  unsigned long long at0 = ext ? a.list_off[p.cb + lane] : 0ull;
   const uint64_t lt = (1ull << lane) - 1ull;
-  uint32_t run = 0;  // lane k: entries already written to child k's list
   constexpr int U = 4;  // chunks whose loads are in flight together
   for (int base = 0; base < p.n; base += U * WAVE) {
     EntryView xs[U];
@@ -301,18 +302,18 @@ __global__ __launch_bounds__(64) void mine_scatter(MineArgs a, int level, int pb
       if (base + u * WAVE >= p.n) break;
       const EntryView &x = xs[u];
       for (int k = 0; k < p.nc; ++k) {
-        const int c = p.cb + k;
-        if (!(a.flags[c] & NODE_EXT)) continue;
+        if (!((extm >> k) & 1ull)) continue;
         double v;
         const bool m = contribution(a, x, p.e, ca[k], v);
         const uint64_t b = __ballot(m);
-        const uint32_t rk = (uint32_t)__builtin_amdgcn_readlane((int)run, k);
+        const unsigned long long at = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(at0 >> 32), k) << 32) |
+                                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)at0, k);
         if (m) {
-          const unsigned long long at = a.list_off[c] + rk + (uint32_t)__popcll(b & lt);
-          a.lout_idx[at] = x.item;
-          if (a.genotype) a.lout_val[at] = v;
+          const unsigned long long q = at + (uint32_t)__popcll(b & lt);
+          a.lout_idx[q] = x.item;
+          if (a.genotype) a.lout_val[q] = v;
         }
-        if (lane == k) run += (uint32_t)__popcll(b);
+        if (lane == k) at0 += (unsigned long long)__popcll(b);
       }
     }
   }

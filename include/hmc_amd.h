@@ -137,7 +137,7 @@ int hmc_write_phase(hmc_ctx *ctx, const char *path);
  * waves: resident E-step waves (0 = automatic). */
 int hmc_set_tuning(hmc_ctx *ctx, int frontier_cap, uint64_t trace_bytes, int waves);
 /* E-step launch shape: wavefronts cooperating on one individual (1..4,
- * default 2) and individuals sharing one CU's LDS (default 4); 0 keeps the
+ * default 3) and individuals sharing one CU's LDS (default 4); 0 keeps the
  * current value.  Results do not depend on the shape. */
 int hmc_set_estep_shape(hmc_ctx *ctx, int waves_per_individual, int individuals_per_cu);
 /* Device time (ms, HIP events on the context stream) of the last E-step
