@@ -5,7 +5,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, hmc_amd
 from hmc_amd import synth
 m = hmc_amd.HaploModel()
-m.set_estep_shape(int(os.environ.get('HMC_NW', '2')), 4)
+m.set_estep_shape(int(os.environ.get('HMC_NW', '3')), 4)
 m.load(hmc_amd.GenoData.from_panel(synth.config_panel(int(sys.argv[1]) if len(sys.argv) > 1 else 2)))
 m.find_patterns()
 for it in range(3):
