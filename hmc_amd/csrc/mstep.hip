@@ -50,6 +50,7 @@ struct EntryView {
   double w;    // sample branch: weight
 };
 
+template <bool WANT_W = true>  // the scatter only needs the allele, not the weight
 __device__ inline EntryView load_entry(const MineArgs &a, bool root, const uint32_t *lidx, const double *lval,
                                        int i, int n, int e) {
   EntryView x;
@@ -65,7 +66,7 @@ __device__ inline EntryView load_entry(const MineArgs &a, bool root, const uint3
       x.g = a.geno_lm[(size_t)e * a.item_stride + x.item];
     } else {
       x.h = a.samp_lm[(size_t)e * a.item_stride + x.item];
-      x.w = a.w[x.item];
+      if (WANT_W) x.w = a.w[x.item];
     }
   }
   return x;
@@ -296,7 +297,7 @@ __global__ __launch_bounds__(64) void mine_scatter(MineArgs a, int level, int pb
   for (int base = 0; base < p.n; base += U * WAVE) {
     EntryView xs[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) xs[u] = load_entry(a, level == 1, p.lidx, p.lval, base + u * WAVE + lane, p.n, p.e);
+    for (int u = 0; u < U; ++u) xs[u] = load_entry<false>(a, level == 1, p.lidx, p.lval, base + u * WAVE + lane, p.n, p.e);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (base + u * WAVE >= p.n) break;

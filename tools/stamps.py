@@ -6,7 +6,7 @@ from hmc_amd import synth
 names = ["pairs/loop", "decode+fwd", "succ gather", "tp/last gather", "key insert", "grouping", "cnt/state", "rounds(create/add)", "trace+clear", "final select", "-", "-"]
 p = synth.config_panel(2)
 wpc = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-m = hmc_amd.HaploModel(); m.set_estep_shape(int(os.environ.get('HMC_NW', '2')), wpc); m.load(hmc_amd.GenoData.from_panel(p)); m.find_patterns()
+m = hmc_amd.HaploModel(); m.set_estep_shape(int(os.environ.get('HMC_NW', '3')), wpc); m.load(hmc_amd.GenoData.from_panel(p)); m.find_patterns()
 for it in range(2):
     ll, H, re = m.resolve_all()
     st = (C.c_uint64 * 20)()
