@@ -46,6 +46,7 @@ _SIGS = [
     ("hmc_load_phase", _i, [_vp, _cp]),
     ("hmc_load_genotypes", _i, [_vp, _i, _i, _P(C.c_int32), _cp]),
     ("hmc_panel_info", _i, [_vp, _P(_i), _P(_i), _P(_i)]),
+    ("hmc_shard_range", _i, [_vp, _P(_i), _P(_i)]),
     ("hmc_allele_table", _i, [_vp, _P(C.c_int32), _P(C.c_int32), _P(_d)]),
     ("hmc_find_patterns", _i, [_vp, _P(_i), _P(_u64)]),
     ("hmc_model_info", _i, [_vp, _P(_i), _P(_i)]),

@@ -303,10 +303,33 @@ struct Ctx {
   }
 
   // ---------------------------------------------------------------- panel --
+  // Contiguous shard of individuals, balanced by E-step cost: a
+  // base of L/8 plus the heterozygous-or-missing loci of each individual; the
+  // boundaries split the prefix sum evenly (identical on every rank).
+  void shard(int N, int L) {
+    if (world == 1) { i0 = 0; i1 = N; return; }
+    std::vector<double> pre((size_t)N + 1, 0.0);
+    for (int i = 0; i < N; ++i) {
+      int h = 0;
+      for (int k = 0; k < L; ++k) {
+        const uint8_t x = pan.idx[((size_t)i * 2) * L + k], y = pan.idx[((size_t)i * 2 + 1) * L + k];
+        h += (x != y || x == MISSING) ? 1 : 0;
+      }
+      pre[i + 1] = pre[i] + L / 8.0 + h;
+    }
+    auto cut = [&](int r) {
+      if (r <= 0) return 0;
+      if (r >= world) return N;
+      const double target = pre[N] * r / world;
+      return (int)(std::lower_bound(pre.begin(), pre.end(), target) - pre.begin());
+    };
+    i0 = cut(rank);
+    i1 = cut(rank + 1);
+  }
+
   int upload_panel() {
     const int N = pan.N, L = pan.L, A = pan.amax;
-    i0 = (int)((long long)N * rank / world);
-    i1 = (int)((long long)N * (rank + 1) / world);
+    shard(N, L);
     std::vector<uchar2> im((size_t)N * L), lm((size_t)L * N);
     for (int i = 0; i < N; ++i)
       for (int k = 0; k < L; ++k) {
@@ -1055,6 +1078,13 @@ int hmc_set_tuning(hmc_ctx *h, int frontier_cap, uint64_t trace_bytes, int waves
   if (frontier_cap > 0) h->c.fcap = std::min(frontier_cap, 65535);
   h->c.trace_bytes = trace_bytes;
   h->c.waves = waves;
+  return HMC_OK;
+}
+
+int hmc_shard_range(const hmc_ctx *h, int *i0, int *i1) {
+  if (!h || !i0 || !i1) return HMC_EARG;
+  *i0 = h->c.i0;
+  *i1 = h->c.i1;
   return HMC_OK;
 }
 

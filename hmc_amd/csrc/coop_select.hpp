@@ -66,6 +66,10 @@ struct Seg {
   uint32_t ltk;   // segment-relative: bits below k
 };
 
+// Lane mask of a predicate; unlike __ballot(int) the predicate stays a mask
+// (no 0/1 materialisation and re-compare).
+__device__ inline uint64_t wave_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
 // A wave ballot seen from this lane's segment (bit k = element k).
 __device__ inline uint32_t seg_bits(uint64_t ballot, const Seg &sg) { return (uint32_t)(ballot >> sg.base) & sg.wm; }
 
@@ -127,7 +131,7 @@ __device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, c
   while (true) {
     heap = heap || (act && last - first > 3 && depth == 0);
     const bool part = act && !heap && last - first > 3;
-    if (!__any(part)) break;
+    if (!wave_ballot(part)) break;
     depth -= part ? 1 : 0;
     // std::__move_median_to_first(first, first+1, mid, last-1) (stl_algo.h:79-102)
     const int a = first + 1, b = first + ((last - first) >> 1), c = last > 0 ? last - 1 : 0;
@@ -152,7 +156,7 @@ __device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, c
     const bool inr = part && sg.k >= first && sg.k < last;
     const bool isL = inr && !isf && !(v > pivot);
     const bool isR = inr && !(pivot > v);
-    const uint32_t Lw = seg_bits(__ballot(isL), sg), Rw = seg_bits(__ballot(isR), sg);
+    const uint32_t Lw = seg_bits(wave_ballot(isL), sg), Rw = seg_bits(wave_ballot(isR), sg);
     const int nL = __popc(Lw), nR = __popc(Rw);
     const int kL = __popc(Lw & sg.ltk);
     const int kR = nR - 1 - __popc(Rw & sg.ltk);
@@ -167,8 +171,8 @@ __device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, c
     const int dest = lsw ? sg.base + qR : (rsw ? sg.base + qL : lane);
     // cut = min(l_K, r_{K-1}): the first left stop that does not swap and the
     // leftmost right stop that does
-    const int lK = seg_lowest(seg_bits(__ballot(isL && !lsw), sg));
-    const int rK = seg_lowest(seg_bits(__ballot(rsw), sg));
+    const int lK = seg_lowest(seg_bits(wave_ballot(isL && !lsw), sg));
+    const int rK = seg_lowest(seg_bits(wave_ballot(rsw), sg));
     const int cut = lK < rK ? lK : rK;
     ss.slik[dest] = v;
     ss.smeta[dest] = m;
@@ -178,7 +182,7 @@ __device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, c
   }
   // Depth limit reached (std::__heap_select + iter_swap, stl_algo.h:1973-1979):
   // rare; the segment's first lane runs the sequential code on the slots.
-  if (__any(heap)) {
+  if (wave_ballot(heap)) {
     if (heap && sg.k == 0) {
       const LinkList wl{sl, sm, 1};
       heap_select(wl, first, nth + 1, last);
@@ -188,7 +192,7 @@ __device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, c
   }
   // std::__insertion_sort of the <= 3 remaining elements (stl_algo.h:1819-1849)
   const bool ins = act && !heap && last - first > 1;
-  if (__any(ins)) {
+  if (wave_ballot(ins)) {
     const int len = last - first;
     const int f0 = first < kmax ? first : kmax;
     const int f1 = first + 1 < kmax ? first + 1 : kmax, f2 = first + 2 < kmax ? first + 2 : kmax;

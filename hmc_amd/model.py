@@ -49,6 +49,27 @@ class GenoData:
         return cls(np.ascontiguousarray(panel.alleles, dtype=np.int32), panel.types)
 
 
+def balanced_shard(alleles: np.ndarray, rank: int, world: int) -> tuple[int, int]:
+    """Individuals [i0, i1) of `rank`: contiguous blocks whose E-step cost
+    (L/8 + heterozygous-or-missing loci per individual) splits evenly — the
+    rule of the library's Ctx::shard (hmc_shard_range)."""
+    a = np.asarray(alleles)
+    N, _, L = a.shape
+    if world == 1:
+        return 0, N
+    het = ((a[:, 0, :] != a[:, 1, :]) | (a[:, 0, :] < 0)).sum(axis=1)
+    pre = np.concatenate([[0.0], np.cumsum(L / 8.0 + het)])
+
+    def cut(r):
+        if r <= 0:
+            return 0
+        if r >= world:
+            return N
+        return int(np.searchsorted(pre, pre[N] * r / world, side="left"))
+
+    return cut(rank), cut(rank + 1)
+
+
 class HaploModel:
     """HaploModel (model "MV", sampling EM) on one MI355X, or one rank of a sharded run."""
 
@@ -144,8 +165,9 @@ class HaploModel:
         n, l, a = C.c_int(), C.c_int(), C.c_int()
         self._check(lib().hmc_panel_info(self._h, C.byref(n), C.byref(l), C.byref(a)))
         self.N, self.L, self.amax = n.value, l.value, a.value
-        self.i0 = self.N * self.rank // self.world
-        self.i1 = self.N * (self.rank + 1) // self.world
+        i0, i1 = C.c_int(), C.c_int()
+        self._check(lib().hmc_shard_range(self._h, C.byref(i0), C.byref(i1)))
+        self.i0, self.i1 = i0.value, i1.value
 
     def allele_table(self):
         num = np.zeros(self.L, np.int32)

@@ -64,6 +64,9 @@ int hmc_load_phase(hmc_ctx *ctx, const char *path);
  * Runs GenoData::checkAlleleSymbol (GenoData.cpp:78-118) and uploads. */
 int hmc_load_genotypes(hmc_ctx *ctx, int N, int L, const int32_t *alleles, const char *types);
 int hmc_panel_info(const hmc_ctx *ctx, int *N, int *L, int *max_alleles);
+/* This rank's individuals [i0, i1): contiguous blocks balanced by E-step cost
+ * (L/8 + heterozygous-or-missing loci per individual); [0, N) on one rank. */
+int hmc_shard_range(const hmc_ctx *ctx, int *i0, int *i1);
 /* Per-locus allele tables: num[L], sym[L][max_alleles], freq[L][max_alleles]
  * (GenoData::allele_num / allele_symbol / allele_frequency, GenoData.h:43-49). */
 int hmc_allele_table(const hmc_ctx *ctx, int32_t *num, int32_t *sym, double *freq);

@@ -25,8 +25,9 @@ def _free_port():
     return p
 
 
-def _shard(N, rank, world):  # same rule as Ctx::upload_panel
-    return N * rank // world, N * (rank + 1) // world
+def _shard(alleles, rank, world):  # the library's rule (Ctx::shard / hmc_shard_range)
+    from hmc_amd.model import balanced_shard
+    return balanced_shard(alleles, rank, world)
 
 
 def _worker(rank, world, port, q):
@@ -49,7 +50,7 @@ def _worker(rank, world, port, q):
         pt = full.patterns()
         min_freq = 1.5 / (2.0 * N)
 
-        i0, i1 = _shard(N, rank, world)
+        i0, i1 = _shard(p.alleles, rank, world)
         o = oracle.Oracle(p.alleles, p.types, sample_size=10)
         o.find_patterns()
         ll_loc = o.resolve_range(i0, i1)

@@ -331,6 +331,29 @@ def test_two_ranks_one_gpu_host_collective(oracle_mod, tmp_path):
     assert np.array_equal(outs[0]["m0_freq"], outs[1]["m0_freq"])
 
 
+def test_shard_ranges_balanced_and_tiling():
+    """Every rank's [i0, i1) from the library equals the documented rule
+    (hmc_amd.model.balanced_shard) and the ranges tile [0, N)."""
+    import ctypes as C
+    from hmc_amd.model import balanced_shard
+    p = panel("miss2")
+    L = hmc_amd.lib()
+    world, prev = 3, 0
+    noop = hmc_amd._lib.ALLREDUCE_FN(lambda buf, n, user: 0)
+    for r in range(world):
+        h = C.c_void_p()
+        assert L.hmc_ctx_create_hostcoll(0, r, world, noop, None, C.byref(h)) == 0
+        al = np.ascontiguousarray(p.alleles, dtype=np.int32)
+        assert L.hmc_load_genotypes(h, p.N, p.L, al.ctypes.data_as(C.POINTER(C.c_int32)), p.types.encode()) == 0
+        i0, i1 = C.c_int(), C.c_int()
+        assert L.hmc_shard_range(h, C.byref(i0), C.byref(i1)) == 0
+        assert (i0.value, i1.value) == balanced_shard(p.alleles, r, world)
+        assert i0.value == prev
+        prev = i1.value
+        L.hmc_ctx_destroy(h)
+    assert prev == p.N
+
+
 @pytest.mark.parametrize("name", ["a3miss5", "cfg1"])
 def test_estep_shape_invariance(oracle_mod, name):
     """1, 2 and 4 wavefronts per individual (and any LDS split) give the
