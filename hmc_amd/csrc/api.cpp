@@ -220,7 +220,7 @@ struct Ctx {
   DevBuf<double> n_freq, n_prefix, n_tp, n_sum;
   DevBuf<uint32_t> n_cnt, n_size, n_pos;
   DevBuf<unsigned long long> d_mstamps;  // diagnostic build: mine_count phase cycles
-  DevBuf<unsigned long long> n_list_off;
+  DevBuf<unsigned long long> n_list_off, n_region, d_r_region;
   size_t node_cap = 0;
   DevBuf<uint32_t> l_idx[2];
   DevBuf<double> l_val[2];
@@ -398,7 +398,7 @@ struct Ctx {
     hipError_t e;
 #define G(b) if ((e = b.grow_keep(cap, used, st))) return hipfail(e, "grow_nodes");
     G(n_parent) G(n_start) G(n_child_base) G(n_link) G(n_allele) G(n_flags) G(n_freq) G(n_prefix) G(n_tp) G(n_sum)
-    G(n_cnt) G(n_size) G(n_pos) G(n_list_off)
+    G(n_cnt) G(n_size) G(n_pos) G(n_list_off) G(n_region)
 #undef G
     node_cap = cap;
     return HMC_OK;
@@ -440,6 +440,8 @@ struct Ctx {
     a.child_base = n_child_base.p;
     a.link = n_link.p;
     a.list_off = n_list_off.p;
+    a.region = n_region.p;
+    a.r_region = d_r_region.p;
     a.r_child_base = d_r_child_base.p;
     a.rm = d_rm.p;
     return a;
@@ -472,9 +474,28 @@ struct Ctx {
     lend[1] = n1;
     int level = 1, pbeg = 0, pend = L;  // level-1 parents are the L roots
     int cur = 0;                        // list buffer holding the parents' lists
+    // child lists of the roots: root r owns npos[r] x n_items slots of the next buffer
+    unsigned long long next_total = 0;
+    {
+      const unsigned long long ni = (unsigned long long)mine_args(genotype).n_items;
+      std::vector<unsigned long long> rr(L);
+      for (int k = 0; k < L; ++k) {
+        rr[k] = next_total;
+        next_total += (unsigned long long)h_npos[k] * ni;
+      }
+      if ((e = d_r_region.ensure(L)) ||
+          (e = hipMemcpyAsync(d_r_region.p, rr.data(), (size_t)L * 8, hipMemcpyHostToDevice, st)))
+        return hipfail(e, "mine");
+    }
     while (true) {
       const int cb = lbeg[level], ce = lend[level], nlev = ce - cb;
+      const int nxt = cur ^ 1;  // children's lists are written here during the count
+      if ((e = l_idx[nxt].ensure(std::max<unsigned long long>(next_total, 1)))) return hipfail(e, "mine lists");
+      if (genotype && (e = l_val[nxt].ensure(std::max<unsigned long long>(next_total, 1))))
+        return hipfail(e, "mine lists");
       MineArgs a = mine_args(genotype);
+      a.lout_idx = l_idx[nxt].p;
+      a.lout_val = genotype ? l_val[nxt].p : nullptr;
       a.denom = genotype ? (double)pan.N : total_weight;
       a.min_freq = mf;
       a.min_len = mnl;
@@ -545,16 +566,8 @@ struct Ctx {
       unsigned long long tot[2];
       if ((e = hipMemcpyAsync(tot, d_totals.p, 16, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
         return hipfail(e, "mine");
-      const size_t list_total = tot[0];
+      next_total = tot[0];  // list slots the next level's children need
       const int nnext = (int)tot[1];
-      const int nxt = cur ^ 1;
-      if (list_total > 0) {
-        if ((e = l_idx[nxt].ensure(list_total))) return hipfail(e, "mine lists");
-        if (genotype && (e = l_val[nxt].ensure(list_total))) return hipfail(e, "mine lists");
-        a.lout_idx = l_idx[nxt].p;
-        a.lout_val = genotype ? l_val[nxt].p : nullptr;
-        if ((e = launch_mine_scatter(a, level, pbeg, pend, st))) return hipfail(e, "mine_scatter");
-      }
       cur = nxt;
       if (nnext == 0) break;
       pbeg = cb;

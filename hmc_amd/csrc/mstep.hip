@@ -19,8 +19,9 @@
 //                 `total_freq += ...` loops.
 //   mine_finalize frequency, prefix frequency, transition probability and the
 //                 accept / extend rules of searchPattern.
-//   mine_scatter  stable partition of the parent list into the children's
-//                 lists (ballot + prefix popcount), for extended children only.
+//                 The same pass writes the stable partition of the parent
+//                 list into the children's lists (child k of a parent with n
+//                 entries owns n slots at region + k*n of the next buffer).
 // After the last level the DFS pre-order of the reference (start L-1 first,
 // then descending allele index; PatternManager.cpp:94-97,112-113) is rebuilt
 // from subtree sizes (bottom-up) and positions (top-down): position = pattern
@@ -143,8 +144,13 @@ constexpr int CROW = WAVE + 18;  // LDS row stride (doubles): one chunk's contri
 #define MSTAMP(k) do { } while (0)
 #endif
 
+// Counting and the matching-list partition in one pass: child k of a parent
+// with n entries owns n slots at region + k*n of the next list buffer, so the
+// children's lists are written while the parent list streams through, before
+// any child is known to be extended (lists of children that are not extended
+// are simply never read).
 __global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg, int pend) {
-  extern __shared__ __align__(16) double cbuf[];  // [nc][CROW]
+  extern __shared__ __align__(16) double cbuf[];  // [nc][CROW] contributions, then [nc][WAVE] items
   const int tid = threadIdx.x, lane = tid;
   const int pidx = pbeg + blockIdx.x;
   if (pidx >= pend) return;
@@ -154,10 +160,13 @@ __global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg
   const ParentView p = parent_view(a, level, pidx);
   MSTAMP(0);
   if (!p.ok) return;
+  uint32_t *ibuf = (uint32_t *)(cbuf + (size_t)p.nc * CROW);
   const uint8_t *ca = a.pos_allele + (size_t)p.e * a.amax;
   const uint64_t lt = (1ull << lane) - 1ull;
+  const unsigned long long region = level == 1 ? a.r_region[pidx] : a.region[pidx];
+  const bool write_lists = a.lout_idx != nullptr;
   double sum = 0.0;
-  uint32_t cnt = 0;
+  uint32_t cnt = 0, run = 0;  // lane k: child k's entries so far
   constexpr int U = 4;  // chunks whose loads are in flight together
   for (int base = 0; base < p.n; base += U * WAVE) {
     EntryView xs[U];
@@ -170,8 +179,8 @@ __global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg
       const EntryView &x = xs[u];
       // Each child's matching entries, compacted in list order.  Non-matching
       // entries would add +0.0, an exact no-op on a sum >= +0, so skipping them
-      // leaves every child's add chain — and its rounding — unchanged.
-      // Rows are pre-filled with +0.0 so the summation below can run whole
+      // leaves every child's add chain — and its rounding — unchanged.  Rows
+      // are pre-filled with +0.0 so the summation below can run whole
       // 16-value batches without predication (x + 0.0 == x exactly).
       int mine = 0;
       for (int k = 0; k < p.nc; ++k) {
@@ -180,13 +189,27 @@ __global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg
         const uint64_t b = __ballot(m);
         cbuf[k * CROW + lane] = 0.0;
         if (lane < 16) cbuf[k * CROW + WAVE + lane] = 0.0;
-        if (m) cbuf[k * CROW + __popcll(b & lt)] = c;
+        if (m) {
+          cbuf[k * CROW + __popcll(b & lt)] = c;
+          ibuf[k * WAVE + __popcll(b & lt)] = x.item;
+        }
         if (lane == k) mine = __popcll(b);
       }
       __syncthreads();
       MSTAMP(2);
+      if (write_lists)  // child k's new entries, one coalesced store per child
+        for (int k = 0; k < p.nc; ++k) {
+          const int mk = __builtin_amdgcn_readlane(mine, k);
+          const uint32_t rk = (uint32_t)__builtin_amdgcn_readlane((int)run, k);
+          if (lane < mk) {
+            const unsigned long long at = region + (unsigned long long)k * (unsigned long long)p.n + rk + lane;
+            a.lout_idx[at] = ibuf[k * WAVE + lane];
+            if (a.genotype) a.lout_val[at] = cbuf[k * CROW + lane];
+          }
+        }
       if (lane < p.nc) {
         cnt += (uint32_t)mine;
+        run += (uint32_t)mine;
         double s = sum;
         const double2 *row = (const double2 *)(cbuf + lane * CROW);
         // 16 values per batch: the reads issue together, the adds stay one
@@ -213,6 +236,7 @@ __global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg
     const uint8_t al = ca[lane_c];
     a.sum[c] = sum;
     a.cnt[c] = cnt;
+    a.list_off[c] = region + (unsigned long long)lane_c * (unsigned long long)p.n;
     a.start[c] = p.start;
     a.allele[c] = al;
     a.prefix[c] = p.pfreq;
@@ -259,7 +283,8 @@ __global__ void mine_finalize(MineArgs a, int level, int b, int e, unsigned long
   const bool acc = (freq >= a.min_freq || level <= a.min_len) && level > 0 && level >= a.min_len;
   const bool ext = (freq >= a.min_freq || level < a.min_len) && (st + level < a.L) && (level < a.max_len);
   a.flags[c] = (acc ? NODE_ACC : 0) | (ext ? NODE_EXT : 0);
-  ext_list[c - b] = ext ? a.cnt[c] : 0ull;
+  // the node's children will need nc x cnt list slots (mine_count)
+  ext_list[c - b] = ext ? (unsigned long long)a.npos[st + level] * a.cnt[c] : 0ull;
   next_children[c - b] = ext ? (int32_t)a.npos[st + level] : 0;
 }
 
@@ -268,7 +293,7 @@ __global__ void mine_apply_offsets(MineArgs a, int b, int e, const unsigned long
   const int c = b + blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= e) return;
   const bool ext = a.flags[c] & NODE_EXT;
-  a.list_off[c] = ext ? list_scan[c - b] : 0ull;
+  a.region[c] = ext ? list_scan[c - b] : 0ull;
   a.child_base[c] = ext ? next_base + child_scan[c - b] : -1;
 }
 
@@ -277,46 +302,6 @@ __global__ void scan_totals(const unsigned long long *ls, const unsigned long lo
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     out[0] = n ? ls[n - 1] + lv[n - 1] : 0ull;
     out[1] = n ? (unsigned long long)(cs[n - 1] + cv[n - 1]) : 0ull;
-  }
-}
-
-__global__ __launch_bounds__(64) void mine_scatter(MineArgs a, int level, int pbeg, int pend) {
-  const int lane = threadIdx.x;
-  const int pidx = pbeg + blockIdx.x;
-  if (pidx >= pend) return;
-  const ParentView p = parent_view(a, level, pidx);
-  if (!p.ok) return;
-  const uint8_t *ca = a.pos_allele + (size_t)p.e * a.amax;
-  // lane k carries child k: extended?, list offset, entries written so far
-  const bool ext = lane < p.nc && (a.flags[p.cb + lane] & NODE_EXT);
-  const uint64_t extm = __ballot(ext);
-  if (!extm) return;
-  unsigned long long at0 = ext ? a.list_off[p.cb + lane] : 0ull;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  constexpr int U = 4;  // chunks whose loads are in flight together
-  for (int base = 0; base < p.n; base += U * WAVE) {
-    EntryView xs[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) xs[u] = load_entry<false>(a, level == 1, p.lidx, p.lval, base + u * WAVE + lane, p.n, p.e);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (base + u * WAVE >= p.n) break;
-      const EntryView &x = xs[u];
-      for (int k = 0; k < p.nc; ++k) {
-        if (!((extm >> k) & 1ull)) continue;
-        double v;
-        const bool m = contribution(a, x, p.e, ca[k], v);
-        const uint64_t b = __ballot(m);
-        const unsigned long long at = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(at0 >> 32), k) << 32) |
-                                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)at0, k);
-        if (m) {
-          const unsigned long long q = at + (uint32_t)__popcll(b & lt);
-          a.lout_idx[q] = x.item;
-          if (a.genotype) a.lout_val[q] = v;
-        }
-        if (lane == k) at0 += (unsigned long long)__popcll(b);
-      }
-    }
   }
 }
 
@@ -443,7 +428,7 @@ __global__ void mine_succ(MineArgs a, PatternTable t, int P) {
 // ---- host-side launch helpers -----------------------------------------------
 hipError_t launch_mine_count(const MineArgs &a, int level, int pbeg, int pend, hipStream_t st) {
   if (pend <= pbeg) return hipSuccess;
-  const size_t lds = (size_t)a.amax * CROW * 8;
+  const size_t lds = (size_t)a.amax * CROW * 8 + (size_t)a.amax * WAVE * 4;
   static size_t lds_attr = 0;
   if (lds > 65536 - 1024 && lds > lds_attr) {  // many alleles: opt in to the CU's full LDS
     hipError_t e = hipFuncSetAttribute((const void *)mine_count, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -481,11 +466,6 @@ size_t mine_scan_tmp_bytes(int n) {
   hipcub::DeviceScan::ExclusiveSum(nullptr, a, (unsigned long long *)nullptr, (unsigned long long *)nullptr, n);
   hipcub::DeviceScan::ExclusiveSum(nullptr, b, (int32_t *)nullptr, (int32_t *)nullptr, n);
   return a > b ? a : b;
-}
-hipError_t launch_mine_scatter(const MineArgs &a, int level, int pbeg, int pend, hipStream_t st) {
-  if (pend <= pbeg) return hipSuccess;
-  hipLaunchKernelGGL(mine_scatter, dim3(pend - pbeg), dim3(WAVE), 0, st, a, level, pbeg, pend);
-  return hipGetLastError();
 }
 hipError_t launch_mine_size(const MineArgs &a, int level, int b, int e, hipStream_t st) {
   if (e <= b) return hipSuccess;

@@ -32,7 +32,9 @@ struct MineArgs {
   double *freq = nullptr, *prefix = nullptr, *tp = nullptr, *sum = nullptr;
   uint32_t *cnt = nullptr, *size = nullptr, *pos = nullptr;
   int32_t *child_base = nullptr, *link = nullptr;
-  unsigned long long *list_off = nullptr;
+  unsigned long long *list_off = nullptr;  // node -> its matching list in the level's list buffer
+  unsigned long long *region = nullptr;    // extended node -> its children's lists in the next buffer (nc x cnt)
+  const unsigned long long *r_region = nullptr;  // [L] the same for the roots
   const int32_t *r_child_base = nullptr;  // [L+1]
   // matching lists of the parent level (in) and the child level (out)
   const uint32_t *lin_idx = nullptr;
@@ -57,7 +59,6 @@ hipError_t launch_mine_offsets(const MineArgs &a, int b, int e, unsigned long lo
                                unsigned long long *list_scan, int32_t *child_scan, int next_base, void *tmp,
                                size_t tmp_bytes, unsigned long long *totals, hipStream_t st);
 size_t mine_scan_tmp_bytes(int n);
-hipError_t launch_mine_scatter(const MineArgs &a, int level, int pbeg, int pend, hipStream_t st);
 hipError_t launch_mine_size(const MineArgs &a, int level, int b, int e, hipStream_t st);
 hipError_t launch_mine_root_size(const MineArgs &a, uint32_t *rsize, hipStream_t st);
 hipError_t launch_mine_pos(const MineArgs &a, int level, int pbeg, int pend, const uint32_t *rpos, hipStream_t st);
