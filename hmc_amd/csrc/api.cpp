@@ -886,12 +886,17 @@ struct Ctx {
   }
 
   // Largest LDS frontier tier that fits lds_waves_per_cu waves per CU.
+  // Largest LDS frontier tier for the block's LDS share; the LDS key table
+  // gets at least `key_factor` x fc slots (a power of two).
+  int lds_key_factor = 1;
   void lds_tier(int S, int &fc, int &hc) const {
     const int budget = 160 * 1024 / std::max(1, lds_waves_per_cu) - 256;
     fc = 0;
     hc = 64;
-    for (int f = 4096; f >= 0; f -= 16) {
-      const int h = next_pow2(std::max(64, 2 * f));
+    int kf = lds_key_factor;
+    if (const char *env = getenv("HMC_KEY_FACTOR")) kf = std::max(1, atoi(env));  // tuning experiments
+    for (int f = 4096; f >= 0; f -= 4) {
+      const int h = next_pow2(std::max(64, kf * f));
       if ((int)estep_lds_bytes(S, f, h, estep_nw) <= budget) { fc = f; hc = h; return; }
     }
   }
