@@ -251,9 +251,21 @@ struct Ctx {
   std::vector<uint8_t> best_res;  // [n][2][L] accepted resolutions (allele index)
   bool have_best = false;
 
+  // split E-step (estep_split.hip): structure pass + value pass, fused
+  // kernel as the exact fallback for underflowing individuals
+  enum { ESTEP_SPLIT = 0, ESTEP_FUSED = 1 };
+  int estep_mode = ESTEP_SPLIT;
+  DevBuf<char> d_scr1, d_scr2;
+  DevBuf<uint32_t> d_rec;
+  DevBuf<unsigned long long> d_rec_off, d_rec_cursor;
+  std::vector<int32_t> h_status1, h_redo;
+  DevBuf<int32_t> d_redo;
+  int n_fallback = 0;  // individuals re-run on the fused kernel by the last E-step
+
   // timings
   hipEvent_t ev[6] = {};
   double ms_fwd = 0, ms_tb = 0, ms_m = 0;
+  double ms_s1 = 0, ms_s2 = 0, ms_fb = 0;  // split E-step: structure, values, fused fallback
 
   int fail(int code, const char *fmt, ...) {
     char buf[1024];
@@ -734,12 +746,14 @@ struct Ctx {
     int Hacc = 0;
     int b = 0, batch = n;
     ms_fwd = ms_tb = 0;
+    ms_s1 = ms_s2 = ms_fb = 0;
+    n_fallback = 0;
     while (b < n) {
       const int bn = std::min(batch, n - b);
       const int hcap = next_pow2(2 * fcap);
       const size_t per = estep_scratch_bytes(fcap, hcap, S, estep_nw);
       const int grid = std::min(G, bn);
-      if ((e = d_scratch.ensure(per * grid))) {
+      if (estep_mode == ESTEP_FUSED && (e = d_scratch.ensure(per * grid))) {
         if (e == hipErrorOutOfMemory && fcap > 256) { fcap /= 2; continue; }
         return hipfail(e, "estep scratch");
       }
@@ -792,7 +806,13 @@ struct Ctx {
       a.fmax = d_fmax.p + b;
       a.stamps = d_stamps.p;
       a.diag_indiv = -1;
+      a.n_order = bn;
       if (const char *di = getenv("HMC_DIAG_INDIV")) a.diag_indiv = atoi(di) - b;
+      if (estep_mode == ESTEP_SPLIT) {
+        const int rc = run_split(a, b, bn, G, cap_bytes, batch);
+        if (rc < 0) return rc;
+        if (rc == 1) continue;
+      } else {
       hipEventRecord(ev[0], st);
       if ((e = launch_estep(a, grid, estep_nw, st))) return hipfail(e, "estep_forward launch");
       hipEventRecord(ev[1], st);
@@ -825,6 +845,7 @@ struct Ctx {
         batch = std::max(1, bn / 2);
         continue;
       }
+      }
       // sample rows of this batch (HaploModel.cpp:105-106: candidates in order, h0 then h1)
       for (int i = b; i < b + bn; ++i) {
         h_sbase[i] = Hacc;
@@ -850,10 +871,12 @@ struct Ctx {
       if ((e = launch_traceback(t, 0, st))) return hipfail(e, "traceback");
       hipEventRecord(ev[3], st);
       if ((e = hipStreamSynchronize(st))) return hipfail(e, "traceback");
-      hipEventElapsedTime(&ms, ev[2], ev[3]);
-      ms_tb += ms;
+      float ms_t = 0;
+      hipEventElapsedTime(&ms_t, ev[2], ev[3]);
+      ms_tb += ms_t;
       b += bn;
     }
+    if (estep_mode == ESTEP_SPLIT) ms_fwd = ms_s1 + ms_s2 + ms_fb;
     H = Hacc;
     if ((e = d_samp_lm.ensure((size_t)std::max(H, 1) * L))) return hipfail(e, "samples");
     if ((e = launch_transpose_u8(d_rows.p, d_samp_lm.p, H, L, H, 0, st))) return hipfail(e, "transpose");
@@ -883,6 +906,204 @@ struct Ctx {
     if (H_out) *H_out = H;
     if (re_out) *re_out = re;
     return HMC_OK;
+  }
+
+  // One batch [b, b+bn) through the split E-step.  Returns 0 when the batch
+  // is done, 1 when it must be re-run (a capacity grew or the batch was
+  // halved), or a negative HMC_E* code.
+  int run_split(EstepArgs &a, int b, int bn, int G, uint64_t cap_bytes, int &batch) {
+    hipError_t e;
+    const int S = a.S, L = pan.L;
+    int dev_cu = 256;
+    hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, device);
+    float ms = 0;
+    // ---- pass 1: structure records ------------------------------------------
+    const int hcap1 = next_pow2(2 * fcap), ccap1 = 8 * fcap;
+    const int bpc1 = std::max(lds_waves_per_cu, bn > 4 * dev_cu ? 8 : 4);
+    const int grid1 = std::max(1, std::min(bn, dev_cu * bpc1));
+    const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1);
+    if ((e = d_scr1.ensure(per1 * grid1))) return hipfail(e, "estep pass-1 scratch");
+    const uint64_t rec_want =
+        std::min<uint64_t>(cap_bytes, std::max<uint64_t>((uint64_t)bn * L * 640 * 4, 64ull << 20));
+    if (d_rec.n * 4 < rec_want) {
+      d_rec.release();
+      if ((e = d_rec.ensure(rec_want / 4))) return hipfail(e, "record alloc");
+    }
+    if ((e = d_rec_off.ensure((size_t)bn * (L + 1))) || (e = d_rec_cursor.ensure(1)) ||
+        (e = hipMemsetAsync(d_rec_cursor.p, 0, 8, st)))
+      return hipfail(e, "record alloc");
+    StructArgs s1;
+    s1.pan = a.pan;
+    s1.mod = a.mod;
+    s1.S = S;
+    s1.indiv_begin = a.indiv_begin;
+    s1.order = a.order;
+    s1.n_order = bn;
+    s1.scratch = d_scr1.p;
+    s1.scratch_stride = per1;
+    s1.fcap = fcap;
+    s1.hcap = hcap1;
+    s1.ccap = ccap1;
+    s1_tier(160 * 1024 / bpc1 - 256, s1.lds_fc, s1.lds_hc, s1.lds_cc);
+    s1.rec = d_rec.p;
+    s1.rec_cap = d_rec.n;
+    s1.rec_cursor = d_rec_cursor.p;
+    s1.rec_off = d_rec_off.p;
+    s1.status = a.status;
+    s1.re_count = a.re_count;
+    s1.fmax = a.fmax;
+    s1.max_states = a.max_states;
+    hipEventRecord(ev[0], st);
+    if ((e = launch_estep_structure(s1, grid1, st))) return hipfail(e, "estep_structure launch");
+    hipEventRecord(ev[1], st);
+    if ((e = hipMemcpyAsync(h_status.data() + b, a.status, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
+        (e = hipStreamSynchronize(st)))
+      return hipfail(e, "estep_structure");
+    hipEventElapsedTime(&ms, ev[0], ev[1]);
+    ms_s1 += ms;
+    bool ovf_front = false, ovf_rec = false;
+    for (int i = b; i < b + bn; ++i) {
+      if (h_status[i] == EST_NO_HEAD_PATTERN) return fail(HMC_ENOPATTERN, "Can not find matching pattern!");
+      if (h_status[i] == EST_OVERFLOW_FRONTIER) ovf_front = true;
+      if (h_status[i] == EST_OVERFLOW_REC) ovf_rec = true;
+    }
+    if (ovf_front) {
+      if (fcap >= 65535) return fail(HMC_EUNSUPPORTED, "frontier exceeds 65535 states");
+      fcap = std::min(65535, fcap * 2);
+      return 1;
+    }
+    if (ovf_rec) {
+      if (d_rec.n * 4 < cap_bytes) {
+        const uint64_t nb = std::min<uint64_t>(cap_bytes, d_rec.n * 4 * 4);
+        d_rec.release();
+        if ((e = d_rec.ensure(nb / 4))) return hipfail(e, "record alloc");
+        return 1;
+      }
+      if (bn == 1) return fail(HMC_ENOMEM, "record store too small for one individual");
+      batch = std::max(1, bn / 2);
+      return 1;
+    }
+    h_status1.assign(h_status.begin() + b, h_status.begin() + b + bn);
+    // ---- pass 2: values --------------------------------------------------------
+    const int grid2 = std::max(1, std::min(G, bn));
+    const size_t per2 = estep_s2_scratch_bytes(fcap, S);
+    if ((e = d_scr2.ensure(per2 * grid2))) return hipfail(e, "estep pass-2 scratch");
+    ValueArgs v;
+    v.S = S;
+    v.L = L;
+    v.head_len = head_len;
+    v.order = a.order;
+    v.n_order = bn;
+    v.rec = d_rec.p;
+    v.rec_off = d_rec_off.p;
+    v.scratch = d_scr2.p;
+    v.scratch_stride = per2;
+    v.fcap = fcap;
+    v.lds_fc = s2_tier(S);
+    v.trace = d_trace.p;
+    v.trace_cap = d_trace.n;
+    v.trace_cursor = d_trace_cursor.p;
+    v.loc_off = d_loc_off.p;
+    v.status = a.status;
+    v.total = a.total;
+    v.ncand = a.ncand;
+    v.cand_state = a.cand_state;
+    v.cand_idx = a.cand_idx;
+    v.prior = a.prior;
+    v.posterior = a.posterior;
+    v.weight = a.weight;
+    v.cost = a.cost;
+    v.stamps = d_stamps.p;
+    hipEventRecord(ev[0], st);
+    if ((e = launch_estep_values(v, grid2, estep_nw, st))) return hipfail(e, "estep_values launch");
+    hipEventRecord(ev[1], st);
+    if ((e = hipMemcpyAsync(h_status.data() + b, a.status, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
+        (e = hipMemcpyAsync(h_ncand.data() + b, a.ncand, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
+        (e = hipStreamSynchronize(st)))
+      return hipfail(e, "estep_values");
+    hipEventElapsedTime(&ms, ev[0], ev[1]);
+    ms_s2 += ms;
+    h_redo.clear();
+    bool ovf_trace = false;
+    for (int i = b; i < b + bn; ++i) {
+      if (h_status[i] == EST_OVERFLOW_TRACE) ovf_trace = true;
+      if (h_status[i] == EST_NEEDS_EXACT) h_redo.push_back(i - b);
+    }
+    if (ovf_trace) {
+      if (d_trace.n * 4 < cap_bytes) {  // grow the store before splitting the batch
+        const uint64_t nb = std::min<uint64_t>(cap_bytes, d_trace.n * 4 * 4);
+        d_trace.release();
+        if ((e = d_trace.ensure(nb / 4))) return hipfail(e, "trace alloc");
+        return 1;
+      }
+      if (bn == 1) return fail(HMC_ENOMEM, "trace store too small for one individual");
+      batch = std::max(1, bn / 2);
+      return 1;
+    }
+    // ---- exact fallback: individuals whose forward likelihood underflowed ----
+    n_fallback += (int)h_redo.size();
+    if (!h_redo.empty()) {
+      const int nr = (int)h_redo.size();
+      const int grid = std::min(G, nr);
+      const size_t per = estep_scratch_bytes(fcap, a.hcap, S, estep_nw);
+      if ((e = d_scratch.ensure(per * grid)) || (e = d_redo.ensure(nr)) ||
+          (e = hipMemcpyAsync(d_redo.p, h_redo.data(), (size_t)nr * 4, hipMemcpyHostToDevice, st)))
+        return hipfail(e, "estep fallback");
+      EstepArgs f = a;
+      f.scratch = d_scratch.p;
+      f.order = d_redo.p;
+      f.n_order = nr;
+      f.trace_cap = d_trace.n;
+      f.trace = d_trace.p;
+      hipEventRecord(ev[0], st);
+      if ((e = launch_estep(f, grid, estep_nw, st))) return hipfail(e, "estep_forward launch");
+      hipEventRecord(ev[1], st);
+      if ((e = hipMemcpyAsync(h_status.data() + b, a.status, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
+          (e = hipMemcpyAsync(h_ncand.data() + b, a.ncand, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
+          (e = hipStreamSynchronize(st)))
+        return hipfail(e, "estep_forward");
+      hipEventElapsedTime(&ms, ev[0], ev[1]);
+      ms_fb += ms;
+      for (int r : h_redo) {
+        const int s = h_status[b + r];
+        if (s == EST_OVERFLOW_FRONTIER) {
+          if (fcap >= 65535) return fail(HMC_EUNSUPPORTED, "frontier exceeds 65535 states");
+          fcap = std::min(65535, fcap * 2);
+          return 1;
+        }
+        if (s == EST_OVERFLOW_TRACE) {
+          if (d_trace.n * 4 >= cap_bytes) {
+            if (bn == 1) return fail(HMC_ENOMEM, "trace store too small for one individual");
+            batch = std::max(1, bn / 2);
+            return 1;
+          }
+          const uint64_t nb = std::min<uint64_t>(cap_bytes, d_trace.n * 4 * 4);
+          d_trace.release();
+          if ((e = d_trace.ensure(nb / 4))) return hipfail(e, "trace alloc");
+          return 1;
+        }
+      }
+    }
+    return 0;
+  }
+
+  // LDS tiers of pass 1 (one wave per individual, `budget` bytes): states per
+  // frontier, key slots (2x, power of two), contributions per locus (2x).
+  static void s1_tier(int budget, int &fc, int &hc, int &cc) {
+    for (int f = 1024; f >= 16; f -= 16) {
+      const int h = next_pow2(2 * f), c = 2 * f;
+      if ((int)estep_s1_lds_bytes(f, h, c) <= budget) { fc = f; hc = h; cc = c; return; }
+    }
+    fc = 0;
+    hc = 16;
+    cc = 0;
+  }
+  // LDS tier of pass 2: states per frontier for the block's LDS share.
+  int s2_tier(int S) const {
+    const int budget = 160 * 1024 / std::max(1, lds_waves_per_cu) - 256;
+    for (int f = 4096; f >= 4; f -= 4)
+      if ((int)estep_s2_lds_bytes(S, f, estep_nw) <= budget) return f;
+    return 0;
   }
 
   // Largest LDS frontier tier that fits lds_waves_per_cu waves per CU.
@@ -1103,6 +1324,22 @@ int hmc_shard_range(const hmc_ctx *h, int *i0, int *i1) {
   if (!h || !i0 || !i1) return HMC_EARG;
   *i0 = h->c.i0;
   *i1 = h->c.i1;
+  return HMC_OK;
+}
+
+int hmc_set_estep_mode(hmc_ctx *h, int mode) {
+  if (!h || mode < 0 || mode > 1) return HMC_EARG;
+  h->c.estep_mode = mode;
+  return HMC_OK;
+}
+
+int hmc_last_estep_split(const hmc_ctx *h, double *structure_ms, double *values_ms, double *fallback_ms,
+                         int *n_fallback) {
+  if (!h) return HMC_EARG;
+  if (structure_ms) *structure_ms = h->c.ms_s1;
+  if (values_ms) *values_ms = h->c.ms_s2;
+  if (fallback_ms) *fallback_ms = h->c.ms_fb;
+  if (n_fallback) *n_fallback = h->c.n_fallback;
   return HMC_OK;
 }
 

@@ -30,17 +30,13 @@
 #include "hmc_internal.hpp"
 #include "select.hpp"
 #include "coop_select.hpp"
+#include "estep_common.hpp"
 
 namespace hmc {
 
 namespace {
 
-constexpr unsigned long long KEY_EMPTY = ~0ull;
-constexpr unsigned long long TRACE_CHUNK = 1ull << 16;  // words per bump allocation
-constexpr int NP_MAX = A_MAX * (A_MAX + 1) / 2;          // allele pairs at a fully missing locus
-constexpr int PROBE_LDS = 16;                            // LDS probes before a key goes to the HBM table
 
-__host__ __device__ inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // HBM-tier arrays of one frontier (states fc .. fcap-1 of the wave).
 struct FrontG {
@@ -109,37 +105,6 @@ __device__ inline void set_link(const Lds &l, const Front &F, int t, int k, doub
   meta_ptr(l, F, t)[k] = m;
 }
 
-// Copy the first ns links of predecessor state s into a successor list at
-// position k0, transformed as by the extension constructor / add
-// (HaploPair.cpp:35-61, 63-80).  Groups of 8 links: the loads of a group
-// issue together, few registers stay live.
-__device__ inline void copy_extended(const double *xl, const uint32_t *xm, double *yl, uint32_t *ym, int k0, int ns,
-                                     uint32_t s, double tpv, bool rev, bool differ) {
-  constexpr int GRP = 8;
-  for (int k = 0; k < ns; k += GRP) {
-    double v[GRP];
-    uint32_t m[GRP];
-#pragma unroll
-    for (int u = 0; u < GRP; ++u)
-      if (k + u < ns) {
-        v[u] = xl[k + u];
-        m[u] = xm[k + u];
-      }
-#pragma unroll
-    for (int u = 0; u < GRP; ++u)
-      if (k + u < ns) {
-        double lk = v[u] * tpv;
-        bool homo = meta_homo(m[u]);
-        if (differ && homo) {
-          if (rev) lk = 0.0;
-          homo = false;
-        }
-        yl[k0 + k + u] = lk;
-        ym[k0 + k + u] = meta_pack(s, (uint32_t)(k + u), rev, homo, false);
-      }
-  }
-}
-
 // Key table replacing m_best_pair: slot ids < hc are LDS slots, >= hc HBM slots.
 struct Keys {
   int hc, nw, o_key, o_cnt, o_state, o_lanes;  // LDS tier (nw lane-mask words per slot)
@@ -147,14 +112,6 @@ struct Keys {
   uint32_t *gcnt, *gstate;
   uint32_t gmask;
 };
-
-__device__ inline uint32_t key_hash(uint32_t lo, uint32_t hi) {
-  uint32_t h = lo * 0x9E3779B1u ^ (hi + 0x7F4A7C15u) * 0x85EBCA77u;
-  h ^= h >> 15;
-  h *= 0x2C1B3C6Du;
-  h ^= h >> 13;
-  return h;
-}
 
 // Insert-or-find: a key lands in the first free or matching slot of its LDS
 // probe sequence (at most PROBE_LDS slots), else in the HBM table.  Slots never
@@ -215,9 +172,6 @@ __device__ inline void clear_slot(const Lds &l, const Keys &K, uint32_t s) {
   }
 }
 
-__device__ inline int lane_id() { return (int)(threadIdx.x & (WAVE - 1)); }
-__device__ inline uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
-
 // Block-wide scalars exchanged through LDS (a block = one individual, NW waves).
 struct BlockShared {
   unsigned long long u[2];
@@ -241,12 +195,6 @@ __device__ inline unsigned long long trace_alloc(const EstepArgs &a, BlockShared
   unsigned long long off = cur;
   cur += words;
   return off;
-}
-
-// Trace record of one locus at word `off`: [Fn][Fn headers][pad to an even
-// word][Fn x S link words]; this is the word index of the link block.
-__host__ __device__ inline unsigned long long trace_links(unsigned long long off, uint32_t F) {
-  return (off + 1 + F + 1) & ~1ull;
 }
 
 // Stream the finished k-best lists of one locus into the trace store.
@@ -458,8 +406,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void e
 
   // Individuals in the host's visit order (heaviest first: blocks b, b+256,
   // ... share a CU, so the heaviest ones land on distinct CUs).
-  const int nbatch = a.indiv_end - a.indiv_begin;
-  for (int q = blockIdx.x; q < nbatch; q += gridDim.x) {
+  const int nvisit = a.order ? a.n_order : a.indiv_end - a.indiv_begin;
+  for (int q = blockIdx.x; q < nvisit; q += gridDim.x) {
     const int bi = a.order ? a.order[q] : q;
     const int gi = a.indiv_begin + bi;
     const uchar2 *g = a.pan.geno_im + (size_t)gi * L;

@@ -1,0 +1,912 @@
+// estep_split.hip — the E-step of the HaploModel EM as two passes on CDNA4.
+//
+// HaploBuilder::resolve (HaploBuilder.cpp:35-126) mixes two kinds of work per
+// locus: the *structure* — which HaploPair states exist, created in which
+// order, and which predecessor contributes to which state in which order
+// (extendAll/extend/addHaploPair, :226-261, keyed by m_best_pair) — and the
+// *values* — forward likelihoods and the k-best link lists (HaploPair.cpp:35-89).
+// The structure only depends on pattern ids and on `forward_likelihood() > 0`
+// (extend, :237), which holds unless a likelihood underflows to zero.  So:
+//
+//   pass 1, estep_structure — one wavefront per individual walks the loci with
+//     the integer work only: successor gathers, the (id_a, id_b) key table in
+//     LDS, creation-order state numbering, per-state contribution lists in add
+//     order, list lengths min(S, sum of predecessor lengths), and the states
+//     whose adds overflow S ("chains", sorted longest first).  It writes one
+//     structure record per locus.
+//   pass 2, estep_values — W wavefronts per individual replay the records:
+//     a thread per state runs the constructor, the in-place appends and the
+//     ordered forward sum; the adds that overflow S run as chains on 2S-lane
+//     segments with the libstdc++-exact segmented nth_element (coop_select.hpp),
+//     each segment pulling the next chain from a block queue.  No hashing, no
+//     gathers of the pattern table, two barriers per locus.
+//
+// If pass 2 meets a forward likelihood of 0 before the last locus (the
+// reference would skip that pair) the individual is flagged EST_NEEDS_EXACT
+// and the host re-runs it on the fused kernel (estep.hip), which evaluates
+// extend()'s test as it goes.  Results are bit-identical to the fused kernel.
+#include "hmc_internal.hpp"
+#include "select.hpp"
+#include "coop_select.hpp"
+#include "estep_common.hpp"
+
+namespace hmc {
+
+namespace {
+
+constexpr unsigned long long REC_CHUNK = 1ull << 16;  // record words per bump allocation
+constexpr int NBUCKET = 32;                           // chain-length buckets (longest first)
+
+// An array whose entries [0, fc) live in LDS and [fc, ..) in HBM scratch.
+template <class T>
+struct Tier {
+  T *l, *g;
+  int fc;
+  __device__ T *at(int t) const { return t < fc ? l + t : g + (t - fc); }
+};
+
+// Visibility of LDS and global (HBM-tier) writes between the lanes of the
+// wave that forms the whole workgroup of pass 1.
+__device__ inline void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ inline int wave_incl_scan(int x) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+// ============================================================ pass 1 ======
+
+// Frontier of pass 1 (m_haplopairs[i] as pattern-id pairs): per state the
+// pattern ids, list length nl, key slot, running sum of predecessor list
+// lengths, and the first contribution's position in the record.  Six u32
+// arrays; entries [0, fc) in LDS, the rest in HBM scratch.
+enum { F_LO, F_HI, F_NL, F_SLOT, F_NS, F_CB, F_NARR };
+struct IdFront {
+  uint32_t *l, *g;
+  int fc, gs;  // LDS entries per array, HBM words per array
+  __device__ uint32_t *at(int k, int t) const { return t < fc ? l + k * fc + t : g + (size_t)k * gs + (t - fc); }
+};
+
+// m_best_pair: slots < hc in LDS, the rest in the HBM table.
+struct K1Keys {
+  unsigned char *l, *g;
+  int hc, hcap;
+  __device__ unsigned long long *key(uint32_t s) const {
+    return s < (uint32_t)hc ? (unsigned long long *)l + s : (unsigned long long *)g + (s - hc);
+  }
+  __device__ unsigned long long *lanes(uint32_t s) const {
+    return s < (uint32_t)hc ? (unsigned long long *)(l + (size_t)hc * 8) + s
+                            : (unsigned long long *)(g + (size_t)hcap * 8) + (s - hc);
+  }
+  __device__ uint32_t *cnt(uint32_t s) const {
+    return s < (uint32_t)hc ? (uint32_t *)(l + (size_t)hc * 16) + s : (uint32_t *)(g + (size_t)hcap * 16) + (s - hc);
+  }
+  __device__ uint32_t *state(uint32_t s) const {
+    return s < (uint32_t)hc ? (uint32_t *)(l + (size_t)hc * 20) + s : (uint32_t *)(g + (size_t)hcap * 20) + (s - hc);
+  }
+};
+
+// The locus's contributions in extendAll order: (pred | reversed), state, rank.
+enum { C_SR, C_ST, C_RK };
+struct CTier {
+  uint32_t *l, *g;
+  int cc, ccap;
+  __device__ uint32_t *at(int k, int c) const {
+    return c < cc ? l + k * cc + c : g + (size_t)k * ccap + (c - cc);
+  }
+};
+
+struct K1Plan {
+  int o_pairs, o_bucket, o_front[2], o_keys, o_contrib, bytes;
+};
+
+__host__ __device__ inline K1Plan k1_plan(int fc, int hc, int cc) {
+  K1Plan p;
+  int o = 0;
+  auto take = [&](int bytes) { int r = o; o += (bytes + 15) & ~15; return r; };
+  p.o_pairs = take((NP_MAX + 2) * 4 + 3 * NP_MAX);
+  p.o_bucket = take(NBUCKET * 4);
+  p.o_front[0] = take(F_NARR * fc * 4);
+  p.o_front[1] = take(F_NARR * fc * 4);
+  p.o_keys = take(hc * 24);
+  p.o_contrib = take(3 * cc * 4);
+  p.bytes = o;
+  return p;
+}
+
+// Insert-or-find of the successor key: the first free or matching slot of its
+// LDS probe sequence, else the HBM table.  Slots never empty during a locus.
+__device__ inline uint32_t k1_key_slot(const K1Keys &K, unsigned long long key, uint32_t h0) {
+  unsigned long long *lk = (unsigned long long *)K.l, *gk = (unsigned long long *)K.g;
+  uint32_t h = h0 & (uint32_t)(K.hc - 1);
+  for (int p = 0; p < PROBE_LDS; ++p) {
+    const unsigned long long prev = atomicCAS(&lk[h], KEY_EMPTY, key);
+    if (prev == KEY_EMPTY || prev == key) return h;
+    h = (h + 1) & (uint32_t)(K.hc - 1);
+  }
+  const uint32_t gmask = (uint32_t)K.hcap - 1u;
+  uint32_t g = (h0 * 0x9E3779B1u) & gmask;
+  while (true) {
+    const unsigned long long prev = atomicCAS(&gk[g], KEY_EMPTY, key);
+    if (prev == KEY_EMPTY || prev == key) return (uint32_t)K.hc + g;
+    g = (g + 1) & gmask;
+  }
+}
+
+__device__ inline unsigned long long ld_acq(unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline uint32_t ld_acq(uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ inline unsigned long long rec_alloc(const StructArgs &a, unsigned long long &cur, unsigned long long &end,
+                                               unsigned long long words) {
+  words = (words + 1) & ~1ull;  // records start on even words (8-byte aligned tpv)
+  if (cur + words > end) {
+    const unsigned long long take = words > REC_CHUNK ? words : REC_CHUNK;
+    unsigned long long base = 0;
+    if (lane_id() == 0) base = atomicAdd(a.rec_cursor, take);
+    base = __shfl(base, 0);
+    cur = base;
+    end = base + take;
+  }
+  const unsigned long long off = cur;
+  cur += words;
+  return off;
+}
+
+}  // namespace
+
+__host__ __device__ inline size_t k1_front_words(int fcap) { return al256((size_t)fcap * 4) / 4; }
+
+size_t estep_s1_scratch_bytes(int fcap, int hcap, int ccap) {
+  return 2 * al256(F_NARR * k1_front_words(fcap) * 4) + al256((size_t)hcap * 24) + al256((size_t)ccap * 12);
+}
+size_t estep_s1_lds_bytes(int fc, int hc, int cc) { return (size_t)k1_plan(fc, hc, cc).bytes; }
+
+__global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const K1Plan plan = k1_plan(a.lds_fc, a.lds_hc, a.lds_cc);
+  const int lane = lane_id();
+  const uint64_t lt = lanemask_lt();
+  const int S = a.S, L = a.pan.L, amax = a.pan.amax, hl = a.mod.head_len;
+  int *pr_off = (int *)(smem + plan.o_pairs);  // [NP_MAX+2]; [NP_MAX+1] = npairs
+  uint8_t *pr_x = (uint8_t *)(pr_off + NP_MAX + 2);
+  uint8_t *pr_y = pr_x + NP_MAX;
+  uint8_t *pr_o = pr_y + NP_MAX;
+  int *bucket = (int *)(smem + plan.o_bucket);
+
+  char *sp = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
+  const int gs = (int)k1_front_words(a.fcap);
+  const IdFront FA{(uint32_t *)(smem + plan.o_front[0]), (uint32_t *)sp, a.lds_fc, gs};
+  sp += al256(F_NARR * (size_t)gs * 4);
+  const IdFront FB{(uint32_t *)(smem + plan.o_front[1]), (uint32_t *)sp, a.lds_fc, gs};
+  sp += al256(F_NARR * (size_t)gs * 4);
+  const K1Keys K{smem + plan.o_keys, (unsigned char *)sp, a.lds_hc, a.hcap};
+  sp += al256((size_t)a.hcap * 24);
+  const CTier CT{(uint32_t *)(smem + plan.o_contrib), (uint32_t *)sp, a.lds_cc, a.ccap};
+
+  auto reset_tables = [&]() {
+    for (int h = lane; h < K.hc + a.hcap; h += WAVE) {
+      *K.key(h) = KEY_EMPTY;
+      *K.lanes(h) = 0ull;
+      *K.cnt(h) = 0;
+    }
+    __threadfence();
+    wsync();
+  };
+  reset_tables();
+
+  for (int q = blockIdx.x; q < a.n_order; q += gridDim.x) {
+    const int bi = a.order[q];
+    const int gi = a.indiv_begin + bi;
+    const uchar2 *g = a.pan.geno_im + (size_t)gi * L;
+    unsigned long long *roff = a.rec_off + (size_t)bi * (L + 1);
+    int status = EST_OK;
+    unsigned long long re = 0;
+    unsigned long long rcur = 0, rend = 0;
+    IdFront X = FA, Y = FB;
+
+    // ---- initHeadList (HaploBuilder.cpp:153-224), head_len == 1 -----------
+    int Fp0 = 0, st0 = EST_OK;
+    if (lane == 0) {
+      const uchar2 g0 = g[0];
+      const bool m0 = g0.x == MISSING, m1 = g0.y == MISSING;
+      for (int hix = 0; hix < a.mod.n_head; ++hix) {
+        const uint32_t head = a.mod.head_ids[hix];
+        const uint8_t ah = a.mod.last[head];
+        if (!(m0 || m1 || g0.x == ah || g0.y == ah)) continue;  // head->isMatch(genotype)
+        uint8_t xs[A_MAX];
+        int nx = 0;
+        const bool hasAllele = g0.x == ah || g0.y == ah;
+        if ((m0 && m1) || ((m0 || m1) && hasAllele)) {
+          for (int x = 0; x < a.pan.anum[0]; ++x)
+            if (a.pan.afreq[x] > 0) xs[nx++] = (uint8_t)x;
+        } else if (!m0 && !m1 && g0.x != g0.y) {
+          xs[nx++] = (ah == g0.x) ? g0.y : g0.x;
+        } else {
+          xs[nx++] = g0.x;  // may be missing: resolved like findLongestMatchPattern
+        }
+        for (int k = 0; k < nx; ++k) {
+          const uint32_t hq = xs[k] == MISSING ? a.mod.head_pat0[amax] : a.mod.head_pat0[xs[k]];
+          if (hq == NONE) { st0 = EST_NO_HEAD_PATTERN; break; }
+          if (hq < head) continue;  // hp->id() >= head->id()
+          if (Fp0 >= a.fcap) { st0 = EST_OVERFLOW_FRONTIER; break; }
+          *X.at(F_LO, Fp0) = head;
+          *X.at(F_HI, Fp0) = hq;
+          *X.at(F_NL, Fp0) = 1;
+          ++Fp0;
+        }
+        if (st0 != EST_OK) break;
+      }
+    }
+    int Fp = __shfl(Fp0, 0);
+    status = __shfl(st0, 0);
+    int fbig = 0;
+    wsync();
+    if (status == EST_OK) {
+      const unsigned long long words = 4 + 4ull * Fp + 1;
+      const unsigned long long o = rec_alloc(a, rcur, rend, words);
+      if (o + words > a.rec_cap) {
+        status = EST_OVERFLOW_REC;
+      } else {
+        uint32_t *R = a.rec + o;
+        double *Rtp = (double *)(R + 4);
+        uint32_t *Rhd = R + 4 + 2 * Fp, *Rcb = Rhd + Fp;
+        for (int t = lane; t < Fp; t += WAVE) {
+          const uint32_t lo = *X.at(F_LO, t), hi = *X.at(F_HI, t);
+          Rtp[t] = a.mod.freq[lo] * a.mod.freq[hi];  // HaploPair.cpp:27
+          Rhd[t] = (uint32_t)a.mod.last[lo] | (uint32_t)a.mod.last[hi] << 8 | 1u << 16 | (lo == hi ? 1u << 24 : 0u);
+          Rcb[t] = 0;
+        }
+        if (lane == 0) {
+          Rcb[Fp] = 0;
+          R[0] = (uint32_t)Fp;
+          R[1] = 0;
+          R[2] = 0;
+          R[3] = 0;
+          roff[hl] = o;
+        }
+        if (lane == 0) re += (unsigned long long)Fp;
+      }
+    }
+
+    // ---- structure of the forward over loci (HaploBuilder.cpp:47-82) -------
+    for (int i = hl; i < L && status == EST_OK; ++i) {
+      if (Fp == 0) { status = EST_UNRESOLVED; break; }
+      const uchar2 gg = g[i];
+      if (lane == 0) {  // allele-pair list in extendAll call order
+        const double *af = a.pan.afreq + (size_t)i * amax;
+        const int an = a.pan.anum[i];
+        int np = 0;
+        auto push = [&](int x, int y) { pr_x[np] = (uint8_t)x; pr_y[np] = (uint8_t)y; pr_o[np] = x == y ? 1 : 2; ++np; };
+        if (gg.x == MISSING && gg.y == MISSING) {
+          for (int j = 0; j < an; ++j)
+            if (af[j] > 0)
+              for (int k = j; k < an; ++k)
+                if (af[k] > 0) push(j, k);
+        } else if (gg.x == MISSING) {
+          for (int j = 0; j < an; ++j)
+            if (af[j] > 0) push(j, gg.y);
+        } else if (gg.y == MISSING) {
+          for (int j = 0; j < an; ++j)
+            if (af[j] > 0) push(j, gg.x);
+        } else {
+          push(gg.x, gg.y);
+        }
+        int off = 0;
+        for (int p = 0; p < np; ++p) { pr_off[p] = off; off += Fp * pr_o[p]; }
+        pr_off[np] = off;
+        pr_off[NP_MAX + 1] = np;
+      }
+      wsync();
+      const int npairs = pr_off[NP_MAX + 1];
+      const int C = pr_off[npairs];
+      if (C > a.ccap) { status = EST_OVERFLOW_FRONTIER; break; }
+      int Fn = 0;
+      for (int c0 = 0; c0 < C; c0 += WAVE) {
+        const int c = c0 + lane;
+        bool valid = c < C;
+        uint32_t s = 0, lo = 0, hi = 0, slot = 0;
+        bool rev = false;
+        if (valid) {
+          int p = 0;
+          while (p + 1 < npairs && c >= pr_off[p + 1]) ++p;
+          const int local = c - pr_off[p];
+          const int o = pr_o[p] == 2 ? (local & 1) : 0;
+          s = pr_o[p] == 2 ? (uint32_t)(local >> 1) : (uint32_t)local;
+          const uint32_t x = o ? pr_y[p] : pr_x[p];
+          const uint32_t y = o ? pr_x[p] : pr_y[p];
+          const uint32_t sa = a.mod.succ[(size_t)*X.at(F_LO, (int)s) * amax + x];
+          const uint32_t sb = a.mod.succ[(size_t)*X.at(F_HI, (int)s) * amax + y];
+          valid = sa != NONE && sb != NONE;
+          rev = sa > sb;  // addHaploPair: id_a > id_b -> swap, reversed
+          lo = rev ? sb : sa;
+          hi = rev ? sa : sb;
+        }
+        if (valid) {
+          slot = k1_key_slot(K, ((unsigned long long)lo << 32) | hi, key_hash(lo, hi));
+          atomicOr(K.lanes(slot), 1ull << lane);
+        }
+        wsync();
+        uint64_t gm = 0;
+        uint32_t cnt0 = 0;
+        if (valid) {
+          gm = slot < (uint32_t)K.hc ? *K.lanes(slot) : ld_acq(K.lanes(slot));
+          cnt0 = *K.cnt(slot);
+        }
+        const int li = __popcll(gm & lt), gsz = __popcll(gm);
+        wsync();
+        if (valid && li == 0) {
+          *K.cnt(slot) = cnt0 + (uint32_t)gsz;
+          *K.lanes(slot) = 0ull;
+        }
+        const bool is_new = valid && cnt0 == 0 && li == 0;
+        const uint64_t nm = __ballot(is_new);
+        const int nnew = __popcll(nm);
+        if (Fn + nnew > a.fcap) { status = EST_OVERFLOW_FRONTIER; break; }
+        uint32_t st = 0;
+        if (is_new) {
+          st = (uint32_t)(Fn + __popcll(nm & lt));
+          *K.state(slot) = st;
+          *Y.at(F_LO, (int)st) = lo;
+          *Y.at(F_HI, (int)st) = hi;
+          *Y.at(F_SLOT, (int)st) = slot;
+          *Y.at(F_NS, (int)st) = 0;
+        }
+        Fn += nnew;
+        wsync();
+        if (valid && !is_new) st = *K.state(slot);
+        if (valid) atomicAdd(Y.at(F_NS, (int)st), *X.at(F_NL, (int)s));
+        if (c < C) {
+          *CT.at(C_SR, c) = s | (rev ? 1u << 16 : 0u);
+          *CT.at(C_ST, c) = valid ? st : NONE;
+          *CT.at(C_RK, c) = cnt0 + (uint32_t)li;
+        }
+      }
+      if (status != EST_OK) break;
+      if (Fn == 0) { status = EST_UNRESOLVED; break; }
+      fbig = Fn > fbig ? Fn : fbig;
+      wsync();
+
+      // contributions per state -> first position (exclusive scan, creation order)
+      int Cv = 0;
+      for (int t0 = 0; t0 < Fn; t0 += WAVE) {
+        const int t = t0 + lane;
+        const int m = t < Fn ? (int)*K.cnt(*Y.at(F_SLOT, t)) : 0;
+        const int incl = wave_incl_scan(m);
+        if (t < Fn) *Y.at(F_CB, t) = (uint32_t)(Cv + incl - m);
+        Cv += __shfl(incl, 63);
+      }
+      const unsigned long long words = 4 + 4ull * Fn + 1 + (unsigned long long)Cv + Fn;
+      const unsigned long long o = rec_alloc(a, rcur, rend, words);
+      if (o + words > a.rec_cap) { status = EST_OVERFLOW_REC; break; }
+      uint32_t *R = a.rec + o;
+      double *Rtp = (double *)(R + 4);
+      uint32_t *Rhd = R + 4 + 2 * Fn, *Rcb = Rhd + Fn, *Rct = Rcb + Fn + 1, *Rch = Rct + Cv;
+      if (lane < NBUCKET) bucket[lane] = 0;
+      wsync();
+      // per state: k-best list length min(S, sum of predecessor lengths) (the
+      // adds keep S once they overflow, HaploPair.cpp:85-88), tp product, last
+      // alleles; states whose lists overflow get a chain entry
+      for (int t0 = 0; t0 < Fn; t0 += WAVE) {
+        const int t = t0 + lane;
+        if (t < Fn) {
+          const uint32_t lo = *Y.at(F_LO, t), hi = *Y.at(F_HI, t);
+          const uint32_t nsum = t < Y.fc ? *Y.at(F_NS, t) : ld_acq(Y.at(F_NS, t));
+          const uint32_t nl = nsum < (uint32_t)S ? nsum : (uint32_t)S;
+          *Y.at(F_NL, t) = nl;
+          re += nl;
+          Rtp[t] = a.mod.tp[lo] * a.mod.tp[hi];  // m_transition_prob, HaploPair.cpp:42
+          Rhd[t] = (uint32_t)a.mod.last[lo] | (uint32_t)a.mod.last[hi] << 8 | nl << 16;
+          Rcb[t] = *Y.at(F_CB, t);
+          if (nsum > (uint32_t)S) {  // bucket 0 = most contributions
+            const int m = (int)*K.cnt(*Y.at(F_SLOT, t));
+            atomicAdd(&bucket[NBUCKET - 1 - (m - 1 < NBUCKET - 1 ? m - 1 : NBUCKET - 1)], 1);
+          }
+        }
+      }
+      wsync();
+      int nch = 0;
+      {
+        const int b = lane < NBUCKET ? bucket[lane] : 0;
+        const int incl = wave_incl_scan(b);
+        nch = __shfl(incl, 63);
+        wsync();
+        if (lane < NBUCKET) bucket[lane] = incl - b;
+      }
+      wsync();
+      for (int t0 = 0; t0 < Fn; t0 += WAVE) {
+        const int t = t0 + lane;
+        if (t < Fn) {
+          const uint32_t nsum = t < Y.fc ? *Y.at(F_NS, t) : ld_acq(Y.at(F_NS, t));
+          if (nsum > (uint32_t)S) {
+            const int m = (int)*K.cnt(*Y.at(F_SLOT, t));
+            const int pos = atomicAdd(&bucket[NBUCKET - 1 - (m - 1 < NBUCKET - 1 ? m - 1 : NBUCKET - 1)], 1);
+            Rch[pos] = (uint32_t)t;
+          }
+        }
+      }
+      // contributions of each state in add order
+      for (int c0 = 0; c0 < C; c0 += WAVE) {
+        const int c = c0 + lane;
+        if (c < C) {
+          const uint32_t st = *CT.at(C_ST, c);
+          if (st != NONE) {
+            const uint32_t w = *CT.at(C_SR, c);
+            const uint32_t ns = *X.at(F_NL, (int)(w & 0xFFFFu));
+            Rct[*Y.at(F_CB, (int)st) + *CT.at(C_RK, c)] = w | ns << 24;
+          }
+        }
+      }
+      if (lane == 0) {
+        Rcb[Fn] = (uint32_t)Cv;
+        R[0] = (uint32_t)Fn;
+        R[1] = (uint32_t)Cv;
+        R[2] = (uint32_t)nch;
+        R[3] = 0;
+        roff[i + 1] = o;
+      }
+      // m_best_pair.clear() for the next locus
+      for (int t0 = 0; t0 < Fn; t0 += WAVE) {
+        const int t = t0 + lane;
+        if (t < Fn) {
+          const uint32_t sl = *Y.at(F_SLOT, t);
+          *K.key(sl) = KEY_EMPTY;
+          *K.cnt(sl) = 0;
+        }
+      }
+      wsync();
+      const IdFront T = X;
+      X = Y;
+      Y = T;
+      Fp = Fn;
+    }
+    if (status == EST_OK && Fp == 0) status = EST_UNRESOLVED;
+    fbig = Fp > fbig ? Fp : fbig;
+    if (status < 0) reset_tables();  // aborted mid-locus: keys may be left
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) re += __shfl_xor(re, o);
+    if (lane == 0) {
+      a.status[bi] = status;
+      a.re_count[bi] = re;
+      a.fmax[bi] = fbig;
+      atomicMax(a.max_states, (unsigned)fbig);
+    }
+  }
+}
+
+// ============================================================ pass 2 ======
+
+namespace {
+
+// Value frontier: forward likelihood, list length, first overflowing add,
+// and the k-best list (S likelihoods + S link words) of every state.  One
+// region per tier, arrays at fixed offsets (8-byte aligned): fwd[n] nl[n]
+// r0[n] lik[n][S] meta[n][S], n = fc (LDS) or fcap (HBM).
+struct VFront {
+  unsigned char *l, *g;
+  int fc, fcap, S;
+  __device__ double *fwd(int t) const {
+    return t < fc ? (double *)l + t : (double *)g + (t - fc);
+  }
+  __device__ uint32_t *nl(int t) const {
+    return t < fc ? (uint32_t *)(l + (size_t)fc * 8) + t : (uint32_t *)(g + (size_t)fcap * 8) + (t - fc);
+  }
+  __device__ uint32_t *r0(int t) const {
+    return t < fc ? (uint32_t *)(l + (size_t)fc * 12) + t : (uint32_t *)(g + (size_t)fcap * 12) + (t - fc);
+  }
+  __device__ double *lik(int t) const {
+    return t < fc ? (double *)(l + (size_t)fc * 16) + t * S : (double *)(g + (size_t)fcap * 16) + (size_t)(t - fc) * S;
+  }
+  __device__ uint32_t *meta(int t) const {
+    return t < fc ? (uint32_t *)(l + (size_t)fc * (16 + 8 * S)) + t * S
+                  : (uint32_t *)(g + (size_t)fcap * (16 + 8 * S)) + (size_t)(t - fc) * S;
+  }
+};
+
+struct K2Shared {
+  unsigned long long u[2];
+  int next;  // chain queue head
+  int flag;  // a forward likelihood hit 0 before the last locus
+  int iters; // diagnostic build: most chain-loop iterations of any wave this locus
+};
+
+struct K2Plan {
+  int o_lpos, o_rpos, o_junk, o_slik, o_smeta, o_bs, o_front[2], bytes;
+};
+
+__host__ __device__ inline K2Plan k2_plan(int S, int fc, int nw) {
+  K2Plan p;
+  int o = 0;
+  auto take = [&](int bytes) { int r = o; o += (bytes + 15) & ~15; return r; };
+  p.o_lpos = take(nw * WAVE * 4);
+  p.o_rpos = take(nw * WAVE * 4);
+  p.o_junk = take(nw * 2 * WAVE * 4);
+  p.o_slik = take(nw * WAVE * 8);
+  p.o_smeta = take(nw * WAVE * 4);
+  p.o_bs = take((int)sizeof(K2Shared));
+  p.o_front[0] = take(fc * (16 + 12 * S));
+  p.o_front[1] = take(fc * (16 + 12 * S));
+  p.bytes = o;
+  return p;
+}
+
+__host__ __device__ inline size_t k2_front_bytes(int fcap, int S) { return al256((size_t)fcap * (16 + 12 * S)); }
+
+// Bump-allocate `words` trace words for this block (block-uniform call).
+__device__ inline unsigned long long k2_trace_alloc(const ValueArgs &a, K2Shared *bs, unsigned long long &cur,
+                                                    unsigned long long &end, unsigned long long words) {
+  if (cur + words > end) {
+    const unsigned long long take = words > TRACE_CHUNK ? words : TRACE_CHUNK;
+    if (threadIdx.x == 0) bs->u[0] = atomicAdd(a.trace_cursor, take);
+    __syncthreads();
+    const unsigned long long base = bs->u[0];
+    __syncthreads();
+    cur = base;
+    end = base + take;
+  }
+  const unsigned long long off = cur;
+  cur += words;
+  return off;
+}
+
+// The finished k-best lists of locus j into the trace store (same layout as
+// the fused kernel: [F][headers][pad][F x S link words]).
+__device__ inline bool k2_write_trace(const ValueArgs &a, K2Shared *bs, const VFront &Y, const uint32_t *Rhd, int F,
+                                      int j, int bi, unsigned long long &cur, unsigned long long &end) {
+  const int S = a.S, NT = (int)blockDim.x;
+  const unsigned long long words = 2ull + (unsigned long long)F * (1 + S);
+  const unsigned long long off = k2_trace_alloc(a, bs, cur, end, words);
+  if (off + words > a.trace_cap) return false;
+  uint32_t *hdr = a.trace + off + 1;
+  uint32_t *lnk = a.trace + trace_links(off, (uint32_t)F);
+  for (int t = threadIdx.x; t < F; t += NT) {
+    const uint32_t n = *Y.nl(t);
+    hdr[t] = (Rhd[t] & 0xFFFFu) | n << 16;
+    const uint32_t *pm = Y.meta(t);
+    uint32_t *dst = lnk + (size_t)t * S;
+    if ((S & 1) == 0) {
+      uint2 v[S_MAX / 2];
+#pragma unroll
+      for (int k = 0; k < S_MAX / 2; ++k)
+        if (2 * k < S) v[k] = ((const uint2 *)pm)[k];
+#pragma unroll
+      for (int k = 0; k < S_MAX / 2; ++k)
+        if (2 * k < S)
+          ((uint2 *)dst)[k] = make_uint2((uint32_t)(2 * k) < n ? v[k].x : 0u, (uint32_t)(2 * k + 1) < n ? v[k].y : 0u);
+    } else {
+      uint32_t v[S_MAX];
+#pragma unroll
+      for (int k = 0; k < S_MAX; ++k)
+        if (k < S) v[k] = pm[k];
+#pragma unroll
+      for (int k = 0; k < S_MAX; ++k)
+        if (k < S) dst[k] = (uint32_t)k < n ? v[k] : 0u;
+    }
+  }
+  if (threadIdx.x == 0) {
+    a.trace[off] = (uint32_t)F;
+    a.loc_off[(size_t)bi * (a.L + 1) + j] = off;
+  }
+  return true;
+}
+
+}  // namespace
+
+// Diagnostic build only (-DHMC_STAMPS): thread 0 accumulates shader cycles of
+// the block's critical path per phase of the value pass.
+#ifdef HMC_STAMPS
+#define K2_T0 unsigned long long k2t = __builtin_amdgcn_s_memtime(); unsigned long long k2acc[16] = {};
+#define K2_ST(k)                                                   \
+  do {                                                             \
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();    \
+    k2acc[k] += t1 - k2t;                                          \
+    k2t = t1;                                                      \
+  } while (0)
+#define K2_CNT(k, v) k2acc[k] += (v)
+#define K2_FLUSH                                                   \
+  if (a.stamps && tid == 0)                                        \
+    for (int k = 0; k < 16; ++k) atomicAdd(&a.stamps[k], k2acc[k]);
+#else
+#define K2_T0
+#define K2_ST(k) do { } while (0)
+#define K2_CNT(k, v) do { } while (0)
+#define K2_FLUSH
+#endif
+
+size_t estep_s2_scratch_bytes(int fcap, int S) { return 2 * k2_front_bytes(fcap, S); }
+size_t estep_s2_lds_bytes(int S, int fc, int nw) { return (size_t)k2_plan(S, fc, nw).bytes; }
+
+__global__ __launch_bounds__(256) void estep_values(ValueArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int S = a.S, L = a.L, hl = a.head_len;
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;
+  const int NT = blockDim.x, NW = NT / WAVE;
+  const K2Plan plan = k2_plan(S, a.lds_fc, NW);
+  K2Shared *bs = (K2Shared *)(smem + plan.o_bs);
+  const SegScratch ss{(int *)(smem + plan.o_lpos) + wv * WAVE, (int *)(smem + plan.o_rpos) + wv * WAVE,
+                      (int *)(smem + plan.o_junk) + wv * 2 * WAVE, (double *)(smem + plan.o_slik) + wv * WAVE,
+                      (uint32_t *)(smem + plan.o_smeta) + wv * WAVE};
+  const Seg sg = make_seg(2 * S);
+  const int G = WAVE / (2 * S);
+  const LinkList W{(double *)(smem + plan.o_slik), (uint32_t *)(smem + plan.o_smeta), 1};  // final selection
+
+  char *sp = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
+  const VFront FA{smem + plan.o_front[0], (unsigned char *)sp, a.lds_fc, a.fcap, S};
+  const VFront FB{smem + plan.o_front[1], (unsigned char *)sp + k2_front_bytes(a.fcap, S), a.lds_fc, a.fcap, S};
+
+  K2_T0
+  for (int q = blockIdx.x; q < a.n_order; q += gridDim.x) {
+    const int bi = a.order[q];
+    const unsigned long long t_indiv = __builtin_amdgcn_s_memtime();
+    int status = a.status[bi];
+    if (status != EST_OK) {  // pass 1 found no resolution (dead frontier)
+      if (tid == 0) {
+        a.total[bi] = 0.0;
+        a.ncand[bi] = 0;
+        a.cost[bi] = 0;
+      }
+      continue;
+    }
+    const unsigned long long *roff = a.rec_off + (size_t)bi * (L + 1);
+    unsigned long long tcur = 0, tend = 0;
+    VFront X = FA, Y = FB;
+
+    // ---- head list (HaploPair.cpp:14-33) -----------------------------------
+    const uint32_t *R = a.rec + roff[hl];
+    int Fp = (int)R[0];
+    {
+      const double *Rtp = (const double *)(R + 4);
+      const uint32_t *Rhd = R + 4 + 2 * Fp;
+      for (int t = tid; t < Fp; t += NT) {
+        const bool homo = (Rhd[t] >> 24) & 1u;
+        const double tpv = Rtp[t];
+        *X.fwd(t) = homo ? tpv : tpv * 2.0;
+        X.lik(t)[0] = tpv;
+        X.meta(t)[0] = meta_pack(0, 0, false, homo, true);
+        *X.nl(t) = 1;
+      }
+      __syncthreads();
+      if (!k2_write_trace(a, bs, X, Rhd, Fp, hl, bi, tcur, tend)) status = EST_OVERFLOW_TRACE;
+    }
+
+    // ---- forward over loci ----------------------------------------------------
+    for (int j = hl + 1; j <= L && status == EST_OK; ++j) {
+      R = a.rec + roff[j];
+      const int F = (int)R[0], C = (int)R[1], NCH = (int)R[2];
+      const double *Rtp = (const double *)(R + 4);
+      const uint32_t *Rhd = R + 4 + 2 * F, *Rcb = Rhd + F, *Rct = Rcb + F + 1, *Rch = Rct + C;
+      K2_ST(0);
+      if (tid == 0) {
+        bs->next = 0;
+        bs->flag = 0;
+        bs->iters = 0;
+      }
+      // A: one thread per state — extension constructor (HaploPair.cpp:35-61),
+      // the appends that still fit (HaploPair::add without selection,
+      // :63-84) and the whole ordered forward sum (:42, :66)
+      for (int t = tid; t < F; t += NT) {
+        const double tpv = Rtp[t];
+        const uint32_t hd = Rhd[t];
+        const bool differ = (hd & 0xFFu) != ((hd >> 8) & 0xFFu);
+        const int cb = (int)Rcb[t], ce = (int)Rcb[t + 1];
+        uint32_t w = Rct[cb];
+        uint32_t s = w & 0xFFFFu, ns = w >> 24;
+        double fwd = *X.fwd((int)s) * tpv;
+        double *yl = Y.lik(t);
+        uint32_t *ym = Y.meta(t);
+        copy_extended(X.lik((int)s), X.meta((int)s), yl, ym, 0, (int)ns, s, tpv, (w >> 16) & 1u, differ);
+        int k = (int)ns, r0 = ce;
+        for (int r = cb + 1; r < ce; ++r) {
+          w = Rct[r];
+          s = w & 0xFFFFu;
+          ns = w >> 24;
+          fwd += *X.fwd((int)s) * tpv;
+          if (r0 == ce) {
+            if (k + (int)ns <= S) {
+              copy_extended(X.lik((int)s), X.meta((int)s), yl, ym, k, (int)ns, s, tpv, (w >> 16) & 1u, differ);
+              k += (int)ns;
+            } else {
+              r0 = r;
+            }
+          }
+        }
+        *Y.fwd(t) = fwd;
+        *Y.nl(t) = (uint32_t)k;
+        *Y.r0(t) = (uint32_t)r0;
+        if (!(fwd > 0.0) && j < L) bs->flag = 1;
+      }
+      __syncthreads();
+      K2_ST(1);
+      K2_CNT(8, NCH);
+      K2_CNT(9, F);
+      if (bs->flag) {
+        status = EST_NEEDS_EXACT;
+        break;
+      }
+      // B: the adds that overflow S, one chain of adds per state, run by 2S-lane
+      // segments that pull chains (longest first) from the block queue; the
+      // list stays in the segment's lanes between adds
+      if (NCH > 0) {
+        int ci = -1, r = 0, re_ = 0, st = 0, k0 = 0, nit = 0;
+#ifdef HMC_STAMPS
+        unsigned long long tstep = __builtin_amdgcn_s_memtime();
+#endif
+        double tpv = 0.0, v = 0.0;
+        uint32_t m = 0;
+        bool differ = false, done = sg.g >= G;
+        while (true) {
+          const bool idle = !done && ci < 0;
+          int got = 0;
+          if (idle && sg.k == 0) got = atomicAdd(&bs->next, 1);
+          got = __shfl(got, sg.base);
+          if (idle) {
+            if (got < NCH) {
+              ci = got;
+              st = (int)Rch[ci];
+              r = (int)*Y.r0(st);
+              re_ = (int)Rcb[st + 1];
+              tpv = Rtp[st];
+              const uint32_t hd = Rhd[st];
+              differ = (hd & 0xFFu) != ((hd >> 8) & 0xFFu);
+              k0 = (int)*Y.nl(st);
+              if (sg.k < k0) {
+                v = Y.lik(st)[sg.k];
+                m = Y.meta(st)[sg.k];
+              }
+            } else {
+              done = true;
+            }
+          }
+          const bool act = ci >= 0;
+          if (!wave_ballot(act)) break;
+          int n = 0;
+          if (act) {
+            const uint32_t w = Rct[r];
+            const uint32_t s = w & 0xFFFFu, ns = w >> 24;
+            const bool rev = (w >> 16) & 1u;
+            n = k0 + (int)ns;
+            if (sg.k >= k0 && sg.k < n) {  // HaploPair::add transformation (HaploPair.cpp:63-80)
+              const int qk = sg.k - k0;
+              const uint32_t mm = X.meta((int)s)[qk];
+              double lk = X.lik((int)s)[qk] * tpv;
+              bool homo = meta_homo(mm);
+              if (differ && homo) {
+                if (rev) lk = 0.0;
+                homo = false;
+              }
+              v = lk;
+              m = meta_pack(s, (uint32_t)qk, rev, homo, false);
+            }
+          }
+          K2_CNT(10, 1);
+          ++nit;
+#ifdef HMC_STAMPS
+          __builtin_amdgcn_s_waitcnt(0);
+          const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+          K2_CNT(14, ts0 - tstep);
+#endif
+          seg_nth_element(v, m, n, S - 1, sg, ss);
+#ifdef HMC_STAMPS
+          __builtin_amdgcn_s_waitcnt(0);
+          tstep = __builtin_amdgcn_s_memtime();
+          K2_CNT(13, tstep - ts0);
+#endif
+          if (act) {
+            k0 = S;
+            if (++r == re_) {
+              if (sg.k < S) {
+                Y.lik(st)[sg.k] = v;
+                Y.meta(st)[sg.k] = m;
+              }
+              if (sg.k == 0) *Y.nl(st) = (uint32_t)S;
+              ci = -1;
+            }
+          }
+        }
+#ifdef HMC_STAMPS
+        if (lane == 0) atomicMax(&bs->iters, nit);
+#endif
+      }
+      __syncthreads();
+      K2_ST(2);
+      K2_CNT(12, bs->iters);
+      if (!k2_write_trace(a, bs, Y, Rhd, F, j, bi, tcur, tend)) status = EST_OVERFLOW_TRACE;
+      K2_ST(3);
+      K2_CNT(11, 1);
+      const VFront T = X;
+      X = Y;
+      Y = T;
+      Fp = F;
+    }
+
+    // ---- final selection (HaploBuilder.cpp:87-116) ------------------------
+    __syncthreads();
+    K2_ST(4);
+    if (tid == 0) {
+      a.cost[bi] = (int32_t)((__builtin_amdgcn_s_memtime() - t_indiv) >> 10);
+      a.status[bi] = status;
+      int cnt = 0;
+      double total = 0.0;
+      if (status == EST_OK) {
+        for (int t = 0; t < Fp; ++t) {
+          total += *X.fwd(t);
+          const uint32_t n = *X.nl(t);
+          for (uint32_t k = 0; k < n; ++k) {
+            double lk = X.lik(t)[k];
+            const bool homo = meta_homo(X.meta(t)[k]);
+            if (!homo) lk *= 2.0;
+            W.set(cnt++, lk, meta_pack((uint32_t)t, k, false, homo, false));
+          }
+          if (cnt > S) {
+            nth_element_greater_masks(W, cnt, S - 1, cnt);
+            cnt = S;
+          }
+        }
+        sort_greater_small(W, cnt);
+        double coverage = 0.0;
+        for (int c = 0; c < cnt; ++c) {
+          const uint32_t mm = W.m(c);
+          const uint32_t t = meta_pred(mm), k = meta_idx(mm);
+          const double own = X.lik((int)t)[k];
+          const double prior = meta_homo(mm) ? own : own * 2.0;  // HaploPair.cpp:97-102
+          const double post = prior / total;
+          coverage += post;
+          a.cand_state[(size_t)bi * S_MAX + c] = t;
+          a.cand_idx[(size_t)bi * S_MAX + c] = k;
+          a.prior[(size_t)bi * S_MAX + c] = prior;
+          a.posterior[(size_t)bi * S_MAX + c] = post;
+        }
+        for (int c = 0; c < cnt; ++c)  // HaploModel.cpp:97-98
+          a.weight[(size_t)bi * S_MAX + c] = a.posterior[(size_t)bi * S_MAX + c] / coverage;
+      }
+      a.total[bi] = total;
+      a.ncand[bi] = cnt;
+    }
+    __syncthreads();
+    K2_ST(5);
+  }
+  K2_FLUSH
+}
+
+hipError_t launch_estep_structure(const StructArgs &a, int grid, hipStream_t st) {
+  if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > 65535 || (a.hcap & (a.hcap - 1)) || a.lds_hc < 1 ||
+      (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || a.lds_cc < 0 || a.ccap < 1 || a.mod.head_len != 1)
+    return hipErrorInvalidValue;
+  const size_t lds = estep_s1_lds_bytes(a.lds_fc, a.lds_hc, a.lds_cc);
+  static size_t lds_attr = 0;
+  if (lds > 65536 && lds > lds_attr) {
+    hipError_t e =
+        hipFuncSetAttribute((const void *)estep_structure, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    lds_attr = lds;
+  }
+  hipLaunchKernelGGL(estep_structure, dim3(grid), dim3(WAVE), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, hipStream_t st) {
+  if (a.S < 1 || a.S > S_MAX || a.fcap > 65535 || a.lds_fc < 0 || nw < 1 || nw > 4) return hipErrorInvalidValue;
+  const size_t lds = estep_s2_lds_bytes(a.S, a.lds_fc, nw);
+  static size_t lds_attr = 0;
+  if (lds > 65536 && lds > lds_attr) {
+    hipError_t e = hipFuncSetAttribute((const void *)estep_values, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    lds_attr = lds;
+  }
+  hipLaunchKernelGGL(estep_values, dim3(grid), dim3(WAVE * nw), lds, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace hmc

@@ -37,6 +37,10 @@ enum EStatus : int32_t {
   EST_OVERFLOW_FRONTIER = -1,  // more states than the per-wave capacity
   EST_OVERFLOW_TRACE = -2,     // trace buffer exhausted
   EST_NO_HEAD_PATTERN = -3,    // "Can not find matching pattern!" (HaploBuilder.cpp:215-217)
+  EST_OVERFLOW_REC = -4,       // structure-record store exhausted (split E-step)
+  EST_NEEDS_EXACT = 2,         // split E-step: a forward likelihood underflowed to 0 before
+                               // the last locus, so extend() would skip that pair
+                               // (HaploBuilder.cpp:237) — re-run on the fused kernel
 };
 
 // Panel resident in HBM.
@@ -88,9 +92,62 @@ struct EstepArgs {
   unsigned int *max_states;      // [1] running maximum frontier size
   int32_t *fmax;                 // [batch] largest frontier of each individual
   const int32_t *order;          // [batch] individuals in block-visit order (nullptr: natural order)
+  int n_order;                   // entries of `order` to visit (the whole batch unless re-running a subset)
   int32_t *cost;                 // [batch] shader kcycles spent per individual (scheduling hint)
   unsigned long long *stamps;    // [20] diagnostic build: shader cycles per phase
   int diag_indiv;                // diagnostic build: stamp only this batch index (-1: all)
+};
+
+// Split E-step, pass 1 (estep_structure): the value-independent part of
+// resolve() — frontier pattern-id pairs, successor keys, m_best_pair dedup in
+// creation order, per-state contribution lists and k-best list lengths — as
+// per-locus structure records.  Pass 2 (estep_values) replays them with the
+// likelihood arithmetic.  Record of locus j at word rec_off[b][j] (even):
+//   [F][C][NCH][0] tpv f64[F] | hdr u32[F] (last allele a | b<<8 | nl<<16 |
+//   homo<<24 at the head) | cbeg u32[F+1] | contrib u32[C] (pred state |
+//   reversed<<16 | pred list length<<24), each state's in add order |
+//   chains u32[NCH] (states whose adds overflow S, most contributions first).
+struct StructArgs {
+  DevPanel pan;
+  DevModel mod;
+  int S;
+  int indiv_begin;
+  const int32_t *order;
+  int n_order;
+  char *scratch;
+  size_t scratch_stride;
+  int fcap, hcap, ccap;           // HBM tier capacities: states, key slots, contributions per locus
+  int lds_fc, lds_hc, lds_cc;     // LDS tier
+  uint32_t *rec;
+  unsigned long long rec_cap;     // words
+  unsigned long long *rec_cursor; // bump allocator
+  unsigned long long *rec_off;    // [batch][L+1]
+  int32_t *status;                // [batch]
+  unsigned long long *re_count;   // [batch]
+  int32_t *fmax;                  // [batch]
+  unsigned int *max_states;
+};
+
+struct ValueArgs {
+  int S, L, head_len;
+  const int32_t *order;
+  int n_order;
+  const uint32_t *rec;
+  const unsigned long long *rec_off;
+  char *scratch;
+  size_t scratch_stride;
+  int fcap, lds_fc;
+  uint32_t *trace;
+  unsigned long long trace_cap;
+  unsigned long long *trace_cursor;
+  unsigned long long *loc_off;
+  int32_t *status;  // in: pass-1 status; out: EST_OK / EST_NEEDS_EXACT / EST_OVERFLOW_TRACE
+  double *total;
+  int32_t *ncand;
+  uint32_t *cand_state, *cand_idx;
+  double *prior, *posterior, *weight;
+  int32_t *cost;
+  unsigned long long *stamps;  // diagnostic build: [16] block-critical-path cycles per phase
 };
 
 struct TracebackArgs {
@@ -109,6 +166,12 @@ size_t estep_scratch_bytes(int fcap, int hcap, int S, int nw);
 size_t estep_lds_bytes(int S, int fc, int hc, int nw);
 hipError_t launch_test_coop_nth(double *lik, uint32_t *tag, const int *off, const int *n, const int *nth, int count, int sw, hipStream_t st);
 hipError_t launch_estep(const EstepArgs &a, int grid, int nw, hipStream_t st);
+size_t estep_s1_scratch_bytes(int fcap, int hcap, int ccap);
+size_t estep_s1_lds_bytes(int fc, int hc, int cc);
+size_t estep_s2_scratch_bytes(int fcap, int S);
+size_t estep_s2_lds_bytes(int S, int fc, int nw);
+hipError_t launch_estep_structure(const StructArgs &a, int grid, hipStream_t st);
+hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, hipStream_t st);
 hipError_t launch_traceback(const TracebackArgs &a, int total_cands, hipStream_t st);
 hipError_t launch_transpose_u8(const uint8_t *in, uint8_t *out, int rows, int cols, int ld_out, int col0,
                                hipStream_t st);

@@ -150,6 +150,15 @@ class HaploModel:
         """E-step launch shape (results are identical for every shape)."""
         self._check(lib().hmc_set_estep_shape(self._h, waves_per_individual, individuals_per_cu))
 
+    def set_estep_mode(self, mode: int):
+        """0 = split E-step (structure pass + value pass, default), 1 = fused kernel."""
+        self._check(lib().hmc_set_estep_mode(self._h, int(mode)))
+
+    def estep_split_stats(self) -> dict:
+        s1, s2, fb, nf = C.c_double(), C.c_double(), C.c_double(), C.c_int()
+        self._check(lib().hmc_last_estep_split(self._h, C.byref(s1), C.byref(s2), C.byref(fb), C.byref(nf)))
+        return dict(structure_ms=s1.value, values_ms=s2.value, fallback_ms=fb.value, n_fallback=nf.value)
+
     # ----------------------------------------------------------------- panel
     def load(self, genos: GenoData):
         a = np.ascontiguousarray(genos.alleles, dtype=np.int32)

@@ -143,6 +143,17 @@ int hmc_set_tuning(hmc_ctx *ctx, int frontier_cap, uint64_t trace_bytes, int wav
  * default 3) and individuals sharing one CU's LDS (default 4); 0 keeps the
  * current value.  Results do not depend on the shape. */
 int hmc_set_estep_shape(hmc_ctx *ctx, int waves_per_individual, int individuals_per_cu);
+/* E-step implementation: 0 (default) = two passes, a structure pass that
+ * replays extendAll/addHaploPair (HaploBuilder.cpp:226-261) on pattern ids
+ * and a value pass with the k-best lists, falling back to 1 for individuals
+ * whose forward likelihood underflows; 1 = the fused single-pass kernel.
+ * Both produce identical results. */
+int hmc_set_estep_mode(hmc_ctx *ctx, int mode);
+/* Split E-step of the last hmc_resolve_all: device ms of the structure pass,
+ * the value pass and the fused fallback, and the number of individuals that
+ * took the fallback. */
+int hmc_last_estep_split(const hmc_ctx *ctx, double *structure_ms, double *values_ms, double *fallback_ms,
+                         int *n_fallback);
 /* Device time (ms, HIP events on the context stream) of the last E-step
  * forward kernel, traceback and whole M-step. */
 int hmc_last_timings(const hmc_ctx *ctx, double *estep_forward_ms, double *estep_traceback_ms, double *mstep_ms);

@@ -75,13 +75,16 @@ def assert_estep_equal(m, o, ll_g, ll_o, H, re_g):
 
 @pytest.mark.parametrize("name", sorted(PANELS))
 @pytest.mark.parametrize("S", [10])
-def test_estep_on_reference_model(oracle_mod, name, S):
-    """E-step kernels fed the restatement's M0 table == HaploModel::resolveAll."""
+@pytest.mark.parametrize("mode", [0, 1], ids=["split", "fused"])
+def test_estep_on_reference_model(oracle_mod, name, S, mode):
+    """E-step kernels fed the restatement's M0 table == HaploModel::resolveAll,
+    for the split (structure + value pass) and the fused E-step."""
     p = panel(name)
     o = oracle_mod.Oracle(p.alleles, p.types, sample_size=S)
     o.find_patterns()
     pt = o.patterns()
     m = gpu_model(p, S)
+    m.set_estep_mode(mode)
     m.set_patterns(pt["start"], pt["len"], pt["freq"], pt["tp"], pt["succ"], last_symbols(pt))
     ll_g, H, re_g = m.resolve_all()
     o.reset_counters()
@@ -223,6 +226,8 @@ def test_underflow_unresolved(oracle_mod):
     assert [x["ll"] for x in m.log] == r["ll"].tolist()
     assert np.isneginf(r["ll"][0])
     assert np.array_equal(res, r["resolutions"])
+    # the split E-step hands the underflowing individuals to the fused kernel
+    assert m.estep_split_stats()["n_fallback"] > 0
 
 
 def _digest_patterns(pt):
@@ -354,17 +359,19 @@ def test_shard_ranges_balanced_and_tiling():
     assert prev == p.N
 
 
-@pytest.mark.parametrize("name", ["a3miss5", "cfg1"])
+@pytest.mark.parametrize("name", ["a3miss5", "cfg1", "n300"])
 def test_estep_shape_invariance(oracle_mod, name):
-    """1, 2 and 4 wavefronts per individual (and any LDS split) give the
-    identical E-step: same LL, resolutions, weights and link count."""
+    """1, 2 and 4 wavefronts per individual (and any LDS split), split or
+    fused E-step, give the identical E-step: same LL, resolutions, weights
+    and link count."""
     p = panel(name)
     o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
     o.find_patterns()
     pt = o.patterns()
     ref = None
-    for nw, ipc in [(1, 4), (2, 4), (4, 2), (2, 1), (2, 16)]:
+    for mode, nw, ipc in [(0, 1, 4), (0, 2, 4), (0, 4, 2), (0, 2, 1), (0, 2, 16), (0, 3, 32), (1, 3, 4), (1, 1, 16)]:
         m = gpu_model(p, 10)
+        m.set_estep_mode(mode)
         m.set_estep_shape(nw, ipc)
         m.set_patterns(pt["start"], pt["len"], pt["freq"], pt["tp"], pt["succ"], last_symbols(pt))
         ll, H, re = m.resolve_all()
@@ -372,7 +379,26 @@ def test_estep_shape_invariance(oracle_mod, name):
         got = (ll, H, re, m.resolutions().tobytes(), er["weight"].tobytes(), er["prior"].tobytes())
         if ref is None:
             ref = got
-        assert got == ref, (nw, ipc)
+        assert got == ref, (mode, nw, ipc)
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["split", "fused"])
+def test_small_frontier_capacity_retries(oracle_mod, mode):
+    """A frontier capacity far below the panel's frontiers: the batch is re-run
+    with doubled capacities (HBM tiers, key tables, contribution lists) until
+    it fits, with results identical to the restatement."""
+    p = panel("n300")
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
+    o.find_patterns()
+    pt = o.patterns()
+    m = gpu_model(p, 10)
+    m.set_estep_mode(mode)
+    m.set_tuning(frontier_cap=8)
+    m.set_patterns(pt["start"], pt["len"], pt["freq"], pt["tp"], pt["succ"], last_symbols(pt))
+    ll_g, H, re_g = m.resolve_all()
+    o.reset_counters()
+    ll_o = o.resolve_all()
+    assert_estep_equal(m, o, ll_g, ll_o, H, re_g)
 
 
 @pytest.mark.parametrize("sw", [32, 20, 8, 2])
