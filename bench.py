@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--individuals", type=int, default=1000, help="per GPU")
     ap.add_argument("--loci", type=int, default=500)
     ap.add_argument("--sample-size", type=int, default=10)
+    ap.add_argument("--alleles", type=int, default=2, help="alleles per locus of the synthetic panel (cfg 5: 8)")
+    ap.add_argument("--missing", type=float, default=0.0, help="missing-allele rate of the synthetic panel")
+    ap.add_argument("--seed", type=int, default=2, help="panel seed (= BASELINE config index)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=100, help="individuals timed for the CPU E-step")
     return ap.parse_args()
@@ -91,7 +94,7 @@ def main():
 
     N = args.individuals * world
     L = args.loci
-    panel = synth.founder_mosaic(N, L, A=2, seed=2)
+    panel = synth.founder_mosaic(N, L, A=args.alleles, missing=args.missing, seed=args.seed)
     genos = hmc_amd.GenoData.from_panel(panel)
 
     uid = None
@@ -122,8 +125,10 @@ def main():
         ll, H, re = m.resolve_all()
         t = m.timings()
         P, rm = m.find_patterns()
-        return dict(ll=ll, H=H, r_e=re, r_m=rm, P=P, fwd_ms=t["estep_forward_ms"], tb_ms=t["estep_traceback_ms"],
-                    mstep_ms=m.timings()["mstep_ms"])
+        sp = m.estep_split_stats()
+        return dict(ll=ll, H=H, r_e=re, r_m=rm, P=P, fwd_ms=t["estep_forward_ms"], struct_ms=sp["structure_ms"],
+                    values_ms=sp["values_ms"], fallback_ms=sp["fallback_ms"], n_fallback=sp["n_fallback"],
+                    tb_ms=t["estep_traceback_ms"], mstep_ms=m.timings()["mstep_ms"])
 
     warm = [em_step() for _ in range(args.warmup)]
     m.clear_samples()
@@ -135,11 +140,13 @@ def main():
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
 
-    # roofline of the dominant kernel (E-step forward): SURVEY.md §8d bytes per
-    # launch = 2 B per genotype allele read (2*n*L) + 8 B per retained k-best link (R_E)
-    fwd_ms = sum(s["fwd_ms"] for s in steps)
-    alg_bytes = sum(2.0 * n_local * L + 8.0 * s["r_e"] for s in steps)
-    achieved = alg_bytes / (fwd_ms * 1e-3) / 1e9 if fwd_ms > 0 else 0.0
+    # roofline of the dominant kernel, the E-step value pass (estep_values):
+    # SURVEY.md §8d prices the E-step at 2 B per genotype allele (2*n*L, read by
+    # the structure pass) + 8 B per retained k-best link (R_E); the value pass
+    # owns the R_E term.  Duration = its HIP-event time on the context stream.
+    val_ms = sum(s["values_ms"] for s in steps)
+    alg_bytes = sum(8.0 * s["r_e"] for s in steps)
+    achieved = alg_bytes / (val_ms * 1e-3) / 1e9 if val_ms > 0 else 0.0
     traffic = pmc_traffic()
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -157,21 +164,24 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic founder-mosaic panel (K=8 founders, rho=0.002, seed=2), generated in-process",
+            "data": f"synthetic founder-mosaic panel (K=8 founders, rho=0.002, A={args.alleles}, "
+                    f"missing={args.missing}, seed={args.seed}), generated in-process",
             "config": {
-                "workload": f"cfg2 per GPU: {args.individuals} individuals x {L} biallelic SNP loci; "
+                "workload": f"{'cfg2 ' if (args.individuals, L, args.alleles) == (1000, 500, 2) else ''}per GPU: "
+                            f"{args.individuals} individuals x {L} SNP loci, {args.alleles} alleles/locus; "
                             f"step = one EM iteration (E_k + M_k) from the genotype-mined model M0",
                 "individuals": N, "loci": L, "sample_size": args.sample_size,
                 "min_freq_abs": 1.5, "pattern_len": [1, 30],
                 "parallelism": f"individual-sharded x{world}, RCCL all-reduce per mining level",
             },
             "roofline": {
-                "bound": "hbm", "kernel": "estep_forward",
+                "bound": "hbm", "kernel": "estep_values",
                 "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "avg_launch_ms": fwd_ms / args.steps,
+                "avg_launch_ms": val_ms / args.steps,
                 # every launch of the process incl. warmup: the figure rocprofv3 --stats averages
-                "avg_launch_ms_all": (fwd_ms + sum(w["fwd_ms"] for w in warm)) / (args.steps + len(warm)),
+                "avg_launch_ms_all": (val_ms + sum(w["values_ms"] for w in warm)) / (args.steps + len(warm)),
+                "estep_ms_per_step": sum(s["fwd_ms"] for s in steps) / args.steps,
                 "alg_bytes_per_launch": alg_bytes / args.steps,
             },
             "cpu_baseline": cpu,
@@ -185,9 +195,9 @@ def main():
 
 
 def pmc_traffic():
-    """HBM bytes per estep_forward launch from the committed rocprofv3 PMC
-    summary (profiles/pmc_estep_forward.json), or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_estep_forward.json")
+    """HBM bytes per estep_values launch from the committed rocprofv3 PMC
+    summary (profiles/pmc_estep_values.json), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_estep_values.json")
     try:
         with open(p) as f:
             return json.load(f).get("hbm_bytes_per_launch")

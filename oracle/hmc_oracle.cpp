@@ -293,6 +293,30 @@ struct Model {
   std::vector<std::vector<int>> best_res;   // accepted resolutions (HaploModel.cpp:132)
   // counters
   uint64_t R_E = 0, R_M = 0;
+  // Tie diagnostics of the last E-step, per individual (bit 0: some key's
+  // union of contributions has a non-zero tie across its S-cut, bit 1: the
+  // same at likelihood 0, bit 2: the final union has a tie across the S-cut,
+  // bit 3: two of the final candidates have equal non-zero priors, bit 4: the
+  // final union has a tie across the S-cut at 0, bit 5: a final candidate has
+  // prior 0).  With none set,
+  // every k-best set is decided by likelihood values alone.
+  std::vector<int> tie_flags;
+  std::vector<std::vector<double>> uni;  // per state of the next locus
+  int tie_cur = 0;
+  void uni_add(int st, const Link *l, int n) {
+    if ((int)uni.size() <= st) uni.resize(st + 1);
+    for (int i = 0; i < n; ++i) uni[st].push_back(l[i].lik);
+  }
+  void uni_check(int nst) {
+    for (int s = 0; s < nst && s < (int)uni.size(); ++s) {
+      std::vector<double> &u = uni[s];
+      if ((int)u.size() > S) {
+        std::sort(u.begin(), u.end(), std::greater<double>());
+        if (u[S - 1] == u[S]) tie_cur |= u[S] == 0.0 ? 2 : 1;
+      }
+      u.clear();
+    }
+  }
   // EM log
   std::vector<double> ll_log;
   std::vector<uint64_t> re_log, rm_log;
@@ -559,6 +583,7 @@ struct Model {
           if (l.homo) { if (rev) l.lik = 0; l.homo = false; }
       nxt.push_back(std::move(x));
       best[key] = (int)nxt.size();
+      uni_add((int)nxt.size() - 1, nxt.back().links.data(), (int)nxt.back().links.size());
     } else {
       Pair &x = nxt[it->second - 1];  // HaploPair::add, HaploPair.cpp:63-89
       x.fwd += pred.fwd * x.tp;
@@ -574,6 +599,7 @@ struct Model {
       if (!aeq(x.alA, x.alB))
         for (int i = k; i < k + n; ++i)
           if (x.links[i].homo) { if (rev) x.links[i].lik = 0; x.links[i].homo = false; }
+      uni_add(it->second - 1, x.links.data() + k, n);
       if ((int)x.links.size() > S) {
         std::nth_element(x.links.begin(), x.links.begin() + S - 1, x.links.end(), GreaterLik());
         x.links.resize(S);
@@ -629,6 +655,7 @@ struct Model {
     int L = g.L, hl = head_len();
     S = prm.sample_size > 1 ? prm.sample_size : 1;
     hp.assign(L + 1, {});
+    tie_cur = 0;
     std::vector<std::unordered_map<uint64_t, int>> best(L + 1);
     initHeadList(gi, best[hl]);
     for (int i = hl; i < L; ++i) {
@@ -647,6 +674,7 @@ struct Model {
       } else {
         extendAll(i, g.at(gi, 0, i), g.at(gi, 1, i), bm);
       }
+      uni_check((int)hp[i + 1].size());
       if (hp[i + 1].empty()) break;
     }
     for (int i = hl; i <= L; ++i)
@@ -656,6 +684,7 @@ struct Model {
     if (!hp[L].empty()) {
       double total = 0;
       std::vector<Link> rl;
+      std::vector<double> fu;
       for (int s = 0; s < (int)hp[L].size(); ++s) {
         const Pair &x = hp[L][s];
         total += x.fwd;
@@ -665,6 +694,7 @@ struct Model {
           rl[i].pred = s;
           rl[i].index = i - k;
           if (!rl[i].homo) rl[i].lik *= 2.0;
+          fu.push_back(rl[i].lik);
         }
         if ((int)rl.size() > S) {
           std::nth_element(rl.begin(), rl.begin() + S - 1, rl.end(), GreaterLik());
@@ -672,6 +702,12 @@ struct Model {
         }
       }
       std::sort(rl.begin(), rl.end(), GreaterLik());
+      std::sort(fu.begin(), fu.end(), std::greater<double>());
+      if ((int)fu.size() > S && fu[S - 1] == fu[S]) tie_cur |= fu[S] == 0.0 ? 16 : 4;
+      for (int i = 1; i < (int)rl.size(); ++i)
+        if (rl[i].lik == rl[i - 1].lik && rl[i].lik != 0.0) tie_cur |= 8;
+      for (auto &l : rl)
+        if (l.lik == 0.0) tie_cur |= 32;
       for (auto &l : rl) {
         Candidate c;
         traceback(L, l.pred, l.index, c.h0, c.h1);
@@ -700,9 +736,11 @@ struct Model {
     res.assign(g.N, {});
     gp.assign(g.N, 0.0);
     resolution.assign(g.N, {});
+    tie_flags.assign(g.N, 0);
     double ll = 0;
     for (int i = 0; i < g.N; ++i) {
       double cov = resolve(i, res[i], resolution[i], gp[i]);
+      tie_flags[i] = tie_cur;
       for (auto &c : res[i]) {
         double w = c.posterior / cov;
         samples.push_back(Sample{c.h0, w});
@@ -1010,4 +1048,9 @@ double ora_resolve_range(void *h, int i0, int i1) {
   return ll;
 }
 
+// Tie diagnostics of the last resolveAll (see Model::tie_flags), [N].
+void ora_tie_flags(void *h, int *out) {
+  Model *m = (Model *)h;
+  for (int i = 0; i < (int)m->tie_flags.size(); ++i) out[i] = m->tie_flags[i];
+}
 }  // extern "C"

@@ -49,6 +49,7 @@ def lib():
         L.ora_patterns.argtypes = [vp, i, i, P(i), P(i), P(d), P(d), P(d), P(i), P(i)]
         L.ora_resolve_all.restype = d
         L.ora_resolve_all.argtypes = [vp]
+        L.ora_tie_flags.argtypes = [vp, P(i)]
         L.ora_sample_count.restype = i
         L.ora_sample_count.argtypes = [vp]
         L.ora_total_weight.restype = d
@@ -172,6 +173,12 @@ class Oracle:
 
     def resolve_all(self) -> float:
         return lib().ora_resolve_all(self.h)
+
+    def tie_flags(self) -> np.ndarray:
+        """Per-individual tie diagnostics of the last E-step (Model::tie_flags)."""
+        out = np.zeros(self.N, np.int32)
+        lib().ora_tie_flags(self.h, _p(out, C.c_int))
+        return out
 
     def samples(self):
         H = lib().ora_sample_count(self.h)
