@@ -57,6 +57,7 @@ _SIGS = [
     ("hmc_resolve_all", _i, [_vp, _P(_d), _P(_i), _P(_u64)]),
     ("hmc_get_estep", _i, [_vp, _P(_d), _P(C.c_int32), _P(C.c_int32), _P(_d), _P(_d), _P(_d)]),
     ("hmc_get_estep_stats", _i, [_vp, _P(C.c_int32)]),
+    ("hmc_get_estep_cost", _i, [_vp, _P(C.c_int32)]),
     ("hmc_get_stamps", _i, [_vp, _P(C.c_uint64)]),
     ("hmc_set_estep_mode", _i, [_vp, _i]),
     ("hmc_last_estep_split", _i, [_vp, _P(_d), _P(_d), _P(_d), _P(_i)]),

@@ -1547,6 +1547,13 @@ int hmc_get_estep_stats(hmc_ctx *h, int32_t *fmax) {
   return HMC_OK;
 }
 
+int hmc_get_estep_cost(hmc_ctx *h, int32_t *cost) {
+  if (!h || !h->c.have_estep || !cost) return HMC_EARG;
+  if ((int)h->c.h_cost.size() != h->c.nloc()) return HMC_EARG;
+  std::copy(h->c.h_cost.begin(), h->c.h_cost.end(), cost);
+  return HMC_OK;
+}
+
 int hmc_get_stamps(hmc_ctx *h, uint64_t *out12) {
   if (!h || !out12 || !h->c.d_stamps.p) return HMC_EARG;
   hipError_t e;

@@ -106,17 +106,22 @@ struct SegScratch {
   uint32_t *smeta;
 };
 
-// std::nth_element(v, v+nth, v+n, greater) on every segment's list (lane
-// g*SW+k holds element k; n, nth uniform inside a segment, n <= SW <= 32;
-// n == 0 marks an idle segment).  Whole-wave call, branch-free per lane.
-// The lists live in the LDS slots slik/smeta (slot = lane) while the
-// partitions run: a partition costs two LDS round trips — one batch that
-// reads the median candidates together with every lane's own element, and the
-// stop pairing — after which each lane writes its element straight into its
-// partner's slot (a swap is an involution).
-__device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, const Seg &sg,
-                                       const SegScratch &ss) {
+// std::nth_element(v, v+nth, v+n, greater) on every segment's list, in
+// place in the LDS slots slik/smeta (segment g's element k in slot
+// g*SW + k; n, nth uniform inside a segment, n <= SW <= 32; n == 0 marks an
+// idle segment).  Whole-wave call, branch-free per lane.
+//
+// One partition costs two LDS round trips: one batch that reads the median
+// candidates, the value at `first` and every lane's own element, and the stop
+// pairing; each lane then writes its element straight into its destination
+// slot (the LDS executes a wave's accesses in order, so no wait).  The median
+// swap (std::__move_median_to_first) is not executed as a data move: the
+// ballots are taken over *positions* (lane p evaluates the value position p
+// holds after the swap: the pivot at `first`, first's value at r), and each
+// lane's element enters the partition at x = tau(lane), tau = (first r).
+__device__ inline void seg_nth_slots(int n, int nth, const Seg &sg, const SegScratch &ss) {
   const int lane = (int)(threadIdx.x & 63);
+  const int k = sg.k;
   int first = 0, last = n, depth = n > 0 ? lg2_floor(n) * 2 : 0;
   const bool act = n > 0 && nth != n && sg.mask != 0ull;
   bool heap = false;
@@ -125,9 +130,6 @@ __device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, c
   int *lp = ss.lpos + sg.base, *rp = ss.rpos + sg.base;
   int *jl = ss.junk + lane, *jr = ss.junk + 64 + lane;
   const int kmax = sg.sw - 1;
-  ss.slik[lane] = v;
-  ss.smeta[lane] = m;
-  wave_lds_sync();
   while (true) {
     heap = heap || (act && last - first > 3 && depth == 0);
     const bool part = act && !heap && last - first > 3;
@@ -136,46 +138,50 @@ __device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, c
     // std::__move_median_to_first(first, first+1, mid, last-1) (stl_algo.h:79-102)
     const int a = first + 1, b = first + ((last - first) >> 1), c = last > 0 ? last - 1 : 0;
     const double va = sl[a], vb = sl[b], vc = sl[c], vf = sl[first];
-    const uint32_t ma = sm[a], mb = sm[b], mc = sm[c], mf = sm[first];
-    v = ss.slik[lane];
-    m = ss.smeta[lane];
+    const double v = sl[k];
+    const uint32_t m = sm[k];
     // which of a (0), b (1), c (2) is the median, as a table over the three
     // comparisons (index ab*4 + bc*2 + ac) so it compiles to selects
     const int idx = (va > vb ? 4 : 0) | (vb > vc ? 2 : 0) | (va > vc ? 1 : 0);
     const int w = (22561 >> (2 * idx)) & 3;
-    const bool w0 = w == 0, w1 = w == 1;
-    const int r = w0 ? a : (w1 ? b : c);
-    const double pivot = w0 ? va : (w1 ? vb : vc);
-    const uint32_t mr = w0 ? ma : (w1 ? mb : mc);
-    const bool isf = part && sg.k == first, isr = part && sg.k == r;
-    const double v1 = isr ? vf : v;
-    const uint32_t m1 = isr ? mf : m;
-    v = isf ? pivot : v1;
-    m = isf ? mr : m1;
-    // stops, numbered inside the segment (left from the left, right from the right)
-    const bool inr = part && sg.k >= first && sg.k < last;
-    const bool isL = inr && !isf && !(v > pivot);
-    const bool isR = inr && !(pivot > v);
-    const uint32_t Lw = seg_bits(wave_ballot(isL), sg), Rw = seg_bits(wave_ballot(isR), sg);
+    const int r = w == 0 ? a : (w == 1 ? b : c);
+    const double pivot = w == 0 ? va : (w == 1 ? vb : vc);
+    // stops by position (std::__unguarded_partition, stl_algo.h:1878-1896):
+    // left scan over [first+1, last) stops at !(x > pivot), right scan over
+    // [first, last) at !(pivot > x)
+    const double pv = k == first ? pivot : (k == r ? vf : v);
+    const bool inr = part && k >= first && k < last;
+    const bool pL = inr && k != first && !(pv > pivot);
+    const bool pR = inr && !(pivot > pv);
+    const uint32_t Lw = seg_bits(wave_ballot(pL), sg), Rw = seg_bits(wave_ballot(pR), sg);
     const int nL = __popc(Lw), nR = __popc(Rw);
-    const int kL = __popc(Lw & sg.ltk);
-    const int kR = nR - 1 - __popc(Rw & sg.ltk);
-    *(isL ? lp + kL : jl) = sg.k;
-    *(isR ? rp + kR : jr) = sg.k;
+    // this lane's element is at position x once the median is at first
+    const int x = !part ? k : (k == first ? r : (k == r ? first : k));
+    const uint32_t xb = (1u << x) - 1u;
+    const bool isL = part && ((Lw >> x) & 1u), isR = part && ((Rw >> x) & 1u);
+    const int kL = __popc(Lw & xb);
+    const int kR = nR - 1 - __popc(Rw & xb);
+    *(isL ? lp + kL : jl) = x;
+    *(isR ? rp + kR : jr) = x;
     wave_lds_sync();
     const int qR = rp[kL < kmax ? kL : kmax];
     const int qL = lp[kR < 0 ? 0 : (kR < kmax ? kR : kmax)];
     // pair k swaps iff l_k < r_k; both roles are checked, a position swaps at most once
-    const bool lsw = isL && kL < nR && sg.k < qR;
-    const bool rsw = isR && kR < nL && qL < sg.k;
-    const int dest = lsw ? sg.base + qR : (rsw ? sg.base + qL : lane);
+    const bool lsw = isL && kL < nR && x < qR;
+    const bool rsw = isR && kR < nL && qL < x;
+    const int dest = lsw ? qR : (rsw ? qL : x);
+    sl[dest] = v;
+    sm[dest] = m;
     // cut = min(l_K, r_{K-1}): the first left stop that does not swap and the
-    // leftmost right stop that does
-    const int lK = seg_lowest(seg_bits(wave_ballot(isL && !lsw), sg));
-    const int rK = seg_lowest(seg_bits(wave_ballot(rsw), sg));
+    // lowest right stop that does.  The ballots below are over lanes, i.e.
+    // over positions tau(lane): position first never qualifies (it is never a
+    // left stop and never swaps), position r is reported by lane `first`.
+    const uint32_t bl = seg_bits(wave_ballot(isL && !lsw), sg), br = seg_bits(wave_ballot(rsw), sg);
+    const uint32_t keep = ~((1u << first) | (1u << r));
+    const uint32_t ml = (bl & keep) | (((bl >> first) & 1u) << r);
+    const uint32_t mr = (br & keep) | (((br >> first) & 1u) << r);
+    const int lK = seg_lowest(ml), rK = seg_lowest(mr);
     const int cut = lK < rK ? lK : rK;
-    ss.slik[dest] = v;
-    ss.smeta[dest] = m;
     wave_lds_sync();
     first = part && cut <= nth ? cut : first;
     last = part && cut > nth ? cut : last;
@@ -183,7 +189,7 @@ __device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, c
   // Depth limit reached (std::__heap_select + iter_swap, stl_algo.h:1973-1979):
   // rare; the segment's first lane runs the sequential code on the slots.
   if (wave_ballot(heap)) {
-    if (heap && sg.k == 0) {
+    if (heap && k == 0) {
       const LinkList wl{sl, sm, 1};
       heap_select(wl, first, nth + 1, last);
       wl.swap(first, nth);
@@ -211,7 +217,7 @@ __device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, c
         x2 = x1; y2 = y1; x1 = t; y1 = u;
       }
     }
-    const int j = sg.k - first;
+    const int j = k - first;
     const bool mine = ins && (j == 0 || j == 1 || (j == 2 && len > 2));
     const double xv = j == 0 ? x0 : (j == 1 ? x1 : x2);
     const uint32_t yv = j == 0 ? y0 : (j == 1 ? y1 : y2);
@@ -222,6 +228,16 @@ __device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, c
     }
     wave_lds_sync();
   }
+}
+
+// Register interface: lane g*SW+k holds element k of segment g's list.
+__device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, const Seg &sg,
+                                       const SegScratch &ss) {
+  const int lane = (int)(threadIdx.x & 63);
+  ss.slik[lane] = v;
+  ss.smeta[lane] = m;
+  wave_lds_sync();
+  seg_nth_slots(n, nth, sg, ss);
   v = ss.slik[lane];
   m = ss.smeta[lane];
 }

@@ -513,6 +513,22 @@ struct VFront {
     return t < fc ? (uint32_t *)(l + (size_t)fc * (16 + 8 * S)) + t * S
                   : (uint32_t *)(g + (size_t)fcap * (16 + 8 * S)) + (size_t)(t - fc) * S;
   }
+  // Link k of state t with address-space-specific loads (ds_read for the LDS
+  // tier, global_load for the HBM tier): a flat load would count against
+  // lgkmcnt and make every later LDS wait also wait on HBM.
+  __device__ void ld_link(int t, int k, double &lk, uint32_t &mt) const {
+    if (t < fc) {
+      typedef __attribute__((address_space(3))) const double lds_f64;
+      typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+      lk = *((lds_f64 *)(l + (size_t)fc * 16) + t * S + k);
+      mt = *((lds_u32 *)(l + (size_t)fc * (16 + 8 * S)) + t * S + k);
+    } else {
+      typedef __attribute__((address_space(1))) const double glb_f64;
+      typedef __attribute__((address_space(1))) const uint32_t glb_u32;
+      lk = *((glb_f64 *)(g + (size_t)fcap * 16) + (size_t)(t - fc) * S + k);
+      mt = *((glb_u32 *)(g + (size_t)fcap * (16 + 8 * S)) + (size_t)(t - fc) * S + k);
+    }
+  }
 };
 
 struct K2Shared {
@@ -736,70 +752,81 @@ __global__ __launch_bounds__(256) void estep_values(ValueArgs a) {
         break;
       }
       // B: the adds that overflow S, one chain of adds per state, run by 2S-lane
-      // segments that pull chains (longest first) from the block queue; the
-      // list stays in the segment's lanes between adds
+      // segments that pull chains (longest first) from the block queue.  The
+      // list lives in the segment's LDS selection slots for the whole chain;
+      // each add writes its transformed links behind it and selects in place.
+      // The contribution word of add r+1 is loaded one add ahead.
       if (NCH > 0) {
-        int ci = -1, r = 0, re_ = 0, st = 0, k0 = 0, nit = 0;
+        int ci = -1, r = 0, re_ = 0, st = 0, k0 = 0;
+        [[maybe_unused]] int nit = 0;
 #ifdef HMC_STAMPS
         unsigned long long tstep = __builtin_amdgcn_s_memtime();
 #endif
-        double tpv = 0.0, v = 0.0;
-        uint32_t m = 0;
+        double tpv = 0.0;
+        uint32_t wc = 0, wn = 0;
         bool differ = false, done = sg.g >= G;
+        double *slot_l = ss.slik + lane;
+        uint32_t *slot_m = ss.smeta + lane;
         while (true) {
           const bool idle = !done && ci < 0;
-          int got = 0;
-          if (idle && sg.k == 0) got = atomicAdd(&bs->next, 1);
-          got = __shfl(got, sg.base);
-          if (idle) {
-            if (got < NCH) {
-              ci = got;
-              st = (int)Rch[ci];
-              r = (int)*Y.r0(st);
-              re_ = (int)Rcb[st + 1];
-              tpv = Rtp[st];
-              const uint32_t hd = Rhd[st];
-              differ = (hd & 0xFFu) != ((hd >> 8) & 0xFFu);
-              k0 = (int)*Y.nl(st);
-              if (sg.k < k0) {
-                v = Y.lik(st)[sg.k];
-                m = Y.meta(st)[sg.k];
+          if (wave_ballot(idle)) {
+            int got = 0;
+            if (idle && sg.k == 0) got = atomicAdd(&bs->next, 1);
+            got = __shfl(got, sg.base);
+            if (idle) {
+              if (got < NCH) {
+                ci = got;
+                st = (int)Rch[ci];
+                r = (int)*Y.r0(st);
+                re_ = (int)Rcb[st + 1];
+                tpv = Rtp[st];
+                const uint32_t hd = Rhd[st];
+                differ = (hd & 0xFFu) != ((hd >> 8) & 0xFFu);
+                k0 = (int)*Y.nl(st);
+                wc = Rct[r];
+                wn = r + 1 < re_ ? Rct[r + 1] : 0u;
+                if (sg.k < k0) {
+                  *slot_l = Y.lik(st)[sg.k];
+                  *slot_m = Y.meta(st)[sg.k];
+                }
+              } else {
+                done = true;
               }
-            } else {
-              done = true;
             }
           }
           const bool act = ci >= 0;
           if (!wave_ballot(act)) break;
           int n = 0;
           if (act) {
-            const uint32_t w = Rct[r];
-            const uint32_t s = w & 0xFFFFu, ns = w >> 24;
-            const bool rev = (w >> 16) & 1u;
+            const uint32_t s = wc & 0xFFFFu, ns = wc >> 24;
+            const bool rev = (wc >> 16) & 1u;
             n = k0 + (int)ns;
             if (sg.k >= k0 && sg.k < n) {  // HaploPair::add transformation (HaploPair.cpp:63-80)
               const int qk = sg.k - k0;
-              const uint32_t mm = X.meta((int)s)[qk];
-              double lk = X.lik((int)s)[qk] * tpv;
-              bool homo = meta_homo(mm);
+              double lk;
+              uint32_t pm;
+              X.ld_link((int)s, qk, lk, pm);
+              lk *= tpv;
+              bool homo = meta_homo(pm);
               if (differ && homo) {
                 if (rev) lk = 0.0;
                 homo = false;
               }
-              v = lk;
-              m = meta_pack(s, (uint32_t)qk, rev, homo, false);
+              *slot_l = lk;
+              *slot_m = meta_pack(s, (uint32_t)qk, rev, homo, false);
             }
+            wc = wn;
+            wn = r + 2 < re_ ? Rct[r + 2] : 0u;
           }
+          wave_lds_sync();
           K2_CNT(10, 1);
           ++nit;
 #ifdef HMC_STAMPS
-          __builtin_amdgcn_s_waitcnt(0);
           const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
           K2_CNT(14, ts0 - tstep);
 #endif
-          seg_nth_element(v, m, n, S - 1, sg, ss);
+          seg_nth_slots(n, S - 1, sg, ss);
 #ifdef HMC_STAMPS
-          __builtin_amdgcn_s_waitcnt(0);
           tstep = __builtin_amdgcn_s_memtime();
           K2_CNT(13, tstep - ts0);
 #endif
@@ -807,8 +834,8 @@ __global__ __launch_bounds__(256) void estep_values(ValueArgs a) {
             k0 = S;
             if (++r == re_) {
               if (sg.k < S) {
-                Y.lik(st)[sg.k] = v;
-                Y.meta(st)[sg.k] = m;
+                Y.lik(st)[sg.k] = *slot_l;
+                Y.meta(st)[sg.k] = *slot_m;
               }
               if (sg.k == 0) *Y.nl(st) = (uint32_t)S;
               ci = -1;

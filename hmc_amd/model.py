@@ -243,6 +243,12 @@ class HaploModel:
         self._check(lib().hmc_get_estep_stats(self._h, _p(out, C.c_int32)))
         return out
 
+    def estep_cost(self) -> np.ndarray:
+        """Per-individual E-step time of the last E-step (units of 1024 shader clocks)."""
+        out = np.zeros(self.i1 - self.i0, np.int32)
+        self._check(lib().hmc_get_estep_cost(self._h, _p(out, C.c_int32)))
+        return out
+
     def samples(self, H: int):
         al = np.zeros((H, self.L), np.int32)
         w = np.zeros(H)

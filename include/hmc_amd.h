@@ -103,6 +103,9 @@ int hmc_get_estep(hmc_ctx *ctx, double *total, int32_t *ncand, int32_t *status, 
 /* Largest number of HaploPair states any locus of each individual held in the
  * last E-step (diagnostic). */
 int hmc_get_estep_stats(hmc_ctx *ctx, int32_t *fmax);
+/* Per individual of the shard: E-step time of the last E-step in units of
+ * 1024 shader clocks (value pass; the scheduling key of the next E-step). */
+int hmc_get_estep_cost(hmc_ctx *ctx, int32_t *cost);
 /* Diagnostic build (libhmc_amd_diag.so) only: 20 shader-cycle / event
  * counters of the E-step phases summed over waves; zeros in the product build. */
 int hmc_get_stamps(hmc_ctx *ctx, uint64_t *out20);
