@@ -38,6 +38,21 @@ namespace hmc {
 namespace {
 
 __device__ inline int32_t root_code(int k) { return -(k + 2); }
+
+// LDS hand-off between the lanes of a one-wavefront block: the LDS executes a
+// wave's accesses in order, so only the compiler must keep program order (a
+// __syncthreads would also wait for every outstanding HBM store).
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ inline double rl_f64(double x, int lane) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
+  return __longlong_as_double((long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo));
+}
 __device__ inline bool is_root(int32_t u) { return u <= -2; }
 __device__ inline int root_start(int32_t u) { return -u - 2; }
 
@@ -131,6 +146,24 @@ __device__ inline ParentView parent_view(const MineArgs &a, int level, int pidx)
 
 // ---------------------------------------------------------------------------
 constexpr int CROW = WAVE + 18;  // LDS row stride (doubles): one chunk's contributions + batch padding
+constexpr int MC_U = 4;           // chunks of 64 list entries per load group of mine_count
+__host__ __device__ inline int mine_count_bufs(int amax) { return amax <= 8 ? MC_U : 1; }
+
+// Child k's matching entries of one chunk (compacted in LDS) to its list:
+// child k of a parent with n entries owns n slots at region + k*n; `mine` and
+// `run` are lane k's entry count in this chunk and before it.
+__device__ inline void store_child_lists(const MineArgs &a, const uint32_t *ibuf, const double *cbuf, int nc, int n,
+                                         unsigned long long region, int mine, int run, int lane) {
+  for (int k = 0; k < nc; ++k) {
+    const int mk = __builtin_amdgcn_readlane(mine, k);
+    const uint32_t rk = (uint32_t)__builtin_amdgcn_readlane(run, k);
+    if (lane < mk) {
+      const unsigned long long at = region + (unsigned long long)k * (unsigned long long)n + rk + lane;
+      a.lout_idx[at] = ibuf[k * WAVE + lane];
+      if (a.genotype) a.lout_val[at] = cbuf[k * CROW + lane];
+    }
+  }
+}
 
 #ifdef HMC_STAMPS
 #define MSTAMP(k)                                                \
@@ -150,7 +183,9 @@ constexpr int CROW = WAVE + 18;  // LDS row stride (doubles): one chunk's contri
 // any child is known to be extended (lists of children that are not extended
 // are simply never read).
 __global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg, int pend) {
-  extern __shared__ __align__(16) double cbuf[];  // [nc][CROW] contributions, then [nc][WAVE] items
+  // [ub][amax][CROW] contributions, then [ub][amax][WAVE] items: one buffer
+  // per chunk of a load group (ub = U when amax <= 8, else 1)
+  extern __shared__ __align__(16) double cbuf0[];
   const int tid = threadIdx.x, lane = tid;
   const int pidx = pbeg + blockIdx.x;
   if (pidx >= pend) return;
@@ -160,23 +195,57 @@ __global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg
   const ParentView p = parent_view(a, level, pidx);
   MSTAMP(0);
   if (!p.ok) return;
-  uint32_t *ibuf = (uint32_t *)(cbuf + (size_t)p.nc * CROW);
+  const int ub = mine_count_bufs(a.amax);
+  uint32_t *ibuf0 = (uint32_t *)(cbuf0 + (size_t)ub * a.amax * CROW);
   const uint8_t *ca = a.pos_allele + (size_t)p.e * a.amax;
   const uint64_t lt = (1ull << lane) - 1ull;
   const unsigned long long region = level == 1 ? a.r_region[pidx] : a.region[pidx];
   const bool write_lists = a.lout_idx != nullptr;
+  // lane k: child k's allele (and, genotype branch, its population frequency),
+  // read once; the child loop takes them with readlane
+  const int my_al = lane < p.nc ? (int)ca[lane] : 0;
+  const double my_af = (a.genotype && lane < p.nc) ? a.afreq[(size_t)p.e * a.amax + my_al] : 0.0;
   double sum = 0.0;
   uint32_t cnt = 0, run = 0;  // lane k: child k's entries so far
-  constexpr int U = 4;  // chunks whose loads are in flight together
+  constexpr int U = MC_U;     // chunks whose loads are in flight together
+  const size_t erow = (size_t)p.e * a.item_stride;
   for (int base = 0; base < p.n; base += U * WAVE) {
+    // loads in two batches over all U chunks: list entries, then the gathers
+    // that depend on them (one exposed latency each per U*64 entries).
+    // Branch-free (lanes past the end load entry n-1 and are masked by `in`),
+    // so each batch is one run of loads and one wait.
     EntryView xs[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) xs[u] = load_entry(a, level == 1, p.lidx, p.lval, base + u * WAVE + lane, p.n, p.e);
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * WAVE + lane;
+      const int ic = i < p.n ? i : p.n - 1;
+      xs[u].in = i < p.n;
+      xs[u].item = level == 1 ? (uint32_t)(a.item_base + ic) : p.lidx[ic];
+      xs[u].v = (a.genotype && level != 1) ? p.lval[ic] : 1.0;
+      xs[u].w = 0.0;
+      xs[u].h = 0xFE;
+      xs[u].g = make_uchar2(0xFE, 0xFE);
+    }
+    if (a.genotype) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) xs[u].g = a.geno_lm[erow + xs[u].item];
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        xs[u].h = a.samp_lm[erow + xs[u].item];
+        xs[u].w = a.w[xs[u].item];
+      }
+    }
     MSTAMP(1);
+    int mine_u[U], run_u[U];  // lane k: child k's entries in chunk u, and before it
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      mine_u[u] = 0;
+      run_u[u] = 0;
       if (base + u * WAVE >= p.n) break;
       const EntryView &x = xs[u];
+      double *cbuf = cbuf0 + (size_t)(ub == U ? u : 0) * a.amax * CROW;
+      uint32_t *ibuf = ibuf0 + (size_t)(ub == U ? u : 0) * a.amax * WAVE;
       // Each child's matching entries, compacted in list order.  Non-matching
       // entries would add +0.0, an exact no-op on a sum >= +0, so skipping them
       // leaves every child's add chain — and its rounding — unchanged.  Rows
@@ -184,8 +253,23 @@ __global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg
       // 16-value batches without predication (x + 0.0 == x exactly).
       int mine = 0;
       for (int k = 0; k < p.nc; ++k) {
+        const uint8_t al = (uint8_t)__builtin_amdgcn_readlane(my_al, k);
         double c;
-        const bool m = contribution(a, x, p.e, ca[k], c);
+        bool m;
+        if (a.genotype) {
+          // getMatchingFrequency (PatternManager.cpp:267-291) x carried product (:243-248)
+          const bool m0 = x.g.x == MISSING, m1 = x.g.y == MISSING;
+          m = x.in && (m0 || m1 || x.g.x == al || x.g.y == al);
+          const double af = rl_f64(my_af, k);
+          const double x0 = m0 ? af : (x.g.x == al ? 1.0 : 0.0);
+          const double x1 = m1 ? af : (x.g.y == al ? 1.0 : 0.0);
+          const double f = (0.0 + x0) + x1;
+          const double t = 1.0 * (0.5 * f);
+          c = m ? x.v * t : 0.0;
+        } else {  // sample branch (:252-263): the haplotype weight
+          m = x.in && x.h == al;
+          c = m ? x.w : 0.0;
+        }
         const uint64_t b = __ballot(m);
         cbuf[k * CROW + lane] = 0.0;
         if (lane < 16) cbuf[k * CROW + WAVE + lane] = 0.0;
@@ -195,18 +279,11 @@ __global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg
         }
         if (lane == k) mine = __popcll(b);
       }
-      __syncthreads();
+      wave_sync();  // one wavefront per block: LDS order suffices, no wait on the list stores
       MSTAMP(2);
-      if (write_lists)  // child k's new entries, one coalesced store per child
-        for (int k = 0; k < p.nc; ++k) {
-          const int mk = __builtin_amdgcn_readlane(mine, k);
-          const uint32_t rk = (uint32_t)__builtin_amdgcn_readlane((int)run, k);
-          if (lane < mk) {
-            const unsigned long long at = region + (unsigned long long)k * (unsigned long long)p.n + rk + lane;
-            a.lout_idx[at] = ibuf[k * WAVE + lane];
-            if (a.genotype) a.lout_val[at] = cbuf[k * CROW + lane];
-          }
-        }
+      mine_u[u] = mine;
+      run_u[u] = (int)run;
+      if (write_lists && ub == 1) store_child_lists(a, ibuf, cbuf, p.nc, p.n, region, mine, (int)run, lane);
       if (lane < p.nc) {
         cnt += (uint32_t)mine;
         run += (uint32_t)mine;
@@ -226,9 +303,17 @@ __global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg
         }
         sum = s;
       }
-      __syncthreads();
+      wave_sync();
       MSTAMP(3);
     }
+    // the group's child lists: all stores after the last chunk, so no chunk
+    // waits on the previous chunk's stores
+    if (write_lists && ub == U)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (base + u * WAVE < p.n)
+          store_child_lists(a, ibuf0 + (size_t)u * a.amax * WAVE, cbuf0 + (size_t)u * a.amax * CROW, p.nc, p.n,
+                            region, mine_u[u], run_u[u], lane);
   }
   const int lane_c = tid;  // child lanes: threads 0..nc-1
   if (lane_c < p.nc) {
@@ -428,7 +513,7 @@ __global__ void mine_succ(MineArgs a, PatternTable t, int P) {
 // ---- host-side launch helpers -----------------------------------------------
 hipError_t launch_mine_count(const MineArgs &a, int level, int pbeg, int pend, hipStream_t st) {
   if (pend <= pbeg) return hipSuccess;
-  const size_t lds = (size_t)a.amax * CROW * 8 + (size_t)a.amax * WAVE * 4;
+  const size_t lds = (size_t)mine_count_bufs(a.amax) * ((size_t)a.amax * CROW * 8 + (size_t)a.amax * WAVE * 4);
   static size_t lds_attr = 0;
   if (lds > 65536 - 1024 && lds > lds_attr) {  // many alleles: opt in to the CU's full LDS
     hipError_t e = hipFuncSetAttribute((const void *)mine_count, hipFuncAttributeMaxDynamicSharedMemorySize,
