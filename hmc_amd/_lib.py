@@ -24,7 +24,8 @@ class HMCError(RuntimeError):
 
 class IterLog(C.Structure):
     _fields_ = [("log_likelihood", C.c_double), ("t_estep_s", C.c_double), ("t_mstep_s", C.c_double),
-                ("r_e", C.c_uint64), ("r_m", C.c_uint64), ("n_patterns", C.c_int), ("n_samples", C.c_int)]
+                ("r_e", C.c_uint64), ("r_m", C.c_uint64), ("n_patterns", C.c_int), ("n_samples", C.c_int),
+                ("switch_error", C.c_double), ("ihp", C.c_double), ("igp", C.c_double)]
 
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_size_t, C.c_void_p)
@@ -66,6 +67,7 @@ _SIGS = [
     ("hmc_clear_samples", _i, [_vp]),
     ("hmc_run", _i, [_vp, _i, _P(IterLog), _i, _P(_i), _P(_d), _P(_u64), _P(_i)]),
     ("hmc_get_best_resolutions", _i, [_vp, _P(C.c_int32)]),
+    ("hmc_haplocomp", _i, [_vp, _P(_d), _P(_d), _P(_d)]),
     ("hmc_write_phase", _i, [_vp, _cp]),
     ("hmc_set_tuning", _i, [_vp, _i, _u64, _i]),
     ("hmc_set_estep_shape", _i, [_vp, _i, _i]),

@@ -1167,6 +1167,66 @@ struct Ctx {
         }
   }
 
+  // ------------------------------------------------------------ HaploComp --
+  // HaploComp compare(&genos, &resolutions) (HaploComp.cpp:29-76, 144-155;
+  // HaploModel.cpp:134): the input panel as given (the "real" phase) against
+  // res = [n][2][L] allele indices of this rank's individuals.  Integer
+  // counters, summed over ranks (HaploComp::operator+=, :78-90), then
+  // out = {switch error, IHP, IGP}.  m_genos_input == m_genos_real there, so
+  // no missing error.
+  int haplocomp(const std::vector<uint8_t> &res, double out[3]) {
+    const int n = nloc(), L = pan.L;
+    auto am = [](uint8_t x, uint8_t y) { return x == MISSING || y == MISSING || x == y; };  // Allele::isMatch
+    double cnt[6] = {0, 0, 0, 0, 0, 0};  // se_num, se_den, ihp_num, ihp_den, igp_num, igp_den
+    for (int i = 0; i < n; ++i) {
+      const uint8_t *r0 = pan.idx.data() + ((size_t)(i0 + i) * 2) * L, *r1 = r0 + L;
+      const uint8_t *f0 = res.data() + ((size_t)i * 2) * L, *f1 = f0 + L;
+      auto hasMissing = [&](int k) { return r0[k] == MISSING || r1[k] == MISSING; };
+      auto match = [&](int k, bool rev) {  // Genotype::isMatch(g, i, reversed) (Genotype.cpp:97-116)
+        return rev ? (am(r0[k], f1[k]) && am(r1[k], f0[k])) : (am(r0[k], f0[k]) && am(r1[k], f1[k]));
+      };
+      int het = 0, miss = 0;  // Genotype::checkGenotype (Genotype.cpp:44-55)
+      for (int k = 0; k < L; ++k) {
+        het += am(r0[k], r1[k]) ? 0 : 1;
+        miss += hasMissing(k) ? 1 : 0;
+      }
+      // getSwitchDistanceIgnoreMissing (Genotype.cpp:224-266)
+      int start = L, sd = 0;
+      for (int k = 0; k < L; ++k)
+        if (!(hasMissing(k) || (match(k, true) && match(k, false)))) { start = k; break; }
+      if (start < L) {
+        bool rev;
+        if (match(start, true)) rev = true;
+        else if (match(start, false)) rev = false;
+        else return fail(HMC_EARG, "Inconsistent genotypes at locus %d!", start);
+        for (int k = start + 1; k < L; ++k) {
+          if (hasMissing(k) || match(k, rev)) continue;
+          if (!match(k, !rev)) return fail(HMC_EARG, "Inconsistent genotypes at locus %d!", k);
+          rev = !rev;
+          ++sd;
+        }
+      }
+      int d1 = 0, d2 = 0;  // getDiffNumIgnoreMissing (Genotype.cpp:160-175)
+      for (int k = 0; k < L; ++k)
+        if (!hasMissing(k)) {
+          d1 += match(k, true) ? 0 : 1;
+          d2 += match(k, false) ? 0 : 1;
+        }
+      cnt[0] += sd;
+      cnt[1] += het - 1;
+      cnt[2] += sd > 0 ? 1 : 0;
+      cnt[3] += het > 1 ? 1 : 0;
+      cnt[4] += d1 < d2 ? d1 : d2;
+      cnt[5] += L - miss;
+    }
+    int rc = allreduce_host(cnt, 6);  // integers < 2^53: exact in any order
+    if (rc) return rc;
+    out[0] = cnt[0] / cnt[1];
+    out[1] = cnt[2] / cnt[3];
+    out[2] = cnt[4] / cnt[5];
+    return HMC_OK;
+  }
+
   // ------------------------------------------------------------------ run --
   int run(int max_iter, hmc_iter_log *log, int cap, int *iters, double *t_m0, uint64_t *rm0, int *np0) {
     using clk = std::chrono::steady_clock;
@@ -1200,6 +1260,11 @@ struct Ctx {
         if ((rc = resolutions_idx(best_res))) return rc;
       }
       hmc_iter_log rec{};
+      double hc[3];
+      if ((rc = haplocomp(best_res, hc))) return rc;  // HaploModel.cpp:134-136
+      rec.switch_error = hc[0];
+      rec.ihp = hc[1];
+      rec.igp = hc[2];
       rec.log_likelihood = ll;
       rec.t_estep_s = te;
       rec.r_e = re;
@@ -1604,6 +1669,17 @@ int hmc_clear_samples(hmc_ctx *h) {
   if (!h) return HMC_EARG;
   h->c.have_samples = false;
   h->c.H = 0;
+  return HMC_OK;
+}
+
+int hmc_haplocomp(hmc_ctx *h, double *switch_error, double *ihp, double *igp) {
+  if (!h || !h->c.have_best) return HMC_EARG;
+  double out[3];
+  const int rc = h->c.haplocomp(h->c.best_res, out);
+  if (rc) return rc;
+  if (switch_error) *switch_error = out[0];
+  if (ihp) *ihp = out[1];
+  if (igp) *igp = out[2];
   return HMC_OK;
 }
 

@@ -283,10 +283,18 @@ class HaploModel:
         self.iterations = it.value
         self.m0 = dict(t_s=tm0.value, r_m=rm0.value, n_patterns=np0.value)
         self.log = [dict(ll=l.log_likelihood, t_e=l.t_estep_s, t_m=l.t_mstep_s, r_e=l.r_e, r_m=l.r_m,
-                         n_patterns=l.n_patterns, n_samples=l.n_samples) for l in logs[:it.value]]
+                         n_patterns=l.n_patterns, n_samples=l.n_samples,
+                         haplocomp=(l.switch_error, l.ihp, l.igp)) for l in logs[:it.value]]
         out = np.zeros((self.i1 - self.i0, 2, self.L), np.int32)
         self._check(lib().hmc_get_best_resolutions(self._h, _p(out, C.c_int32)))
         return out
+
+    def haplocomp(self):
+        """HaploComp (switch error, IHP, IGP) of the input panel against the
+        accepted resolutions of the last run (HaploComp.cpp:29-155)."""
+        se, ihp, igp = C.c_double(), C.c_double(), C.c_double()
+        self._check(lib().hmc_haplocomp(self._h, C.byref(se), C.byref(ihp), C.byref(igp)))
+        return se.value, ihp.value, igp.value
 
     def write_phase(self, path: str):
         self._check(lib().hmc_write_phase(self._h, path.encode()))

@@ -125,12 +125,20 @@ typedef struct hmc_iter_log {
   uint64_t r_e, r_m;
   int n_patterns;              /* patterns after M_k */
   int n_samples;
+  /* HaploComp of the input panel (phase as given) against the accepted
+   * resolutions after E_k (HaploModel.cpp:134-136) */
+  double switch_error, ihp, igp;
 } hmc_iter_log;
 /* Runs M0 + up to max_iteration EM iterations with the reference's
  * convergence rule.  log[] receives up to log_cap iterations; *iterations the
  * number run; *t_m0_s, *r_m0, *n_patterns0 describe M0. */
 int hmc_run(hmc_ctx *ctx, int max_iteration, hmc_iter_log *log, int log_cap, int *iterations, double *t_m0_s,
             uint64_t *r_m0, int *n_patterns0);
+/* HaploComp (HaploComp.cpp:29-155) of the input panel, phase as given,
+ * against the accepted resolutions: switch error, incorrect-haplotype and
+ * incorrect-genotype percentages over all ranks' individuals.  Replaces the
+ * HaploComp compare(&genos, &resolutions) of HaploModel.cpp:134. */
+int hmc_haplocomp(hmc_ctx *ctx, double *switch_error, double *ihp, double *igp);
 /* Accepted resolutions of the last hmc_run ([n][2][L] symbols). */
 int hmc_get_best_resolutions(hmc_ctx *ctx, int32_t *out);
 /* HaploFile::writeGenoData (HaploFile.cpp:120-153) of the accepted

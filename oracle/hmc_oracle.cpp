@@ -20,6 +20,7 @@
 // tie order is the one a g++-11 build of the reference would produce.
 // ============================================================================
 #include <algorithm>
+#include <array>
 #include <cfloat>
 #include <chrono>
 #include <cmath>
@@ -30,6 +31,7 @@
 #include <string>
 #include <unordered_map>
 #include <vector>
+#include <array>
 
 namespace ora {
 
@@ -754,6 +756,64 @@ struct Model {
     return ll;
   }
 
+  // HaploComp (HaploComp.cpp:29-76, 144-155) of the input panel (the "real"
+  // phase, as given) against inferred haplotypes infer[i] = [2][L] symbols;
+  // m_genos_input == m_genos_real, so no missing error.  out = {switch error,
+  // IHP, IGP}; returns false where the reference would stop with
+  // "Inconsistent genotypes" (Genotype.cpp:246-263).
+  bool haploComp(const std::vector<std::vector<int>> &infer, double out[3]) const {
+    const int L = g.L;
+    long long se_n = 0, se_d = 0, ig_n = 0, ig_d = 0, ih_n = 0, ih_d = 0;
+    for (int i = 0; i < g.N; ++i) {
+      const int *f = infer[i].data();
+      auto hasMissing = [&](int k) { return missing(g.at(i, 0, k)) || missing(g.at(i, 1, k)); };
+      // Genotype::isMatch(g, i, reversed) (Genotype.cpp:97-116)
+      auto match = [&](int k, bool rev) {
+        return rev ? (amatch(g.at(i, 0, k), f[L + k]) && amatch(g.at(i, 1, k), f[k]))
+                   : (amatch(g.at(i, 0, k), f[k]) && amatch(g.at(i, 1, k), f[L + k]));
+      };
+      int het = 0, miss = 0;  // Genotype::checkGenotype (Genotype.cpp:44-55)
+      for (int k = 0; k < L; ++k) {
+        if (!amatch(g.at(i, 0, k), g.at(i, 1, k))) ++het;
+        if (hasMissing(k)) ++miss;
+      }
+      // getSwitchDistanceIgnoreMissing (Genotype.cpp:224-266)
+      int start = L;
+      for (int k = 0; k < L; ++k)
+        if (!(hasMissing(k) || (match(k, true) && match(k, false)))) { start = k; break; }
+      int sd = 0;
+      if (start < L) {
+        bool rev;
+        if (match(start, true)) rev = true;
+        else if (match(start, false)) rev = false;
+        else return false;
+        for (int k = start + 1; k < L; ++k) {
+          if (hasMissing(k) || match(k, rev)) continue;
+          if (match(k, !rev)) { rev = !rev; ++sd; }
+          else return false;
+        }
+      }
+      // getDiffNumIgnoreMissing (Genotype.cpp:160-175)
+      int d1 = 0, d2 = 0;
+      for (int k = 0; k < L; ++k)
+        if (!hasMissing(k)) {
+          if (!match(k, true)) ++d1;
+          if (!match(k, false)) ++d2;
+        }
+      se_n += sd;
+      se_d += het - 1;
+      ig_n += d1 < d2 ? d1 : d2;
+      ig_d += L - miss;
+      if (sd > 0) ++ih_n;
+      if (het > 1) ++ih_d;
+    }
+    out[0] = (double)se_n / se_d;
+    out[1] = (double)ih_n / ih_d;
+    out[2] = (double)ig_n / ig_d;
+    return true;
+  }
+  std::vector<std::array<double, 3>> comp_log;
+
   // HaploModel.cpp:117-155 (MV, sampling EM).
   void run() {
     using clk = std::chrono::steady_clock;
@@ -768,7 +828,7 @@ struct Model {
       best_res[i].assign(2 * g.L, 0);
       for (int k = 0; k < g.L; ++k) { best_res[i][k] = g.at(i, 0, k); best_res[i][g.L + k] = g.at(i, 1, k); }
     }
-    ll_log.clear(); re_log.clear(); t_e_log.clear(); t_m_log.clear();
+    ll_log.clear(); re_log.clear(); t_e_log.clear(); t_m_log.clear(); comp_log.clear();
     double old_ll = -DBL_MAX;
     iterations = 0;
     for (int it = 1; it <= prm.max_iter; ++it) {
@@ -780,6 +840,9 @@ struct Model {
       ll_log.push_back(ll);
       iterations = it;
       if (ll >= old_ll) best_res = resolution;
+      std::array<double, 3> hc{};  // HaploComp compare(&genos, &resolutions) (HaploModel.cpp:134)
+      if (!haploComp(best_res, hc.data())) hc.fill(std::nan(""));
+      comp_log.push_back(hc);
       if (it < prm.max_iter && ll >= old_ll && (old_ll - ll) / old_ll > 0.0001) {
         uint64_t rm0 = R_M;
         auto t2 = clk::now();
@@ -939,6 +1002,19 @@ void ora_run_log(void *h, double *ll, uint64_t *re, uint64_t *rm, int *npat, dou
   for (size_t i = 0; i < m->npat_log.size(); ++i) npat[i] = m->npat_log[i];
   for (size_t i = 0; i < m->t_m_log.size(); ++i) t_m[i] = m->t_m_log[i];
   *t_m0 = m->t_m0;
+}
+// HaploComp triple {switch error, IHP, IGP} of every iteration of run(): [iters][3]
+void ora_run_comp_log(void *h, double *out) {
+  Model *m = (Model *)h;
+  for (size_t i = 0; i < m->comp_log.size(); ++i)
+    for (int j = 0; j < 3; ++j) out[i * 3 + j] = m->comp_log[i][j];
+}
+// HaploComp of the panel against infer[N][2][L] symbols; 0 ok, -1 inconsistent
+int ora_haplocomp(void *h, const int *infer, double *out3) {
+  Model *m = (Model *)h;
+  std::vector<std::vector<int>> f(m->g.N);
+  for (int i = 0; i < m->g.N; ++i) f[i].assign(infer + (size_t)i * 2 * m->g.L, infer + (size_t)(i + 1) * 2 * m->g.L);
+  return m->haploComp(f, out3) ? 0 : -1;
 }
 // accepted resolutions after run(): [N][2][L]
 void ora_best_resolutions(void *h, int *out) {

@@ -50,6 +50,9 @@ def lib():
         L.ora_resolve_all.restype = d
         L.ora_resolve_all.argtypes = [vp]
         L.ora_tie_flags.argtypes = [vp, P(i)]
+        L.ora_run_comp_log.argtypes = [vp, P(d)]
+        L.ora_haplocomp.restype = i
+        L.ora_haplocomp.argtypes = [vp, P(i), P(d)]
         L.ora_sample_count.restype = i
         L.ora_sample_count.argtypes = [vp]
         L.ora_total_weight.restype = d
@@ -227,9 +230,20 @@ class Oracle:
                           _p(npat, C.c_int), _p(te, C.c_double), _p(tm, C.c_double), C.byref(tm0))
         best = np.zeros((self.N, 2, self.L), np.int32)
         lib().ora_best_resolutions(self.h, _p(best, C.c_int))
+        comp = np.zeros((it, 3), np.float64)
+        lib().ora_run_comp_log(self.h, _p(comp, C.c_double))
         n_m = max(0, it - 1) if len(ll) and np.isfinite(ll).all() else max(0, it - 1)
         return dict(iterations=it, ll=ll, R_E=re, R_M=rm, n_patterns=npat, t_e=te, t_m=tm,
-                    t_m0=tm0.value, resolutions=best, n_m=n_m)
+                    t_m0=tm0.value, resolutions=best, n_m=n_m, haplocomp=comp)
+
+    def haplocomp(self, infer: np.ndarray):
+        """HaploComp (switch error, IHP, IGP) of the input panel against
+        infer[N][2][L] symbols, or None where the reference exits on
+        inconsistent genotypes."""
+        f = np.ascontiguousarray(infer, np.int32)
+        out = np.zeros(3, np.float64)
+        rc = lib().ora_haplocomp(self.h, _p(f, C.c_int), _p(out, C.c_double))
+        return None if rc else out
 
 
 def std_nth_element(lik: np.ndarray, tag: np.ndarray, nth: int):

@@ -144,6 +144,10 @@ def test_full_em(oracle_mod, name):
         assert m.log[k]["r_m"] == r["R_M"][k + 1]
         assert m.log[k]["n_patterns"] == r["n_patterns"][k + 1]
     assert np.array_equal(res, r["resolutions"])
+    # HaploComp log line of every iteration (HaploModel.cpp:134-136): integer
+    # counts, so the ratios are bit-equal
+    np.testing.assert_array_equal(np.array([x["haplocomp"] for x in m.log]), r["haplocomp"])
+    np.testing.assert_array_equal(np.array(m.haplocomp()), r["haplocomp"][-1])
 
 
 @pytest.mark.parametrize("gname", ["cfg1", "miss_a3", "snp_miss", "s3"])

@@ -105,3 +105,39 @@ def test_missing_allele_head_quirk(oracle_mod):
     o.resolve_all()
     nc, gp = o.estep_summary()
     assert nc[0] > 0 and gp[0] > 0
+
+
+def test_haplocomp_known_answers(oracle_mod):
+    """HaploComp (HaploComp.cpp:29-155, Genotype.cpp:160-266) worked by hand on
+    one individual: loci (1,2) (2,1) (1,2) (2,1) (1,1) (1,2), five heterozygous."""
+    A = np.array([[[49, 50, 49, 50, 49, 49], [50, 49, 50, 49, 49, 50]]], np.int32)
+    o = oracle_mod.Oracle(A, "S" * 6)
+    assert o.haplocomp(A).tolist() == [0.0, 0.0, 0.0]
+    B = A.copy()
+    B[0, :, 3:] = B[0, ::-1, 3:]  # phase flipped from locus 3 on
+    # one switch over 5-1 heterozygous steps; the haplotype is wrong; the best
+    # orientation mismatches loci 3 and 5 of the 6 non-missing loci
+    assert o.haplocomp(B).tolist() == [0.25, 1.0, 2 / 6]
+    C = A.copy()
+    C[0, 0, 0] = 50  # not the input genotype: the reference exits
+    assert o.haplocomp(C) is None
+    # a missing allele: locus 1 leaves every count, the wildcard matches
+    M = A.copy()
+    M[0, 0, 1] = -1
+    o2 = oracle_mod.Oracle(M, "S" * 6)
+    F = A.copy()
+    F[0, :, 2:] = F[0, ::-1, 2:]
+    # heterozygous: loci 0,2,3,5 (locus 1 has a missing allele, which matches
+    # anything); switch at locus 2; mismatches of the best orientation: locus 0
+    assert o2.haplocomp(F).tolist() == [1 / 3, 1.0, 1 / 5]
+
+
+def test_haplocomp_logged_per_iteration(oracle_mod):
+    from hmc_amd import synth
+
+    p = synth.founder_mosaic(40, 30, A=2, seed=4)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10, max_iter=5)
+    r = o.run()
+    assert r["haplocomp"].shape == (r["iterations"], 3)
+    assert np.isfinite(r["haplocomp"]).all() and (r["haplocomp"] >= 0).all()
+    np.testing.assert_array_equal(o.haplocomp(r["resolutions"]), r["haplocomp"][-1])

@@ -59,6 +59,8 @@ int main(int argc, char **argv) {
   printf("Found haplotype patterns: %d (%.3f s)\n", np0, t_m0);
   double solve = t_m0;
   for (int k = 0; k < iters && k < 256; ++k) {
+    printf("  Switch Error = %f, IHP = %f, IGP = %f, LL = %f\n", log[k].switch_error, log[k].ihp, log[k].igp,
+           log[k].log_likelihood);  // HaploModel.cpp:135-136
     printf("  iteration %d: LL = %f, patterns = %d, E %.3f s, M %.3f s\n", k + 1, log[k].log_likelihood,
            log[k].n_patterns, log[k].t_estep_s, log[k].t_mstep_s);
     solve += log[k].t_estep_s + log[k].t_mstep_s;
