@@ -207,6 +207,16 @@ struct Ctx {
 
   // model
   int P = 0, head_len = 1;
+  // HaploModel::setModel (HaploModel.cpp:26-36): 0 MV, 1 MC, 2 MA
+  int model = 0, mc_order = 1;
+  // head_len > 1: alleles of the head patterns and initHeadList's pairs per
+  // individual of the shard (host restatement, uploaded for the E-step)
+  std::vector<uint32_t> h_head_ids;
+  std::vector<uint8_t> h_head_al;  // [n_head][head_len]
+  DevBuf<uint8_t> d_head_al;       // [P][head_len]
+  DevBuf<uint32_t> d_hf_off, d_hf_pairs;
+  DevBuf<int32_t> d_hf_status;
+  bool hf_valid = false;
   bool have_model = false;
   DevBuf<int32_t> t_start, t_len, t_node;
   DevBuf<double> t_freq, t_prefix, t_tp;
@@ -474,7 +484,11 @@ struct Ctx {
     int mxl = max_len <= 0 ? L : max_len;
     int mnl = std::max(min_len, 1);
     mxl = std::max(mxl, mnl);
-    const double mf = current_min_freq();
+    double mf = current_min_freq();
+    if (model == 1) {  // MC: findPatternBlock(mc_order+1) (PatternManager.cpp:72-88)
+      mnl = mxl = std::max(1, mc_order + 1);
+      mf = -1.0;
+    }
     if ((e = d_rm.ensure(RM_SLOTS * 16)) || (e = d_totals.ensure(2)) || (e = hipMemsetAsync(d_rm.p, 0, RM_SLOTS * 16 * 8, st)))
       return hipfail(e, "mine");
     std::vector<int> lbeg{0, 0}, lend{0, 0};  // per level node ranges (index = level)
@@ -619,7 +633,7 @@ struct Ctx {
       if ((e = launch_mine_emit(a, lv, lbeg[lv], lend[lv], t, st))) return hipfail(e, "mine_emit");
     if ((e = launch_mine_succ(a, t, P, st))) return hipfail(e, "mine_succ");
     head_len = mnl;
-    if ((rc = build_heads_from_nodes(a))) return rc;
+    if ((rc = build_heads_from_nodes(a, mnl <= maxlev ? lbeg[mnl] : 0, mnl <= maxlev ? lend[mnl] : 0))) return rc;
     std::vector<unsigned long long> rm_slots((size_t)RM_SLOTS * 16);
     if ((e = hipMemcpyAsync(rm_slots.data(), d_rm.p, rm_slots.size() * 8, hipMemcpyDeviceToHost, st)))
       return hipfail(e, "mine");
@@ -683,8 +697,11 @@ struct Ctx {
     return HMC_OK;
   }
 
-  int build_heads_from_nodes(const MineArgs &) {
+  int build_heads_from_nodes(const MineArgs &, int hb, int he) {
     std::vector<std::pair<uint32_t, uint8_t>> heads;
+    hf_valid = false;
+    h_head_ids.clear();
+    h_head_al.clear();
     if (head_len == 1 && pan.L > 0) {
       const int n0 = h_npos[0];
       std::vector<int32_t> rcb(1);
@@ -703,14 +720,146 @@ struct Ctx {
       }
       for (int k = 0; k < n0; ++k)
         if (fl[k] & NODE_ACC) heads.push_back({pos[k], alle[k]});
+    } else if (head_len > 1 && he > hb) {
+      // head list = accepted start-0 nodes of level head_len; their alleles by
+      // walking parent links (levels 1..head_len are nodes [0, he))
+      hipError_t e;
+      std::vector<int32_t> par(he), stt(he);
+      std::vector<uint8_t> fl(he), alle(he);
+      std::vector<uint32_t> pos(he);
+      if ((e = hipMemcpyAsync(par.data(), n_parent.p, (size_t)he * 4, hipMemcpyDeviceToHost, st)) ||
+          (e = hipMemcpyAsync(stt.data(), n_start.p, (size_t)he * 4, hipMemcpyDeviceToHost, st)) ||
+          (e = hipMemcpyAsync(fl.data(), n_flags.p, (size_t)he, hipMemcpyDeviceToHost, st)) ||
+          (e = hipMemcpyAsync(alle.data(), n_allele.p, (size_t)he, hipMemcpyDeviceToHost, st)) ||
+          (e = hipMemcpyAsync(pos.data(), n_pos.p, (size_t)he * 4, hipMemcpyDeviceToHost, st)) ||
+          (e = hipStreamSynchronize(st)))
+        return hipfail(e, "heads");
+      std::vector<std::pair<uint32_t, std::vector<uint8_t>>> hs;
+      for (int v = hb; v < he; ++v) {
+        if (stt[v] != 0 || !(fl[v] & NODE_ACC)) continue;
+        std::vector<uint8_t> al(head_len);
+        int32_t w = v;
+        for (int q = head_len - 1; q >= 0; --q) {
+          al[q] = alle[w];
+          w = par[w];
+        }
+        hs.push_back({pos[v], al});
+      }
+      std::sort(hs.begin(), hs.end());
+      std::vector<uint8_t> tab((size_t)std::max(P, 1) * head_len, 0);
+      for (auto &h : hs) {
+        heads.push_back({h.first, h.second[head_len - 1]});
+        h_head_ids.push_back(h.first);
+        h_head_al.insert(h_head_al.end(), h.second.begin(), h.second.end());
+        std::copy(h.second.begin(), h.second.end(), tab.begin() + (size_t)h.first * head_len);
+      }
+      if ((e = d_head_al.ensure(tab.size())) ||
+          (e = hipMemcpyAsync(d_head_al.p, tab.data(), tab.size(), hipMemcpyHostToDevice, st)) ||
+          (e = hipStreamSynchronize(st)))
+        return hipfail(e, "heads");
     }
     return set_heads(heads);
+  }
+
+  // initHeadList (HaploBuilder.cpp:153-224) for head_len > 1, on the host: the
+  // head pairs of every individual of the shard, in the reference's order
+  // (head list in id order; allele sequences expanded locus by locus;
+  // findLongestMatchPattern(head_len, as) must give a start-0 pattern).
+  int build_head_frontier() {
+    const int n = nloc(), hl = head_len;
+    const int nh = (int)h_head_ids.size();
+    if (nh == 0 && !h_head_al.empty()) return fail(HMC_EARG, "head alleles without heads");
+    // the start-0 length-hl pattern matching `as` (MISSING = wildcard): the
+    // trie walk of PatternTree.cpp:98-134 goes from locus hl-1 down and keeps
+    // the first full-length hit, i.e. the smallest allele index at the
+    // highest missing locus first
+    auto lookup = [&](const std::vector<uint8_t> &as) -> uint32_t {
+      int best = -1;
+      for (int h = 0; h < nh; ++h) {
+        const uint8_t *al = h_head_al.data() + (size_t)h * hl;
+        bool ok = true;
+        for (int k = 0; k < hl && ok; ++k) ok = as[k] == MISSING || as[k] == al[k];
+        if (!ok) continue;
+        if (best < 0) { best = h; continue; }
+        const uint8_t *bl = h_head_al.data() + (size_t)best * hl;
+        for (int k = hl - 1; k >= 0; --k)
+          if (al[k] != bl[k]) {
+            if (al[k] < bl[k]) best = h;
+            break;
+          }
+      }
+      return best < 0 ? NONE : h_head_ids[best];
+    };
+    std::vector<uint32_t> off(n + 1, 0), pairs;
+    std::vector<int32_t> status(n, EST_OK);
+    for (int i = 0; i < n; ++i) {
+      off[i] = (uint32_t)(pairs.size() / 2);
+      const uint8_t *g0 = pan.idx.data() + ((size_t)(i0 + i) * 2) * pan.L, *g1 = g0 + pan.L;
+      for (int h = 0; h < nh && status[i] == EST_OK; ++h) {
+        const uint8_t *H = h_head_al.data() + (size_t)h * hl;
+        bool match = true;  // HaploPattern::isMatch(genotype): every locus matches one allele
+        for (int j = 0; j < hl && match; ++j)
+          match = g0[j] == MISSING || g1[j] == MISSING || g0[j] == H[j] || g1[j] == H[j];
+        if (!match) continue;
+        std::vector<std::vector<uint8_t>> last(1), next;
+        for (int j = 0; j < hl; ++j) {
+          next.clear();
+          const bool miss0 = g0[j] == MISSING, miss1 = g1[j] == MISSING;
+          const bool isMissing = miss0 && miss1, hasMissing = miss0 || miss1;
+          const bool hasAllele = g0[j] == H[j] || g1[j] == H[j];  // Allele == (missing == missing)
+          const bool het = !(hasMissing || g0[j] == g1[j]);
+          if (isMissing || (hasMissing && hasAllele)) {
+            for (auto &as : last)
+              for (int k = 0; k < (int)pan.sym[j].size(); ++k)
+                if (pan.sym[j][k].second > 0) {
+                  next.push_back(as);
+                  next.back().push_back((uint8_t)k);
+                }
+          } else if (het) {
+            for (auto &as : last) {
+              next.push_back(as);
+              next.back().push_back(H[j] == g0[j] ? g1[j] : g0[j]);
+            }
+          } else {
+            for (auto &as : last) {
+              next.push_back(as);
+              next.back().push_back(g0[j]);
+            }
+          }
+          last.swap(next);
+        }
+        for (auto &as : last) {
+          const uint32_t q = lookup(as);
+          if (q == NONE) { status[i] = EST_NO_HEAD_PATTERN; break; }
+          if (q >= h_head_ids[h]) {
+            pairs.push_back(h_head_ids[h]);
+            pairs.push_back(q);
+          }
+        }
+      }
+    }
+    off[n] = (uint32_t)(pairs.size() / 2);
+    hipError_t e;
+    if ((e = d_hf_off.ensure(n + 1)) || (e = d_hf_pairs.ensure(std::max<size_t>(pairs.size(), 2))) ||
+        (e = d_hf_status.ensure(std::max(n, 1))) ||
+        (e = hipMemcpyAsync(d_hf_off.p, off.data(), (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st)) ||
+        (!pairs.empty() && (e = hipMemcpyAsync(d_hf_pairs.p, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, st))) ||
+        (n && (e = hipMemcpyAsync(d_hf_status.p, status.data(), (size_t)n * 4, hipMemcpyHostToDevice, st))) ||
+        (e = hipStreamSynchronize(st)))
+      return hipfail(e, "head frontier");
+    hf_valid = true;
+    return HMC_OK;
   }
 
   // ---------------------------------------------------------------- E-step --
   int estep(double *ll_out, int *H_out, uint64_t *re_out) {
     if (!have_model) return fail(HMC_EARG, "no pattern model");
-    if (head_len != 1) return fail(HMC_EUNSUPPORTED, "GPU E-step implements min_pattern_len == 1 only");
+    if (head_len > 1) {
+      if (h_head_al.size() != h_head_ids.size() * (size_t)head_len || (h_head_ids.empty() && n_head > 0))
+        return fail(HMC_EUNSUPPORTED, "head_len > 1 needs the head patterns' alleles (mined tables only)");
+      int rc = build_head_frontier();
+      if (rc) return rc;
+    }
     const int L = pan.L, S = this->S(), n = nloc();
     if (S > S_MAX) return fail(HMC_EUNSUPPORTED, "sample_size > %d", S_MAX);
     hipError_t e;
@@ -858,6 +1007,8 @@ struct Ctx {
       t.S = S;
       t.head_len = head_len;
       t.nbatch = bn;
+      t.indiv_begin = i0 + b;
+      t.mod = dev_model();
       t.trace = d_trace.p;
       t.loc_off = d_loc_off.p;
       t.ncand = d_ncand.p + b;
@@ -1139,6 +1290,13 @@ struct Ctx {
     m.head_len = head_len;
     m.head_ids = d_head_ids.p;
     m.head_pat0 = d_head_pat0.p;
+    if (head_len > 1) {
+      m.hf_base = i0;
+      m.hf_off = d_hf_off.p;
+      m.hf_pairs = d_hf_pairs.p;
+      m.hf_status = d_hf_status.p;
+      m.head_al = d_head_al.p;
+    }
     return m;
   }
 
@@ -1366,6 +1524,18 @@ void hmc_ctx_destroy(hmc_ctx *h) {
 
 const char *hmc_ctx_error(const hmc_ctx *h) { return h ? h->c.err.c_str() : "null context"; }
 
+int hmc_set_model(hmc_ctx *h, const char *model, int mc_order) {
+  if (!h || !model) return HMC_EARG;
+  const std::string m(model);
+  if (m == "MV") h->c.model = 0;
+  else if (m == "MC") h->c.model = 1;
+  else if (m == "MA") h->c.model = 2;
+  else return h->c.fail(HMC_EARG, "Unknown model %s!", model);  // HaploModel.cpp:33-34
+  if (mc_order < 0) return h->c.fail(HMC_EARG, "mc_order must be >= 0");
+  h->c.mc_order = mc_order;
+  return HMC_OK;
+}
+
 int hmc_set_params(hmc_ctx *h, double min_freq_abs, double min_freq, int min_len, int max_len, int sample_size) {
   if (!h) return HMC_EARG;
   h->c.min_freq_abs = min_freq_abs;
@@ -1567,6 +1737,8 @@ int hmc_set_patterns(hmc_ctx *h, int P, const int32_t *start, const int32_t *len
     return c.hipfail(e, "set_patterns");
   c.P = P;
   c.head_len = hl;
+  c.h_head_ids.clear();  // head alleles unknown: the E-step supports head_len 1 only here
+  c.h_head_al.clear();
   c.node_cap = 0;  // allele strings are not known for an injected table
   rc = c.set_heads(heads);
   if (rc) return rc;

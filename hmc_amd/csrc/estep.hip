@@ -418,8 +418,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void e
     int fbig = 0;
     Front X = FA, Y = FB;
 
-    // ---- initHeadList (HaploBuilder.cpp:153-224), head_len == 1 ---------
-    if (tid == 0) {
+    // ---- initHeadList (HaploBuilder.cpp:153-224) --------------------------
+    // head_len == 1 on the device; longer heads from the host's list
+    if (tid == 0 && hl > 1) {
+      int Fp0 = 0;
+      const int li = gi - a.mod.hf_base;
+      int st0 = a.mod.hf_status[li];
+      for (uint32_t t = a.mod.hf_off[li]; t < a.mod.hf_off[li + 1] && st0 == EST_OK; ++t) {
+        if (Fp0 >= a.fcap) { st0 = EST_OVERFLOW_FRONTIER; break; }
+        const uint32_t head = a.mod.hf_pairs[2 * t], q = a.mod.hf_pairs[2 * t + 1];
+        const double tpv = a.mod.freq[head] * a.mod.freq[q];  // HaploPair.cpp:27-32
+        const bool homo = (q == head);
+        set_fwd(l, X, Fp0, homo ? tpv : tpv * 2.0);
+        set_lo(l, X, Fp0, head);
+        set_hi(l, X, Fp0, q);
+        set_nl(l, X, Fp0, 1);
+        set_link(l, X, Fp0, 0, tpv, meta_pack(0, 0, false, homo, true));
+        ++Fp0;
+      }
+      bs->i[0] = Fp0;
+      bs->i[1] = st0;
+    }
+    if (tid == 0 && hl == 1) {
       int Fp0 = 0, st0 = EST_OK;
       const uchar2 g0 = g[0];
       const bool m0 = g0.x == MISSING, m1 = g0.y == MISSING;
@@ -792,6 +812,16 @@ __global__ __launch_bounds__(256) void estep_traceback(TracebackArgs a) {
   const uint32_t hdr = a.trace[lo[a.head_len] + 1 + st];
   row[ra][a.head_len - 1] = (uint8_t)(hdr & 0xFF);
   row[rb][a.head_len - 1] = (uint8_t)((hdr >> 8) & 0xFF);
+  if (a.head_len > 1) {  // the head pair's patterns cover loci 0..head_len-1 (HaploPair.cpp:112-120)
+    const int li = a.indiv_begin + bi - a.mod.hf_base;
+    const uint32_t t = a.mod.hf_off[li] + st;
+    const uint8_t *pa = a.mod.head_al + (size_t)a.mod.hf_pairs[2 * t] * a.head_len;
+    const uint8_t *pb = a.mod.head_al + (size_t)a.mod.hf_pairs[2 * t + 1] * a.head_len;
+    for (int k = 0; k < a.head_len - 1; ++k) {
+      row[ra][k] = pa[k];
+      row[rb][k] = pb[k];
+    }
+  }
   const double w = a.weight[(size_t)bi * S_MAX + c];
   a.w_out[h0] = w;
   a.w_out[h0 + 1] = w;

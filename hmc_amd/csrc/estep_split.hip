@@ -217,9 +217,21 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
     unsigned long long rcur = 0, rend = 0;
     IdFront X = FA, Y = FB;
 
-    // ---- initHeadList (HaploBuilder.cpp:153-224), head_len == 1 -----------
+    // ---- initHeadList (HaploBuilder.cpp:153-224) ----------------------------
+    // head_len == 1 on the device; longer heads from the host's list
     int Fp0 = 0, st0 = EST_OK;
-    if (lane == 0) {
+    if (lane == 0 && hl > 1) {
+      const int li = gi - a.mod.hf_base;
+      st0 = a.mod.hf_status[li];
+      for (uint32_t t = a.mod.hf_off[li]; t < a.mod.hf_off[li + 1] && st0 == EST_OK; ++t) {
+        if (Fp0 >= a.fcap) { st0 = EST_OVERFLOW_FRONTIER; break; }
+        *X.at(F_LO, Fp0) = a.mod.hf_pairs[2 * t];
+        *X.at(F_HI, Fp0) = a.mod.hf_pairs[2 * t + 1];
+        *X.at(F_NL, Fp0) = 1;
+        ++Fp0;
+      }
+    }
+    if (lane == 0 && hl == 1) {
       const uchar2 g0 = g[0];
       const bool m0 = g0.x == MISSING, m1 = g0.y == MISSING;
       for (int hix = 0; hix < a.mod.n_head; ++hix) {
@@ -909,7 +921,8 @@ __global__ __launch_bounds__(256) void estep_values(ValueArgs a) {
 
 hipError_t launch_estep_structure(const StructArgs &a, int grid, hipStream_t st) {
   if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > 65535 || (a.hcap & (a.hcap - 1)) || a.lds_hc < 1 ||
-      (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || a.lds_cc < 0 || a.ccap < 1 || a.mod.head_len != 1)
+      (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || a.lds_cc < 0 || a.ccap < 1 || a.mod.head_len < 1 ||
+      (a.mod.head_len > 1 && (!a.mod.hf_off || !a.mod.hf_pairs || !a.mod.hf_status)))
     return hipErrorInvalidValue;
   const size_t lds = estep_s1_lds_bytes(a.lds_fc, a.lds_hc, a.lds_cc);
   static size_t lds_attr = 0;

@@ -62,6 +62,13 @@ struct DevModel {
   int n_head = 0, head_len = 1;
   uint32_t *head_ids = nullptr;   // [n_head], id order
   uint32_t *head_pat0 = nullptr;  // [amax+1] pattern id of (locus 0, allele x); [amax] = missing allele
+  // head_len > 1: initHeadList's head pairs per individual, computed on the
+  // host (HaploBuilder.cpp:153-224), indexed by global individual - hf_base
+  int hf_base = 0;
+  const uint32_t *hf_off = nullptr;    // [n+1]
+  const uint32_t *hf_pairs = nullptr;  // [2 x total] (head id, matching pattern id)
+  const int32_t *hf_status = nullptr;  // [n] EST_OK or EST_NO_HEAD_PATTERN
+  const uint8_t *head_al = nullptr;    // [P][head_len] alleles of the start-0 length-head_len patterns
 };
 
 struct EstepArgs {
@@ -152,6 +159,8 @@ struct ValueArgs {
 
 struct TracebackArgs {
   int L, S, head_len, nbatch;
+  int indiv_begin;                 // global index of the batch's first individual
+  DevModel mod;                    // head pairs / alleles when head_len > 1
   const uint32_t *trace;
   const unsigned long long *loc_off;
   const int32_t *ncand;

@@ -341,7 +341,12 @@ __global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg
   }
   // R_M: spread over RM_SLOTS counters a cache line apart (one shared counter
   // serialises every wave of the level in a single L2 channel)
-  if (tid == 0) atomicAdd(&a.rm[(blockIdx.x % RM_SLOTS) * 16], (unsigned long long)p.n * (unsigned long long)p.nc);
+  // A parent with an empty matching list sends every child through
+  // checkFrequency's full scan (checkFrequencyWithExtension, PatternManager.cpp:
+  // 197-199); no item matches a child of an unmatched parent, so only the count
+  // changes.  (Zero-frequency parents are extended under MC, or below min_len.)
+  const unsigned long long scanned = (p.n == 0 && level > 1) ? (unsigned long long)a.n_items : (unsigned long long)p.n;
+  if (tid == 0) atomicAdd(&a.rm[(blockIdx.x % RM_SLOTS) * 16], scanned * (unsigned long long)p.nc);
 #ifdef HMC_STAMPS
   MSTAMP(4);
   if (tid == 0 && a.stamps) {  // one private slot per block: no contended atomics

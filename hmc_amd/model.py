@@ -110,6 +110,8 @@ class HaploModel:
         self.max_pattern_len = 30
         self.sample_size = 10
         self.max_iteration = 1
+        self.model = "MV"  # HaploModel::setModel: MV, MC or MA (HMC.cpp:35)
+        self.mc_order = 1  # HMC.cpp:41
         self.N = self.L = self.amax = 0
         self.iterations = 0
         self.log: list[dict] = []
@@ -123,6 +125,7 @@ class HaploModel:
         self._check(lib().hmc_set_params(self._h, float(self.min_freq_abs), float(self.min_freq),
                                          int(self.min_pattern_len), int(self.max_pattern_len),
                                          int(self.sample_size)))
+        self._check(lib().hmc_set_model(self._h, str(self.model).encode(), int(self.mc_order)))
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:
@@ -192,6 +195,12 @@ class HaploModel:
         n, rm = C.c_int(), C.c_uint64()
         self._check(lib().hmc_find_patterns(self._h, C.byref(n), C.byref(rm)))
         return n.value, rm.value
+
+    def head_len(self) -> int:
+        """PatternManager::head_len of the current model (min pattern length)."""
+        P, hl = C.c_int(), C.c_int()
+        self._check(lib().hmc_model_info(self._h, C.byref(P), C.byref(hl)))
+        return hl.value
 
     def patterns(self, maxlen: int | None = None) -> dict:
         P, hl = C.c_int(), C.c_int()

@@ -57,6 +57,12 @@ const char *hmc_ctx_error(const hmc_ctx *ctx);
 int hmc_set_params(hmc_ctx *ctx, double min_freq_abs, double min_freq, int min_pattern_len, int max_pattern_len,
                    int sample_size);
 
+/* HaploModel::setModel + mc_order (HaploModel.cpp:26-36, 65-76; HMC.cpp:35,41):
+ * "MV" (default; patterns by frequency), "MC" (Markov chain of order mc_order:
+ * PatternManager::findPatternBlock(mc_order+1), every candidate of that length,
+ * head length mc_order+1), "MA" (MV; its adjustFrequency only range-checks). */
+int hmc_set_model(hmc_ctx *ctx, const char *model, int mc_order);
+
 /* ---- panel (GenoData / HaploFile) --------------------------------------- */
 /* HaploFile::readGenoData for the PHASE format (HaploFile.cpp:54-118). */
 int hmc_load_phase(hmc_ctx *ctx, const char *path);

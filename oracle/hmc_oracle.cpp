@@ -273,6 +273,8 @@ struct Params {
   int max_len = 30;           // HMC.cpp:40
   int sample_size = 10;       // HMC.cpp:43
   int max_iter = 1;           // HMC.cpp:46
+  int model = 0;              // HaploModel::setModel (HaploModel.cpp:26-36): 0 MV, 1 MC, 2 MA
+  int mc_order = 1;           // HMC.cpp:41
 };
 
 struct Timing { double m0 = 0, e = 0, m = 0; };
@@ -496,7 +498,16 @@ struct Model {
   // HaploModel.cpp:52-63
   void findPatterns() {
     if (prm.min_freq_abs > 0) prm.min_freq = prm.min_freq_abs / (2.0 * g.N);
-    findPatternByFreq(prm.min_freq, prm.min_len, prm.max_len);
+    if (prm.model == 1) {
+      // MC: findPatternBlock(mc_order+1) (PatternManager.cpp:72-88): every
+      // candidate of length mc_order+1 (m_min_freq = -1 accepts all)
+      const int len = std::max(1, prm.mc_order + 1);
+      findPatternByFreq(-1.0, len, len);
+    } else {
+      // MV, and MA whose adjustFrequency (PatternManager.cpp:320-345) only
+      // range-checks the table
+      findPatternByFreq(prm.min_freq, prm.min_len, prm.max_len);
+    }
   }
 
   // ------------------------------------------------------------ E-step ----
@@ -1124,6 +1135,12 @@ double ora_resolve_range(void *h, int i0, int i1) {
   return ll;
 }
 
+// HaploModel::setModel / mc_order (HaploModel.cpp:26-36, HMC.cpp:41): 0 MV, 1 MC, 2 MA
+void ora_set_model(void *h, int model, int mc_order) {
+  Model *m = (Model *)h;
+  m->prm.model = model;
+  m->prm.mc_order = mc_order;
+}
 // Tie diagnostics of the last resolveAll (see Model::tie_flags), [N].
 void ora_tie_flags(void *h, int *out) {
   Model *m = (Model *)h;

@@ -150,6 +150,55 @@ def test_full_em(oracle_mod, name):
     np.testing.assert_array_equal(np.array(m.haplocomp()), r["haplocomp"][-1])
 
 
+@pytest.mark.parametrize("name,model,order,min_len", [
+    ("n60", "MC", 1, 1), ("a3miss5", "MC", 1, 1), ("n60", "MC", 2, 1), ("a4", "MC", 1, 1),
+    ("miss2", "MA", 1, 1), ("n60", "MV", 1, 2), ("a3miss5", "MV", 1, 3)])
+def test_full_em_models(oracle_mod, name, model, order, min_len):
+    """The other models of HaploModel::setModel (HaploModel.cpp:26-36, 65-76) and
+    min_pattern_len > 1: MC mines every length-(order+1) candidate
+    (findPatternBlock, PatternManager.cpp:72-88) and starts the E-step from
+    length-(order+1) heads (initHeadList, HaploBuilder.cpp:153-224, on the host);
+    MA is MV plus range checks.  Whole-EM parity as in test_full_em, including the
+    per-iteration pattern tables' sizes, R_E / R_M and the HaploComp log."""
+    p = panel(name)
+    m = gpu_model(p, max_iteration=12, model=model, mc_order=order, min_pattern_len=min_len)
+    res = m.run()
+    o = oracle_mod.Oracle(p.alleles, p.types, min_len=min_len, sample_size=10, max_iter=12)
+    o.set_model(model, order)
+    r = o.run()
+    assert m.iterations == r["iterations"]
+    assert [x["ll"] for x in m.log] == r["ll"].tolist()
+    assert [x["r_e"] for x in m.log] == r["R_E"].tolist()
+    assert m.m0["r_m"] == r["R_M"][0] and m.m0["n_patterns"] == r["n_patterns"][0]
+    for k in range(r["iterations"] - 1):
+        assert m.log[k]["r_m"] == r["R_M"][k + 1]
+        assert m.log[k]["n_patterns"] == r["n_patterns"][k + 1]
+    assert np.array_equal(res, r["resolutions"])
+    np.testing.assert_array_equal(np.array([x["haplocomp"] for x in m.log]), r["haplocomp"])
+
+
+def test_mc_model_estep_and_table(oracle_mod):
+    """MC, one E-step and one M-step compared in full: pattern table (every
+    length-2 candidate, zero-frequency ones included), head pairs through the
+    traceback (samples), weights and the next table."""
+    p = panel("a3miss5")
+    m = gpu_model(p, model="MC", mc_order=1)
+    m._push_params()
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
+    o.set_model("MC", 1)
+    m.find_patterns()
+    o.find_patterns()
+    assert_tables_equal(m.patterns(), o.patterns())
+    assert m.head_len() == o.head_len() == 2
+    o.reset_counters()
+    ll_g, H, re_g = m.resolve_all()
+    ll_o = o.resolve_all()
+    assert_estep_equal(m, o, ll_g, ll_o, H, re_g)
+    m.find_patterns()
+    o.find_patterns()
+    assert_tables_equal(m.patterns(), o.patterns())
+
+
 @pytest.mark.parametrize("gname", ["cfg1", "miss_a3", "snp_miss", "s3"])
 def test_against_golden_fixtures(gname):
     sys.path.insert(0, os.path.join(HERE, "golden"))
