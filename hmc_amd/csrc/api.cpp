@@ -187,6 +187,7 @@ struct Ctx {
   std::string err;
   // parameters (HaploModel.h:15-26 with the CLI defaults of HMC.cpp:35-47)
   double min_freq_abs = 1.5, min_freq = -1.0;
+  int num_patterns = -1;  // HaploModel::num_patterns (HMC.cpp:38): > 0 selects findPatternByNum
   int min_len = 1, max_len = 30, sample_size = 10;
   // tuning
   int fcap = 2048, waves = 0;
@@ -474,7 +475,31 @@ struct Ctx {
     return min_freq;
   }
 
+  // PatternManager::findPatternByNum (PatternManager.cpp:44-70) runs rounds of
+  // searchPattern(true) at thresholds 1.0, 0.9, 0.81, ... keeping the
+  // candidates that fail a round for the next one.  Every candidate it ever
+  // generates is in the plain candidate tree mined at the last round's
+  // threshold, so the tree is mined on the GPU at theta_k and the rounds are
+  // replayed on the host over it (bynum_replay); when a round needs an
+  // extension the tree does not have, the tree is mined again deeper.
+  static constexpr int MINE_RETRY = 1000;
+  int bynum_need = 0;  // round the replay needed beyond the mined tree
   int mine(int *P_out, uint64_t *rm_out) {
+    if (!(num_patterns > 0 && model != 1)) return mine_impl(P_out, rm_out, 0);
+    int k = 8;
+    while (true) {
+      const int rc = mine_impl(P_out, rm_out, k);
+      if (rc != MINE_RETRY) return rc;
+      k = std::max(bynum_need, 2 * k);
+    }
+  }
+  static double bynum_theta(int r) {  // m_min_freq of round r: 1.0 then *= 0.9
+    double t = 1.0;
+    for (int i = 1; i < r; ++i) t *= 0.9;
+    return t;
+  }
+
+  int mine_impl(int *P_out, uint64_t *rm_out, int bynum_rounds) {
     if (!have_panel) return fail(HMC_EARG, "no panel loaded");
     const bool genotype = !have_samples;
     const int L = pan.L;
@@ -489,6 +514,7 @@ struct Ctx {
       mnl = mxl = std::max(1, mc_order + 1);
       mf = -1.0;
     }
+    if (bynum_rounds > 0) mf = bynum_theta(bynum_rounds);
     if ((e = d_rm.ensure(RM_SLOTS * 16)) || (e = d_totals.ensure(2)) || (e = hipMemsetAsync(d_rm.p, 0, RM_SLOTS * 16 * 8, st)))
       return hipfail(e, "mine");
     std::vector<int> lbeg{0, 0}, lend{0, 0};  // per level node ranges (index = level)
@@ -605,8 +631,13 @@ struct Ctx {
     }
     const int maxlev = level;
     const int ntot = lend[maxlev];
-    // DFS pre-order ids from subtree sizes
     MineArgs a = mine_args(genotype);
+    uint64_t rm_bynum = 0;
+    if (bynum_rounds > 0) {
+      rc = bynum_replay(a, ntot, mnl, mxl, bynum_rounds, rm_bynum);
+      if (rc) return rc;
+    } else {
+    // DFS pre-order ids from subtree sizes
     for (int lv = maxlev; lv >= 1; --lv)
       if ((e = launch_mine_size(a, lv, lbeg[lv], lend[lv], st))) return hipfail(e, "mine_size");
     if ((e = d_rsize.ensure(L)) || (e = d_rpos.ensure(L))) return hipfail(e, "mine");
@@ -627,6 +658,7 @@ struct Ctx {
     if ((e = launch_mine_pos(a, 1, 0, L, d_rpos.p, st))) return hipfail(e, "mine_pos");
     for (int lv = 2; lv <= maxlev; ++lv)
       if ((e = launch_mine_pos(a, lv, lbeg[lv - 1], lend[lv - 1], d_rpos.p, st))) return hipfail(e, "mine_pos");
+    }
     if ((rc = alloc_table(P))) return rc;
     PatternTable t = table();
     for (int lv = 1; lv <= maxlev; ++lv)
@@ -641,6 +673,7 @@ struct Ctx {
     if ((e = hipStreamSynchronize(st))) return hipfail(e, "mine");
     unsigned long long rm = 0;
     for (int k = 0; k < RM_SLOTS; ++k) rm += rm_slots[(size_t)k * 16];
+    if (bynum_rounds > 0) rm = rm_bynum;  // the scans of the candidates the rounds generated
     float ms = 0;
     hipEventElapsedTime(&ms, ev[4], ev[5]);
     ms_m = ms;
@@ -694,6 +727,94 @@ struct Ctx {
     if ((e = hipMemcpyAsync(d_head_pat0.p, pat0.data(), pat0.size() * 4, hipMemcpyHostToDevice, st)) ||
         (e = hipStreamSynchronize(st)))
       return hipfail(e, "set_heads");
+    return HMC_OK;
+  }
+
+  // The rounds of findPatternByNum over the candidate tree mined at
+  // theta(rounds): acceptance order, the last round sorted by frequency
+  // (std::sort, HaploPattern::greater_frequency) and cut; then node flags and
+  // positions so that mine_emit / mine_succ build the table in that order.
+  int bynum_replay(const MineArgs &, int ntot, int mnl, int mxl, int, uint64_t &rm_out) {
+    const int L = pan.L;
+    hipError_t e;
+    std::vector<uint8_t> fl(ntot);
+    std::vector<int32_t> cb(ntot), stt(ntot);
+    std::vector<double> fr(ntot);
+    std::vector<uint32_t> cnt(ntot);
+    if (ntot > 0 &&
+        ((e = hipMemcpyAsync(fl.data(), n_flags.p, (size_t)ntot, hipMemcpyDeviceToHost, st)) ||
+         (e = hipMemcpyAsync(cb.data(), n_child_base.p, (size_t)ntot * 4, hipMemcpyDeviceToHost, st)) ||
+         (e = hipMemcpyAsync(stt.data(), n_start.p, (size_t)ntot * 4, hipMemcpyDeviceToHost, st)) ||
+         (e = hipMemcpyAsync(fr.data(), n_freq.p, (size_t)ntot * 8, hipMemcpyDeviceToHost, st)) ||
+         (e = hipMemcpyAsync(cnt.data(), n_cnt.p, (size_t)ntot * 4, hipMemcpyDeviceToHost, st)) ||
+         (e = hipStreamSynchronize(st))))
+      return hipfail(e, "bynum");
+    const unsigned long long n_items = (unsigned long long)mine_args(!have_samples).n_items;
+    struct C { int32_t v; int len; };  // v < 0: root of start -v-1 (the empty pattern)
+    std::vector<C> stack, kept;
+    std::vector<int32_t> out;
+    for (int s0 = 0; s0 < L; ++s0) stack.push_back({-(s0 + 1), 0});  // generateCandidates
+    uint64_t rm = 0;
+    double theta = 1.0;
+    int max_num = num_patterns, last_size = 0;
+    // searchPattern(true) at threshold theta (PatternManager.cpp:100-144)
+    auto search = [&](int round) -> int {
+      kept.clear();
+      while (!stack.empty()) {
+        const C c = stack.back();
+        stack.pop_back();
+        const bool root = c.v < 0;
+        const int start = root ? -c.v - 1 : stt[c.v];
+        const double f = root ? 1.0 : fr[c.v];  // the empty pattern has frequency 1
+        const int end = start + c.len;
+        if (f >= theta || c.len < mnl) {
+          if (end < L && c.len < mxl) {
+            if (!root && !(fl[c.v] & NODE_EXT)) return round;  // the mined tree is too shallow
+            const int base = root ? [&] { int b = 0; for (int k = 0; k < start; ++k) b += h_npos[k]; return b; }()
+                                  : cb[c.v];
+            const unsigned long long scan = root ? n_items : (cnt[c.v] > 0 ? cnt[c.v] : n_items);
+            for (int j = 0; j < h_npos[end]; ++j) {
+              stack.push_back({base + j, c.len + 1});
+              rm += scan;  // checkFrequencyWithExtension of the new candidate
+            }
+          }
+        }
+        if (f >= theta || c.len <= mnl) {
+          if (c.len > 0 && c.len >= mnl) out.push_back(c.v);
+        } else {
+          kept.push_back(c);
+        }
+      }
+      stack.swap(kept);
+      return 0;
+    };
+    int round = 1;
+    if (int need = search(round)) { bynum_need = need; return MINE_RETRY; }
+    max_num = std::max(max_num, (int)out.size());
+    while ((int)out.size() < max_num && theta > 1e-38) {
+      if (stack.empty()) break;  // nothing left to accept: later rounds change nothing
+      last_size = (int)out.size();
+      theta *= 0.9;
+      ++round;
+      if (int need = search(round)) { bynum_need = need; return MINE_RETRY; }
+    }
+    if ((int)out.size() > max_num) {
+      std::sort(out.begin() + last_size, out.end(), [&](int32_t x, int32_t y) { return fr[x] > fr[y]; });
+      out.resize(max_num);
+    }
+    std::vector<uint32_t> pos(ntot, 0);
+    for (int32_t v = 0; v < ntot; ++v) fl[v] &= (uint8_t)~NODE_ACC;
+    for (size_t i = 0; i < out.size(); ++i) {
+      fl[out[i]] |= NODE_ACC;
+      pos[out[i]] = (uint32_t)i;
+    }
+    if (ntot > 0 &&
+        ((e = hipMemcpyAsync(n_flags.p, fl.data(), (size_t)ntot, hipMemcpyHostToDevice, st)) ||
+         (e = hipMemcpyAsync(n_pos.p, pos.data(), (size_t)ntot * 4, hipMemcpyHostToDevice, st)) ||
+         (e = hipStreamSynchronize(st))))
+      return hipfail(e, "bynum");
+    P = (int)out.size();
+    rm_out = rm;
     return HMC_OK;
   }
 
@@ -1523,6 +1644,12 @@ void hmc_ctx_destroy(hmc_ctx *h) {
 }
 
 const char *hmc_ctx_error(const hmc_ctx *h) { return h ? h->c.err.c_str() : "null context"; }
+
+int hmc_set_num_patterns(hmc_ctx *h, int num_patterns) {
+  if (!h) return HMC_EARG;
+  h->c.num_patterns = num_patterns;
+  return HMC_OK;
+}
 
 int hmc_set_model(hmc_ctx *h, const char *model, int mc_order) {
   if (!h || !model) return HMC_EARG;

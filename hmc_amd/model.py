@@ -112,6 +112,7 @@ class HaploModel:
         self.max_iteration = 1
         self.model = "MV"  # HaploModel::setModel: MV, MC or MA (HMC.cpp:35)
         self.mc_order = 1  # HMC.cpp:41
+        self.num_patterns = -1  # HMC.cpp:38: > 0 mines with findPatternByNum
         self.N = self.L = self.amax = 0
         self.iterations = 0
         self.log: list[dict] = []
@@ -126,6 +127,7 @@ class HaploModel:
                                          int(self.min_pattern_len), int(self.max_pattern_len),
                                          int(self.sample_size)))
         self._check(lib().hmc_set_model(self._h, str(self.model).encode(), int(self.mc_order)))
+        self._check(lib().hmc_set_num_patterns(self._h, int(self.num_patterns)))
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:

@@ -62,6 +62,10 @@ int hmc_set_params(hmc_ctx *ctx, double min_freq_abs, double min_freq, int min_p
  * PatternManager::findPatternBlock(mc_order+1), every candidate of that length,
  * head length mc_order+1), "MA" (MV; its adjustFrequency only range-checks). */
 int hmc_set_model(hmc_ctx *ctx, const char *model, int mc_order);
+/* HaploModel::num_patterns (HMC.cpp:38): > 0 mines with
+ * PatternManager::findPatternByNum (PatternManager.cpp:44-70, models MV/MA);
+ * <= 0 (default) with findPatternByFreq. */
+int hmc_set_num_patterns(hmc_ctx *ctx, int num_patterns);
 
 /* ---- panel (GenoData / HaploFile) --------------------------------------- */
 /* HaploFile::readGenoData for the PHASE format (HaploFile.cpp:54-118). */

@@ -274,6 +274,7 @@ struct Params {
   int sample_size = 10;       // HMC.cpp:43
   int max_iter = 1;           // HMC.cpp:46
   int model = 0;              // HaploModel::setModel (HaploModel.cpp:26-36): 0 MV, 1 MC, 2 MA
+  int num_patterns = -1;      // HMC.cpp:38 (findPatternByNum when > 0)
   int mc_order = 1;           // HMC.cpp:41
 };
 
@@ -421,23 +422,13 @@ struct Model {
     }
   }
 
-  // PatternManager.cpp:27-42, 90-144 — DFS mining; output order = DFS pre-order.
-  void findPatternByFreq(double mf, int mnl, int mxl) {
-    int L = g.L;
-    mxl = mxl <= 0 ? L : mxl;
-    mnl = std::max(mnl, 1);
-    mxl = std::max(mxl, mnl);
-    minlen.resize(L, mnl);  // vector::resize keeps old values (PatternManager.cpp:33-34)
-    maxlen.resize(L, mxl);
-    P.clear();
-    std::vector<Cand *> stack;
-    for (int s = 0; s < L; ++s) {  // generateCandidates (:90-98)
-      Cand *c = new Cand;
-      c->p.start = c->p.end = s;
-      stack.push_back(c);
-    }
-    min_freq = mf;
-    while (!stack.empty()) {  // searchPattern (:100-144)
+  // PatternManager::searchPattern (:100-144) on an explicit candidate stack;
+  // with `reserve`, candidates that fail the threshold are kept (in pop order)
+  // for the next round instead of deleted.
+  std::vector<Cand *> searchPattern(std::vector<Cand *> &stack, bool reserve) {
+    const int L = g.L;
+    std::vector<Cand *> kept;
+    while (!stack.empty()) {
       Cand *pc = stack.back();
       stack.pop_back();
       const Pat &hp = pc->p;
@@ -462,9 +453,68 @@ struct Model {
       }
       if (hp.freq >= min_freq || hp.len() <= minlen[hp.start]) {
         if (hp.len() > 0 && hp.len() >= minlen[hp.start]) P.push_back(pc->p);
+        delete pc;
+      } else if (reserve) {
+        kept.push_back(pc);
+      } else {
+        delete pc;
       }
-      delete pc;
     }
+    return kept;
+  }
+
+  // generateCandidates (:90-98): one empty pattern per start locus
+  std::vector<Cand *> generateCandidates() {
+    std::vector<Cand *> stack;
+    for (int s = 0; s < g.L; ++s) {
+      Cand *c = new Cand;
+      c->p.start = c->p.end = s;
+      stack.push_back(c);
+    }
+    return stack;
+  }
+
+  // PatternManager.cpp:27-42 — DFS mining; output order = DFS pre-order.
+  void findPatternByFreq(double mf, int mnl, int mxl) {
+    int L = g.L;
+    mxl = mxl <= 0 ? L : mxl;
+    mnl = std::max(mnl, 1);
+    mxl = std::max(mxl, mnl);
+    minlen.resize(L, mnl);  // vector::resize keeps old values (PatternManager.cpp:33-34)
+    maxlen.resize(L, mxl);
+    P.clear();
+    std::vector<Cand *> stack = generateCandidates();
+    min_freq = mf;
+    searchPattern(stack, false);
+    initialize();
+  }
+
+  // PatternManager::findPatternByNum (:44-70): thresholds 1.0, 0.9, 0.81, ...
+  // over rounds of searchPattern(true) until max_num patterns; the last
+  // round's patterns sorted by frequency (std::sort, greater_frequency) and cut.
+  void findPatternByNum(int max_num, int mnl, int mxl) {
+    int L = g.L;
+    mxl = mxl <= 0 ? L : mxl;
+    mnl = std::max(mnl, 1);
+    mxl = std::max(mxl, mnl);
+    minlen.resize(L, mnl);
+    maxlen.resize(L, mxl);
+    P.clear();
+    std::vector<Cand *> stack = generateCandidates();
+    min_freq = 1.0;
+    stack = searchPattern(stack, true);
+    max_num = std::max(max_num, (int)P.size());
+    int last_size = 0;
+    while ((int)P.size() < max_num && min_freq > 1e-38) {
+      last_size = (int)P.size();
+      min_freq *= 0.9;
+      stack = searchPattern(stack, true);
+    }
+    if ((int)P.size() > max_num) {
+      std::sort(P.begin() + last_size, P.end(), [](const Pat &a, const Pat &b) { return a.freq > b.freq; });
+      P.resize(max_num);
+    }
+    for (Cand *c : stack) delete c;
     initialize();
   }
 
@@ -503,6 +553,8 @@ struct Model {
       // candidate of length mc_order+1 (m_min_freq = -1 accepts all)
       const int len = std::max(1, prm.mc_order + 1);
       findPatternByFreq(-1.0, len, len);
+    } else if (prm.num_patterns > 0) {  // HaploModel.cpp:58-60, 70-72
+      findPatternByNum(prm.num_patterns, prm.min_len, prm.max_len);
     } else {
       // MV, and MA whose adjustFrequency (PatternManager.cpp:320-345) only
       // range-checks the table
@@ -1141,6 +1193,8 @@ void ora_set_model(void *h, int model, int mc_order) {
   m->prm.model = model;
   m->prm.mc_order = mc_order;
 }
+// HaploModel::num_patterns (HMC.cpp:38): > 0 selects findPatternByNum
+void ora_set_num_patterns(void *h, int n) { ((Model *)h)->prm.num_patterns = n; }
 // Tie diagnostics of the last resolveAll (see Model::tie_flags), [N].
 void ora_tie_flags(void *h, int *out) {
   Model *m = (Model *)h;

@@ -51,6 +51,7 @@ def lib():
         L.ora_resolve_all.argtypes = [vp]
         L.ora_tie_flags.argtypes = [vp, P(i)]
         L.ora_set_model.argtypes = [vp, i, i]
+        L.ora_set_num_patterns.argtypes = [vp, i]
         L.ora_run_comp_log.argtypes = [vp, P(d)]
         L.ora_haplocomp.restype = i
         L.ora_haplocomp.argtypes = [vp, P(i), P(d)]
@@ -182,6 +183,10 @@ class Oracle:
         """HaploModel::setModel: MV (default), MC (Markov chain of order
         mc_order: all patterns of length mc_order+1), MA (MV + range checks)."""
         lib().ora_set_model(self.h, {"MV": 0, "MC": 1, "MA": 2}[model], int(mc_order))
+
+    def set_num_patterns(self, n: int):
+        """HaploModel::num_patterns: > 0 mines with findPatternByNum."""
+        lib().ora_set_num_patterns(self.h, int(n))
 
     def tie_flags(self) -> np.ndarray:
         """Per-individual tie diagnostics of the last E-step (Model::tie_flags)."""

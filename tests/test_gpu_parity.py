@@ -199,6 +199,43 @@ def test_mc_model_estep_and_table(oracle_mod):
     assert_tables_equal(m.patterns(), o.patterns())
 
 
+@pytest.mark.parametrize("K,N,L,min_len,num", [
+    (2, 40, 30, 1, 20), (2, 40, 30, 1, 150), (2, 40, 30, 1, 400), (2, 40, 30, 2, 150), (2, 40, 30, 2, 400),
+    (3, 50, 40, 1, 150), (3, 50, 40, 1, 400), (3, 50, 40, 2, 60)])
+def test_find_pattern_by_num(oracle_mod, K, N, L, min_len, num):
+    """findPatternByNum (PatternManager.cpp:44-70): rounds of searchPattern(true)
+    at thresholds 1.0, 0.9, ... with reserved candidates, the last round sorted
+    by frequency (std::sort) and cut at num_patterns.  Low-diversity panels
+    (K founders, monomorphic stretches) make the rounds and the cut matter.
+    Pattern tables after M0 and M1 in full, then the whole EM."""
+    p = synth.founder_mosaic(N, L, A=2, K=K, seed=5)
+    m = gpu_model(p, num_patterns=num, min_pattern_len=min_len)
+    o = oracle_mod.Oracle(p.alleles, p.types, min_len=min_len, sample_size=10)
+    o.set_num_patterns(num)
+    o.reset_counters()
+    P0, rm0 = m.find_patterns()
+    o.find_patterns()
+    assert_tables_equal(m.patterns(), o.patterns())
+    assert rm0 == o.counters()[1]
+    o.reset_counters()
+    ll_g, H, re_g = m.resolve_all()
+    ll_o = o.resolve_all()
+    assert_estep_equal(m, o, ll_g, ll_o, H, re_g)
+    o.reset_counters()
+    P1, rm1 = m.find_patterns()
+    o.find_patterns()
+    assert_tables_equal(m.patterns(), o.patterns())
+    assert rm1 == o.counters()[1]
+    m2 = gpu_model(p, max_iteration=10, num_patterns=num, min_pattern_len=min_len)
+    res = m2.run()
+    o2 = oracle_mod.Oracle(p.alleles, p.types, min_len=min_len, sample_size=10, max_iter=10)
+    o2.set_num_patterns(num)
+    r = o2.run()
+    assert m2.iterations == r["iterations"]
+    assert [x["ll"] for x in m2.log] == r["ll"].tolist()
+    assert np.array_equal(res, r["resolutions"])
+
+
 @pytest.mark.parametrize("gname", ["cfg1", "miss_a3", "snp_miss", "s3"])
 def test_against_golden_fixtures(gname):
     sys.path.insert(0, os.path.join(HERE, "golden"))

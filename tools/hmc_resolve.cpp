@@ -18,7 +18,7 @@ int main(int argc, char **argv) {
   int max_iteration = 1, sample_size = 10, min_len = 1, max_len = 30, device = 0;
   const char *input = nullptr;
   std::string model = "MV";
-  int mc_order = 1;
+  int mc_order = 1, num_patterns = -1;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> const char * {
@@ -34,6 +34,7 @@ int main(int argc, char **argv) {
     else if (a == "-d" || a == "--device") device = atoi(next());
     else if (a == "-m" || a == "--model") model = next();             // HMC.cpp:35
     else if (a == "-o" || a == "--mc-order") mc_order = atoi(next());  // HMC.cpp:41
+    else if (a == "-n" || a == "--num-patterns") num_patterns = atoi(next());  // HMC.cpp:38
     else if (a[0] == '-') { fprintf(stderr, "unknown option %s\n", a.c_str()); return 1; }
     else input = argv[i];
   }
@@ -51,6 +52,7 @@ int main(int argc, char **argv) {
   if (rc) die("hmc_ctx_create");
   if ((rc = hmc_set_params(ctx, min_freq_abs, min_freq, min_len, max_len, sample_size))) die("hmc_set_params");
   if ((rc = hmc_set_model(ctx, model.c_str(), mc_order))) die("hmc_set_model");
+  if ((rc = hmc_set_num_patterns(ctx, num_patterns))) die("hmc_set_num_patterns");
   printf("Reading genotype file ...\n");
   if ((rc = hmc_load_phase(ctx, input))) die("hmc_load_phase");
   int N = 0, L = 0, A = 0;
