@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/hmc_amd.h"
+#include "haplofile.hpp"
 #include "hmc_internal.hpp"
 #include "mstep.hpp"
 #include "select.hpp"
@@ -188,6 +189,7 @@ struct Ctx {
   // parameters (HaploModel.h:15-26 with the CLI defaults of HMC.cpp:35-47)
   double min_freq_abs = 1.5, min_freq = -1.0;
   int num_patterns = -1;  // HaploModel::num_patterns (HMC.cpp:38): > 0 selects findPatternByNum
+  FileData file_meta;     // ids / marker names / positions of the last hmc_load_file
   int min_len = 1, max_len = 30, sample_size = 10;
   // tuning
   int fcap = 2048, waves = 0;
@@ -1734,6 +1736,63 @@ int hmc_load_genotypes(hmc_ctx *h, int N, int L, const int32_t *alleles, const c
   if (!p.build_tables(err)) return h->c.fail(HMC_EUNSUPPORTED, "%s", err.c_str());
   h->c.pan = std::move(p);
   return h->c.upload_panel();
+}
+
+int hmc_parse_file(const char *format, const char *path, const char *path2, int *N, int *L, int32_t *alleles,
+                   char *types) {
+  if (!format || !path) return HMC_EARG;
+  hmc::FileData d;
+  std::string err;
+  if (!hmc::read_geno_file(format, path, path2, d, err)) return HMC_EIO;
+  if (N) *N = d.N;
+  if (L) *L = d.L;
+  if (alleles) std::copy(d.al.begin(), d.al.end(), alleles);
+  if (types) {
+    std::copy(d.types.begin(), d.types.end(), types);
+    types[d.L] = 0;
+  }
+  return HMC_OK;
+}
+
+int hmc_load_file(hmc_ctx *h, const char *format, const char *path, const char *path2) {
+  if (!h || !format || !path) return HMC_EARG;
+  if (std::string(format) == "PHASE") return hmc_load_phase(h, path);
+  hmc::FileData d;
+  std::string err;
+  if (!hmc::read_geno_file(format, path, path2, d, err)) return h->c.fail(HMC_EIO, "%s", err.c_str());
+  if (d.N <= 0 || d.L <= 0) return h->c.fail(HMC_EIO, "Invalid file type!");
+  const int rc = hmc_load_genotypes(h, d.N, d.L, d.al.data(), d.types.c_str());
+  if (rc) return rc;
+  h->c.file_meta = std::move(d);
+  h->c.file_meta.al.clear();
+  return HMC_OK;
+}
+
+int hmc_write_file(hmc_ctx *h, const char *format, const char *path, const char *path2) {
+  if (!h || !format || !path || !h->c.have_best || h->c.world != 1) return HMC_EARG;
+  if (std::string(format) == "PHASE") return hmc_write_phase(h, path);
+  hmc::Ctx &c = h->c;
+  hmc::FileData d = c.file_meta;
+  d.N = c.pan.N;
+  d.L = c.pan.L;
+  d.types = c.pan.types;
+  if ((int)d.ids.size() != d.N) {
+    d.ids.resize(d.N);
+    for (int i = 0; i < d.N; ++i) d.ids[i] = std::to_string(i + 1);
+  }
+  if ((int)d.names.size() != d.L || (int)d.pos.size() != d.L) {
+    d.names.resize(d.L);
+    d.pos.resize(d.L);
+    for (int k = 0; k < d.L; ++k) {
+      d.names[k] = "M" + std::to_string(k + 1);
+      d.pos[k] = k * 1000;
+    }
+  }
+  std::vector<int32_t> hap((size_t)d.N * 2 * d.L);
+  c.to_symbols(c.best_res, hap.data());
+  std::string err;
+  if (!hmc::write_geno_file(format, path, path2, d, hap, err)) return c.fail(HMC_EIO, "%s", err.c_str());
+  return HMC_OK;
 }
 
 int hmc_panel_info(const hmc_ctx *h, int *N, int *L, int *amax) {

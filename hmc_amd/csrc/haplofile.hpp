@@ -1,0 +1,22 @@
+// haplofile.hpp — HPM / HPM2 / BENCH2 genotype files (HaploFile.cpp:205-640).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace hmc {
+
+struct FileData {
+  int N = 0, L = 0;
+  std::vector<int32_t> al;          // [N][2][L] symbols, -1 missing
+  std::string types;                // per locus 'S' (character allele) or 'M' (integer)
+  std::vector<std::string> ids;     // [N]
+  std::vector<std::string> names;   // [L] marker names
+  std::vector<int> pos;             // [L] marker positions
+};
+
+bool read_geno_file(const std::string &format, const char *path, const char *path2, FileData &d, std::string &err);
+bool write_geno_file(const std::string &format, const char *path, const char *path2, const FileData &d,
+                     const std::vector<int32_t> &hap, std::string &err);
+
+}  // namespace hmc

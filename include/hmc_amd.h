@@ -154,6 +154,17 @@ int hmc_get_best_resolutions(hmc_ctx *ctx, int32_t *out);
 /* HaploFile::writeGenoData (HaploFile.cpp:120-153) of the accepted
  * resolutions (single-rank contexts). */
 int hmc_write_phase(hmc_ctx *ctx, const char *path);
+/* The other HaploFile formats (HaploFile.cpp:13-52, 205-640): format "PHASE",
+ * "HPM", "HPM2" (one file) or "BENCH2" (genotype file + position file in
+ * path2).  hmc_parse_file needs no context or device: it returns the panel
+ * (alleles [N][2][L] symbols, -1 missing; types [L+1] 'S'/'M'); pass NULL
+ * buffers first to learn N and L.  hmc_load_file = parse + hmc_load_genotypes
+ * (keeps ids, marker names, positions for hmc_write_file).  hmc_write_file
+ * writes the accepted resolutions in that format (BENCH2: + position file). */
+int hmc_parse_file(const char *format, const char *path, const char *path2, int *N, int *L, int32_t *alleles,
+                   char *types);
+int hmc_load_file(hmc_ctx *ctx, const char *format, const char *path, const char *path2);
+int hmc_write_file(hmc_ctx *ctx, const char *format, const char *path, const char *path2);
 
 /* ---- tuning -------------------------------------------------------------- */
 /* frontier_cap: states per locus per wave before a batch is re-run with a
