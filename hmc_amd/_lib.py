@@ -73,6 +73,7 @@ _SIGS = [
     ("hmc_parse_file", _i, [_cp, _cp, _cp, _P(_i), _P(_i), _P(C.c_int32), _cp]),
     ("hmc_load_file", _i, [_vp, _cp, _cp, _cp]),
     ("hmc_write_file", _i, [_vp, _cp, _cp, _cp]),
+    ("hmc_write_patterns", _i, [_vp, _cp]),
     ("hmc_write_phase", _i, [_vp, _cp]),
     ("hmc_set_tuning", _i, [_vp, _i, _u64, _i]),
     ("hmc_set_estep_shape", _i, [_vp, _i, _i]),

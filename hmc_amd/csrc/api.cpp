@@ -1795,6 +1795,35 @@ int hmc_write_file(hmc_ctx *h, const char *format, const char *path, const char 
   return HMC_OK;
 }
 
+int hmc_write_patterns(hmc_ctx *h, const char *path) {
+  if (!h || !path || !h->c.have_model || h->c.node_cap <= 0) return HMC_EARG;
+  hmc::Ctx &c = h->c;
+  const int P = c.P, L = c.pan.L;
+  std::vector<int32_t> st(P), ln(P);
+  std::vector<double> fr(P);
+  int rc = hmc_get_patterns(h, st.data(), ln.data(), fr.data(), nullptr, nullptr, nullptr, nullptr, 0);
+  if (rc) return rc;
+  int maxlen = 1;
+  for (int i = 0; i < P; ++i) maxlen = std::max(maxlen, ln[i]);
+  std::vector<int32_t> al((size_t)P * maxlen);
+  if ((rc = hmc_get_patterns(h, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, al.data(), maxlen))) return rc;
+  FILE *fp = fopen(path, "w");
+  if (!fp) return c.fail(HMC_EIO, "Can not open file %s!", path);
+  fprintf(fp, "Frequency\tLength\t");
+  for (int k = 0; k < L; ++k)
+    fprintf(fp, "%s ", (int)c.file_meta.names.size() == L ? c.file_meta.names[k].c_str() : ("M" + std::to_string(k + 1)).c_str());
+  fprintf(fp, "\n");
+  for (int i = 0; i < P; ++i) {  // HaploPattern::write(buf, true): -1 outside [start, end), 'M' integers
+    fprintf(fp, "%f\t%d\t", fr[i] / c.pan.N, ln[i]);
+    for (int k = 0; k < st[i]; ++k) fprintf(fp, "-1 ");
+    for (int k = 0; k < ln[i]; ++k) fprintf(fp, "%d ", al[(size_t)i * maxlen + k]);
+    for (int k = st[i] + ln[i]; k < L; ++k) fprintf(fp, "-1 ");
+    fprintf(fp, "\n");
+  }
+  fclose(fp);
+  return HMC_OK;
+}
+
 int hmc_panel_info(const hmc_ctx *h, int *N, int *L, int *amax) {
   if (!h || !h->c.have_panel) return HMC_EARG;
   if (N) *N = h->c.pan.N;

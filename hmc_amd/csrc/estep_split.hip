@@ -729,9 +729,26 @@ __global__ __launch_bounds__(256) void estep_values(ValueArgs a) {
         const uint32_t hd = Rhd[t];
         const bool differ = (hd & 0xFFu) != ((hd >> 8) & 0xFFu);
         const int cb = (int)Rcb[t], ce = (int)Rcb[t + 1];
+        // ordered forward sum (HaploPair.cpp:42, :66): words and predecessor
+        // likelihoods of 8 contributions loaded together, the adds in order
+        double fwd = 0.0;
+        for (int rb = cb; rb < ce; rb += 8) {
+          uint32_t ws[8];
+          double fs[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) ws[u] = rb + u < ce ? Rct[rb + u] : Rct[cb];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) fs[u] = *X.fwd((int)(ws[u] & 0xFFFFu));
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (rb + u < ce) {
+              const double v = fs[u] * tpv;
+              fwd = rb + u == cb ? v : fwd + v;
+            }
+        }
+        // extension constructor + the appends that still fit
         uint32_t w = Rct[cb];
         uint32_t s = w & 0xFFFFu, ns = w >> 24;
-        double fwd = *X.fwd((int)s) * tpv;
         double *yl = Y.lik(t);
         uint32_t *ym = Y.meta(t);
         copy_extended(X.lik((int)s), X.meta((int)s), yl, ym, 0, (int)ns, s, tpv, (w >> 16) & 1u, differ);
@@ -740,14 +757,12 @@ __global__ __launch_bounds__(256) void estep_values(ValueArgs a) {
           w = Rct[r];
           s = w & 0xFFFFu;
           ns = w >> 24;
-          fwd += *X.fwd((int)s) * tpv;
-          if (r0 == ce) {
-            if (k + (int)ns <= S) {
-              copy_extended(X.lik((int)s), X.meta((int)s), yl, ym, k, (int)ns, s, tpv, (w >> 16) & 1u, differ);
-              k += (int)ns;
-            } else {
-              r0 = r;
-            }
+          if (k + (int)ns <= S) {
+            copy_extended(X.lik((int)s), X.meta((int)s), yl, ym, k, (int)ns, s, tpv, (w >> 16) & 1u, differ);
+            k += (int)ns;
+          } else {
+            r0 = r;
+            break;
           }
         }
         *Y.fwd(t) = fwd;

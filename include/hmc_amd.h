@@ -165,6 +165,13 @@ int hmc_parse_file(const char *format, const char *path, const char *path2, int 
                    char *types);
 int hmc_load_file(hmc_ctx *ctx, const char *format, const char *path, const char *path2);
 int hmc_write_file(hmc_ctx *ctx, const char *format, const char *path, const char *path2);
+/* HaploFile::writePattern (HaploFile.cpp:155-171; HMC.cpp:229-232, the
+ * --output-patterns ".patterns" file) of the current pattern table: header
+ * "Frequency\tLength\t<marker names>", one line per pattern in id order with
+ * frequency / N, length and the long-format alleles (-1 outside the pattern).
+ * The reference divides by genotype_num() of a GenoData that no longer exists
+ * when it writes, so the N used here is the panel's: unpinned. */
+int hmc_write_patterns(hmc_ctx *ctx, const char *path);
 
 /* ---- tuning -------------------------------------------------------------- */
 /* frontier_cap: states per locus per wave before a batch is re-run with a

@@ -114,3 +114,26 @@ def test_write_read_round_trip(tmp_path, fmt):
     assert np.array_equal(al, res)
     if fmt == "BENCH2":
         assert open(out2).read().splitlines()[3].split() == ["3", "rs3", "30"]
+
+
+@pytest.mark.gpu
+def test_write_patterns(tmp_path):
+    """writePattern (.patterns): one line per pattern in id order with freq/N,
+    the length and the long-format alleles; checked against the table."""
+    p = synth.founder_mosaic(30, 20, A=2, seed=3)
+    m = hmc_amd.HaploModel()
+    m.load(hmc_amd.GenoData.from_panel(p))
+    m.find_patterns()
+    out = str(tmp_path / "x.patterns")
+    assert hmc_amd.lib().hmc_write_patterns(m._h, out.encode()) == 0
+    pt = m.patterns()
+    lines = open(out).read().splitlines()
+    assert lines[0].split("\t")[:2] == ["Frequency", "Length"]
+    assert len(lines) == 1 + len(pt["start"])
+    for i in (0, len(lines) // 2, len(lines) - 2):
+        f, ln, al = lines[i + 1].split("\t")
+        assert float(f) == pytest.approx(pt["freq"][i] / p.N, abs=5e-7) and int(ln) == pt["len"][i]
+        v = [int(x) for x in al.split()]
+        s, n = pt["start"][i], pt["len"][i]
+        assert len(v) == p.L and v[:s] == [-1] * s and v[s + n:] == [-1] * (p.L - s - n)
+        assert v[s:s + n] == pt["alleles"][i, :n].tolist()
