@@ -326,21 +326,44 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
       const int C = pr_off[npairs];
       if (C > a.ccap) { status = EST_OVERFLOW_FRONTIER; break; }
       int Fn = 0;
+      // successor gathers of up to GB chunks issued together (one exposed
+      // latency per GB*64 contributions), then the chunks' keys in order
+      constexpr int GB = 4;
+      uint32_t g_sa[GB], g_sb[GB], g_s[GB];
       for (int c0 = 0; c0 < C; c0 += WAVE) {
         const int c = c0 + lane;
+        const int gq = (c0 / WAVE) % GB;
+        if (gq == 0) {
+#pragma unroll
+          for (int q = 0; q < GB; ++q) {
+            const int cq = c + q * WAVE;
+            g_sa[q] = g_sb[q] = NONE;
+            g_s[q] = 0;
+            if (cq < C) {
+              int p = 0;
+              while (p + 1 < npairs && cq >= pr_off[p + 1]) ++p;
+              const int local = cq - pr_off[p];
+              const int o = pr_o[p] == 2 ? (local & 1) : 0;
+              g_s[q] = pr_o[p] == 2 ? (uint32_t)(local >> 1) : (uint32_t)local;
+              const uint32_t x = o ? pr_y[p] : pr_x[p];
+              const uint32_t y = o ? pr_x[p] : pr_y[p];
+              g_sa[q] = a.mod.succ[(size_t)*X.at(F_LO, (int)g_s[q]) * amax + x];
+              g_sb[q] = a.mod.succ[(size_t)*X.at(F_HI, (int)g_s[q]) * amax + y];
+            }
+          }
+        }
+        uint32_t sa = g_sa[0], sb = g_sb[0], s = g_s[0];
+#pragma unroll
+        for (int q = 1; q < GB; ++q)
+          if (gq == q) {
+            sa = g_sa[q];
+            sb = g_sb[q];
+            s = g_s[q];
+          }
         bool valid = c < C;
-        uint32_t s = 0, lo = 0, hi = 0, slot = 0;
+        uint32_t lo = 0, hi = 0, slot = 0;
         bool rev = false;
         if (valid) {
-          int p = 0;
-          while (p + 1 < npairs && c >= pr_off[p + 1]) ++p;
-          const int local = c - pr_off[p];
-          const int o = pr_o[p] == 2 ? (local & 1) : 0;
-          s = pr_o[p] == 2 ? (uint32_t)(local >> 1) : (uint32_t)local;
-          const uint32_t x = o ? pr_y[p] : pr_x[p];
-          const uint32_t y = o ? pr_x[p] : pr_y[p];
-          const uint32_t sa = a.mod.succ[(size_t)*X.at(F_LO, (int)s) * amax + x];
-          const uint32_t sb = a.mod.succ[(size_t)*X.at(F_HI, (int)s) * amax + y];
           valid = sa != NONE && sb != NONE;
           rev = sa > sb;  // addHaploPair: id_a > id_b -> swap, reversed
           lo = rev ? sb : sa;
