@@ -146,7 +146,10 @@ __device__ inline ParentView parent_view(const MineArgs &a, int level, int pidx)
 
 // ---------------------------------------------------------------------------
 constexpr int CROW = WAVE + 18;  // LDS row stride (doubles): one chunk's contributions + batch padding
-constexpr int MC_U = 4;           // chunks of 64 list entries per load group of mine_count
+#ifndef MC_U_DEF
+#define MC_U_DEF 4
+#endif
+constexpr int MC_U = MC_U_DEF;    // chunks of 64 list entries per load group of mine_count
 __host__ __device__ inline int mine_count_bufs(int amax) { return amax <= 8 ? MC_U : 1; }
 
 // Child k's matching entries of one chunk (compacted in LDS) to its list:

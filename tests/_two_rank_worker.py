@@ -15,6 +15,7 @@ from hmc_amd import synth  # noqa: E402
 
 def main():
     rank, out = int(sys.argv[1]), sys.argv[2]
+    variant = sys.argv[3] if len(sys.argv) > 3 else "MV"
     dist.init_process_group("gloo", rank=rank, world_size=2)
 
     def allreduce(arr):
@@ -24,12 +25,17 @@ def main():
     p = synth.founder_mosaic(80, 60, A=3, missing=0.05, seed=5)
     m = hmc_amd.HaploModel(device=0, rank=rank, world=2, host_allreduce=allreduce)
     m.max_iteration = 10
+    if variant == "MC":
+        m.model = "MC"
+    elif variant == "BYNUM":
+        m.num_patterns, m.min_pattern_len = 150, 2
     m.load(hmc_amd.GenoData.from_panel(p))
     m.find_patterns()
     m0_freq = m.patterns()["freq"]
     m.clear_samples()
     res = m.run()
-    np.savez(os.path.join(out, f"rank{rank}.npz"), ll=np.array([x["ll"] for x in m.log]), res=res, m0_freq=m0_freq)
+    np.savez(os.path.join(out, f"rank{rank}.npz"), ll=np.array([x["ll"] for x in m.log]), res=res, m0_freq=m0_freq,
+             comp=np.array([x["haplocomp"] for x in m.log]))
     dist.barrier()
     dist.destroy_process_group()
 

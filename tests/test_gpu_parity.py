@@ -400,20 +400,27 @@ def _free_port():
     return port
 
 
-def test_two_ranks_one_gpu_host_collective(oracle_mod, tmp_path):
+@pytest.mark.parametrize("variant", ["MV", "MC", "BYNUM"])
+def test_two_ranks_one_gpu_host_collective(oracle_mod, tmp_path, variant):
     """The sharded multi-rank path (individual shards, per-level all-reduce of
-    candidate sums, all-reduced LL / total weight) with 2 ranks on one GPU and a
-    gloo host collective.  Sums are reassociated across ranks, so frequencies
-    agree to 1e-12 relative; LL and resolutions are compared to the restatement."""
+    candidate sums, all-reduced LL / total weight, the HaploComp counters) with
+    2 ranks on one GPU and a gloo host collective, for MV, MC and
+    findPatternByNum.  Sums are reassociated across ranks, so frequencies agree
+    to 1e-12 relative; LL and resolutions are compared to the restatement."""
     script = os.path.join(HERE, "_two_rank_worker.py")
     port = _free_port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
-    procs = [subprocess.Popen([sys.executable, script, str(r), str(tmp_path)], env=dict(env, RANK=str(r)))
+    procs = [subprocess.Popen([sys.executable, script, str(r), str(tmp_path), variant], env=dict(env, RANK=str(r)))
              for r in range(2)]
     for pr in procs:
         assert pr.wait(timeout=300) == 0
     p = panel("a3miss5")
-    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10, max_iter=10)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10, max_iter=10,
+                          min_len=2 if variant == "BYNUM" else 1)
+    if variant == "MC":
+        o.set_model("MC", 1)
+    elif variant == "BYNUM":
+        o.set_num_patterns(150)
     r = o.run()
     outs = [np.load(tmp_path / f"rank{k}.npz") for k in range(2)]
     ll = outs[0]["ll"]
@@ -424,6 +431,9 @@ def test_two_ranks_one_gpu_host_collective(oracle_mod, tmp_path):
     same = np.mean(np.all(res == r["resolutions"], axis=(1, 2)))
     assert same >= 0.97, same
     assert np.array_equal(outs[0]["m0_freq"], outs[1]["m0_freq"])
+    assert np.array_equal(outs[0]["comp"], outs[1]["comp"])  # HaploComp over both shards
+    if same == 1.0:
+        np.testing.assert_array_equal(outs[0]["comp"][-1], r["haplocomp"][-1])
 
 
 def test_shard_ranges_balanced_and_tiling():
