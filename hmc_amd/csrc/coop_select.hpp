@@ -124,15 +124,15 @@ __device__ inline void seg_nth_slots(int n, int nth, const Seg &sg, const SegScr
   const int k = sg.k;
   int first = 0, last = n, depth = n > 0 ? lg2_floor(n) * 2 : 0;
   const bool act = n > 0 && nth != n && sg.mask != 0ull;
-  bool heap = false;
   double *sl = ss.slik + sg.base;
   uint32_t *sm = ss.smeta + sg.base;
   int *lp = ss.lpos + sg.base, *rp = ss.rpos + sg.base;
   int *jl = ss.junk + lane, *jr = ss.junk + 64 + lane;
   const int kmax = sg.sw - 1;
   while (true) {
-    heap = heap || (act && last - first > 3 && depth == 0);
-    const bool part = act && !heap && last - first > 3;
+    // a segment whose depth budget is spent stops here with > 3 elements left
+    // and finishes with the heap select below (its range no longer changes)
+    const bool part = act && last - first > 3 && depth > 0;
     if (!wave_ballot(part)) break;
     depth -= part ? 1 : 0;
     // std::__move_median_to_first(first, first+1, mid, last-1) (stl_algo.h:79-102)
@@ -150,10 +150,13 @@ __device__ inline void seg_nth_slots(int n, int nth, const Seg &sg, const SegScr
     // left scan over [first+1, last) stops at !(x > pivot), right scan over
     // [first, last) at !(pivot > x)
     const double pv = k == first ? pivot : (k == r ? vf : v);
-    const bool inr = part && k >= first && k < last;
-    const bool pL = inr && k != first && !(pv > pivot);
-    const bool pR = inr && !(pivot > pv);
-    const uint32_t Lw = seg_bits(wave_ballot(pL), sg), Rw = seg_bits(wave_ballot(pR), sg);
+    // each ballot of a single comparison stays a lane mask; the conjunctions
+    // are scalar ANDs (a ballot of a && b would be materialised and re-compared)
+    const uint64_t b_part = wave_ballot(part), b_in = wave_ballot(k > first) & wave_ballot(k < last);
+    const uint64_t b_first = wave_ballot(k == first);
+    const uint64_t b_le = wave_ballot(!(pv > pivot)), b_ge = wave_ballot(!(pivot > pv));
+    const uint32_t Lw = seg_bits(b_part & b_in & b_le, sg);
+    const uint32_t Rw = seg_bits(b_part & (b_in | b_first) & b_ge, sg);
     const int nL = __popc(Lw), nR = __popc(Rw);
     // this lane's element is at position x once the median is at first
     const int x = !part ? k : (k == first ? r : (k == r ? first : k));
@@ -188,6 +191,7 @@ __device__ inline void seg_nth_slots(int n, int nth, const Seg &sg, const SegScr
   }
   // Depth limit reached (std::__heap_select + iter_swap, stl_algo.h:1973-1979):
   // rare; the segment's first lane runs the sequential code on the slots.
+  const bool heap = act && last - first > 3;
   if (wave_ballot(heap)) {
     if (heap && k == 0) {
       const LinkList wl{sl, sm, 1};
