@@ -45,12 +45,22 @@ struct DevBuf {
     p = nullptr;
     n = 0;
   }
-  hipError_t ensure(size_t m) {  // contents not preserved
+  // Contents not preserved.  A buffer that has to grow takes 1.5x headroom:
+  // large allocations are mapped eagerly by the HIP runtime (~1 s per 10-20 GB),
+  // so slowly growing per-level buffers must not be re-allocated every level.
+  hipError_t ensure(size_t m) {
     if (m <= n && p) return hipSuccess;
+    const size_t want = std::max<size_t>(m, 1), grown = n ? std::max(want, n + n / 2) : want;
     release();
-    hipError_t e = hipMalloc((void **)&p, std::max<size_t>(m, 1) * sizeof(T));
+    size_t got = grown;
+    hipError_t e = hipMalloc((void **)&p, got * sizeof(T));
+    if (e != hipSuccess && grown > want) {
+      (void)hipGetLastError();
+      got = want;
+      e = hipMalloc((void **)&p, got * sizeof(T));
+    }
     if (e != hipSuccess) { p = nullptr; return e; }
-    n = std::max<size_t>(m, 1);
+    n = got;
     return hipSuccess;
   }
   hipError_t grow_keep(size_t m, size_t used, hipStream_t st) {  // preserve the first `used` elements
@@ -419,7 +429,8 @@ struct Ctx {
   // --------------------------------------------------------------- mining --
   int grow_nodes(size_t need, size_t used) {
     if (need <= node_cap) return HMC_OK;
-    size_t cap = std::max<size_t>(need, node_cap + node_cap / 2);
+    // doubling (each growth re-maps and copies 15 arrays)
+    size_t cap = std::max<size_t>(need, 2 * node_cap);
     hipError_t e;
 #define G(b) if ((e = b.grow_keep(cap, used, st))) return hipfail(e, "grow_nodes");
     G(n_parent) G(n_start) G(n_child_base) G(n_link) G(n_allele) G(n_flags) G(n_freq) G(n_prefix) G(n_tp) G(n_sum)
@@ -1001,8 +1012,13 @@ struct Ctx {
     // individual-locus), grow up to the budget on overflow, then split batches
     size_t freeb = 0, totb = 0;
     hipMemGetInfo(&freeb, &totb);
-    const uint64_t cap_bytes =
-        std::max<uint64_t>(trace_bytes ? trace_bytes : (uint64_t)((freeb + d_trace.n * 4) * 0.35), 1ull << 20);
+    // The trace store and the record store each grow up to this budget; past it
+    // the batch of individuals is halved.  At most 24 GiB each: first-touch
+    // mapping of huge allocations costs ~1 s per 10-20 GB with the system ROCm
+    // runtime, far more than the few extra launches of smaller batches.
+    const uint64_t cap_bytes = std::max<uint64_t>(
+        trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)((freeb + d_trace.n * 4) * 0.35), 24ull << 30),
+        1ull << 20);
     const uint64_t want = std::min<uint64_t>(cap_bytes, std::max<uint64_t>((uint64_t)n * L * (1 + S) * 4 * 96, 64ull << 20));
     if (d_trace.n * 4 < want) {
       d_trace.release();

@@ -150,7 +150,9 @@ constexpr int CROW = WAVE + 18;  // LDS row stride (doubles): one chunk's contri
 #define MC_U_DEF 4
 #endif
 constexpr int MC_U = MC_U_DEF;    // chunks of 64 list entries per load group of mine_count
-__host__ __device__ inline int mine_count_bufs(int amax) { return amax <= 8 ? MC_U : 1; }
+// one LDS buffer per chunk only while the block stays small (occupancy of the
+// one-wave blocks matters more than the deferred stores for many alleles)
+__host__ __device__ inline int mine_count_bufs(int amax) { return amax <= 2 ? MC_U : 1; }
 
 // Child k's matching entries of one chunk (compacted in LDS) to its list:
 // child k of a parent with n entries owns n slots at region + k*n; `mine` and

@@ -348,6 +348,53 @@ def test_cfg2_full_size_against_oracle_digest():
     assert hashlib.sha256(np.ascontiguousarray(res, np.int32).tobytes()).hexdigest() == d["resolutions_sha256"]
 
 
+def test_cfg5_full_size_properties():
+    """BASELINE config 5 at full size (10 000 individuals x 1 000 loci, 8 alleles
+    per locus: the divergent multi-allelic frontier): every selected pair is a
+    phasing of its genotype, priors sorted, weights sum to 1 per individual,
+    the M1 table is a proper pattern table (checked successors are suffixes),
+    and E1 repeats bit for bit."""
+    import time
+    t0 = time.time()
+    p = synth.config_panel(5)
+    m = gpu_model(p)
+    m.find_patterns()
+    ll, H, re1 = m.resolve_all()
+    print(f"cfg5 M0+E1 {time.time() - t0:.1f} s", flush=True)
+    er = m.estep_results()
+    g = p.alleles
+    nc = er["ncand"]
+    assert np.all(nc > 0) and np.isfinite(ll) and H == int(2 * nc.sum())
+    k = np.arange(er["prior"].shape[1])
+    valid = k[None, :] < nc[:, None]
+    pr = np.where(valid, er["prior"], -np.inf)
+    assert np.all(np.diff(pr, axis=1)[valid[:, 1:]] <= 0)
+    assert np.all(np.abs(np.where(valid, er["weight"], 0.0).sum(1) - 1.0) < 1e-12)
+    res = m.resolutions()
+    ok = ((res[:, 0] == g[:, 0]) & (res[:, 1] == g[:, 1])) | ((res[:, 0] == g[:, 1]) & (res[:, 1] == g[:, 0]))
+    assert ok.all()
+    ll2, H2, re2 = m.resolve_all()
+    assert (ll2, H2, re2) == (ll, H, re1)
+    print(f"cfg5 E1 again {time.time() - t0:.1f} s", flush=True)
+    P, _ = m.find_patterns()
+    pt = m.patterns()
+    print(f"cfg5 M1 {P} patterns {time.time() - t0:.1f} s", flush=True)
+    num, sym, _ = m.allele_table()
+    assert np.all(pt["freq"] > 0) and np.all(pt["freq"] <= 1) and np.all(pt["tp"] <= 1)
+    rng = np.random.default_rng(5)
+    for i in rng.choice(P, 500, replace=False):
+        e = pt["start"][i] + pt["len"][i]
+        if e >= p.L:
+            continue
+        for j in range(num[e]):
+            s = pt["succ"][i, j]
+            if s < 0:
+                continue
+            ext = np.append(pt["alleles"][i, :pt["len"][i]], sym[e, j])
+            assert pt["start"][s] + pt["len"][s] == e + 1
+            assert np.array_equal(pt["alleles"][s, :pt["len"][s]], ext[len(ext) - pt["len"][s]:])
+
+
 def test_cfg2_properties():
     """Size-independent properties at full size: samples are phasings of the
     genotypes, weights of each individual sum to 1, priors are sorted, successors
