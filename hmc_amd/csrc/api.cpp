@@ -81,6 +81,25 @@ struct DevBuf {
   }
 };
 
+// Page-locked host buffer for small per-level readbacks: a DtoH copy into pageable
+// memory goes through a staging buffer and a second copy on every mining level.
+template <class T>
+struct PinnedBuf {
+  T *p = nullptr;
+  PinnedBuf() = default;
+  PinnedBuf(const PinnedBuf &) = delete;
+  PinnedBuf &operator=(const PinnedBuf &) = delete;
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  hipError_t ensure(size_t m) {
+    if (p) return hipSuccess;
+    hipError_t e = hipHostMalloc((void **)&p, std::max<size_t>(m, 1) * sizeof(T), hipHostMallocDefault);
+    if (e != hipSuccess) p = nullptr;
+    return e;
+  }
+};
+
 struct Err {
   int code;
 };
@@ -248,6 +267,7 @@ struct Ctx {
   DevBuf<uint32_t> l_idx[2];
   DevBuf<double> l_val[2];
   DevBuf<unsigned long long> s_ext, s_lscan, d_totals, d_rm;
+  PinnedBuf<unsigned long long> h_totals;  // fixed 2 slots (next list slots, next nodes)
   DevBuf<int32_t> s_child, s_cscan;
   DevBuf<char> s_tmp;
   DevBuf<uint32_t> d_rsize, d_rpos;
@@ -528,7 +548,8 @@ struct Ctx {
       mf = -1.0;
     }
     if (bynum_rounds > 0) mf = bynum_theta(bynum_rounds);
-    if ((e = d_rm.ensure(RM_SLOTS * 16)) || (e = d_totals.ensure(2)) || (e = hipMemsetAsync(d_rm.p, 0, RM_SLOTS * 16 * 8, st)))
+    if ((e = d_rm.ensure(RM_SLOTS * 16)) || (e = d_totals.ensure(2)) || (e = h_totals.ensure(2)) ||
+        (e = hipMemsetAsync(d_rm.p, 0, RM_SLOTS * 16 * 8, st)))
       return hipfail(e, "mine");
     std::vector<int> lbeg{0, 0}, lend{0, 0};  // per level node ranges (index = level)
     int n1 = 0;
@@ -628,8 +649,8 @@ struct Ctx {
       if ((e = launch_mine_offsets(a, cb, ce, s_ext.p, s_child.p, s_lscan.p, s_cscan.p, ce, s_tmp.p, s_tmp.n, d_totals.p,
                                    st)))
         return hipfail(e, "mine_offsets");
-      unsigned long long tot[2];
-      if ((e = hipMemcpyAsync(tot, d_totals.p, 16, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+      const unsigned long long *tot = h_totals.p;
+      if ((e = hipMemcpyAsync(h_totals.p, d_totals.p, 16, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
         return hipfail(e, "mine");
       next_total = tot[0];  // list slots the next level's children need
       const int nnext = (int)tot[1];
