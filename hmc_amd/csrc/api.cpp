@@ -266,9 +266,9 @@ struct Ctx {
   size_t node_cap = 0;
   DevBuf<uint32_t> l_idx[2];
   DevBuf<double> l_val[2];
-  DevBuf<unsigned long long> s_ext, s_lscan, d_totals, d_rm;
+  DevBuf<unsigned long long> s_ext, d_totals, d_rm;
   PinnedBuf<unsigned long long> h_totals;  // fixed 2 slots (next list slots, next nodes)
-  DevBuf<int32_t> s_child, s_cscan;
+  DevBuf<int32_t> s_child;
   DevBuf<char> s_tmp;
   DevBuf<uint32_t> d_rsize, d_rpos;
 
@@ -640,13 +640,12 @@ struct Ctx {
         hipEventDestroy(dm1);
       }
       if ((rc = allreduce_sum(n_sum.p + cb, nlev))) return rc;
-      if ((e = s_ext.ensure(nlev)) || (e = s_lscan.ensure(nlev)) || (e = s_child.ensure(nlev)) ||
-          (e = s_cscan.ensure(nlev)))
+      if ((e = s_ext.ensure(nlev)) || (e = s_child.ensure(nlev)))
         return hipfail(e, "mine");
       const size_t tmpb = mine_scan_tmp_bytes(nlev);
       if ((e = s_tmp.ensure(tmpb))) return hipfail(e, "mine");
       if ((e = launch_mine_finalize(a, level, cb, ce, s_ext.p, s_child.p, st))) return hipfail(e, "mine_finalize");
-      if ((e = launch_mine_offsets(a, cb, ce, s_ext.p, s_child.p, s_lscan.p, s_cscan.p, ce, s_tmp.p, s_tmp.n, d_totals.p,
+      if ((e = launch_mine_offsets(a, cb, ce, s_ext.p, s_child.p, ce, s_tmp.p, s_tmp.n, d_totals.p,
                                    st)))
         return hipfail(e, "mine_offsets");
       const unsigned long long *tot = h_totals.p;

@@ -383,20 +383,35 @@ __global__ void mine_finalize(MineArgs a, int level, int b, int e, unsigned long
   next_children[c - b] = ext ? (int32_t)a.npos[st + level] : 0;
 }
 
-__global__ void mine_apply_offsets(MineArgs a, int b, int e, const unsigned long long *list_scan,
-                                   const int32_t *child_scan, int next_base) {
+// Both per-node counts of a level scanned together (one device scan instead of two).
+struct LevelOffsets {
+  unsigned long long list;  // list slots before this node
+  long long child;          // children before this node
+};
+struct LevelOffsetsSum {
+  __host__ __device__ LevelOffsets operator()(const LevelOffsets &x, const LevelOffsets &y) const {
+    return {x.list + y.list, x.child + y.child};
+  }
+};
+struct LevelCounts {
+  const unsigned long long *ext_list;
+  const int32_t *next_children;
+  __host__ __device__ LevelOffsets operator()(int i) const { return {ext_list[i], (long long)next_children[i]}; }
+};
+// Offsets applied to the level's nodes; the last node's thread also writes the level
+// totals (list slots and nodes of the next level) for the host readback.
+__global__ void mine_apply_offsets(MineArgs a, int b, int e, const LevelOffsets *scan,
+                                   const unsigned long long *ext_list, const int32_t *next_children, int next_base,
+                                   unsigned long long *totals) {
   const int c = b + blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= e) return;
+  const LevelOffsets o = scan[c - b];
   const bool ext = a.flags[c] & NODE_EXT;
-  a.region[c] = ext ? list_scan[c - b] : 0ull;
-  a.child_base[c] = ext ? next_base + child_scan[c - b] : -1;
-}
-
-__global__ void scan_totals(const unsigned long long *ls, const unsigned long long *lv, const int32_t *cs,
-                            const int32_t *cv, int n, unsigned long long *out) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    out[0] = n ? ls[n - 1] + lv[n - 1] : 0ull;
-    out[1] = n ? (unsigned long long)(cs[n - 1] + cv[n - 1]) : 0ull;
+  a.region[c] = ext ? o.list : 0ull;
+  a.child_base[c] = ext ? next_base + (int)o.child : -1;
+  if (c == e - 1) {
+    totals[0] = o.list + ext_list[c - b];
+    totals[1] = (unsigned long long)(o.child + next_children[c - b]);
   }
 }
 
@@ -540,28 +555,31 @@ hipError_t launch_mine_finalize(const MineArgs &a, int level, int b, int e, unsi
   hipLaunchKernelGGL(mine_finalize, dim3((e - b + 255) / 256), dim3(256), 0, st, a, level, b, e, ext_list, next_children);
   return hipGetLastError();
 }
+static size_t scan_storage_bytes(int n) {
+  size_t need = 0;
+  hipcub::TransformInputIterator<LevelOffsets, LevelCounts, hipcub::CountingInputIterator<int>> in(
+      hipcub::CountingInputIterator<int>(0), LevelCounts{nullptr, nullptr});
+  hipcub::DeviceScan::ExclusiveScan(nullptr, need, in, (LevelOffsets *)nullptr, LevelOffsetsSum(), LevelOffsets{0, 0},
+                                    n);
+  return (need + 255) & ~(size_t)255;
+}
 hipError_t launch_mine_offsets(const MineArgs &a, int b, int e, unsigned long long *ext_list, int32_t *next_children,
-                               unsigned long long *list_scan, int32_t *child_scan, int next_base, void *tmp,
-                               size_t tmp_bytes, unsigned long long *totals, hipStream_t st) {
+                               int next_base, void *tmp, size_t tmp_bytes, unsigned long long *totals, hipStream_t st) {
   const int n = e - b;
   if (n <= 0) return hipSuccess;
-  size_t need = tmp_bytes;
-  hipError_t err = hipcub::DeviceScan::ExclusiveSum(tmp, need, ext_list, list_scan, n, st);
+  size_t need = scan_storage_bytes(n);
+  if (need + (size_t)n * sizeof(LevelOffsets) > tmp_bytes) return hipErrorInvalidValue;
+  LevelOffsets *scan = (LevelOffsets *)((char *)tmp + need);
+  hipcub::TransformInputIterator<LevelOffsets, LevelCounts, hipcub::CountingInputIterator<int>> in(
+      hipcub::CountingInputIterator<int>(0), LevelCounts{ext_list, next_children});
+  hipError_t err =
+      hipcub::DeviceScan::ExclusiveScan(tmp, need, in, scan, LevelOffsetsSum(), LevelOffsets{0, 0}, n, st);
   if (err != hipSuccess) return err;
-  need = tmp_bytes;
-  err = hipcub::DeviceScan::ExclusiveSum(tmp, need, next_children, child_scan, n, st);
-  if (err != hipSuccess) return err;
-  hipLaunchKernelGGL(mine_apply_offsets, dim3((n + 255) / 256), dim3(256), 0, st, a, b, e, list_scan, child_scan,
-                     next_base);
-  hipLaunchKernelGGL(scan_totals, dim3(1), dim3(1), 0, st, list_scan, ext_list, child_scan, next_children, n, totals);
+  hipLaunchKernelGGL(mine_apply_offsets, dim3((n + 255) / 256), dim3(256), 0, st, a, b, e, scan, ext_list,
+                     next_children, next_base, totals);
   return hipGetLastError();
 }
-size_t mine_scan_tmp_bytes(int n) {
-  size_t a = 0, b = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, a, (unsigned long long *)nullptr, (unsigned long long *)nullptr, n);
-  hipcub::DeviceScan::ExclusiveSum(nullptr, b, (int32_t *)nullptr, (int32_t *)nullptr, n);
-  return a > b ? a : b;
-}
+size_t mine_scan_tmp_bytes(int n) { return scan_storage_bytes(n) + (size_t)n * sizeof(LevelOffsets); }
 hipError_t launch_mine_size(const MineArgs &a, int level, int b, int e, hipStream_t st) {
   if (e <= b) return hipSuccess;
   hipLaunchKernelGGL(mine_size, dim3((e - b + 255) / 256), dim3(256), 0, st, a, level, b, e);

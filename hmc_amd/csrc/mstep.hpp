@@ -56,8 +56,8 @@ hipError_t launch_mine_count(const MineArgs &a, int level, int pbeg, int pend, h
 hipError_t launch_mine_finalize(const MineArgs &a, int level, int b, int e, unsigned long long *ext_list,
                                 int32_t *next_children, hipStream_t st);
 hipError_t launch_mine_offsets(const MineArgs &a, int b, int e, unsigned long long *ext_list, int32_t *next_children,
-                               unsigned long long *list_scan, int32_t *child_scan, int next_base, void *tmp,
-                               size_t tmp_bytes, unsigned long long *totals, hipStream_t st);
+                               int next_base, void *tmp, size_t tmp_bytes, unsigned long long *totals,
+                               hipStream_t st);
 size_t mine_scan_tmp_bytes(int n);
 hipError_t launch_mine_size(const MineArgs &a, int level, int b, int e, hipStream_t st);
 hipError_t launch_mine_root_size(const MineArgs &a, uint32_t *rsize, hipStream_t st);
