@@ -269,6 +269,8 @@ struct Ctx {
   DevBuf<unsigned long long> s_ext, d_totals, d_rm;
   PinnedBuf<unsigned long long> h_totals;  // fixed 2 slots (next list slots, next nodes)
   DevBuf<int32_t> s_child;
+  DevBuf<int> d_lev_begin;  // node offset of each mining level (1..maxlev) + end
+  std::vector<int> h_lev_begin;
   DevBuf<char> s_tmp;
   DevBuf<uint32_t> d_rsize, d_rpos;
 
@@ -694,8 +696,12 @@ struct Ctx {
     }
     if ((rc = alloc_table(P))) return rc;
     PatternTable t = table();
-    for (int lv = 1; lv <= maxlev; ++lv)
-      if ((e = launch_mine_emit(a, lv, lbeg[lv], lend[lv], t, st))) return hipfail(e, "mine_emit");
+    h_lev_begin.assign(lbeg.begin(), lbeg.begin() + maxlev + 1);
+    h_lev_begin.push_back(lend[maxlev]);
+    if ((e = d_lev_begin.ensure(h_lev_begin.size())) ||
+        (e = hipMemcpyAsync(d_lev_begin.p, h_lev_begin.data(), h_lev_begin.size() * 4, hipMemcpyHostToDevice, st)) ||
+        (e = launch_mine_emit(a, d_lev_begin.p, maxlev, lend[maxlev] - lbeg[1], t, st)))
+      return hipfail(e, "mine_emit");
     if ((e = launch_mine_succ(a, t, P, st))) return hipfail(e, "mine_succ");
     head_len = mnl;
     if ((rc = build_heads_from_nodes(a, mnl <= maxlev ? lbeg[mnl] : 0, mnl <= maxlev ? lend[mnl] : 0))) return rc;

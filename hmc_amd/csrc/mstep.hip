@@ -459,13 +459,21 @@ __global__ void mine_pos(MineArgs a, int level, int pbeg, int pend, const uint32
   }
 }
 
-__global__ void mine_emit(MineArgs a, int level, int b, int e, PatternTable t) {
-  const int c = b + blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= e) return;
+// All levels in one launch: node c's level (= pattern length) is found by binary
+// search over the level start offsets lev_begin[1..maxlev+1].
+__global__ void mine_emit(MineArgs a, const int *lev_begin, int maxlev, PatternTable t) {
+  const int c = lev_begin[1] + blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= lev_begin[maxlev + 1]) return;
   if (!(a.flags[c] & NODE_ACC)) return;
+  int lo = 1, hi = maxlev;  // largest level whose begin <= c
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (lev_begin[mid] <= c) lo = mid;
+    else hi = mid - 1;
+  }
   const uint32_t id = a.pos[c];
   t.start[id] = a.start[c];
-  t.len[id] = level;
+  t.len[id] = lo;
   t.freq[id] = a.freq[c];
   t.prefix[id] = a.prefix[c];
   t.tp[id] = a.tp[c];
@@ -594,9 +602,10 @@ hipError_t launch_mine_pos(const MineArgs &a, int level, int pbeg, int pend, con
   hipLaunchKernelGGL(mine_pos, dim3((pend - pbeg + 255) / 256), dim3(256), 0, st, a, level, pbeg, pend, rpos);
   return hipGetLastError();
 }
-hipError_t launch_mine_emit(const MineArgs &a, int level, int b, int e, const PatternTable &t, hipStream_t st) {
-  if (e <= b) return hipSuccess;
-  hipLaunchKernelGGL(mine_emit, dim3((e - b + 255) / 256), dim3(256), 0, st, a, level, b, e, t);
+hipError_t launch_mine_emit(const MineArgs &a, const int *lev_begin, int maxlev, int n, const PatternTable &t,
+                            hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mine_emit, dim3((n + 255) / 256), dim3(256), 0, st, a, lev_begin, maxlev, t);
   return hipGetLastError();
 }
 hipError_t launch_mine_succ(const MineArgs &a, const PatternTable &t, int P, hipStream_t st) {

@@ -62,7 +62,8 @@ size_t mine_scan_tmp_bytes(int n);
 hipError_t launch_mine_size(const MineArgs &a, int level, int b, int e, hipStream_t st);
 hipError_t launch_mine_root_size(const MineArgs &a, uint32_t *rsize, hipStream_t st);
 hipError_t launch_mine_pos(const MineArgs &a, int level, int pbeg, int pend, const uint32_t *rpos, hipStream_t st);
-hipError_t launch_mine_emit(const MineArgs &a, int level, int b, int e, const PatternTable &t, hipStream_t st);
+hipError_t launch_mine_emit(const MineArgs &a, const int *lev_begin, int maxlev, int n, const PatternTable &t,
+                            hipStream_t st);
 hipError_t launch_mine_succ(const MineArgs &a, const PatternTable &t, int P, hipStream_t st);
 
 }  // namespace hmc
