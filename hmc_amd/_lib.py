@@ -62,6 +62,7 @@ _SIGS = [
     ("hmc_get_stamps", _i, [_vp, _P(C.c_uint64)]),
     ("hmc_set_estep_mode", _i, [_vp, _i]),
     ("hmc_last_estep_split", _i, [_vp, _P(_d), _P(_d), _P(_d), _P(_i)]),
+    ("hmc_last_estep_passes", _i, [_vp, _P(_i), _P(_i)]),
     ("hmc_get_samples", _i, [_vp, _P(C.c_int32), _P(_d), _P(_d)]),
     ("hmc_get_resolutions", _i, [_vp, _P(C.c_int32)]),
     ("hmc_clear_samples", _i, [_vp]),
@@ -73,6 +74,10 @@ _SIGS = [
     ("hmc_parse_file", _i, [_cp, _cp, _cp, _P(_i), _P(_i), _P(C.c_int32), _cp]),
     ("hmc_load_file", _i, [_vp, _cp, _cp, _cp]),
     ("hmc_write_file", _i, [_vp, _cp, _cp, _cp]),
+    ("hmc_parse_files", _i, [_cp, _P(_cp), _i, _P(_i), _P(_i), _P(C.c_int32), _cp, _P(_i)]),
+    ("hmc_load_files", _i, [_vp, _cp, _P(_cp), _i]),
+    ("hmc_write_files", _i, [_vp, _cp, _P(_cp), _i]),
+    ("hmc_unphased_num", _i, [_vp, _P(_i)]),
     ("hmc_write_patterns", _i, [_vp, _cp]),
     ("hmc_write_phase", _i, [_vp, _cp]),
     ("hmc_set_tuning", _i, [_vp, _i, _u64, _i]),

@@ -107,6 +107,7 @@ struct Err {
 // ----------------------------------------------------------------- panel --
 struct Panel {
   int N = 0, L = 0, amax = 0;
+  int unphased = 0;  // GenoData::unphased_num (GenoData.h:37): HaploComp covers individuals [0, unphased)
   std::vector<int32_t> al;  // [N][2][L] symbols, -1 missing
   std::string types;
   std::vector<std::vector<std::pair<int32_t, double>>> sym;  // per locus (symbol, frequency), ascending
@@ -115,6 +116,7 @@ struct Panel {
   // GenoData::checkAlleleSymbol (GenoData.cpp:78-118): distinct non-missing
   // symbols sorted by value; frequency = count / non-missing count.
   bool build_tables(std::string &err) {
+    unphased = N;  // GenoData::setGenotypeNum (GenoData.cpp:46-57)
     sym.assign(L, {});
     idx.assign((size_t)N * 2 * L, MISSING);
     amax = 0;
@@ -156,8 +158,11 @@ struct Panel {
 };
 
 // HaploFile::readGenoData (HaploFile.cpp:54-118) with AlleleSequence::read
-// (Allele.cpp:55-153): ids on, `P` positions line optional, per-locus type.
-static bool read_phase(const char *path, Panel &pn, std::string &err) {
+// (Allele.cpp:55-153): ids on (the first token of the id line, :96-100),
+// `P` positions line optional (default k * 1000, GenoData.cpp:59-76), marker
+// names "M<k+1>", per-locus type.  ids / positions / names go to `meta` for
+// writeGenoData.
+static bool read_phase(const char *path, Panel &pn, FileData &meta, std::string &err) {
   FILE *fp = fopen(path, "r");
   if (!fp) { err = std::string("Can not open file ") + path + "!"; return false; }
   auto fail = [&](const char *m) { fclose(fp); err = m; return false; };
@@ -170,7 +175,24 @@ static bool read_phase(const char *path, Panel &pn, std::string &err) {
   const char *D = " \t\r\n";
   if (!fgets(line.data(), (int)line.size(), fp)) return fail("Truncated file!");
   char *s = line.data() + strspn(line.data(), D);
+  meta = FileData();
+  meta.N = n;
+  meta.L = l;
+  meta.pos.resize(l);
+  meta.names.resize(l);
+  for (int k = 0; k < l; ++k) {
+    meta.pos[k] = k * 1000;  // Constant::average_marker_distance (Constant.cpp:5)
+    meta.names[k] = "M" + std::to_string(k + 1);
+  }
+  meta.ids.assign(n, "");
   if (s[0] == 'P') {
+    s += strcspn(s, D);
+    s += strspn(s, D);
+    for (int k = 0; k < l; ++k) {  // setAllelePosition(i, atoi(s)) (HaploFile.cpp:80-84)
+      meta.pos[k] = atoi(s);
+      s += strcspn(s, D);
+      s += strspn(s, D);
+    }
     if (!fgets(line.data(), (int)line.size(), fp)) return fail("Truncated file!");
     s = line.data() + strspn(line.data(), D);
   }
@@ -182,6 +204,10 @@ static bool read_phase(const char *path, Panel &pn, std::string &err) {
   }
   for (int i = 0; i < n; ++i) {
     if (!fgets(line.data(), (int)line.size(), fp)) return fail("Truncated file!");  // id line
+    {
+      const char *t = line.data() + strspn(line.data(), D);
+      meta.ids[i] = std::string(t, strcspn(t, D));  // sscanf(line, "%s", buf)
+    }
     for (int h = 0; h < 2; ++h) {
       if (!fgets(line.data(), (int)line.size(), fp)) return fail("Truncated file!");
       char *b = line.data();
@@ -289,8 +315,11 @@ struct Ctx {
   DevBuf<unsigned long long> d_stamps;
   std::vector<double> h_total;
   std::vector<int32_t> h_ncand, h_status, h_sbase;
-  std::vector<int32_t> h_cost, h_order;  // E-step scheduling: per-individual cost, block-visit order
-  DevBuf<int32_t> d_cost, d_order;
+  std::vector<int32_t> h_cost;  // E-step scheduling: per-individual cost (heaviest first)
+  DevBuf<int32_t> d_cost, d_order, d_order2, d_rowmap;
+  DevBuf<double> d_wslot;                               // sample weights in slot layout
+  DevBuf<unsigned long long> d_tbase, d_rbase, d_rneed, d_tneed;  // per-individual store regions / needs
+  std::vector<int32_t> h_rowmap;                        // dense sample h -> slot row
   std::vector<unsigned long long> h_re;
   bool have_estep = false;
   std::vector<uint8_t> best_res;  // [n][2][L] accepted resolutions (allele index)
@@ -654,6 +683,8 @@ struct Ctx {
       if ((e = hipMemcpyAsync(h_totals.p, d_totals.p, 16, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
         return hipfail(e, "mine");
       next_total = tot[0];  // list slots the next level's children need
+      if (tot[1] > (unsigned long long)INT32_MAX - (unsigned long long)ce)
+        return fail(HMC_EUNSUPPORTED, "candidate tree exceeds 2^31 nodes at length %d", level + 1);
       const int nnext = (int)tot[1];
       cur = nxt;
       if (nnext == 0) break;
@@ -686,7 +717,7 @@ struct Ctx {
       rpos[s] = (uint32_t)acc;
       acc += rsize[s];
     }
-    if (acc >= 0xFFFFFFFFull) return fail(HMC_EUNSUPPORTED, "too many patterns (%llu)", (unsigned long long)acc);
+    if (acc > (uint64_t)INT32_MAX) return fail(HMC_EUNSUPPORTED, "too many patterns (%llu)", (unsigned long long)acc);
     P = (int)acc;
     if ((e = hipMemcpyAsync(d_rpos.p, rpos.data(), (size_t)L * 4, hipMemcpyHostToDevice, st)))
       return hipfail(e, "mine");
@@ -1012,6 +1043,19 @@ struct Ctx {
   }
 
   // ---------------------------------------------------------------- E-step --
+  // HaploModel::resolveAll (HaploModel.cpp:79-115) over this rank's shard.
+  //
+  // Store sizing.  Each individual keeps its structure records (split E-step)
+  // and its k-best trace until its traceback; at the first E-step of a large
+  // panel they exceed HBM (cfg 3: ~10^11 links), so individuals pass in groups.
+  // The structure pass reports every individual's exact record and trace
+  // words; an individual whose records do not fit the store keeps walking its
+  // loci without writing (status EST_OVERFLOW_REC), so one pass learns every
+  // size.  Groups are then cut from the heaviest-first order by prefix sums,
+  // each individual gets its own region of both stores, and no pass is re-run.
+  // Sample rows go to fixed slots (2*S per individual) and are gathered into
+  // the reference's sample order (individuals in order, HaploModel.cpp:105-106)
+  // by the transpose that builds the locus-major samples.
   int estep(double *ll_out, int *H_out, uint64_t *re_out) {
     if (!have_model) return fail(HMC_EARG, "no pattern model");
     if (head_len > 1) {
@@ -1023,186 +1067,83 @@ struct Ctx {
     const int L = pan.L, S = this->S(), n = nloc();
     if (S > S_MAX) return fail(HMC_EUNSUPPORTED, "sample_size > %d", S_MAX);
     hipError_t e;
-    int dev_cu = 256;
-    hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, device);
-    int G = waves > 0 ? waves : dev_cu * 8;
-    G = std::max(1, std::min(G, n));
     if ((e = d_total.ensure(n)) || (e = d_ncand.ensure(n)) || (e = d_status.ensure(n)) || (e = d_re.ensure(n)) ||
         (e = d_sbase.ensure(n)) || (e = d_prior.ensure((size_t)n * S_MAX)) || (e = d_post.ensure((size_t)n * S_MAX)) ||
         (e = d_weight.ensure((size_t)n * S_MAX)) || (e = d_cstate.ensure((size_t)n * S_MAX)) ||
         (e = d_cidx.ensure((size_t)n * S_MAX)) || (e = d_rows.ensure((size_t)2 * S * n * L)) ||
-        (e = d_w.ensure((size_t)2 * S * n)) || (e = d_trace_cursor.ensure(1)) || (e = d_maxst.ensure(1)) ||
-        (e = d_fmax.ensure(n)))
+        (e = d_wslot.ensure((size_t)2 * S * n)) || (e = d_trace_cursor.ensure(1)) || (e = d_maxst.ensure(1)) ||
+        (e = d_fmax.ensure(n)) || (e = d_loc_off.ensure((size_t)n * (L + 1))) || (e = d_order.ensure(n)) ||
+        (e = d_order2.ensure(n)) || (e = d_cost.ensure(n)) || (e = d_tbase.ensure(n)) || (e = d_rbase.ensure(n)) ||
+        (e = d_rneed.ensure(n)) || (e = d_tneed.ensure(n)))
       return hipfail(e, "estep alloc");
-    // trace store: start from an estimate (96 states of 1+S words per
-    // individual-locus), grow up to the budget on overflow, then split batches
+    // store budgets: trace store and record store grow (never shrink) up to these
     size_t freeb = 0, totb = 0;
     hipMemGetInfo(&freeb, &totb);
-    // The trace store and the record store each grow up to this budget; past it
-    // the batch of individuals is halved.  At most 24 GiB each: first-touch
-    // mapping of huge allocations costs ~1 s per 10-20 GB with the system ROCm
-    // runtime, far more than the few extra launches of smaller batches.
-    const uint64_t cap_bytes = std::max<uint64_t>(
-        trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)((freeb + d_trace.n * 4) * 0.35), 24ull << 30),
-        1ull << 20);
-    const uint64_t want = std::min<uint64_t>(cap_bytes, std::max<uint64_t>((uint64_t)n * L * (1 + S) * 4 * 96, 64ull << 20));
-    if (d_trace.n * 4 < want) {
-      d_trace.release();
-      if ((e = d_trace.ensure(want / 4))) return hipfail(e, "trace alloc");
-    }
+    const double avail = (double)freeb + (double)d_trace.n * 4 + (double)d_rec.n * 4;
+    trace_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.45), 96ull << 30),
+                                      1ull << 20) / 4;
+    rec_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.25), 48ull << 30),
+                                    1ull << 20) / 4;
     h_total.assign(n, 0.0);
     h_ncand.assign(n, 0);
     h_status.assign(n, 0);
-    h_sbase.assign(n, 0);
     h_re.assign(n, 0);
-    hipMemsetAsync(d_maxst.p, 0, 4, st);
+    h_sbase.assign(n, 0);
+    for (int i = 0; i < n; ++i) h_sbase[i] = 2 * S * i;  // sample slots of individual i
+    if ((e = hipMemcpyAsync(d_sbase.p, h_sbase.data(), (size_t)n * 4, hipMemcpyHostToDevice, st)) ||
+        (e = hipMemsetAsync(d_maxst.p, 0, 4, st)) || (e = hipMemsetAsync(d_ncand.p, 0, (size_t)n * 4, st)))
+      return hipfail(e, "estep");
     if ((e = d_stamps.ensure(20)) || (e = hipMemsetAsync(d_stamps.p, 0, 20 * 8, st))) return hipfail(e, "stamps");
-    int Hacc = 0;
-    int b = 0, batch = n;
+    // heaviest individuals first (cost of the previous E-step; before the
+    // first one, the number of heterozygous or missing loci)
+    if ((int)h_cost.size() != n) {
+      h_cost.assign(n, 0);
+      for (int i = 0; i < n; ++i)
+        for (int k = 0; k < L; ++k) {
+          const uint8_t x = pan.idx[((size_t)(i0 + i) * 2) * L + k], y = pan.idx[((size_t)(i0 + i) * 2 + 1) * L + k];
+          h_cost[i] += (x != y || x == MISSING) ? 1 : 0;
+        }
+    }
+    std::vector<int32_t> order(n);
+    for (int q = 0; q < n; ++q) order[q] = q;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return h_cost[x] > h_cost[y]; });
+    if ((e = hipMemcpyAsync(d_cost.p, h_cost.data(), (size_t)n * 4, hipMemcpyHostToDevice, st)))
+      return hipfail(e, "estep");
     ms_fwd = ms_tb = 0;
     ms_s1 = ms_s2 = ms_fb = 0;
     n_fallback = 0;
-    while (b < n) {
-      const int bn = std::min(batch, n - b);
-      const int hcap = next_pow2(2 * fcap);
-      const size_t per = estep_scratch_bytes(fcap, hcap, S, estep_nw);
-      const int grid = std::min(G, bn);
-      if (estep_mode == ESTEP_FUSED && (e = d_scratch.ensure(per * grid))) {
-        if (e == hipErrorOutOfMemory && fcap > 256) { fcap /= 2; continue; }
-        return hipfail(e, "estep scratch");
-      }
-      if ((e = d_loc_off.ensure((size_t)bn * (L + 1)))) return hipfail(e, "estep loc_off");
-      if ((e = hipMemsetAsync(d_trace_cursor.p, 0, 8, st))) return hipfail(e, "estep");
-      EstepArgs a;
-      a.pan = dev_panel();
-      a.mod = dev_model();
-      a.S = S;
-      a.indiv_begin = i0 + b;
-      a.indiv_end = i0 + b + bn;
-      // heaviest individuals first (cost of the previous E-step; before the
-      // first one, the number of heterozygous or missing loci)
-      if ((int)h_cost.size() != n) {
-        h_cost.assign(n, 0);
-        for (int i = 0; i < n; ++i)
-          for (int k = 0; k < L; ++k) {
-            const uint8_t x = pan.idx[((size_t)(i0 + i) * 2) * L + k], y = pan.idx[((size_t)(i0 + i) * 2 + 1) * L + k];
-            h_cost[i] += (x != y || x == MISSING) ? 1 : 0;
-          }
-      }
-      h_order.resize(bn);
-      for (int q = 0; q < bn; ++q) h_order[q] = q;
-      std::stable_sort(h_order.begin(), h_order.end(),
-                       [&](int x, int y) { return h_cost[b + x] > h_cost[b + y]; });
-      if ((e = d_order.ensure(bn)) || (e = d_cost.ensure(n)) ||
-          (e = hipMemcpyAsync(d_order.p, h_order.data(), (size_t)bn * 4, hipMemcpyHostToDevice, st)))
-        return hipfail(e, "estep order");
-      a.order = d_order.p;
-      a.cost = d_cost.p + b;
-      a.scratch = d_scratch.p;
-      a.scratch_stride = per;
-      a.fcap = fcap;
-      a.hcap = hcap;
-      lds_tier(S, a.lds_fc, a.lds_hc);
-      a.trace = d_trace.p;
-      a.trace_cap = d_trace.n;
-      a.trace_cursor = d_trace_cursor.p;
-      a.loc_off = d_loc_off.p;
-      a.total = d_total.p + b;
-      a.ncand = d_ncand.p + b;
-      a.status = d_status.p + b;
-      a.cand_state = d_cstate.p + (size_t)b * S_MAX;
-      a.cand_idx = d_cidx.p + (size_t)b * S_MAX;
-      a.prior = d_prior.p + (size_t)b * S_MAX;
-      a.posterior = d_post.p + (size_t)b * S_MAX;
-      a.weight = d_weight.p + (size_t)b * S_MAX;
-      a.re_count = d_re.p + b;
-      a.max_states = d_maxst.p;
-      a.fmax = d_fmax.p + b;
-      a.stamps = d_stamps.p;
-      a.diag_indiv = -1;
-      a.n_order = bn;
-      if (const char *di = getenv("HMC_DIAG_INDIV")) a.diag_indiv = atoi(di) - b;
-      if (estep_mode == ESTEP_SPLIT) {
-        const int rc = run_split(a, b, bn, G, cap_bytes, batch);
-        if (rc < 0) return rc;
-        if (rc == 1) continue;
-      } else {
-      hipEventRecord(ev[0], st);
-      if ((e = launch_estep(a, grid, estep_nw, st))) return hipfail(e, "estep_forward launch");
-      hipEventRecord(ev[1], st);
-      if ((e = hipMemcpyAsync(h_status.data() + b, d_status.p + b, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
-          (e = hipMemcpyAsync(h_ncand.data() + b, d_ncand.p + b, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
-          (e = hipStreamSynchronize(st)))
-        return hipfail(e, "estep_forward");
-      float ms = 0;
-      hipEventElapsedTime(&ms, ev[0], ev[1]);
-      ms_fwd += ms;
-      bool ovf_trace = false, ovf_front = false;
-      for (int i = b; i < b + bn; ++i) {
-        if (h_status[i] == EST_OVERFLOW_TRACE) ovf_trace = true;
-        if (h_status[i] == EST_OVERFLOW_FRONTIER) ovf_front = true;
-        if (h_status[i] == EST_NO_HEAD_PATTERN) return fail(HMC_ENOPATTERN, "Can not find matching pattern!");
-      }
-      if (ovf_front) {
-        if (fcap >= 65535) return fail(HMC_EUNSUPPORTED, "frontier exceeds 65535 states");
-        fcap = std::min(65535, fcap * 2);
-        continue;
-      }
-      if (ovf_trace) {
-        if (d_trace.n * 4 < cap_bytes) {  // grow the store before splitting the batch
-          const uint64_t nb = std::min<uint64_t>(cap_bytes, d_trace.n * 4 * 4);
-          d_trace.release();
-          if ((e = d_trace.ensure(nb / 4))) return hipfail(e, "trace alloc");
-          continue;
-        }
-        if (bn == 1) return fail(HMC_ENOMEM, "trace store too small for one individual");
-        batch = std::max(1, bn / 2);
-        continue;
-      }
-      }
-      // sample rows of this batch (HaploModel.cpp:105-106: candidates in order, h0 then h1)
-      for (int i = b; i < b + bn; ++i) {
-        h_sbase[i] = Hacc;
-        Hacc += 2 * h_ncand[i];
-      }
-      if ((e = hipMemcpyAsync(d_sbase.p + b, h_sbase.data() + b, (size_t)bn * 4, hipMemcpyHostToDevice, st)))
-        return hipfail(e, "estep");
-      TracebackArgs t;
-      t.L = L;
-      t.S = S;
-      t.head_len = head_len;
-      t.nbatch = bn;
-      t.indiv_begin = i0 + b;
-      t.mod = dev_model();
-      t.trace = d_trace.p;
-      t.loc_off = d_loc_off.p;
-      t.ncand = d_ncand.p + b;
-      t.cand_state = d_cstate.p + (size_t)b * S_MAX;
-      t.cand_idx = d_cidx.p + (size_t)b * S_MAX;
-      t.weight = d_weight.p + (size_t)b * S_MAX;
-      t.sample_base = d_sbase.p + b;
-      t.rows = d_rows.p;
-      t.w_out = d_w.p;
-      hipEventRecord(ev[2], st);
-      if ((e = launch_traceback(t, 0, st))) return hipfail(e, "traceback");
-      hipEventRecord(ev[3], st);
-      if ((e = hipStreamSynchronize(st))) return hipfail(e, "traceback");
-      float ms_t = 0;
-      hipEventElapsedTime(&ms_t, ev[2], ev[3]);
-      ms_tb += ms_t;
-      b += bn;
+    n_struct_passes = n_value_passes = 0;
+    int rc = 0;
+    while (true) {  // a frontier overflow (fcap grows) restarts the E-step
+      rc = estep_mode == ESTEP_SPLIT ? estep_split(order) : estep_fused(order);
+      if (rc != ESTEP_RESTART) break;
     }
+    if (rc) return rc;
     if (estep_mode == ESTEP_SPLIT) ms_fwd = ms_s1 + ms_s2 + ms_fb;
-    H = Hacc;
-    if ((e = d_samp_lm.ensure((size_t)std::max(H, 1) * L))) return hipfail(e, "samples");
-    if ((e = launch_transpose_u8(d_rows.p, d_samp_lm.p, H, L, H, 0, st))) return hipfail(e, "transpose");
-    if ((e = hipMemcpyAsync(h_total.data(), d_total.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
+    // samples in the reference's order: individuals in order, candidates in
+    // order, h0 then h1 (HaploModel.cpp:105-106)
+    std::vector<int32_t> rowmap;
+    rowmap.reserve((size_t)2 * S * n);
+    for (int i = 0; i < n; ++i)
+      for (int c = 0; c < 2 * h_ncand[i]; ++c) rowmap.push_back(h_sbase[i] + c);
+    H = (int)rowmap.size();
+    std::vector<double> wslot((size_t)2 * S * n), w(H);
+    if ((e = d_samp_lm.ensure((size_t)std::max(H, 1) * L)) || (e = d_rowmap.ensure(std::max(H, 1))) ||
+        (e = d_w.ensure(std::max(H, 1))))
+      return hipfail(e, "samples");
+    if ((H && (e = hipMemcpyAsync(d_rowmap.p, rowmap.data(), (size_t)H * 4, hipMemcpyHostToDevice, st))) ||
+        (e = launch_transpose_rows_u8(d_rows.p, d_rowmap.p, d_samp_lm.p, H, L, st)) ||
+        (e = hipMemcpyAsync(wslot.data(), d_wslot.p, wslot.size() * 8, hipMemcpyDeviceToHost, st)) ||
+        (e = hipMemcpyAsync(h_total.data(), d_total.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
         (e = hipMemcpyAsync(h_re.data(), d_re.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
-        (e = hipMemcpyAsync(h_cost.data(), d_cost.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)))
+        (e = hipMemcpyAsync(h_cost.data(), d_cost.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
+        (e = hipStreamSynchronize(st)))
       return hipfail(e, "estep");
-    std::vector<double> w(H);
-    if (H && (e = hipMemcpyAsync(w.data(), d_w.p, (size_t)H * 8, hipMemcpyDeviceToHost, st))) return hipfail(e, "estep");
-    if ((e = hipStreamSynchronize(st))) return hipfail(e, "estep");
+    for (int h = 0; h < H; ++h) w[h] = wslot[rowmap[h]];
+    if (H && ((e = hipMemcpyAsync(d_w.p, w.data(), (size_t)H * 8, hipMemcpyHostToDevice, st)) ||
+              (e = hipStreamSynchronize(st))))
+      return hipfail(e, "estep");
+    h_rowmap.swap(rowmap);
     // ll += log(genotype probability) in individual order (HaploModel.cpp:110)
     double ll = 0.0;
     for (int i = 0; i < n; ++i) ll += log(h_total[i]);
@@ -1210,7 +1151,7 @@ struct Ctx {
     double tw = 0.0;
     for (int h = 0; h < H; ++h) tw += w[h];
     double red[2] = {ll, tw};
-    int rc = allreduce_host(red, 2);
+    rc = allreduce_host(red, 2);
     if (rc) return rc;
     ll = red[0];
     total_weight = red[1];
@@ -1224,183 +1165,361 @@ struct Ctx {
     return HMC_OK;
   }
 
-  // One batch [b, b+bn) through the split E-step.  Returns 0 when the batch
-  // is done, 1 when it must be re-run (a capacity grew or the batch was
-  // halved), or a negative HMC_E* code.
-  int run_split(EstepArgs &a, int b, int bn, int G, uint64_t cap_bytes, int &batch) {
+  static constexpr int ESTEP_RESTART = 1;
+  uint64_t trace_budget = 0, rec_budget = 0;  // words
+  int n_struct_passes = 0, n_value_passes = 0;
+
+  // Grow a store (contents dropped) to hold `words`, within `budget`.
+  int ensure_store(DevBuf<uint32_t> &b, uint64_t words, uint64_t budget, const char *what) {
+    if (b.n >= words && b.p) return HMC_OK;
+    if (words > budget) return fail(HMC_ENOMEM, "%s: one individual needs %llu words (budget %llu)", what,
+                                    (unsigned long long)words, (unsigned long long)budget);
+    b.release();  // 1.25x headroom: a store of tens of GB is mapped eagerly, re-allocations are slow
+    hipError_t e = b.ensure(std::min<uint64_t>(budget, words + words / 4));
+    if (e) return hipfail(e, what);
+    return HMC_OK;
+  }
+
+  EstepArgs estep_args(int S) {
+    EstepArgs a;
+    a.pan = dev_panel();
+    a.mod = dev_model();
+    a.S = S;
+    a.indiv_begin = i0;
+    a.indiv_end = i1;
+    a.scratch = d_scratch.p;
+    a.fcap = fcap;
+    a.hcap = next_pow2(2 * fcap);
+    a.scratch_stride = estep_scratch_bytes(fcap, a.hcap, S, estep_nw);
+    lds_tier(S, a.lds_fc, a.lds_hc);
+    a.trace = d_trace.p;
+    a.trace_cap = d_trace.n;
+    a.trace_cursor = d_trace_cursor.p;
+    a.trace_base = nullptr;
+    a.loc_off = d_loc_off.p;
+    a.total = d_total.p;
+    a.ncand = d_ncand.p;
+    a.status = d_status.p;
+    a.cand_state = d_cstate.p;
+    a.cand_idx = d_cidx.p;
+    a.prior = d_prior.p;
+    a.posterior = d_post.p;
+    a.weight = d_weight.p;
+    a.re_count = d_re.p;
+    a.max_states = d_maxst.p;
+    a.fmax = d_fmax.p;
+    a.order = nullptr;
+    a.n_order = 0;
+    a.cost = d_cost.p;
+    a.stamps = d_stamps.p;
+    a.diag_indiv = -1;
+    if (const char *di = getenv("HMC_DIAG_INDIV")) a.diag_indiv = atoi(di);
+    return a;
+  }
+
+  int upload_order(DevBuf<int32_t> &d, const int32_t *v, int k) {
     hipError_t e;
-    const int S = a.S, L = pan.L;
+    if (k > 0 && ((e = hipMemcpyAsync(d.p, v, (size_t)k * 4, hipMemcpyHostToDevice, st)) ||
+                  (e = hipStreamSynchronize(st))))
+      return hipfail(e, "estep order");
+    return HMC_OK;
+  }
+
+  // Traceback of the individuals in d_order2[0, k) into their sample slots.
+  int traceback_group(int k) {
+    TracebackArgs t;
+    t.L = pan.L;
+    t.S = S();
+    t.head_len = head_len;
+    t.nbatch = k;
+    t.order = d_order2.p;
+    t.indiv_begin = i0;
+    t.mod = dev_model();
+    t.trace = d_trace.p;
+    t.loc_off = d_loc_off.p;
+    t.ncand = d_ncand.p;
+    t.cand_state = d_cstate.p;
+    t.cand_idx = d_cidx.p;
+    t.weight = d_weight.p;
+    t.sample_base = d_sbase.p;
+    t.rows = d_rows.p;
+    t.w_out = d_wslot.p;
+    hipError_t e;
+    hipEventRecord(ev[2], st);
+    if ((e = launch_traceback(t, 0, st))) return hipfail(e, "traceback");
+    hipEventRecord(ev[3], st);
+    if ((e = hipStreamSynchronize(st))) return hipfail(e, "traceback");
+    float ms = 0;
+    hipEventElapsedTime(&ms, ev[2], ev[3]);
+    ms_tb += ms;
+    return HMC_OK;
+  }
+
+  int read_status(const std::vector<int32_t> &ids, int k, bool ncand) {
+    // per-individual status (and candidate counts) of ids[0, k): whole arrays, small
+    hipError_t e;
+    const int n = nloc();
+    if ((e = hipMemcpyAsync(h_status.data(), d_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
+        (ncand && (e = hipMemcpyAsync(h_ncand.data(), d_ncand.p, (size_t)n * 4, hipMemcpyDeviceToHost, st))) ||
+        (e = hipStreamSynchronize(st)))
+      return hipfail(e, "estep status");
+    (void)ids;
+    (void)k;
+    return HMC_OK;
+  }
+
+  // Fused single-pass E-step (estep.hip) over `pending`: trace sizes are not
+  // known in advance, so groups are tried and halved on a trace overflow.
+  int estep_fused(const std::vector<int32_t> &order) {
+    const int S = this->S(), n = nloc();
     int dev_cu = 256;
     hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, device);
-    float ms = 0;
-    // ---- pass 1: structure records ------------------------------------------
-    const int hcap1 = next_pow2(2 * fcap), ccap1 = 8 * fcap;
-    const int bpc1 = std::max(lds_waves_per_cu, bn > 4 * dev_cu ? 8 : 4);
-    const int grid1 = std::max(1, std::min(bn, dev_cu * bpc1));
-    const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1);
-    if ((e = d_scr1.ensure(per1 * grid1))) return hipfail(e, "estep pass-1 scratch");
-    const uint64_t rec_want =
-        std::min<uint64_t>(cap_bytes, std::max<uint64_t>((uint64_t)bn * L * 640 * 4, 64ull << 20));
-    if (d_rec.n * 4 < rec_want) {
-      d_rec.release();
-      if ((e = d_rec.ensure(rec_want / 4))) return hipfail(e, "record alloc");
+    const int G = std::max(1, std::min(waves > 0 ? waves : dev_cu * 8, n));
+    hipError_t e;
+    size_t pos = 0;
+    int batch = n;
+    if (d_trace.n == 0) {
+      int rc = ensure_store(d_trace, std::min<uint64_t>(trace_budget, std::max<uint64_t>((uint64_t)n * pan.L * (1 + S) * 96, 16ull << 20)),
+                            trace_budget, "trace store");
+      if (rc) return rc;
     }
-    if ((e = d_rec_off.ensure((size_t)bn * (L + 1))) || (e = d_rec_cursor.ensure(1)) ||
-        (e = hipMemsetAsync(d_rec_cursor.p, 0, 8, st)))
-      return hipfail(e, "record alloc");
-    StructArgs s1;
-    s1.pan = a.pan;
-    s1.mod = a.mod;
-    s1.S = S;
-    s1.indiv_begin = a.indiv_begin;
-    s1.order = a.order;
-    s1.n_order = bn;
-    s1.scratch = d_scr1.p;
-    s1.scratch_stride = per1;
-    s1.fcap = fcap;
-    s1.hcap = hcap1;
-    s1.ccap = ccap1;
-    s1_tier(160 * 1024 / bpc1 - 256, s1.lds_fc, s1.lds_hc, s1.lds_cc);
-    s1.rec = d_rec.p;
-    s1.rec_cap = d_rec.n;
-    s1.rec_cursor = d_rec_cursor.p;
-    s1.rec_off = d_rec_off.p;
-    s1.status = a.status;
-    s1.re_count = a.re_count;
-    s1.fmax = a.fmax;
-    s1.max_states = a.max_states;
-    hipEventRecord(ev[0], st);
-    if ((e = launch_estep_structure(s1, grid1, st))) return hipfail(e, "estep_structure launch");
-    hipEventRecord(ev[1], st);
-    if ((e = hipMemcpyAsync(h_status.data() + b, a.status, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
-        (e = hipStreamSynchronize(st)))
-      return hipfail(e, "estep_structure");
-    hipEventElapsedTime(&ms, ev[0], ev[1]);
-    ms_s1 += ms;
-    bool ovf_front = false, ovf_rec = false;
-    for (int i = b; i < b + bn; ++i) {
-      if (h_status[i] == EST_NO_HEAD_PATTERN) return fail(HMC_ENOPATTERN, "Can not find matching pattern!");
-      if (h_status[i] == EST_OVERFLOW_FRONTIER) ovf_front = true;
-      if (h_status[i] == EST_OVERFLOW_REC) ovf_rec = true;
-    }
-    if (ovf_front) {
-      if (fcap >= 65535) return fail(HMC_EUNSUPPORTED, "frontier exceeds 65535 states");
-      fcap = std::min(65535, fcap * 2);
-      return 1;
-    }
-    if (ovf_rec) {
-      if (d_rec.n * 4 < cap_bytes) {
-        const uint64_t nb = std::min<uint64_t>(cap_bytes, d_rec.n * 4 * 4);
-        d_rec.release();
-        if ((e = d_rec.ensure(nb / 4))) return hipfail(e, "record alloc");
-        return 1;
-      }
-      if (bn == 1) return fail(HMC_ENOMEM, "record store too small for one individual");
-      batch = std::max(1, bn / 2);
-      return 1;
-    }
-    h_status1.assign(h_status.begin() + b, h_status.begin() + b + bn);
-    // ---- pass 2: values --------------------------------------------------------
-    const int grid2 = std::max(1, std::min(G, bn));
-    const size_t per2 = estep_s2_scratch_bytes(fcap, S);
-    if ((e = d_scr2.ensure(per2 * grid2))) return hipfail(e, "estep pass-2 scratch");
-    ValueArgs v;
-    v.S = S;
-    v.L = L;
-    v.head_len = head_len;
-    v.order = a.order;
-    v.n_order = bn;
-    v.rec = d_rec.p;
-    v.rec_off = d_rec_off.p;
-    v.scratch = d_scr2.p;
-    v.scratch_stride = per2;
-    v.fcap = fcap;
-    v.lds_fc = s2_tier(S);
-    v.trace = d_trace.p;
-    v.trace_cap = d_trace.n;
-    v.trace_cursor = d_trace_cursor.p;
-    v.loc_off = d_loc_off.p;
-    v.status = a.status;
-    v.total = a.total;
-    v.ncand = a.ncand;
-    v.cand_state = a.cand_state;
-    v.cand_idx = a.cand_idx;
-    v.prior = a.prior;
-    v.posterior = a.posterior;
-    v.weight = a.weight;
-    v.cost = a.cost;
-    v.stamps = d_stamps.p;
-    hipEventRecord(ev[0], st);
-    if ((e = launch_estep_values(v, grid2, estep_nw, st))) return hipfail(e, "estep_values launch");
-    hipEventRecord(ev[1], st);
-    if ((e = hipMemcpyAsync(h_status.data() + b, a.status, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
-        (e = hipMemcpyAsync(h_ncand.data() + b, a.ncand, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
-        (e = hipStreamSynchronize(st)))
-      return hipfail(e, "estep_values");
-    hipEventElapsedTime(&ms, ev[0], ev[1]);
-    ms_s2 += ms;
-    h_redo.clear();
-    bool ovf_trace = false;
-    for (int i = b; i < b + bn; ++i) {
-      if (h_status[i] == EST_OVERFLOW_TRACE) ovf_trace = true;
-      if (h_status[i] == EST_NEEDS_EXACT) h_redo.push_back(i - b);
-    }
-    if (ovf_trace) {
-      if (d_trace.n * 4 < cap_bytes) {  // grow the store before splitting the batch
-        const uint64_t nb = std::min<uint64_t>(cap_bytes, d_trace.n * 4 * 4);
-        d_trace.release();
-        if ((e = d_trace.ensure(nb / 4))) return hipfail(e, "trace alloc");
-        return 1;
-      }
-      if (bn == 1) return fail(HMC_ENOMEM, "trace store too small for one individual");
-      batch = std::max(1, bn / 2);
-      return 1;
-    }
-    // ---- exact fallback: individuals whose forward likelihood underflowed ----
-    n_fallback += (int)h_redo.size();
-    if (!h_redo.empty()) {
-      const int nr = (int)h_redo.size();
-      const int grid = std::min(G, nr);
-      const size_t per = estep_scratch_bytes(fcap, a.hcap, S, estep_nw);
-      if ((e = d_scratch.ensure(per * grid)) || (e = d_redo.ensure(nr)) ||
-          (e = hipMemcpyAsync(d_redo.p, h_redo.data(), (size_t)nr * 4, hipMemcpyHostToDevice, st)))
-        return hipfail(e, "estep fallback");
-      EstepArgs f = a;
-      f.scratch = d_scratch.p;
-      f.order = d_redo.p;
-      f.n_order = nr;
-      f.trace_cap = d_trace.n;
-      f.trace = d_trace.p;
+    while (pos < order.size()) {
+      const int k = (int)std::min<size_t>(batch, order.size() - pos);
+      EstepArgs a = estep_args(S);
+      const int grid = std::min(G, k);
+      if ((e = d_scratch.ensure(a.scratch_stride * grid))) return hipfail(e, "estep scratch");
+      a.scratch = d_scratch.p;
+      int rc = upload_order(d_order2, order.data() + pos, k);
+      if (rc) return rc;
+      a.order = d_order2.p;
+      a.n_order = k;
+      if ((e = hipMemsetAsync(d_trace_cursor.p, 0, 8, st))) return hipfail(e, "estep");
       hipEventRecord(ev[0], st);
-      if ((e = launch_estep(f, grid, estep_nw, st))) return hipfail(e, "estep_forward launch");
+      if ((e = launch_estep(a, grid, estep_nw, st))) return hipfail(e, "estep_forward launch");
       hipEventRecord(ev[1], st);
-      if ((e = hipMemcpyAsync(h_status.data() + b, a.status, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
-          (e = hipMemcpyAsync(h_ncand.data() + b, a.ncand, (size_t)bn * 4, hipMemcpyDeviceToHost, st)) ||
-          (e = hipStreamSynchronize(st)))
-        return hipfail(e, "estep_forward");
+      if ((rc = read_status(order, k, true))) return rc;
+      float ms = 0;
       hipEventElapsedTime(&ms, ev[0], ev[1]);
-      ms_fb += ms;
-      for (int r : h_redo) {
-        const int s = h_status[b + r];
+      ms_fwd += ms;
+      bool ovf_trace = false;
+      for (int q = 0; q < k; ++q) {
+        const int s = h_status[order[pos + q]];
+        if (s == EST_NO_HEAD_PATTERN) return fail(HMC_ENOPATTERN, "Can not find matching pattern!");
         if (s == EST_OVERFLOW_FRONTIER) {
           if (fcap >= 65535) return fail(HMC_EUNSUPPORTED, "frontier exceeds 65535 states");
           fcap = std::min(65535, fcap * 2);
-          return 1;
+          return ESTEP_RESTART;
         }
-        if (s == EST_OVERFLOW_TRACE) {
-          if (d_trace.n * 4 >= cap_bytes) {
-            if (bn == 1) return fail(HMC_ENOMEM, "trace store too small for one individual");
-            batch = std::max(1, bn / 2);
-            return 1;
-          }
-          const uint64_t nb = std::min<uint64_t>(cap_bytes, d_trace.n * 4 * 4);
-          d_trace.release();
-          if ((e = d_trace.ensure(nb / 4))) return hipfail(e, "trace alloc");
-          return 1;
+        if (s == EST_OVERFLOW_TRACE) ovf_trace = true;
+      }
+      if (ovf_trace) {
+        if (d_trace.n < trace_budget) {  // grow the store before splitting the group
+          if ((rc = ensure_store(d_trace, std::min<uint64_t>(trace_budget, d_trace.n * 4), trace_budget, "trace store")))
+            return rc;
+          continue;
+        }
+        if (k == 1) return fail(HMC_ENOMEM, "trace store too small for one individual");
+        batch = std::max(1, k / 2);
+        continue;
+      }
+      if ((rc = traceback_group(k))) return rc;
+      pos += k;
+    }
+    return HMC_OK;
+  }
+
+  // Split E-step (estep_split.hip): structure pass, value pass, fused fallback
+  // for individuals whose forward likelihood underflows.
+  int estep_split(const std::vector<int32_t> &order) {
+    const int S = this->S(), n = nloc(), L = pan.L;
+    int dev_cu = 256;
+    hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, device);
+    const int G = std::max(1, std::min(waves > 0 ? waves : dev_cu * 8, n));
+    hipError_t e;
+    float ms = 0;
+    std::vector<int32_t> pending(order), sset, rest;
+    std::vector<unsigned long long> rneed(n, 0), tneed(n, 0), base(n, 0);
+    bool known = false;  // rneed / tneed hold the exact needs of `pending`
+    int rc;
+    while (!pending.empty()) {
+      // ---- pass 1: structure records --------------------------------------
+      int np = (int)pending.size();
+      if (known) {  // the prefix whose records and traces fit the budgets
+        uint64_t r = 0, t = 0;
+        int k = 0;
+        while (k < np && (k == 0 || (r + rneed[pending[k]] <= rec_budget && t + tneed[pending[k]] <= trace_budget))) {
+          base[pending[k]] = r;
+          r += rneed[pending[k]];
+          t += tneed[pending[k]];
+          ++k;
+        }
+        np = k;
+        if ((rc = ensure_store(d_rec, r, rec_budget, "record store"))) return rc;
+        std::vector<unsigned long long> rb(n, 0);
+        for (int q = 0; q < np; ++q) rb[pending[q]] = base[pending[q]];
+        if ((e = hipMemcpyAsync(d_rbase.p, rb.data(), (size_t)n * 8, hipMemcpyHostToDevice, st)))
+          return hipfail(e, "estep");
+      } else if (d_rec.n == 0) {
+        if ((rc = ensure_store(d_rec, std::min<uint64_t>(rec_budget, std::max<uint64_t>((uint64_t)n * L * 640, 16ull << 20)),
+                               rec_budget, "record store")))
+          return rc;
+      }
+      const int hcap1 = next_pow2(2 * fcap), ccap1 = 8 * fcap;
+      const int bpc1 = std::max(lds_waves_per_cu, np > 4 * dev_cu ? 8 : 4);
+      const int grid1 = std::max(1, std::min(np, dev_cu * bpc1));
+      const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1);
+      if ((e = d_scr1.ensure(per1 * grid1)) || (e = d_rec_off.ensure((size_t)n * (L + 1))) ||
+          (e = d_rec_cursor.ensure(1)) || (e = hipMemsetAsync(d_rec_cursor.p, 0, 8, st)))
+        return hipfail(e, "estep pass-1 alloc");
+      if ((rc = upload_order(d_order, pending.data(), np))) return rc;
+      StructArgs s1;
+      s1.pan = dev_panel();
+      s1.mod = dev_model();
+      s1.S = S;
+      s1.indiv_begin = i0;
+      s1.order = d_order.p;
+      s1.n_order = np;
+      s1.scratch = d_scr1.p;
+      s1.scratch_stride = per1;
+      s1.fcap = fcap;
+      s1.hcap = hcap1;
+      s1.ccap = ccap1;
+      s1_tier(160 * 1024 / bpc1 - 256, s1.lds_fc, s1.lds_hc, s1.lds_cc);
+      s1.rec = d_rec.p;
+      s1.rec_cap = d_rec.n;
+      s1.rec_cursor = d_rec_cursor.p;
+      s1.rec_base = known ? d_rbase.p : nullptr;
+      s1.rec_off = d_rec_off.p;
+      s1.rec_need = d_rneed.p;
+      s1.trace_need = d_tneed.p;
+      s1.status = d_status.p;
+      s1.re_count = d_re.p;
+      s1.fmax = d_fmax.p;
+      s1.max_states = d_maxst.p;
+      hipEventRecord(ev[0], st);
+      if ((e = launch_estep_structure(s1, grid1, st))) return hipfail(e, "estep_structure launch");
+      hipEventRecord(ev[1], st);
+      if ((e = hipMemcpyAsync(rneed.data(), d_rneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
+          (e = hipMemcpyAsync(tneed.data(), d_tneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)))
+        return hipfail(e, "estep_structure");
+      if ((rc = read_status(pending, np, false))) return rc;
+      hipEventElapsedTime(&ms, ev[0], ev[1]);
+      ms_s1 += ms;
+      ++n_struct_passes;
+      sset.clear();
+      rest.clear();
+      for (int q = 0; q < np; ++q) {
+        const int bi = pending[q], s = h_status[bi];
+        if (s == EST_NO_HEAD_PATTERN) return fail(HMC_ENOPATTERN, "Can not find matching pattern!");
+        if (s == EST_OVERFLOW_FRONTIER) {
+          if (fcap >= 65535) return fail(HMC_EUNSUPPORTED, "frontier exceeds 65535 states");
+          fcap = std::min(65535, fcap * 2);
+          return ESTEP_RESTART;
+        }
+        if (s == EST_OVERFLOW_REC) {
+          if (known) return fail(HMC_EHIP, "record store overflow with exact sizes");
+          rest.push_back(bi);
+        } else {
+          sset.push_back(bi);
         }
       }
+      for (int q = np; q < (int)pending.size(); ++q) rest.push_back(pending[q]);
+      known = true;  // every individual of `rest` now has its exact needs
+      // ---- pass 2: values, in groups whose traces fit the store -------------
+      size_t pos = 0;
+      while (pos < sset.size()) {
+        uint64_t t = 0;
+        size_t k = 0;
+        while (pos + k < sset.size() && (k == 0 || t + tneed[sset[pos + k]] <= trace_budget)) {
+          base[sset[pos + k]] = t;
+          t += tneed[sset[pos + k]];
+          ++k;
+        }
+        if ((rc = ensure_store(d_trace, std::max<uint64_t>(t, 1), trace_budget, "trace store"))) return rc;
+        std::vector<unsigned long long> tb(n, 0);
+        for (size_t q = 0; q < k; ++q) tb[sset[pos + q]] = base[sset[pos + q]];
+        if ((e = hipMemcpyAsync(d_tbase.p, tb.data(), (size_t)n * 8, hipMemcpyHostToDevice, st)))
+          return hipfail(e, "estep");
+        if ((rc = upload_order(d_order2, sset.data() + pos, (int)k))) return rc;
+        const int grid2 = std::max(1, std::min<int>(G, (int)k));
+        const size_t per2 = estep_s2_scratch_bytes(fcap, S);
+        if ((e = d_scr2.ensure(per2 * grid2))) return hipfail(e, "estep pass-2 scratch");
+        ValueArgs v;
+        v.S = S;
+        v.L = L;
+        v.head_len = head_len;
+        v.order = d_order2.p;
+        v.n_order = (int)k;
+        v.rec = d_rec.p;
+        v.rec_off = d_rec_off.p;
+        v.scratch = d_scr2.p;
+        v.scratch_stride = per2;
+        v.fcap = fcap;
+        v.lds_fc = s2_tier(S);
+        v.trace = d_trace.p;
+        v.trace_cap = d_trace.n;
+        v.trace_cursor = d_trace_cursor.p;
+        v.trace_base = d_tbase.p;
+        v.loc_off = d_loc_off.p;
+        v.status = d_status.p;
+        v.total = d_total.p;
+        v.ncand = d_ncand.p;
+        v.cand_state = d_cstate.p;
+        v.cand_idx = d_cidx.p;
+        v.prior = d_prior.p;
+        v.posterior = d_post.p;
+        v.weight = d_weight.p;
+        v.cost = d_cost.p;
+        v.stamps = d_stamps.p;
+        hipEventRecord(ev[0], st);
+        if ((e = launch_estep_values(v, grid2, estep_nw, st))) return hipfail(e, "estep_values launch");
+        hipEventRecord(ev[1], st);
+        if ((rc = read_status(sset, (int)k, true))) return rc;
+        hipEventElapsedTime(&ms, ev[0], ev[1]);
+        ms_s2 += ms;
+        ++n_value_passes;
+        h_redo.clear();
+        for (size_t q = 0; q < k; ++q) {
+          const int bi = sset[pos + q];
+          if (h_status[bi] == EST_OVERFLOW_TRACE) return fail(HMC_EHIP, "trace store overflow with exact sizes");
+          if (h_status[bi] == EST_NEEDS_EXACT) h_redo.push_back(bi);
+        }
+        // ---- exact fallback: individuals whose forward likelihood underflowed.
+        // The fused kernel's frontiers are subsets of pass 1's (it skips pairs
+        // with fwd <= 0, HaploBuilder.cpp:237), so it fits the same region.
+        n_fallback += (int)h_redo.size();
+        if (!h_redo.empty()) {
+          const int nr = (int)h_redo.size();
+          EstepArgs f = estep_args(S);
+          const int grid = std::min(G, nr);
+          if ((e = d_scratch.ensure(f.scratch_stride * grid)) || (e = d_redo.ensure(nr))) return hipfail(e, "estep fallback");
+          if ((rc = upload_order(d_redo, h_redo.data(), nr))) return rc;
+          f.scratch = d_scratch.p;
+          f.order = d_redo.p;
+          f.n_order = nr;
+          f.trace_base = d_tbase.p;
+          hipEventRecord(ev[0], st);
+          if ((e = launch_estep(f, grid, estep_nw, st))) return hipfail(e, "estep_forward launch");
+          hipEventRecord(ev[1], st);
+          if ((rc = read_status(sset, (int)k, true))) return rc;
+          hipEventElapsedTime(&ms, ev[0], ev[1]);
+          ms_fb += ms;
+          for (int r : h_redo) {
+            const int s = h_status[r];
+            if (s == EST_OVERFLOW_FRONTIER) {
+              if (fcap >= 65535) return fail(HMC_EUNSUPPORTED, "frontier exceeds 65535 states");
+              fcap = std::min(65535, fcap * 2);
+              return ESTEP_RESTART;
+            }
+            if (s == EST_OVERFLOW_TRACE) return fail(HMC_EHIP, "fallback trace exceeds its region");
+          }
+        }
+        if ((rc = traceback_group((int)k))) return rc;
+        pos += k;
+      }
+      pending.swap(rest);
     }
-    return 0;
+    return HMC_OK;
   }
 
   // LDS tiers of pass 1 (one wave per individual, `budget` bytes): states per
@@ -1502,6 +1621,7 @@ struct Ctx {
     auto am = [](uint8_t x, uint8_t y) { return x == MISSING || y == MISSING || x == y; };  // Allele::isMatch
     double cnt[6] = {0, 0, 0, 0, 0, 0};  // se_num, se_den, ihp_num, ihp_den, igp_num, igp_den
     for (int i = 0; i < n; ++i) {
+      if (i0 + i >= pan.unphased) break;  // m_genotype_num = unphased_num() (HaploComp.cpp:40)
       const uint8_t *r0 = pan.idx.data() + ((size_t)(i0 + i) * 2) * L, *r1 = r0 + L;
       const uint8_t *f0 = res.data() + ((size_t)i * 2) * L, *f1 = f0 + L;
       auto hasMissing = [&](int k) { return r0[k] == MISSING || r1[k] == MISSING; };
@@ -1749,6 +1869,13 @@ int hmc_last_estep_split(const hmc_ctx *h, double *structure_ms, double *values_
   return HMC_OK;
 }
 
+int hmc_last_estep_passes(const hmc_ctx *h, int *structure_passes, int *value_passes) {
+  if (!h) return HMC_EARG;
+  if (structure_passes) *structure_passes = h->c.n_struct_passes;
+  if (value_passes) *value_passes = h->c.n_value_passes;
+  return HMC_OK;
+}
+
 int hmc_set_estep_shape(hmc_ctx *h, int waves_per_individual, int individuals_per_cu) {
   if (!h) return HMC_EARG;
   if (waves_per_individual < 0 || waves_per_individual > 4 || individuals_per_cu < 0) return HMC_EARG;
@@ -1760,9 +1887,11 @@ int hmc_set_estep_shape(hmc_ctx *h, int waves_per_individual, int individuals_pe
 int hmc_load_phase(hmc_ctx *h, const char *path) {
   if (!h || !path) return HMC_EARG;
   hmc::Panel p;
+  hmc::FileData meta;
   std::string err;
-  if (!hmc::read_phase(path, p, err)) return h->c.fail(HMC_EIO, "%s", err.c_str());
+  if (!hmc::read_phase(path, p, meta, err)) return h->c.fail(HMC_EIO, "%s", err.c_str());
   h->c.pan = std::move(p);
+  h->c.file_meta = std::move(meta);
   return h->c.upload_panel();
 }
 
@@ -1777,17 +1906,38 @@ int hmc_load_genotypes(hmc_ctx *h, int N, int L, const int32_t *alleles, const c
   std::string err;
   if (!p.build_tables(err)) return h->c.fail(HMC_EUNSUPPORTED, "%s", err.c_str());
   h->c.pan = std::move(p);
+  h->c.file_meta = hmc::FileData();  // no ids / positions: writers use the defaults
   return h->c.upload_panel();
 }
 
-int hmc_parse_file(const char *format, const char *path, const char *path2, int *N, int *L, int32_t *alleles,
-                   char *types) {
-  if (!format || !path) return HMC_EARG;
+static std::vector<std::string> path_list(const char *const *paths, int n) {
+  std::vector<std::string> v;
+  for (int i = 0; i < n; ++i) v.push_back(paths[i] ? paths[i] : "");
+  return v;
+}
+
+// Any format of HaploFile::getHaploFile (HaploFile.cpp:28-47) into FileData.
+static bool parse_any(const char *format, const std::vector<std::string> &paths, hmc::FileData &d, std::string &err) {
+  if (std::string(format) == "PHASE") {
+    if (paths.empty()) { err = "PHASE needs 1 file name"; return false; }
+    hmc::Panel p;
+    if (!hmc::read_phase(paths[0].c_str(), p, d, err)) return false;
+    d.al = std::move(p.al);
+    d.types = p.types;
+    return true;
+  }
+  return hmc::read_geno_file(format, paths, d, err);
+}
+
+int hmc_parse_files(const char *format, const char *const *paths, int n_paths, int *N, int *L, int32_t *alleles,
+                    char *types, int *unphased) {
+  if (!format || !paths || n_paths <= 0) return HMC_EARG;
   hmc::FileData d;
   std::string err;
-  if (!hmc::read_geno_file(format, path, path2, d, err)) return HMC_EIO;
+  if (!parse_any(format, path_list(paths, n_paths), d, err)) return HMC_EIO;
   if (N) *N = d.N;
   if (L) *L = d.L;
+  if (unphased) *unphased = d.unphased < 0 ? d.N : d.unphased;
   if (alleles) std::copy(d.al.begin(), d.al.end(), alleles);
   if (types) {
     std::copy(d.types.begin(), d.types.end(), types);
@@ -1796,24 +1946,43 @@ int hmc_parse_file(const char *format, const char *path, const char *path2, int 
   return HMC_OK;
 }
 
-int hmc_load_file(hmc_ctx *h, const char *format, const char *path, const char *path2) {
-  if (!h || !format || !path) return HMC_EARG;
-  if (std::string(format) == "PHASE") return hmc_load_phase(h, path);
+int hmc_parse_file(const char *format, const char *path, const char *path2, int *N, int *L, int32_t *alleles,
+                   char *types) {
+  if (!path) return HMC_EARG;
+  const char *ps[2] = {path, path2};
+  return hmc_parse_files(format, ps, path2 ? 2 : 1, N, L, alleles, types, nullptr);
+}
+
+int hmc_load_files(hmc_ctx *h, const char *format, const char *const *paths, int n_paths) {
+  if (!h || !format || !paths || n_paths <= 0) return HMC_EARG;
+  if (std::string(format) == "PHASE") return hmc_load_phase(h, paths[0]);
   hmc::FileData d;
   std::string err;
-  if (!hmc::read_geno_file(format, path, path2, d, err)) return h->c.fail(HMC_EIO, "%s", err.c_str());
+  if (!hmc::read_geno_file(format, path_list(paths, n_paths), d, err)) return h->c.fail(HMC_EIO, "%s", err.c_str());
   if (d.N <= 0 || d.L <= 0) return h->c.fail(HMC_EIO, "Invalid file type!");
   const int rc = hmc_load_genotypes(h, d.N, d.L, d.al.data(), d.types.c_str());
   if (rc) return rc;
+  if (d.unphased >= 0) h->c.pan.unphased = d.unphased;
   h->c.file_meta = std::move(d);
   h->c.file_meta.al.clear();
   return HMC_OK;
 }
 
-int hmc_write_file(hmc_ctx *h, const char *format, const char *path, const char *path2) {
-  if (!h || !format || !path || !h->c.have_best || h->c.world != 1) return HMC_EARG;
-  if (std::string(format) == "PHASE") return hmc_write_phase(h, path);
-  hmc::Ctx &c = h->c;
+int hmc_load_file(hmc_ctx *h, const char *format, const char *path, const char *path2) {
+  if (!path) return HMC_EARG;
+  const char *ps[2] = {path, path2};
+  return hmc_load_files(h, format, ps, path2 ? 2 : 1);
+}
+
+int hmc_unphased_num(const hmc_ctx *h, int *n) {
+  if (!h || !n || !h->c.have_panel) return HMC_EARG;
+  *n = h->c.pan.unphased;
+  return HMC_OK;
+}
+
+// Writer metadata: the loaded file's ids / marker names / positions, or the
+// reference's defaults (ids "1".."N", names "M<k+1>", positions k * 1000).
+static hmc::FileData writer_meta(const hmc::Ctx &c) {
   hmc::FileData d = c.file_meta;
   d.N = c.pan.N;
   d.L = c.pan.L;
@@ -1830,11 +1999,26 @@ int hmc_write_file(hmc_ctx *h, const char *format, const char *path, const char 
       d.pos[k] = k * 1000;
     }
   }
+  return d;
+}
+
+int hmc_write_files(hmc_ctx *h, const char *format, const char *const *paths, int n_paths) {
+  if (!h || !format || !paths || n_paths <= 0 || !h->c.have_best || h->c.world != 1) return HMC_EARG;
+  if (std::string(format) == "PHASE") return hmc_write_phase(h, paths[0]);
+  hmc::Ctx &c = h->c;
+  const hmc::FileData d = writer_meta(c);
   std::vector<int32_t> hap((size_t)d.N * 2 * d.L);
   c.to_symbols(c.best_res, hap.data());
   std::string err;
-  if (!hmc::write_geno_file(format, path, path2, d, hap, err)) return c.fail(HMC_EIO, "%s", err.c_str());
+  if (!hmc::write_geno_file(format, paths[0], n_paths > 1 ? paths[1] : nullptr, d, hap, err))
+    return c.fail(HMC_EIO, "%s", err.c_str());
   return HMC_OK;
+}
+
+int hmc_write_file(hmc_ctx *h, const char *format, const char *path, const char *path2) {
+  if (!path) return HMC_EARG;
+  const char *ps[2] = {path, path2};
+  return hmc_write_files(h, format, ps, path2 ? 2 : 1);
 }
 
 int hmc_write_patterns(hmc_ctx *h, const char *path) {
@@ -2062,13 +2246,15 @@ int hmc_get_samples(hmc_ctx *h, int32_t *alleles, double *weights, double *total
   Ctx &c = h->c;
   const int H = c.H, L = c.pan.L;
   hipError_t e;
-  if (alleles && H) {
-    std::vector<uint8_t> rows((size_t)H * L);
+  if (alleles && H) {  // sample rows live in per-individual slots; h_rowmap gives the sample order
+    int32_t top = 0;
+    for (int s = 0; s < H; ++s) top = std::max(top, c.h_rowmap[s] + 1);
+    std::vector<uint8_t> rows((size_t)top * L);
     if ((e = hipMemcpyAsync(rows.data(), c.d_rows.p, rows.size(), hipMemcpyDeviceToHost, c.st)) ||
         (e = hipStreamSynchronize(c.st)))
       return c.hipfail(e, "get_samples");
     for (int s = 0; s < H; ++s)
-      for (int k = 0; k < L; ++k) alleles[(size_t)s * L + k] = c.pan.symbol(k, rows[(size_t)s * L + k]);
+      for (int k = 0; k < L; ++k) alleles[(size_t)s * L + k] = c.pan.symbol(k, rows[(size_t)c.h_rowmap[s] * L + k]);
   }
   if (weights && H) {
     if ((e = hipMemcpyAsync(weights, c.d_w.p, (size_t)H * 8, hipMemcpyDeviceToHost, c.st)) ||
@@ -2124,11 +2310,13 @@ int hmc_write_phase(hmc_ctx *h, const char *path) {
   FILE *fp = fopen(path, "w");
   if (!fp) return c.fail(HMC_EIO, "Can not open file %s!", path);
   const int N = c.pan.N, L = c.pan.L;
+  const hmc::FileData d = writer_meta(c);
   fprintf(fp, "%d\n%d\nP", N, L);
-  for (int k = 0; k < L; ++k) fprintf(fp, " %d", k * 1000);  // Constant::average_marker_distance
+  for (int k = 0; k < L; ++k) fprintf(fp, " %d", d.pos[k]);
   fprintf(fp, "\n%s\n", c.pan.types.c_str());
   for (int i = 0; i < N; ++i) {
-    fprintf(fp, "#%d\n", i + 1);
+    const std::string &id = d.ids[i];  // '#' only before an id starting with a digit (HaploFile.cpp:141-147)
+    fprintf(fp, (!id.empty() && id[0] >= '0' && id[0] <= '9') ? "#%s\n" : "%s\n", id.c_str());
     for (int hh = 0; hh < 2; ++hh) {
       for (int k = 0; k < L; ++k) {
         const int32_t a = c.pan.symbol(k, c.best_res[((size_t)i * 2 + hh) * L + k]);

@@ -413,6 +413,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void e
     const uchar2 *g = a.pan.geno_im + (size_t)gi * L;
     const int hl = a.mod.head_len;
     const unsigned long long t_indiv = __builtin_amdgcn_s_memtime();
+    if (a.trace_base) {  // this individual's reserved trace region (exact sizes from the structure pass)
+      tcur = a.trace_base[bi];
+      tend = ~0ull;
+    }
     int status = EST_OK;
     unsigned long long re = 0;
     int fbig = 0;
@@ -788,9 +792,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void e
 // individual, one per candidate; walks the trace store from locus L back to
 // the head locus and writes both haplotypes as sample rows.
 __global__ __launch_bounds__(256) void estep_traceback(TracebackArgs a) {
-  const int bi = blockIdx.x * 16 + threadIdx.x / 16;
+  const int q = blockIdx.x * 16 + threadIdx.x / 16;
   const int c = threadIdx.x % 16;
-  if (bi >= a.nbatch || c >= a.ncand[bi]) return;
+  if (q >= a.nbatch) return;
+  const int bi = a.order ? a.order[q] : q;
+  if (c >= a.ncand[bi]) return;
   const int L = a.L, S = a.S;
   const size_t h0 = (size_t)a.sample_base[bi] + 2 * c;
   uint8_t *row[2] = {a.rows + h0 * L, a.rows + (h0 + 1) * L};
@@ -825,6 +831,24 @@ __global__ __launch_bounds__(256) void estep_traceback(TracebackArgs a) {
   const double w = a.weight[(size_t)bi * S_MAX + c];
   a.w_out[h0] = w;
   a.w_out[h0 + 1] = w;
+}
+
+// Sample rows in slot layout -> locus-major dense samples: out[l][r] =
+// in[rowmap[r]][l] (64x64 LDS tiles; rowmap lists the dense sample order,
+// individuals in order, candidates in order, h0 then h1: HaploModel.cpp:105-106).
+__global__ __launch_bounds__(256) void transpose_rows_u8(const uint8_t *in, const int32_t *rowmap, uint8_t *out,
+                                                         int rows, int cols) {
+  __shared__ uint8_t tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  for (int k = threadIdx.x; k < 64 * 64; k += 256) {
+    const int r = k / 64, c = k % 64;
+    if (r0 + r < rows && c0 + c < cols) tile[r][c] = in[(size_t)rowmap[r0 + r] * cols + c0 + c];
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 64 * 64; k += 256) {
+    const int c = k / 64, r = k % 64;
+    if (r0 + r < rows && c0 + c < cols) out[(size_t)(c0 + c) * rows + r0 + r] = tile[r][c];
+  }
 }
 
 // [rows][cols] -> out[c][col0 + r] with leading dimension ld_out, 64x64 LDS tiles.
@@ -957,6 +981,14 @@ hipError_t launch_transpose_u8(const uint8_t *in, uint8_t *out, int rows, int co
   if (rows <= 0 || cols <= 0) return hipSuccess;
   hipLaunchKernelGGL(transpose_u8, dim3((cols + 63) / 64, (rows + 63) / 64), dim3(256), 0, st, in, out, rows, cols,
                      ld_out, col0);
+  return hipGetLastError();
+}
+
+hipError_t launch_transpose_rows_u8(const uint8_t *in, const int32_t *rowmap, uint8_t *out, int rows, int cols,
+                                    hipStream_t st) {
+  if (rows <= 0 || cols <= 0) return hipSuccess;
+  hipLaunchKernelGGL(transpose_rows_u8, dim3((cols + 63) / 64, (rows + 63) / 64), dim3(256), 0, st, in, rowmap, out,
+                     rows, cols);
   return hipGetLastError();
 }
 

@@ -214,7 +214,11 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
     unsigned long long *roff = a.rec_off + (size_t)bi * (L + 1);
     int status = EST_OK;
     unsigned long long re = 0;
-    unsigned long long rcur = 0, rend = 0;
+    // records: this individual's reserved region, else the bump allocator; once
+    // a record does not fit, `counting` keeps the walk going without writes
+    unsigned long long rcur = a.rec_base ? a.rec_base[bi] : 0, rend = a.rec_base ? ~0ull : 0;
+    bool counting = false;
+    unsigned long long rneed = 0, tneed = 0;  // exact record / trace words (lane-uniform)
     IdFront X = FA, Y = FB;
 
     // ---- initHeadList (HaploBuilder.cpp:153-224) ----------------------------
@@ -268,9 +272,12 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
     wsync();
     if (status == EST_OK) {
       const unsigned long long words = 4 + 4ull * Fp + 1;
+      rneed += (words + 1) & ~1ull;
+      tneed += trace_locus_words((unsigned long long)Fp, S);
       const unsigned long long o = rec_alloc(a, rcur, rend, words);
       if (o + words > a.rec_cap) {
-        status = EST_OVERFLOW_REC;
+        counting = true;
+        if (lane == 0) re += (unsigned long long)Fp;
       } else {
         uint32_t *R = a.rec + o;
         double *Rtp = (double *)(R + 4);
@@ -424,9 +431,11 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
         Cv += __shfl(incl, 63);
       }
       const unsigned long long words = 4 + 4ull * Fn + 1 + (unsigned long long)Cv + Fn;
-      const unsigned long long o = rec_alloc(a, rcur, rend, words);
-      if (o + words > a.rec_cap) { status = EST_OVERFLOW_REC; break; }
-      uint32_t *R = a.rec + o;
+      rneed += (words + 1) & ~1ull;
+      tneed += trace_locus_words((unsigned long long)Fn, S);
+      const unsigned long long o = counting ? 0 : rec_alloc(a, rcur, rend, words);
+      if (!counting && o + words > a.rec_cap) counting = true;
+      uint32_t *R = a.rec + (counting ? 0 : o);  // not dereferenced while counting
       double *Rtp = (double *)(R + 4);
       uint32_t *Rhd = R + 4 + 2 * Fn, *Rcb = Rhd + Fn, *Rct = Rcb + Fn + 1, *Rch = Rct + Cv;
       if (lane < NBUCKET) bucket[lane] = 0;
@@ -442,10 +451,12 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
           const uint32_t nl = nsum < (uint32_t)S ? nsum : (uint32_t)S;
           *Y.at(F_NL, t) = nl;
           re += nl;
-          Rtp[t] = a.mod.tp[lo] * a.mod.tp[hi];  // m_transition_prob, HaploPair.cpp:42
-          Rhd[t] = (uint32_t)a.mod.last[lo] | (uint32_t)a.mod.last[hi] << 8 | nl << 16;
-          Rcb[t] = *Y.at(F_CB, t);
-          if (nsum > (uint32_t)S) {  // bucket 0 = most contributions
+          if (!counting) {
+            Rtp[t] = a.mod.tp[lo] * a.mod.tp[hi];  // m_transition_prob, HaploPair.cpp:42
+            Rhd[t] = (uint32_t)a.mod.last[lo] | (uint32_t)a.mod.last[hi] << 8 | nl << 16;
+            Rcb[t] = *Y.at(F_CB, t);
+          }
+          if (!counting && nsum > (uint32_t)S) {  // bucket 0 = most contributions
             const int m = (int)*K.cnt(*Y.at(F_SLOT, t));
             atomicAdd(&bucket[NBUCKET - 1 - (m - 1 < NBUCKET - 1 ? m - 1 : NBUCKET - 1)], 1);
           }
@@ -461,7 +472,7 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
         if (lane < NBUCKET) bucket[lane] = incl - b;
       }
       wsync();
-      for (int t0 = 0; t0 < Fn; t0 += WAVE) {
+      for (int t0 = 0; t0 < Fn && !counting; t0 += WAVE) {
         const int t = t0 + lane;
         if (t < Fn) {
           const uint32_t nsum = t < Y.fc ? *Y.at(F_NS, t) : ld_acq(Y.at(F_NS, t));
@@ -473,7 +484,7 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
         }
       }
       // contributions of each state in add order
-      for (int c0 = 0; c0 < C; c0 += WAVE) {
+      for (int c0 = 0; c0 < C && !counting; c0 += WAVE) {
         const int c = c0 + lane;
         if (c < C) {
           const uint32_t st = *CT.at(C_ST, c);
@@ -484,7 +495,7 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
           }
         }
       }
-      if (lane == 0) {
+      if (lane == 0 && !counting) {
         Rcb[Fn] = (uint32_t)Cv;
         R[0] = (uint32_t)Fn;
         R[1] = (uint32_t)Cv;
@@ -508,11 +519,14 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
       Fp = Fn;
     }
     if (status == EST_OK && Fp == 0) status = EST_UNRESOLVED;
+    if (counting && status != EST_OVERFLOW_FRONTIER && status != EST_NO_HEAD_PATTERN) status = EST_OVERFLOW_REC;
     fbig = Fp > fbig ? Fp : fbig;
     if (status < 0) reset_tables();  // aborted mid-locus: keys may be left
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) re += __shfl_xor(re, o);
     if (lane == 0) {
+      a.rec_need[bi] = rneed;
+      a.trace_need[bi] = tneed;
       a.status[bi] = status;
       a.re_count[bi] = re;
       a.fmax[bi] = fbig;
@@ -617,7 +631,7 @@ __device__ inline unsigned long long k2_trace_alloc(const ValueArgs &a, K2Shared
 __device__ inline bool k2_write_trace(const ValueArgs &a, K2Shared *bs, const VFront &Y, const uint32_t *Rhd, int F,
                                       int j, int bi, unsigned long long &cur, unsigned long long &end) {
   const int S = a.S, NT = (int)blockDim.x;
-  const unsigned long long words = 2ull + (unsigned long long)F * (1 + S);
+  const unsigned long long words = trace_locus_words((unsigned long long)F, S);
   const unsigned long long off = k2_trace_alloc(a, bs, cur, end, words);
   if (off + words > a.trace_cap) return false;
   uint32_t *hdr = a.trace + off + 1;
@@ -711,7 +725,8 @@ __global__ __launch_bounds__(256) void estep_values(ValueArgs a) {
       continue;
     }
     const unsigned long long *roff = a.rec_off + (size_t)bi * (L + 1);
-    unsigned long long tcur = 0, tend = 0;
+    // the individual's reserved trace region, else the bump allocator
+    unsigned long long tcur = a.trace_base ? a.trace_base[bi] : 0, tend = a.trace_base ? ~0ull : 0;
     VFront X = FA, Y = FB;
 
     // ---- head list (HaploPair.cpp:14-33) -----------------------------------

@@ -13,9 +13,11 @@
 //   BENCH2 genotype file (one haplotype per line: L characters, '0' missing,
 //          '9' = the heterozygous placeholder, then "number 0 id") + position
 //          file ("index name position")
-// BENCH3 adds a children file of phased trios; phased genotypes are not on the
-// GPU path (HaploModel::resolveAll skips them, checkFrequency weighs them
-// differently), so it is rejected.
+//   BENCH3 BENCH2 + a children file in the same layout (HaploFile.cpp:446-484).
+//          The children are appended as ordinary genotypes: setHaplotypes
+//          leaves every genotype unphased (Genotype.cpp:40), so the EM resolves
+//          them like the parents; only HaploComp stops at unphased_num = the
+//          parents (HaploFile.cpp:475, HaploComp.cpp:40).
 #include "haplofile.hpp"
 
 #include <cstdio>
@@ -174,9 +176,47 @@ bool read_hpm(const char *path, bool hpm2, FileData &d, std::string &err) {
   return true;
 }
 
-// HaploFileBench::readGenoData / readHaploFile / readHaplotype /
-// readPositionInfo (HaploFile.cpp:446-484, 528-588, 605-624)
-bool read_bench(const char *geno, const char *posinfo, FileData &d, std::string &err) {
+// HaploFileBench::readHaploFile + readHaplotype (HaploFile.cpp:528-564, 605-624):
+// one haplotype per line, appended to haps/hid; the heterozygous placeholder
+// restarts at '1' in every file.
+bool read_bench_haplos(const char *path, int L, std::vector<std::vector<int32_t>> &haps, std::vector<std::string> &hid,
+                       std::string &err) {
+  std::vector<std::string> lines;
+  if (!read_lines(path, lines, err)) return false;
+  const size_t before = haps.size();
+  int het = 1;  // '9' = the heterozygous placeholder: '1' on the first haplotype, '2' on the second
+  for (size_t ln = 0; ln < lines.size(); ++ln) {
+    if (blank(lines[ln])) continue;
+    const char *buf = lines[ln].c_str();
+    buf += strspn(buf, DELIM);
+    if ((int)strcspn(buf, DELIM) != L) {
+      err = "Incorrect haplotype data in line " + std::to_string(ln + 1) + " of " + path + "!";
+      return false;
+    }
+    std::vector<int32_t> h(L);
+    for (int k = 0; k < L; ++k) {
+      const char c = buf[k];
+      h[k] = c == '0' ? -1 : (c == '9' ? '0' + het : (int32_t)(unsigned char)c);
+    }
+    const char *s = buf + L;
+    for (int f = 0; f < 2; ++f) {  // skip the number and the 0
+      s += strspn(s, DELIM);
+      s += strcspn(s, DELIM);
+    }
+    s += strspn(s, DELIM);
+    hid.push_back(std::string(s, strcspn(s, "\r\n")));
+    haps.push_back(std::move(h));
+    het = 3 - het;
+  }
+  if ((haps.size() - before) % 2) {
+    err = "Incorrect haplotype data in line " + std::to_string(haps.size() - before + 2) + "!";
+    return false;
+  }
+  return true;
+}
+
+// HaploFileBench::readGenoData / readPositionInfo (HaploFile.cpp:446-484, 566-588)
+bool read_bench(const char *geno, const char *posinfo, const char *children, FileData &d, std::string &err) {
   std::vector<std::string> lines;
   if (!read_lines(geno, lines, err)) return false;
   if (lines.empty()) {
@@ -197,34 +237,10 @@ bool read_bench(const char *geno, const char *posinfo, FileData &d, std::string 
   }
   std::vector<std::vector<int32_t>> haps;
   std::vector<std::string> hid;
-  int het = 1;  // '9' = the heterozygous placeholder: '1' on the first haplotype, '2' on the second
-  for (size_t ln = 0; ln < lines.size(); ++ln) {
-    if (blank(lines[ln])) continue;
-    const char *buf = lines[ln].c_str();
-    buf += strspn(buf, DELIM);
-    if ((int)strcspn(buf, DELIM) != d.L) {
-      err = "Incorrect haplotype data in line " + std::to_string(ln + 1) + " of " + geno + "!";
-      return false;
-    }
-    std::vector<int32_t> h(d.L);
-    for (int k = 0; k < d.L; ++k) {
-      const char c = buf[k];
-      h[k] = c == '0' ? -1 : (c == '9' ? '0' + het : (int32_t)(unsigned char)c);
-    }
-    const char *s = buf + d.L;
-    for (int f = 0; f < 2; ++f) {  // skip the number and the 0
-      s += strspn(s, DELIM);
-      s += strcspn(s, DELIM);
-    }
-    s += strspn(s, DELIM);
-    hid.push_back(std::string(s, strcspn(s, "\r\n")));
-    haps.push_back(std::move(h));
-    het = 3 - het;
-  }
-  if (haps.size() % 2) {
-    err = "Incorrect haplotype data in line " + std::to_string(haps.size() + 2) + "!";
-    return false;
-  }
+  if (!read_bench_haplos(geno, d.L, haps, hid, err)) return false;
+  const int parents = (int)haps.size() / 2;
+  if (children && !read_bench_haplos(children, d.L, haps, hid, err)) return false;
+  d.unphased = children ? parents : -1;  // setUnphasedNum(m_parents_num) (HaploFile.cpp:475)
   d.N = (int)haps.size() / 2;
   d.al.assign((size_t)d.N * 2 * d.L, -1);
   d.ids.assign(d.N, "");
@@ -249,22 +265,26 @@ bool read_bench(const char *geno, const char *posinfo, FileData &d, std::string 
 
 }  // namespace
 
-bool read_geno_file(const std::string &format, const char *path, const char *path2, FileData &d, std::string &err) {
-  if (format == "HPM") return read_hpm(path, false, d, err);
-  if (format == "HPM2") return read_hpm(path, true, d, err);
-  if (format == "BENCH2") {
-    if (!path2) {
-      err = "BENCH2 needs a genotype file and a position file";
-      return false;
-    }
-    return read_bench(path, path2, d, err);
-  }
-  if (format == "BENCH3") {
-    err = "BENCH3 (phased children) is not supported: phased genotypes are outside the GPU EM path";
+int geno_file_count(const std::string &format) {
+  if (format == "PHASE" || format == "HPM" || format == "HPM2") return 1;
+  if (format == "BENCH2") return 2;
+  if (format == "BENCH3") return 3;
+  return 0;
+}
+
+bool read_geno_file(const std::string &format, const std::vector<std::string> &paths, FileData &d, std::string &err) {
+  const int need = geno_file_count(format);
+  if (need == 0 || format == "PHASE") {
+    err = "Unknown file format " + format;
     return false;
   }
-  err = "Unknown file format " + format;
-  return false;
+  if ((int)paths.size() < need) {
+    err = format + " needs " + std::to_string(need) + " file names";
+    return false;
+  }
+  if (format == "HPM") return read_hpm(paths[0].c_str(), false, d, err);
+  if (format == "HPM2") return read_hpm(paths[0].c_str(), true, d, err);
+  return read_bench(paths[0].c_str(), paths[1].c_str(), format == "BENCH3" ? paths[2].c_str() : nullptr, d, err);
 }
 
 // HaploFileHPM(2)::writeGenoData + writeHaplotype (HaploFile.cpp:266-286,
@@ -299,7 +319,7 @@ bool write_geno_file(const std::string &format, const char *path, const char *pa
         }
         fprintf(fp, "\n");
       }
-  } else if (format == "BENCH2") {
+  } else if (format == "BENCH2" || format == "BENCH3") {
     for (int i = 0; i < N; ++i)
       for (int h = 0; h < 2; ++h) {
         for (int k = 0; k < L; ++k) {
@@ -314,7 +334,7 @@ bool write_geno_file(const std::string &format, const char *path, const char *pa
     return false;
   }
   fclose(fp);
-  if (format == "BENCH2" && path2) {
+  if ((format == "BENCH2" || format == "BENCH3") && path2) {
     FILE *fq = fopen(path2, "w");
     if (!fq) {
       err = std::string("Can not open file ") + path2 + "!";

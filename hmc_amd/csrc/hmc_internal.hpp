@@ -84,7 +84,8 @@ struct EstepArgs {
   // trace store
   uint32_t *trace;
   unsigned long long trace_cap;     // words
-  unsigned long long *trace_cursor; // bump allocator
+  unsigned long long *trace_cursor; // bump allocator (when trace_base is null)
+  const unsigned long long *trace_base;  // [batch] reserved trace region of each individual, or null
   unsigned long long *loc_off;      // [batch][L+1] word offsets
   // per-individual outputs (indexed by individual - indiv_begin)
   double *total;
@@ -127,13 +128,25 @@ struct StructArgs {
   int lds_fc, lds_hc, lds_cc;     // LDS tier
   uint32_t *rec;
   unsigned long long rec_cap;     // words
-  unsigned long long *rec_cursor; // bump allocator
+  unsigned long long *rec_cursor; // bump allocator (when rec_base is null)
+  const unsigned long long *rec_base;  // [batch] reserved record region of each individual, or null
   unsigned long long *rec_off;    // [batch][L+1]
+  // Exact store needs of each individual (words): its records and its value-pass
+  // trace.  An individual whose records do not fit the store keeps walking the
+  // loci without writing them (status EST_OVERFLOW_REC) so both are known.
+  unsigned long long *rec_need;   // [batch]
+  unsigned long long *trace_need; // [batch]
   int32_t *status;                // [batch]
   unsigned long long *re_count;   // [batch]
   int32_t *fmax;                  // [batch]
   unsigned int *max_states;
 };
+
+// Trace words one locus with F states takes (header, F header words, pad, F x S
+// link words; the layout of trace_links()).
+__host__ __device__ inline unsigned long long trace_locus_words(unsigned long long F, int S) {
+  return 2ull + F * (1ull + (unsigned long long)S);
+}
 
 struct ValueArgs {
   int S, L, head_len;
@@ -147,6 +160,7 @@ struct ValueArgs {
   uint32_t *trace;
   unsigned long long trace_cap;
   unsigned long long *trace_cursor;
+  const unsigned long long *trace_base;  // [batch] reserved trace region of each individual, or null
   unsigned long long *loc_off;
   int32_t *status;  // in: pass-1 status; out: EST_OK / EST_NEEDS_EXACT / EST_OVERFLOW_TRACE
   double *total;
@@ -158,7 +172,8 @@ struct ValueArgs {
 };
 
 struct TracebackArgs {
-  int L, S, head_len, nbatch;
+  int L, S, head_len, nbatch;      // nbatch: entries of `order` (or individuals 0..nbatch-1 when null)
+  const int32_t *order;
   int indiv_begin;                 // global index of the batch's first individual
   DevModel mod;                    // head pairs / alleles when head_len > 1
   const uint32_t *trace;
@@ -182,6 +197,8 @@ size_t estep_s2_lds_bytes(int S, int fc, int nw);
 hipError_t launch_estep_structure(const StructArgs &a, int grid, hipStream_t st);
 hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, hipStream_t st);
 hipError_t launch_traceback(const TracebackArgs &a, int total_cands, hipStream_t st);
+hipError_t launch_transpose_rows_u8(const uint8_t *in, const int32_t *rowmap, uint8_t *out, int rows, int cols,
+                                    hipStream_t st);
 hipError_t launch_transpose_u8(const uint8_t *in, uint8_t *out, int rows, int cols, int ld_out, int col0,
                                hipStream_t st);
 hipError_t launch_gather_resolutions(const uint8_t *rows, int L, const int32_t *sbase, const int32_t *ncand,

@@ -503,21 +503,33 @@ __global__ void mine_succ(MineArgs a, PatternTable t, int P) {
       if (u == -1) {
         // Chain broken: the suffix dropped `depth` alleles is no candidate.
         // Navigate the shorter suffixes from their roots (rare; exact walk).
+        // The pattern's alleles are read through a window of AW positions,
+        // refilled by walking the parent chain, so any pattern length works.
+        constexpr int AW = 128;
         const int vs = t.start[id];
-        uint8_t al[256];
-        int32_t w = t.node[id];
         const int L0 = t.len[id];
-        for (int q = L0 - 1; q >= 0 && L0 <= 256; --q) {
-          al[q] = a.allele[w];
-          w = a.parent[w];
-        }
+        uint8_t al[AW];
+        int w0 = -1;  // first position held in the window (-1: empty)
+        auto allele_at = [&](int q) -> uint8_t {
+          if (w0 < 0 || q < w0 || q >= w0 + AW) {
+            w0 = q;
+            const int hi = min(q + AW, L0) - 1;
+            int32_t w = t.node[id];
+            for (int r = L0 - 1; r > hi; --r) w = a.parent[w];
+            for (int r = hi; r >= q; --r) {
+              al[r - q] = a.allele[w];
+              w = a.parent[w];
+            }
+          }
+          return al[q - w0];
+        };
         for (int d = depth + 1; d <= L0 && res == NONE; ++d) {
           const int ks = vs + d;  // suffix start
           int32_t nd = root_code(ks);
           bool ok = true;
           for (int q = d; q < L0 && ok; ++q) {
             const int loc = vs + q;
-            const uint8_t r = a.rank_of[(size_t)loc * a.amax + al[q]];
+            const uint8_t r = a.rank_of[(size_t)loc * a.amax + allele_at(q)];
             if (r == 0xFF) { ok = false; break; }
             if (is_root(nd)) nd = a.r_child_base[root_start(nd)] + r;
             else if (a.flags[nd] & NODE_EXT) nd = a.child_base[nd] + r;

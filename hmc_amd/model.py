@@ -162,7 +162,10 @@ class HaploModel:
     def estep_split_stats(self) -> dict:
         s1, s2, fb, nf = C.c_double(), C.c_double(), C.c_double(), C.c_int()
         self._check(lib().hmc_last_estep_split(self._h, C.byref(s1), C.byref(s2), C.byref(fb), C.byref(nf)))
-        return dict(structure_ms=s1.value, values_ms=s2.value, fallback_ms=fb.value, n_fallback=nf.value)
+        ps, pv = C.c_int(), C.c_int()
+        self._check(lib().hmc_last_estep_passes(self._h, C.byref(ps), C.byref(pv)))
+        return dict(structure_ms=s1.value, values_ms=s2.value, fallback_ms=fb.value, n_fallback=nf.value,
+                    structure_passes=ps.value, value_passes=pv.value)
 
     # ----------------------------------------------------------------- panel
     def load(self, genos: GenoData):
@@ -174,6 +177,24 @@ class HaploModel:
     def load_phase(self, path: str):
         self._check(lib().hmc_load_phase(self._h, path.encode()))
         self._info()
+
+    def load_files(self, fmt: str, paths: list[str]):
+        """HaploFile::getHaploFile(format, names)->readGenoData: PHASE, HPM,
+        HPM2 (one file), BENCH2 (genotypes, positions), BENCH3 (genotypes,
+        positions, children)."""
+        arr = (C.c_char_p * len(paths))(*[p.encode() for p in paths])
+        self._check(lib().hmc_load_files(self._h, fmt.encode(), arr, len(paths)))
+        self._info()
+
+    def write_files(self, fmt: str, paths: list[str]):
+        """writeGenoData of the accepted resolutions in `fmt`."""
+        arr = (C.c_char_p * len(paths))(*[p.encode() for p in paths])
+        self._check(lib().hmc_write_files(self._h, fmt.encode(), arr, len(paths)))
+
+    def unphased_num(self) -> int:
+        n = C.c_int()
+        self._check(lib().hmc_unphased_num(self._h, C.byref(n)))
+        return n.value
 
     def _info(self):
         n, l, a = C.c_int(), C.c_int(), C.c_int()

@@ -152,15 +152,32 @@ int hmc_haplocomp(hmc_ctx *ctx, double *switch_error, double *ihp, double *igp);
 /* Accepted resolutions of the last hmc_run ([n][2][L] symbols). */
 int hmc_get_best_resolutions(hmc_ctx *ctx, int32_t *out);
 /* HaploFile::writeGenoData (HaploFile.cpp:120-153) of the accepted
- * resolutions (single-rank contexts). */
+ * resolutions (single-rank contexts): the loaded file's positions ("P" line)
+ * and ids ('#' prepended only to an id starting with a digit), or the
+ * defaults k*1000 and 1..N for a panel loaded from memory. */
 int hmc_write_phase(hmc_ctx *ctx, const char *path);
-/* The other HaploFile formats (HaploFile.cpp:13-52, 205-640): format "PHASE",
- * "HPM", "HPM2" (one file) or "BENCH2" (genotype file + position file in
- * path2).  hmc_parse_file needs no context or device: it returns the panel
- * (alleles [N][2][L] symbols, -1 missing; types [L+1] 'S'/'M'); pass NULL
- * buffers first to learn N and L.  hmc_load_file = parse + hmc_load_genotypes
- * (keeps ids, marker names, positions for hmc_write_file).  hmc_write_file
- * writes the accepted resolutions in that format (BENCH2: + position file). */
+/* HaploFile::getHaploFile(format, file names) + readGenoData / writeGenoData
+ * (HaploFile.cpp:13-52, 54-153, 205-640).  format / file names:
+ *   "PHASE", "HPM", "HPM2"  one file;
+ *   "BENCH2"                genotype file, position file;
+ *   "BENCH3"                genotype file, position file, children file — the
+ *                           children are appended as ordinary unphased
+ *                           genotypes, unphased_num = the parents, and HaploComp
+ *                           covers the parents only (HaploFile.cpp:446-484,
+ *                           HaploComp.cpp:40).
+ * hmc_parse_files needs no context or device: it returns the panel (alleles
+ * [N][2][L] symbols, -1 missing; types [L+1] 'S'/'M'; unphased_num); pass NULL
+ * buffers first to learn N and L.  hmc_load_files = parse + hmc_load_genotypes
+ * (keeps ids, marker names, positions for the writers).  hmc_write_files
+ * writes the accepted resolutions in that format (BENCH2/3: genotype file +
+ * position file). */
+int hmc_parse_files(const char *format, const char *const *paths, int n_paths, int *N, int *L, int32_t *alleles,
+                    char *types, int *unphased_num);
+int hmc_load_files(hmc_ctx *ctx, const char *format, const char *const *paths, int n_paths);
+int hmc_write_files(hmc_ctx *ctx, const char *format, const char *const *paths, int n_paths);
+/* GenoData::unphased_num (GenoData.h:37) of the loaded panel. */
+int hmc_unphased_num(const hmc_ctx *ctx, int *unphased_num);
+/* One- and two-file shorthands of the three calls above (path2 may be NULL). */
 int hmc_parse_file(const char *format, const char *path, const char *path2, int *N, int *L, int32_t *alleles,
                    char *types);
 int hmc_load_file(hmc_ctx *ctx, const char *format, const char *path, const char *path2);
@@ -193,6 +210,9 @@ int hmc_set_estep_mode(hmc_ctx *ctx, int mode);
  * took the fallback. */
 int hmc_last_estep_split(const hmc_ctx *ctx, double *structure_ms, double *values_ms, double *fallback_ms,
                          int *n_fallback);
+/* Launches of the last hmc_resolve_all: structure passes and value passes
+ * (individuals pass in groups when their records / traces exceed the stores). */
+int hmc_last_estep_passes(const hmc_ctx *ctx, int *structure_passes, int *value_passes);
 /* Device time (ms, HIP events on the context stream) of the last E-step
  * forward kernel, traceback and whole M-step. */
 int hmc_last_timings(const hmc_ctx *ctx, double *estep_forward_ms, double *estep_traceback_ms, double *mstep_ms);

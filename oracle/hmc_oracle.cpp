@@ -28,12 +28,33 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
-#include <array>
 
 namespace ora {
+
+// Worker threads for the digest generators (tests/golden/make_*_digest.py):
+// mining splits the start loci (each root's DFS subtree is independent,
+// PatternManager.cpp:94-97,106-108), initialize() the successor lookups and
+// resolveAll() the individuals (HaploModel.cpp:86 is independent per
+// individual).  Every result is assembled in the reference's order, so the
+// outputs are identical to the single-threaded run (default 1).
+static int g_threads = 1;
+template <class F>
+static void parallel_for(int n, int chunk, F f) {  // f(begin, end), dynamic chunks
+  const int nt = std::max(1, std::min(g_threads, (n + chunk - 1) / std::max(chunk, 1)));
+  if (nt <= 1) { if (n > 0) f(0, n); return; }
+  std::atomic<int> next{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&] {
+      for (int b; (b = next.fetch_add(chunk)) < n;) f(b, std::min(n, b + chunk));
+    });
+  for (auto &x : th) x.join();
+}
 
 // ---------------------------------------------------------------- alleles --
 // Allele.h:11-36 — an int, negative = missing; isMatch treats missing as a
@@ -306,8 +327,9 @@ struct Model {
   // prior 0).  With none set,
   // every k-best set is decided by likelihood values alone.
   std::vector<int> tie_flags;
-  std::vector<std::vector<double>> uni;  // per state of the next locus
-  int tie_cur = 0;
+  static thread_local std::vector<std::vector<double>> uni;  // per state of the next locus
+  static thread_local int tie_cur;
+  static thread_local uint64_t tl_rm;  // R_M of this thread's scans, folded into R_M per search
   void uni_add(int st, const Link *l, int n) {
     if ((int)uni.size() <= st) uni.resize(st + 1);
     for (int i = 0; i < n; ++i) uni[st].push_back(l[i].lik);
@@ -375,7 +397,7 @@ struct Model {
     double tot = 0;
     if (samples.empty()) {
       for (int i = 0; i < g.N; ++i) {
-        ++R_M;
+        ++tl_rm;
         if (genoMatch(i, p, p.start, p.len())) {
           double f = matchFreq(i, p.al.data(), p.start, p.len());
           tot += f;
@@ -385,7 +407,7 @@ struct Model {
       p.freq = tot / g.N;
     } else {
       for (int i = 0; i < (int)samples.size(); ++i) {
-        ++R_M;
+        ++tl_rm;
         if (hapMatch(samples[i], p, p.start, p.len())) {
           tot += samples[i].w;
           ms.push_back({i, 0.0});
@@ -402,7 +424,7 @@ struct Model {
     double tot = 0;
     if (samples.empty()) {
       for (auto &e : oms) {
-        ++R_M;
+        ++tl_rm;
         if (genoMatch(e.first, p, start, 1)) {
           double f = e.second * matchFreq(e.first, &p.al[start - p.start], start, 1);
           tot += f;
@@ -412,7 +434,7 @@ struct Model {
       p.freq = tot / g.N;
     } else {
       for (auto &e : oms) {
-        ++R_M;
+        ++tl_rm;
         if (hapMatch(samples[e.first], p, start, 1)) {
           tot += samples[e.first].w;
           ms.push_back({e.first, 0.0});
@@ -425,7 +447,8 @@ struct Model {
   // PatternManager::searchPattern (:100-144) on an explicit candidate stack;
   // with `reserve`, candidates that fail the threshold are kept (in pop order)
   // for the next round instead of deleted.
-  std::vector<Cand *> searchPattern(std::vector<Cand *> &stack, bool reserve) {
+  std::vector<Cand *> searchPattern(std::vector<Cand *> &stack, bool reserve) { return searchPattern(stack, reserve, P); }
+  std::vector<Cand *> searchPattern(std::vector<Cand *> &stack, bool reserve, std::vector<Pat> &out) {
     const int L = g.L;
     std::vector<Cand *> kept;
     while (!stack.empty()) {
@@ -452,7 +475,7 @@ struct Model {
         }
       }
       if (hp.freq >= min_freq || hp.len() <= minlen[hp.start]) {
-        if (hp.len() > 0 && hp.len() >= minlen[hp.start]) P.push_back(pc->p);
+        if (hp.len() > 0 && hp.len() >= minlen[hp.start]) out.push_back(pc->p);
         delete pc;
       } else if (reserve) {
         kept.push_back(pc);
@@ -460,6 +483,8 @@ struct Model {
         delete pc;
       }
     }
+    __atomic_fetch_add(&R_M, tl_rm, __ATOMIC_RELAXED);
+    tl_rm = 0;
     return kept;
   }
 
@@ -483,9 +508,35 @@ struct Model {
     minlen.resize(L, mnl);  // vector::resize keeps old values (PatternManager.cpp:33-34)
     maxlen.resize(L, mxl);
     P.clear();
-    std::vector<Cand *> stack = generateCandidates();
     min_freq = mf;
-    searchPattern(stack, false);
+    if (g_threads <= 1) {
+      std::vector<Cand *> stack = generateCandidates();
+      searchPattern(stack, false);
+    } else {
+      // roots are popped from the back (start L-1 first): chunk c of start
+      // loci [c*K, c*K+K) yields the DFS blocks of its roots in descending
+      // start order, and the chunks concatenate in descending order
+      const int K = 4, nch = (L + K - 1) / K;
+      std::vector<std::vector<Pat>> part(nch);
+      parallel_for(nch, 1, [&](int b, int e) {
+        for (int c = b; c < e; ++c) {
+          std::vector<Cand *> stack;
+          for (int s = c * K; s < std::min(L, c * K + K); ++s) {
+            Cand *x = new Cand;
+            x->p.start = x->p.end = s;
+            stack.push_back(x);
+          }
+          searchPattern(stack, false, part[c]);
+        }
+      });
+      size_t tot = 0;
+      for (auto &v : part) tot += v.size();
+      P.reserve(tot);
+      for (int c = nch - 1; c >= 0; --c) {
+        for (auto &p : part[c]) P.push_back(std::move(p));
+        std::vector<Pat>().swap(part[c]);
+      }
+    }
     initialize();
   }
 
@@ -528,21 +579,23 @@ struct Model {
       tree.add(P, i);
       if (P[i].start == 0 && P[i].len() == head_len()) head_list.push_back(i);
     }
-    std::vector<int> tmp;
-    for (int i = 0; i < n; ++i) {
-      Pat &p = P[i];
-      p.succ.clear();
-      if (p.end < g.L) {
-        tmp = p.al;
-        tmp.push_back(-1);
-        for (int j = 0; j < g.num(p.end); ++j) {
-          tmp.back() = g.symbol(p.end, j);
-          int s = tree.longest(P, p.end + 1, tmp, p.start);
-          p.succ.resize(j + 1);
-          p.succ[j] = s;
+    parallel_for(n, 4096, [&](int b, int e) {
+      std::vector<int> tmp;
+      for (int i = b; i < e; ++i) {
+        Pat &p = P[i];
+        p.succ.clear();
+        if (p.end < g.L) {
+          tmp = p.al;
+          tmp.push_back(-1);
+          for (int j = 0; j < g.num(p.end); ++j) {
+            tmp.back() = g.symbol(p.end, j);
+            int s = tree.longest(P, p.end + 1, tmp, p.start);
+            p.succ.resize(j + 1);
+            p.succ[j] = s;
+          }
         }
       }
-    }
+    });
   }
 
   // HaploModel.cpp:52-63
@@ -563,8 +616,8 @@ struct Model {
   }
 
   // ------------------------------------------------------------ E-step ----
-  std::vector<std::vector<Pair>> hp;  // m_haplopairs
-  int S = 1;
+  static thread_local std::vector<std::vector<Pair>> hp;  // m_haplopairs
+  static thread_local int S;
 
   int succOf(int pi, int a, int locus) const {  // HaploPattern.h:36-37
     int j = g.index(locus, a);
@@ -742,8 +795,10 @@ struct Model {
       uni_check((int)hp[i + 1].size());
       if (hp[i + 1].empty()) break;
     }
+    uint64_t re = 0;
     for (int i = hl; i <= L; ++i)
-      for (auto &x : hp[i]) R_E += x.links.size();
+      for (auto &x : hp[i]) re += x.links.size();
+    __atomic_fetch_add(&R_E, re, __ATOMIC_RELAXED);
     out.clear();
     double coverage = 0;
     if (!hp[L].empty()) {
@@ -802,12 +857,18 @@ struct Model {
     gp.assign(g.N, 0.0);
     resolution.assign(g.N, {});
     tie_flags.assign(g.N, 0);
+    std::vector<double> cov(g.N, 0.0);
+    parallel_for(g.N, 1, [&](int b, int e) {
+      for (int i = b; i < e; ++i) {
+        cov[i] = resolve(i, res[i], resolution[i], gp[i]);
+        tie_flags[i] = tie_cur;
+      }
+      hp.clear();
+    });
     double ll = 0;
     for (int i = 0; i < g.N; ++i) {
-      double cov = resolve(i, res[i], resolution[i], gp[i]);
-      tie_flags[i] = tie_cur;
       for (auto &c : res[i]) {
-        double w = c.posterior / cov;
+        double w = c.posterior / cov[i];
         samples.push_back(Sample{c.h0, w});
         samples.push_back(Sample{c.h1, w});
       }
@@ -827,7 +888,8 @@ struct Model {
   bool haploComp(const std::vector<std::vector<int>> &infer, double out[3]) const {
     const int L = g.L;
     long long se_n = 0, se_d = 0, ig_n = 0, ig_d = 0, ih_n = 0, ih_d = 0;
-    for (int i = 0; i < g.N; ++i) {
+    const int nc = unphased >= 0 ? std::min(unphased, g.N) : g.N;  // HaploComp.cpp:40
+    for (int i = 0; i < nc; ++i) {
       const int *f = infer[i].data();
       auto hasMissing = [&](int k) { return missing(g.at(i, 0, k)) || missing(g.at(i, 1, k)); };
       // Genotype::isMatch(g, i, reversed) (Genotype.cpp:97-116)
@@ -876,6 +938,7 @@ struct Model {
     return true;
   }
   std::vector<std::array<double, 3>> comp_log;
+  int unphased = -1;  // GenoData::unphased_num (BENCH3: the parents); -1 = all
 
   // HaploModel.cpp:117-155 (MV, sampling EM).
   void run() {
@@ -921,6 +984,12 @@ struct Model {
   }
 };
 
+thread_local int Model::tie_cur = 0;
+thread_local uint64_t Model::tl_rm = 0;
+thread_local std::vector<std::vector<double>> Model::uni;
+thread_local std::vector<std::vector<Pair>> Model::hp;
+thread_local int Model::S = 1;
+
 }  // namespace ora
 
 // ============================================================== C API ======
@@ -949,6 +1018,8 @@ void *ora_create_from_phase(const char *path) {
 }
 
 void ora_destroy(void *h) { delete (Model *)h; }
+// worker threads for mining, successors and resolveAll (results unchanged)
+void ora_set_threads(int n) { ora::g_threads = n > 1 ? n : 1; }
 
 void ora_set_params(void *h, double min_freq_abs, int min_len, int max_len, int sample_size, int max_iter) {
   Model *m = (Model *)h;
@@ -1163,6 +1234,33 @@ double ora_time_find_patterns(void *h) {
   return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// Time the sampling M-step (searchPattern + initialize) restricted to the
+// start loci [s0, s1): each root's DFS subtree is independent
+// (PatternManager.cpp:94-97,106-108), so a subset of roots is a bounded
+// sample of findPatternByFreq.  Leaves the subset's table installed.
+double ora_time_find_patterns_roots(void *h, int s0, int s1) {
+  Model *m = (Model *)h;
+  ora::Params &pr = m->prm;
+  if (pr.min_freq_abs > 0) pr.min_freq = pr.min_freq_abs / (2.0 * m->g.N);
+  const int L = m->g.L;
+  int mxl = pr.max_len <= 0 ? L : pr.max_len, mnl = std::max(pr.min_len, 1);
+  mxl = std::max(mxl, mnl);
+  m->minlen.resize(L, mnl);
+  m->maxlen.resize(L, mxl);
+  auto t0 = std::chrono::steady_clock::now();
+  m->P.clear();
+  m->min_freq = pr.min_freq;
+  std::vector<ora::Model::Cand *> stack;
+  for (int s = std::max(0, s0); s < std::min(L, s1); ++s) {
+    auto *c = new ora::Model::Cand;
+    c->p.start = c->p.end = s;
+    stack.push_back(c);
+  }
+  m->searchPattern(stack, false);
+  m->initialize();
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 // HaploModel::resolveAll restricted to individuals [i0, i1) (the shard one
 // rank of the sharded E-step owns); samples/results cover only that range.
 double ora_resolve_range(void *h, int i0, int i1) {
@@ -1193,6 +1291,8 @@ void ora_set_model(void *h, int model, int mc_order) {
   m->prm.model = model;
   m->prm.mc_order = mc_order;
 }
+// GenoData::unphased_num (HaploFile.cpp:475): HaploComp covers [0, n)
+void ora_set_unphased(void *h, int n) { ((Model *)h)->unphased = n; }
 // HaploModel::num_patterns (HMC.cpp:38): > 0 selects findPatternByNum
 void ora_set_num_patterns(void *h, int n) { ((Model *)h)->prm.num_patterns = n; }
 // Tie diagnostics of the last resolveAll (see Model::tie_flags), [N].

@@ -50,6 +50,8 @@ def lib():
         L.ora_resolve_all.restype = d
         L.ora_resolve_all.argtypes = [vp]
         L.ora_tie_flags.argtypes = [vp, P(i)]
+        L.ora_set_threads.argtypes = [i]
+        L.ora_set_unphased.argtypes = [vp, i]
         L.ora_set_model.argtypes = [vp, i, i]
         L.ora_set_num_patterns.argtypes = [vp, i]
         L.ora_run_comp_log.argtypes = [vp, P(d)]
@@ -79,6 +81,8 @@ def lib():
         L.ora_set_samples.argtypes = [vp, i, P(i), P(d)]
         L.ora_time_find_patterns.restype = d
         L.ora_time_find_patterns.argtypes = [vp]
+        L.ora_time_find_patterns_roots.restype = d
+        L.ora_time_find_patterns_roots.argtypes = [vp, i, i]
         L.ora_resolve_range.restype = d
         L.ora_resolve_range.argtypes = [vp, i, i]
         _lib = L
@@ -173,6 +177,10 @@ class Oracle:
     def time_find_patterns(self) -> float:
         return lib().ora_time_find_patterns(self.h)
 
+    def time_find_patterns_roots(self, s0: int, s1: int) -> float:
+        """Seconds of searchPattern + initialize over the start loci [s0, s1)."""
+        return lib().ora_time_find_patterns_roots(self.h, s0, s1)
+
     def resolve_range(self, i0: int, i1: int) -> float:
         return lib().ora_resolve_range(self.h, i0, i1)
 
@@ -183,6 +191,10 @@ class Oracle:
         """HaploModel::setModel: MV (default), MC (Markov chain of order
         mc_order: all patterns of length mc_order+1), MA (MV + range checks)."""
         lib().ora_set_model(self.h, {"MV": 0, "MC": 1, "MA": 2}[model], int(mc_order))
+
+    def set_unphased(self, n: int):
+        """GenoData::unphased_num: HaploComp covers individuals [0, n) (BENCH3 parents)."""
+        lib().ora_set_unphased(self.h, int(n))
 
     def set_num_patterns(self, n: int):
         """HaploModel::num_patterns: > 0 mines with findPatternByNum."""
@@ -255,6 +267,12 @@ class Oracle:
         out = np.zeros(3, np.float64)
         rc = lib().ora_haplocomp(self.h, _p(f, C.c_int), _p(out, C.c_double))
         return None if rc else out
+
+
+def set_threads(n: int):
+    """Worker threads of mining, successors and resolveAll (results do not
+    depend on it; used by the full-size digest generators)."""
+    lib().ora_set_threads(int(n))
 
 
 def std_nth_element(lik: np.ndarray, tag: np.ndarray, nth: int):

@@ -127,6 +127,31 @@ def test_mine_genotypes_and_samples(oracle_mod, name):
     assert_tables_equal(m.patterns(), o.patterns())
 
 
+def test_long_patterns_near_monomorphic(oracle_mod):
+    """Patterns far longer than 256 loci (max_pattern_len 0 = L on a
+    near-monomorphic panel): M0 and M1 tables, successors included, and the
+    E-step between them equal the restatement's."""
+    rng = np.random.default_rng(17)
+    N, L = 20, 300
+    a = np.full((N, 2, L), ord("1"), np.int32)
+    for k in (40, 150, 260):  # three polymorphic loci
+        a[:, :, k] = np.where(rng.random((N, 2)) < 0.3, ord("2"), ord("1"))
+    p = synth.Panel(alleles=a, types="S" * L)
+    o = oracle_mod.Oracle(a, p.types, sample_size=4, max_len=0)
+    o.find_patterns()
+    m = gpu_model(p, S=4, max_pattern_len=0)
+    P0, _ = m.find_patterns()
+    g = m.patterns()
+    assert g["len"].max() > 256
+    assert_tables_equal(g, o.patterns())
+    ll_g, H, re_g = m.resolve_all()
+    o.reset_counters()
+    assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
+    m.find_patterns()
+    o.find_patterns()
+    assert_tables_equal(m.patterns(), o.patterns())
+
+
 @pytest.mark.parametrize("name", ["cfg1", "n60", "a4", "miss2", "a3miss5", "a8"])
 def test_full_em(oracle_mod, name):
     """HaploModel::run: iteration count, per-iteration LL / R_E / R_M / pattern
