@@ -131,14 +131,23 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(m, panel, args)
+        print(f"[bench] cpu baseline {cpu['value']:.4g} {cpu['unit']} ({cpu['t_iter_s']:.0f} s/iteration)",
+              file=sys.stderr, flush=True)
         m.clear_samples()
         m.find_patterns()
+
+    def progress(msg):
+        if rank == 0:
+            print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+    progress(f"M0 {P0} patterns in {t_m0:.1f} s")
 
     def em_step():
         ll, H, re = m.resolve_all()
         t = m.timings()
         sp = m.estep_split_stats()
         P, rm = m.find_patterns()
+        progress(f"EM step: LL {ll:.6f}, R_E {re}, E {t['estep_forward_ms']:.0f} ms, M {m.timings()['mstep_ms']:.0f} ms")
         return dict(ll=ll, H=H, r_e=re, r_m=rm, P=P, estep_ms=t["estep_forward_ms"] + t["estep_traceback_ms"],
                     struct_ms=sp["structure_ms"], values_ms=sp["values_ms"], fallback_ms=sp["fallback_ms"],
                     n_fallback=sp["n_fallback"], struct_passes=sp["structure_passes"],

@@ -41,6 +41,8 @@ _SIGS = [
     ("hmc_rccl_unique_id", _i, [_vp]),
     ("hmc_ctx_create_dist", _i, [_i, _i, _i, _vp, _P(_vp)]),
     ("hmc_ctx_create_hostcoll", _i, [_i, _i, _i, ALLREDUCE_FN, _vp, _P(_vp)]),
+    ("hmc_ctx_create_comm", _i, [_i, _vp, _P(_vp)]),
+    ("hmc_set_reduction", _i, [_vp, _i]),
     ("hmc_ctx_destroy", None, [_vp]),
     ("hmc_ctx_error", _cp, [_vp]),
     ("hmc_set_params", _i, [_vp, _d, _d, _i, _i, _i]),

@@ -240,6 +240,20 @@ struct Ctx {
   ncclComm_t comm = nullptr;
   hmc_allreduce_fn host_fn = nullptr;  // host-callback collective (tests, gloo)
   void *host_user = nullptr;
+  bool own_comm = true;  // false: the caller's RCCL communicator (hmc_ctx_create_comm)
+  // Cross-rank sums (M-step candidate sums, LL, total weight): ORDERED passes
+  // each running sum from rank r-1 to rank r, which continues the chain over
+  // its contiguous block of items — the reference's sequential sums
+  // (PatternManager.cpp:254-262, HaploModel.cpp:110, HaploData.cpp:120-126),
+  // bit for bit; ALLREDUCE sums the ranks' partial sums (fewer steps, last-bit
+  // drift).
+  enum { RED_ORDERED = 0, RED_ALLREDUCE = 1 };
+  int reduction = RED_ORDERED;
+  // A one-rank context on a one-rank RCCL communicator runs every collective
+  // anyway (test hook, HMC_FORCE_COLLECTIVES=1 at creation): results are
+  // unchanged, so the RCCL calls can be exercised on a one-GPU machine.
+  bool force_coll = false;
+  bool multi() const { return world > 1 || force_coll; }
   std::string err;
   // parameters (HaploModel.h:15-26 with the CLI defaults of HMC.cpp:35-47)
   double min_freq_abs = 1.5, min_freq = -1.0;
@@ -360,7 +374,7 @@ struct Ctx {
 
   // ---------------------------------------------------------- collectives --
   int allreduce_sum(double *dptr, size_t n) {
-    if (world == 1 || n == 0) return HMC_OK;
+    if (!multi() || n == 0) return HMC_OK;
     if (host_fn) {
       std::vector<double> h(n);
       hipError_t e;
@@ -374,8 +388,48 @@ struct Ctx {
     if (r != ncclSuccess) return fail(HMC_ERCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
     return HMC_OK;
   }
+  // Everyone receives rank `src`'s n doubles (device buffer).  RCCL:
+  // ncclBroadcast; host callback: an all-reduce in which every other rank
+  // contributes +0.0 (x + 0.0 == x exactly).
+  int bcast(double *dptr, size_t n, int src) {
+    if (!multi() || n == 0) return HMC_OK;
+    if (host_fn) {
+      std::vector<double> h(n, 0.0);
+      hipError_t e;
+      if (rank == src && ((e = hipMemcpyAsync(h.data(), dptr, n * 8, hipMemcpyDeviceToHost, st)) ||
+                          (e = hipStreamSynchronize(st))))
+        return hipfail(e, "bcast");
+      if (host_fn(h.data(), n, host_user) != 0) return fail(HMC_ERCCL, "host collective callback failed");
+      if ((e = hipMemcpyAsync(dptr, h.data(), n * 8, hipMemcpyHostToDevice, st)) || (e = hipStreamSynchronize(st)))
+        return hipfail(e, "bcast");
+      return HMC_OK;
+    }
+    ncclResult_t r = ncclBroadcast(dptr, dptr, n, ncclDouble, src, comm, st);
+    if (r != ncclSuccess) return fail(HMC_ERCCL, "ncclBroadcast: %s", ncclGetErrorString(r));
+    return HMC_OK;
+  }
+  int bcast_host(double *h, size_t n, int src) {  // small host vectors
+    if (!multi() || n == 0) return HMC_OK;
+    if (host_fn) {
+      std::vector<double> v(h, h + n);
+      if (rank != src) std::fill(v.begin(), v.end(), 0.0);
+      if (host_fn(v.data(), n, host_user) != 0) return fail(HMC_ERCCL, "host collective callback failed");
+      std::copy(v.begin(), v.end(), h);
+      return HMC_OK;
+    }
+    DevBuf<double> tmp;
+    hipError_t e = tmp.ensure(n);
+    if (e) return hipfail(e, "bcast_host");
+    if ((e = hipMemcpyAsync(tmp.p, h, n * 8, hipMemcpyHostToDevice, st))) return hipfail(e, "bcast_host");
+    int rc = bcast(tmp.p, n, src);
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(h, tmp.p, n * 8, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+      return hipfail(e, "bcast_host");
+    return HMC_OK;
+  }
+
   int allreduce_host(double *h, size_t n) {  // small host vectors
-    if (world == 1 || n == 0) return HMC_OK;
+    if (!multi() || n == 0) return HMC_OK;
     if (host_fn) return host_fn(h, n, host_user) == 0 ? HMC_OK : fail(HMC_ERCCL, "host all-reduce callback failed");
     DevBuf<double> tmp;
     hipError_t e = tmp.ensure(n);
@@ -633,7 +687,18 @@ struct Ctx {
         a.stamps = d_mstamps.p;
       }
 #endif
-      if ((e = launch_mine_count(a, level, pbeg, pend, st))) return hipfail(e, "mine_count");
+      if (multi() && reduction == RED_ORDERED) {
+        // rank r continues every child's sum from ranks 0..r-1 (items in order)
+        for (int r = 0; r < world; ++r) {
+          if (r == rank) {
+            a.seeded = r > 0;
+            if ((e = launch_mine_count(a, level, pbeg, pend, st))) return hipfail(e, "mine_count");
+          }
+          if ((rc = bcast(n_sum.p + cb, nlev, r))) return rc;
+        }
+      } else if ((e = launch_mine_count(a, level, pbeg, pend, st))) {
+        return hipfail(e, "mine_count");
+      }
       if (diag_mine) {  // per-level list statistics of the parents (diagnostic)
         hipEventRecord(dm1, st);
         hipStreamSynchronize(st);
@@ -670,7 +735,7 @@ struct Ctx {
         hipEventDestroy(dm0);
         hipEventDestroy(dm1);
       }
-      if ((rc = allreduce_sum(n_sum.p + cb, nlev))) return rc;
+      if (!(multi() && reduction == RED_ORDERED) && (rc = allreduce_sum(n_sum.p + cb, nlev))) return rc;
       if ((e = s_ext.ensure(nlev)) || (e = s_child.ensure(nlev)))
         return hipfail(e, "mine");
       const size_t tmpb = mine_scan_tmp_bytes(nlev);
@@ -1144,16 +1209,26 @@ struct Ctx {
               (e = hipStreamSynchronize(st))))
       return hipfail(e, "estep");
     h_rowmap.swap(rowmap);
-    // ll += log(genotype probability) in individual order (HaploModel.cpp:110)
-    double ll = 0.0;
-    for (int i = 0; i < n; ++i) ll += log(h_total[i]);
-    // HaploData::checkTotalWeight (HaploData.cpp:120-126)
-    double tw = 0.0;
-    for (int h = 0; h < H; ++h) tw += w[h];
-    double red[2] = {ll, tw};
-    rc = allreduce_host(red, 2);
-    if (rc) return rc;
-    ll = red[0];
+    // ll += log(genotype probability) in individual order (HaploModel.cpp:110);
+    // HaploData::checkTotalWeight (HaploData.cpp:120-126) in sample order
+    double red[2] = {0.0, 0.0};
+    auto local_sums = [&](double *acc) {
+      double ll = acc[0], tw = acc[1];
+      for (int i = 0; i < n; ++i) ll += log(h_total[i]);
+      for (int h = 0; h < H; ++h) tw += w[h];
+      acc[0] = ll;
+      acc[1] = tw;
+    };
+    if (multi() && reduction == RED_ORDERED) {
+      for (int r = 0; r < world; ++r) {  // the chain continues rank by rank
+        if (r == rank) local_sums(red);
+        if ((rc = bcast_host(red, 2, r))) return rc;
+      }
+    } else {
+      local_sums(red);
+      if ((rc = allreduce_host(red, 2))) return rc;
+    }
+    const double ll = red[0];
     total_weight = red[1];
     uint64_t re = 0;
     for (int i = 0; i < n; ++i) re += h_re[i];
@@ -1776,12 +1851,37 @@ int hmc_ctx_create_dist(int device, int rank, int world, const void *unique_id, 
   if (rc) return rc;
   h->c.rank = rank;
   h->c.world = world;
-  if (world > 1) {
+  if (world == 1 && getenv("HMC_FORCE_COLLECTIVES")) h->c.force_coll = true;
+  if (world > 1 || h->c.force_coll) {
     ncclUniqueId id;
     memcpy(&id, unique_id, sizeof id);
     ncclResult_t r = ncclCommInitRank(&h->c.comm, world, id, rank);
     if (r != ncclSuccess) return h->c.fail(HMC_ERCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
   }
+  return HMC_OK;
+}
+
+int hmc_ctx_create_comm(int device, void *rccl_comm, hmc_ctx **out) {
+  if (!out || !rccl_comm) return HMC_EARG;
+  hmc_ctx *h = new hmc_ctx;
+  *out = h;
+  int rc = ctx_init(h, device);
+  if (rc) return rc;
+  ncclComm_t comm = (ncclComm_t)rccl_comm;
+  int r = 0, w = 1;
+  if (ncclCommUserRank(comm, &r) != ncclSuccess || ncclCommCount(comm, &w) != ncclSuccess)
+    return h->c.fail(HMC_ERCCL, "not an RCCL communicator");
+  h->c.comm = comm;
+  h->c.own_comm = false;
+  h->c.rank = r;
+  h->c.world = w;
+  if (w == 1 && getenv("HMC_FORCE_COLLECTIVES")) h->c.force_coll = true;
+  return HMC_OK;
+}
+
+int hmc_set_reduction(hmc_ctx *h, int mode) {
+  if (!h || mode < 0 || mode > 1) return HMC_EARG;
+  h->c.reduction = mode;
   return HMC_OK;
 }
 
@@ -1800,7 +1900,7 @@ int hmc_ctx_create_hostcoll(int device, int rank, int world, hmc_allreduce_fn fn
 
 void hmc_ctx_destroy(hmc_ctx *h) {
   if (!h) return;
-  if (h->c.comm) ncclCommDestroy(h->c.comm);
+  if (h->c.comm && h->c.own_comm) ncclCommDestroy(h->c.comm);
   for (auto &ev : h->c.ev)
     if (ev) hipEventDestroy(ev);
   if (h->c.st) hipStreamDestroy(h->c.st);

@@ -210,7 +210,9 @@ __global__ __launch_bounds__(64) void mine_count(MineArgs a, int level, int pbeg
   // read once; the child loop takes them with readlane
   const int my_al = lane < p.nc ? (int)ca[lane] : 0;
   const double my_af = (a.genotype && lane < p.nc) ? a.afreq[(size_t)p.e * a.amax + my_al] : 0.0;
-  double sum = 0.0;
+  // lane k: child k's ordered sum, continued from the previous ranks' running
+  // sum in ordered-reduction mode (the adds below extend the same chain)
+  double sum = (a.seeded && lane < p.nc) ? a.sum[p.cb + lane] : 0.0;
   uint32_t cnt = 0, run = 0;  // lane k: child k's entries so far
   constexpr int U = MC_U;     // chunks whose loads are in flight together
   const size_t erow = (size_t)p.e * a.item_stride;

@@ -42,6 +42,10 @@ struct MineArgs {
   uint32_t *lout_idx = nullptr;
   double *lout_val = nullptr;
   unsigned long long *rm = nullptr;      // R_M counter
+  // Ordered reduction over ranks: every child's sum starts from sum[c] (the
+  // running sum of the ranks before this one, whose items precede this
+  // rank's in the reference's order) instead of 0.
+  bool seeded = false;
 };
 
 // Pattern table in id (= DFS pre-order) order.

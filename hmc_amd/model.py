@@ -74,11 +74,13 @@ class HaploModel:
     """HaploModel (model "MV", sampling EM) on one MI355X, or one rank of a sharded run."""
 
     def __init__(self, device: int = 0, rank: int = 0, world: int = 1, unique_id: bytes | None = None,
-                 host_allreduce=None):
+                 host_allreduce=None, rccl_comm: int | None = None):
         """world > 1 shards individuals over ranks.  The M-step collective is
-        RCCL (unique_id from HaploModel.unique_id() on rank 0), or, when
-        `host_allreduce(np.ndarray)` is given, that callable, which must sum the
-        float64 array across ranks in place (e.g. torch.distributed gloo)."""
+        RCCL (unique_id from HaploModel.unique_id() on rank 0, or an RCCL
+        communicator the caller owns, `rccl_comm` = its ncclComm_t address), or,
+        when `host_allreduce(np.ndarray)` is given, that callable, which must
+        sum the float64 array across ranks in place (e.g. torch.distributed
+        gloo)."""
         L = lib()
         h = C.c_void_p()
         self._cb = None
@@ -92,13 +94,16 @@ class HaploModel:
                     return 1
             self._cb = ALLREDUCE_FN(_cb)
             rc = L.hmc_ctx_create_hostcoll(device, rank, world, self._cb, None, C.byref(h))
-        elif world > 1:
+        elif rccl_comm is not None:
+            rc = L.hmc_ctx_create_comm(device, C.c_void_p(rccl_comm), C.byref(h))
+        elif world > 1 or unique_id is not None:
             uid = C.create_string_buffer(unique_id, 128)
             rc = L.hmc_ctx_create_dist(device, rank, world, C.cast(uid, C.c_void_p), C.byref(h))
         else:
             rc = L.hmc_ctx_create(device, C.byref(h))
         self._h = h
         self.rank, self.world = rank, world
+        self._comm_keepalive = rccl_comm
         if rc:
             msg = L.hmc_ctx_error(h).decode() if h else ""
             self.close()
@@ -154,6 +159,11 @@ class HaploModel:
     def set_estep_shape(self, waves_per_individual: int = 0, individuals_per_cu: int = 0):
         """E-step launch shape (results are identical for every shape)."""
         self._check(lib().hmc_set_estep_shape(self._h, waves_per_individual, individuals_per_cu))
+
+    def set_reduction(self, mode: str):
+        """Cross-rank sums: "ordered" (default, bit-exact with one rank) or
+        "allreduce" (one collective per mining level, last-bit drift)."""
+        self._check(lib().hmc_set_reduction(self._h, {"ordered": 0, "allreduce": 1}[mode]))
 
     def set_estep_mode(self, mode: int):
         """0 = split E-step (structure pass + value pass, default), 1 = fused kernel."""

@@ -43,6 +43,12 @@ int hmc_ctx_create(int device, hmc_ctx **out);
  * sharded in contiguous blocks; the M-step all-reduces per-level sums. */
 int hmc_rccl_unique_id(void *out128);
 int hmc_ctx_create_dist(int device, int rank, int world, const void *unique_id, hmc_ctx **out);
+/* Multi-GPU on a communicator the caller already owns (an ncclComm_t, RCCL):
+ * rank and world are taken from it; hmc_ctx_destroy leaves it alive.  The
+ * seam of SURVEY.md §8(b) (hmc_ctx_create(device, rccl_comm_or_null, ...)),
+ * replacing HaploModel's construction (HaploModel.h:29) inside a host that
+ * runs its own RCCL. */
+int hmc_ctx_create_comm(int device, void *rccl_comm, hmc_ctx **out);
 /* Same sharding with a caller-supplied collective instead of RCCL: fn must
  * sum `n` doubles element-wise across ranks in place and return 0.  Lets
  * several ranks share one GPU (tests) or run over any host transport. */
@@ -50,6 +56,16 @@ typedef int (*hmc_allreduce_fn)(double *buf, size_t n, void *user);
 int hmc_ctx_create_hostcoll(int device, int rank, int world, hmc_allreduce_fn fn, void *user, hmc_ctx **out);
 void hmc_ctx_destroy(hmc_ctx *ctx);
 const char *hmc_ctx_error(const hmc_ctx *ctx);
+
+/* Cross-rank sums of a sharded run (M-step candidate sums per mining level,
+ * log-likelihood, total sample weight).  0 (default) = ordered: rank r
+ * continues each running sum of ranks 0..r-1 over its contiguous block of
+ * items, which reproduces the reference's sequential sums
+ * (PatternManager.cpp:254-262, HaploModel.cpp:110, HaploData.cpp:120-126) bit
+ * for bit — W chained steps per mining level; 1 = all-reduce of per-rank
+ * partial sums (one collective, sums reassociated: last-bit drift, which can
+ * flip a pattern at the min_freq threshold). */
+int hmc_set_reduction(hmc_ctx *ctx, int mode);
 
 /* HaploModel public parameters (HaploModel.h:15-26; CLI defaults HMC.cpp:35-47).
  * min_freq_abs > 0 overrides min_freq exactly as HaploModel::findPatterns does

@@ -16,6 +16,7 @@ from hmc_amd import synth  # noqa: E402
 def main():
     rank, out = int(sys.argv[1]), sys.argv[2]
     variant = sys.argv[3] if len(sys.argv) > 3 else "MV"
+    reduction = sys.argv[4] if len(sys.argv) > 4 else "ordered"
     dist.init_process_group("gloo", rank=rank, world_size=2)
 
     def allreduce(arr):
@@ -25,6 +26,7 @@ def main():
     p = synth.founder_mosaic(80, 60, A=3, missing=0.05, seed=5)
     m = hmc_amd.HaploModel(device=0, rank=rank, world=2, host_allreduce=allreduce)
     m.max_iteration = 10
+    m.set_reduction(reduction)
     if variant == "MC":
         m.model = "MC"
     elif variant == "BYNUM":

@@ -1,33 +1,46 @@
 #!/bin/bash
 # Profile set for one round (run on the GPU box from the repo root):
-#   PMC FETCH_SIZE / WRITE_SIZE passes (separate runs) on the dominant kernel
-#   estep_values, kernel-trace stats, and the bench line, all of the same
-#   command.  Summaries are copied to profiles/<TAG>/ and
-#   profiles/pmc_estep_values.json (read by bench.py for roofline.traffic).
-# usage: bash tools/profile_round.sh OUTDIR TAG   (copy OUTDIR/commit/TAG to profiles/TAG afterwards)
+#   HBM traffic of the dominant kernel estep_values from two separate PMC
+#   passes (FETCH_SIZE, WRITE_SIZE) over the bench command itself, the
+#   kernel-trace stats of the same command, and SQ counter passes (instruction
+#   mix, LDS waits / bank conflicts, wave cycles) on a short run.
+# usage: bash tools/profile_round.sh OUTDIR TAG CONFIG
+#   -> OUTDIR/commit/TAG/ (copy to profiles/TAG afterwards); the PMC summary is
+#      profiles/TAG/pmc_estep_values_cfgCONFIG.json, which bench.py reads.
 set -euo pipefail
 OUT=${1:-gpurun_out/prof}
-TAG=${2:-r01}
+TAG=${2:-r02}
+CFG=${3:-3}
 DEST=$OUT/commit/$TAG
 mkdir -p "$OUT" "$DEST"
 export TMPDIR=/tmp
 K=estep_values
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex $K --output-format csv \
-  -d "$OUT/pmc_fetch" -o f -- python3 bench.py --no-cpu-baseline > "$OUT/pmc_fetch.log" 2>&1
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex $K --output-format csv \
-  -d "$OUT/pmc_write" -o w -- python3 bench.py --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1
+BENCH="bench.py --config $CFG --no-cpu-baseline"
+echo "[profile] FETCH_SIZE pass" >&2
+timeout -s KILL 500 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex $K --output-format csv \
+  -d "$OUT/pmc_fetch" -o f -- python3 $BENCH > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
+echo "[profile] WRITE_SIZE pass" >&2
+timeout -s KILL 500 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex $K --output-format csv \
+  -d "$OUT/pmc_write" -o w -- python3 $BENCH > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err"
 FC=$(find "$OUT/pmc_fetch" -name "*counter_collection.csv" | head -n 1)
 WC=$(find "$OUT/pmc_write" -name "*counter_collection.csv" | head -n 1)
-python3 tools/pmc_traffic.py "$FC" "$WC" \
-  $K "$OUT/pmc_$K.json" "rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE (separate passes) --kernel-include-regex $K -- python3 bench.py --no-cpu-baseline"
-cp "$OUT/pmc_$K.json" profiles/pmc_$K.json
-cp "$OUT/pmc_$K.json" "$DEST/"
-cp "$FC" "$DEST/pmc_fetch_size.csv"
-cp "$WC" "$DEST/pmc_write_size.csv"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-  python3 bench.py --no-cpu-baseline > "$OUT/trace.log" 2>&1
-cp "$(find "$OUT/trace" -name "*kernel_stats.csv" | head -n 1)" "$DEST/kernel_stats.csv"
-tail -1 "$OUT/trace.log" > "$DEST/bench_under_rocprof.json"
-timeout -k 10 600 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
-tail -1 "$OUT/bench.json" > "$DEST/bench.json"
-tail -1 "$OUT/bench.json"
+python3 tools/pmc_traffic.py "$FC" "$WC" $K "$DEST/pmc_${K}_cfg$CFG.json" \
+  "rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE (separate passes) --kernel-include-regex $K -- python3 $BENCH" \
+  "$OUT/pmc_fetch.json"
+cp "$FC" "$DEST/pmc_fetch_size_cfg$CFG.csv"
+cp "$WC" "$DEST/pmc_write_size_cfg$CFG.csv"
+echo "[profile] kernel trace" >&2
+timeout -s KILL 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+  python3 $BENCH > "$OUT/trace.json" 2> "$OUT/trace.err"
+cp "$(find "$OUT/trace" -name "*kernel_stats.csv" | head -n 1)" "$DEST/kernel_stats_cfg$CFG.csv"
+tail -1 "$OUT/trace.json" > "$DEST/bench_under_rocprof_cfg$CFG.json"
+SHORT="bench.py --config $CFG --no-cpu-baseline --steps 2 --warmup 0"
+for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU" \
+         "SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM"; do
+  N=$(echo "$P" | awk '{print $1}')
+  echo "[profile] SQ pass $N" >&2
+  timeout -s KILL 300 rocprofv3 --pmc $P --kernel-include-regex $K --output-format csv -d "$OUT/sq_$N" -o s -- \
+    python3 $SHORT > "$OUT/sq_$N.json" 2> "$OUT/sq_$N.err"
+  cp "$(find "$OUT/sq_$N" -name "*counter_collection.csv" | head -n 1)" "$DEST/sq_${N}_cfg$CFG.csv"
+done
+echo "[profile] done" >&2
