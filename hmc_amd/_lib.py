@@ -42,6 +42,8 @@ _SIGS = [
     ("hmc_ctx_create_dist", _i, [_i, _i, _i, _vp, _P(_vp)]),
     ("hmc_ctx_create_hostcoll", _i, [_i, _i, _i, ALLREDUCE_FN, _vp, _P(_vp)]),
     ("hmc_ctx_create_comm", _i, [_i, _vp, _P(_vp)]),
+    ("hmc_rccl_comm_init", _i, [_i, _i, _i, _vp, _P(_vp)]),
+    ("hmc_rccl_comm_destroy", _i, [_vp]),
     ("hmc_set_reduction", _i, [_vp, _i]),
     ("hmc_ctx_destroy", None, [_vp]),
     ("hmc_ctx_error", _cp, [_vp]),
@@ -73,6 +75,8 @@ _SIGS = [
     ("hmc_haplocomp", _i, [_vp, _P(_d), _P(_d), _P(_d)]),
     ("hmc_set_model", _i, [_vp, _cp, _i]),
     ("hmc_set_num_patterns", _i, [_vp, _i]),
+    ("hmc_set_exact_estimate", _i, [_vp, _i]),
+    ("hmc_last_exact_stats", _i, [_vp, _P(_i), _P(_u64), _P(_d)]),
     ("hmc_parse_file", _i, [_cp, _cp, _cp, _P(_i), _P(_i), _P(C.c_int32), _cp]),
     ("hmc_load_file", _i, [_vp, _cp, _cp, _cp]),
     ("hmc_write_file", _i, [_vp, _cp, _cp, _cp]),

@@ -27,6 +27,7 @@
 #include "haplofile.hpp"
 #include "hmc_internal.hpp"
 #include "mstep.hpp"
+#include "exact.hpp"
 #include "select.hpp"
 
 namespace hmc {
@@ -262,8 +263,8 @@ struct Ctx {
   int min_len = 1, max_len = 30, sample_size = 10;
   // tuning
   int fcap = 2048, waves = 0;
-  int lds_waves_per_cu = 4;  // E-step individuals (blocks) sharing one CU's 160 KiB LDS
-  int estep_nw = 3;          // E-step waves per individual
+  int lds_waves_per_cu = 8;  // E-step individuals (blocks) sharing one CU's 160 KiB LDS
+  int estep_nw = 2;          // E-step waves per individual (shape sweep at cfg 3: 2:8 beats 3:4 by 25%)
   uint64_t trace_bytes = 0;
 
   Panel pan;
@@ -532,12 +533,33 @@ struct Ctx {
   }
 
   // --------------------------------------------------------------- mining --
+  // The E-step's record and trace stores hold most of HBM between E-steps;
+  // a miner allocation that fails gives them back and tries again.
+  template <class T>
+  hipError_t ensure_or_release(DevBuf<T> &b, size_t n) {
+    hipError_t e = b.ensure(n);
+    if (e == hipErrorOutOfMemory && (d_trace.p || d_rec.p)) {
+      (void)hipGetLastError();
+      d_trace.release();
+      d_rec.release();
+      e = b.ensure(n);
+    }
+    return e;
+  }
+
   int grow_nodes(size_t need, size_t used) {
     if (need <= node_cap) return HMC_OK;
     // doubling (each growth re-maps and copies 15 arrays)
     size_t cap = std::max<size_t>(need, 2 * node_cap);
     hipError_t e;
-#define G(b) if ((e = b.grow_keep(cap, used, st))) return hipfail(e, "grow_nodes");
+#define G(b)                                                                 \
+  if ((e = b.grow_keep(cap, used, st)) == hipErrorOutOfMemory && (d_trace.p || d_rec.p)) { \
+    (void)hipGetLastError();                                                   \
+    d_trace.release();                                                         \
+    d_rec.release();                                                           \
+    e = b.grow_keep(cap, used, st);                                            \
+  }                                                                            \
+  if (e) return hipfail(e, "grow_nodes");
     G(n_parent) G(n_start) G(n_child_base) G(n_link) G(n_allele) G(n_flags) G(n_freq) G(n_prefix) G(n_tp) G(n_sum)
     G(n_cnt) G(n_size) G(n_pos) G(n_list_off) G(n_region)
 #undef G
@@ -602,7 +624,409 @@ struct Ctx {
   // extension the tree does not have, the tree is mined again deeper.
   static constexpr int MINE_RETRY = 1000;
   int bynum_need = 0;  // round the replay needed beyond the mined tree
+  // ------------------------------------------------------- exact M-step --
+  // PatternManager::estimatePatterns (PatternManager.cpp:364-410) and
+  // extendPatterns (:412-438) on the host, HaploBuilder::estimateFrequency
+  // (HaploBuilder.cpp:274-450) on the device (exact.hip) once per round.
+  struct Cands {  // candidate patterns: alleles as allele indices
+    std::vector<int32_t> start, len;
+    std::vector<int64_t> aoff;
+    std::vector<uint8_t> al;
+    std::vector<double> freq, prefix, tp;
+    size_t size() const { return start.size(); }
+    const uint8_t *alleles(size_t i) const { return al.data() + aoff[i]; }
+    void push(int32_t s, int32_t l, const uint8_t *a, uint8_t extra, bool with_extra, double f, double pre = 1.0,
+              double t = 1.0) {
+      start.push_back(s);
+      len.push_back(l);
+      aoff.push_back((int64_t)al.size());
+      al.insert(al.end(), a, a + (with_extra ? l - 1 : l));
+      if (with_extra) al.push_back(extra);
+      freq.push_back(f);
+      prefix.push_back(pre);
+      tp.push_back(t);
+    }
+  };
+  bool exact_estimate = false;
+  bool table_on_host = false;  // the pattern table came from the exact M-step (alleles below)
+  Cands ht;                    // that table, id order
+  std::vector<int32_t> ht_succ;  // [P][amax]
+  DevBuf<int32_t> d_tr_child, d_tr_data, d_tr_root, d_xstatus, d_xfmax;
+  DevBuf<unsigned long long> d_xre, d_xacc;
+  DevBuf<double> d_xscr;
+  int tr_maxd = 0;
+  int exact_rounds = 0;
+  uint64_t exact_candidates = 0;
+
+  // The current table with allele strings (mined: from the candidate tree;
+  // exact: the host copy).
+  int table_to_host(Cands &c, std::vector<int32_t> &succ) {
+    if (table_on_host) {
+      c = ht;
+      succ = ht_succ;
+      return HMC_OK;
+    }
+    const int P = this->P, A = pan.amax;
+    std::vector<int32_t> st(P), ln(P), node(P);
+    std::vector<double> fr(P), pre(P), tp(P);
+    std::vector<uint32_t> su((size_t)P * A);
+    hipError_t e;
+    if ((e = hipMemcpyAsync(st.data(), t_start.p, (size_t)P * 4, hipMemcpyDeviceToHost, this->st)) ||
+        (e = hipMemcpyAsync(ln.data(), t_len.p, (size_t)P * 4, hipMemcpyDeviceToHost, this->st)) ||
+        (e = hipMemcpyAsync(node.data(), t_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, this->st)) ||
+        (e = hipMemcpyAsync(fr.data(), t_freq.p, (size_t)P * 8, hipMemcpyDeviceToHost, this->st)) ||
+        (e = hipMemcpyAsync(pre.data(), t_prefix.p, (size_t)P * 8, hipMemcpyDeviceToHost, this->st)) ||
+        (e = hipMemcpyAsync(tp.data(), t_tp.p, (size_t)P * 8, hipMemcpyDeviceToHost, this->st)) ||
+        (e = hipMemcpyAsync(su.data(), t_succ.p, su.size() * 4, hipMemcpyDeviceToHost, this->st)) ||
+        (e = hipStreamSynchronize(this->st)))
+      return hipfail(e, "exact: table");
+    if (node_cap == 0) return fail(HMC_EUNSUPPORTED, "exact M-step needs a mined or estimated table (allele strings)");
+    int nmax = 0;
+    for (int i = 0; i < P; ++i) nmax = std::max(nmax, node[i] + 1);
+    std::vector<int32_t> par(nmax);
+    std::vector<uint8_t> alc(nmax);
+    if (nmax && ((e = hipMemcpyAsync(par.data(), n_parent.p, (size_t)nmax * 4, hipMemcpyDeviceToHost, this->st)) ||
+                 (e = hipMemcpyAsync(alc.data(), n_allele.p, (size_t)nmax, hipMemcpyDeviceToHost, this->st)) ||
+                 (e = hipStreamSynchronize(this->st))))
+      return hipfail(e, "exact: table");
+    c = Cands();
+    std::vector<uint8_t> buf;
+    for (int i = 0; i < P; ++i) {
+      buf.assign(ln[i], 0);
+      int32_t v = node[i];
+      for (int k = ln[i] - 1; k >= 0; --k) {
+        buf[k] = alc[v];
+        v = par[v];
+      }
+      c.push(st[i], ln[i], buf.data(), 0, false, fr[i], pre[i], tp[i]);
+    }
+    succ.resize((size_t)P * A);
+    for (size_t i = 0; i < su.size(); ++i) succ[i] = su[i] == NONE ? -1 : (int32_t)su[i];
+    return HMC_OK;
+  }
+
+  // One round: HaploBuilder::estimateFrequency(patterns) for c[b, e) —
+  // ForwardPatternTree, then every individual of the shard through the
+  // structure pass (forward links), exact_fb and exact_walk; fixed-point
+  // sums over ranks; freq / prefix / tp as at HaploBuilder.cpp:317-331.
+  int estimate_round(Cands &c, size_t b, size_t e) {
+    const int L = pan.L, A = pan.amax, N = pan.N;
+    std::vector<int32_t> child, data, root(L, -1);
+    int maxd = 0;
+    auto new_node = [&]() {
+      child.insert(child.end(), A, -1);
+      data.push_back(-1);
+      return (int32_t)data.size() - 1;
+    };
+    for (size_t k = b; k < e; ++k) {  // ForwardPatternTree::addPattern (PatternTree.cpp:188-212)
+      const int s = c.start[k];
+      if (root[s] < 0) root[s] = new_node();
+      int32_t u = root[s];
+      const uint8_t *al = c.alleles(k);
+      for (int q = 0; q < c.len[k]; ++q) {
+        if (al[q] >= A) return fail(HMC_EUNSUPPORTED, "exact M-step: pattern with a missing allele");
+        int32_t v = child[(size_t)u * A + al[q]];
+        if (v < 0) {
+          v = new_node();
+          child[(size_t)u * A + al[q]] = v;
+        }
+        u = v;
+      }
+      data[u] = (int32_t)(k - b);
+      maxd = std::max(maxd, (int)c.len[k]);
+    }
+    const size_t nc = e - b;
+    hipError_t er;
+    if ((er = d_tr_child.ensure(std::max<size_t>(child.size(), 1))) || (er = d_tr_data.ensure(std::max<size_t>(data.size(), 1))) ||
+        (er = d_tr_root.ensure(L)) || (er = d_xacc.ensure(2 * std::max<size_t>(nc, 1))) ||
+        (!child.empty() && (er = hipMemcpyAsync(d_tr_child.p, child.data(), child.size() * 4, hipMemcpyHostToDevice, st))) ||
+        (!data.empty() && (er = hipMemcpyAsync(d_tr_data.p, data.data(), data.size() * 4, hipMemcpyHostToDevice, st))) ||
+        (er = hipMemcpyAsync(d_tr_root.p, root.data(), (size_t)L * 4, hipMemcpyHostToDevice, st)) ||
+        (er = hipMemsetAsync(d_xacc.p, 0, 2 * nc * 8, st)))
+      return hipfail(er, "exact: trie");
+    tr_maxd = maxd;
+    // the individuals of the shard, heaviest first, through the split machinery
+    const int n = nloc();
+    if ((er = d_xstatus.ensure(n)) || (er = d_xre.ensure(n)) || (er = d_xfmax.ensure(n))) return hipfail(er, "exact");
+    std::vector<int32_t> order(n);
+    for (int q = 0; q < n; ++q) order[q] = q;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return h_cost[x] > h_cost[y]; });
+    xacc_nc = nc;
+    int rc;
+    while (true) {
+      rc = estep_split(order, true);
+      if (rc != ESTEP_RESTART) break;
+      if ((er = hipMemsetAsync(d_xacc.p, 0, 2 * nc * 8, st))) return hipfail(er, "exact");
+    }
+    if (rc) return rc;
+    std::vector<unsigned long long> acc(2 * nc);
+    if ((er = hipMemcpyAsync(acc.data(), d_xacc.p, acc.size() * 8, hipMemcpyDeviceToHost, st)) ||
+        (er = hipStreamSynchronize(st)))
+      return hipfail(er, "exact");
+    if (multi()) {  // integer sums over ranks, exactly: 32-bit halves through the double collective
+      std::vector<double> h(4 * nc);
+      for (size_t i = 0; i < 2 * nc; ++i) {
+        h[2 * i] = (double)(acc[i] & 0xFFFFFFFFull);
+        h[2 * i + 1] = (double)(acc[i] >> 32);
+      }
+      if ((rc = allreduce_host(h.data(), h.size()))) return rc;
+      for (size_t i = 0; i < 2 * nc; ++i) acc[i] = ((unsigned long long)h[2 * i + 1] << 32) + (unsigned long long)h[2 * i];
+    }
+    for (size_t k = 0; k < nc; ++k) {  // HaploBuilder.cpp:317-331
+      double freq = std::min((double)acc[k] / EXACT_FIXED_SCALE, (double)N);
+      const double pre = std::min((double)acc[nc + k] / EXACT_FIXED_SCALE, (double)N);
+      freq = std::min(freq, pre);
+      c.freq[b + k] = freq / N;
+      c.prefix[b + k] = pre / N;
+      const double t = pre > 0 ? freq / pre : freq / N;
+      c.tp[b + k] = t < 1.0 ? t : 1.0;  // HaploPattern::setTransitionProb (HaploPattern.h:47)
+    }
+    ++exact_rounds;
+    exact_candidates += nc;
+    return HMC_OK;
+  }
+  size_t xacc_nc = 0;
+
+  // exact_fb + exact_walk over the group d_order2[0, k) (structure records in place)
+  int exact_group(const int32_t *ids, int k) {
+    const int L = pan.L;
+    int dev_cu = 256;
+    hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, device);
+    hipError_t e;
+    ExactArgs x;
+    x.L = L;
+    x.head_len = head_len;
+    x.width = pan.amax;
+    x.order = d_order2.p;
+    x.n_order = k;
+    x.rec = d_rec.p;
+    x.rec_off = d_rec_off.p;
+    x.status = d_xstatus.p;
+    x.gprob = d_total.p;
+    x.x = d_trace.p;
+    x.x_base = d_tbase.p;
+    x.x_off = d_loc_off.p;
+    x.tr_child = d_tr_child.p;
+    x.tr_data = d_tr_data.p;
+    x.tr_root = d_tr_root.p;
+    x.max_depth = tr_maxd;
+    x.head_al = d_head_al.p;
+    x.acc_freq = d_xacc.p;
+    x.acc_prefix = d_xacc.p + xacc_nc;
+    if ((e = launch_exact_fb(x, std::max(1, std::min(k, dev_cu * 8)), st))) return hipfail(e, "exact_fb");
+    const int n = nloc();
+    std::vector<int32_t> xs(n), fm(n);
+    if ((e = hipMemcpyAsync(xs.data(), d_xstatus.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
+        (e = hipMemcpyAsync(fm.data(), d_xfmax.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
+        (e = hipStreamSynchronize(st)))
+      return hipfail(e, "exact_fb");
+    int fmax = 1;
+    for (int q = 0; q < k; ++q) {
+      if (xs[ids[q]] == EST_NEEDS_EXACT)
+        return fail(HMC_EUNSUPPORTED, "exact M-step: a forward likelihood underflows (individual %d)", i0 + ids[q]);
+      fmax = std::max(fmax, fm[ids[q]]);
+    }
+    x.fmax = fmax;
+    x.scratch_stride = (size_t)(tr_maxd + 1) * 3 * fmax + tr_maxd + 2;
+    const long long items = (long long)k * L;
+    const int grid = (int)std::max<long long>(1, std::min<long long>(items, (long long)dev_cu * 16));
+    if ((e = d_xscr.ensure(x.scratch_stride * grid))) return hipfail(e, "exact scratch");
+    x.scratch = d_xscr.p;
+    hipEventRecord(ev[0], st);
+    if ((e = launch_exact_walk(x, grid, st))) return hipfail(e, "exact_walk");
+    hipEventRecord(ev[1], st);
+    if ((e = hipStreamSynchronize(st))) return hipfail(e, "exact_walk");
+    float ms = 0;
+    hipEventElapsedTime(&ms, ev[0], ev[1]);
+    ms_walk += ms;
+    return HMC_OK;
+  }
+  double ms_walk = 0;
+
+  // Successors of a pattern set (PatternManager::initialize, :308-317):
+  // successor[j] = the longest stored suffix of (pattern + allele j) with start
+  // >= the pattern's start; found through a trie of the set per start locus.
+  void host_successors(const Cands &c, std::vector<int32_t> &succ) {
+    const int L = pan.L, A = pan.amax;
+    const size_t P = c.size();
+    std::vector<int32_t> child, data, root(L, -1);
+    auto new_node = [&]() {
+      child.insert(child.end(), A, -1);
+      data.push_back(-1);
+      return (int32_t)data.size() - 1;
+    };
+    for (size_t k = 0; k < P; ++k) {
+      const int s = c.start[k];
+      if (root[s] < 0) root[s] = new_node();
+      int32_t u = root[s];
+      const uint8_t *al = c.alleles(k);
+      for (int q = 0; q < c.len[k]; ++q) {
+        int32_t v = child[(size_t)u * A + al[q]];
+        if (v < 0) {
+          v = new_node();
+          child[(size_t)u * A + al[q]] = v;
+        }
+        u = v;
+      }
+      data[u] = (int32_t)k;
+    }
+    succ.assign(P * A, -1);
+    for (size_t k = 0; k < P; ++k) {
+      const int s = c.start[k], ln = c.len[k], e = s + ln;
+      if (e >= L) continue;
+      const uint8_t *al = c.alleles(k);
+      for (int j = 0; j < h_anum[e]; ++j) {
+        int32_t res = -1;
+        for (int s2 = s; s2 <= e && res < 0; ++s2) {  // longest first
+          int32_t u = root[s2];
+          for (int q = s2 - s; q < ln && u >= 0; ++q) u = child[(size_t)u * A + al[q]];
+          if (u >= 0) u = child[(size_t)u * A + j];
+          if (u >= 0) res = data[u];
+        }
+        succ[k * A + j] = res;
+      }
+    }
+  }
+
+  // Install a host-built table (id order) on the device: SoA, successors,
+  // heads (PatternManager.cpp:293-318).
+  int install_host_table(Cands &c, std::vector<int32_t> &succ) {
+    const int P = (int)c.size(), A = pan.amax;
+    if ((int64_t)P > INT32_MAX) return fail(HMC_EUNSUPPORTED, "too many patterns");
+    int rc = alloc_table(std::max(P, 1));
+    if (rc) return rc;
+    std::vector<uint8_t> last(P);
+    std::vector<int32_t> node(P, -1);
+    std::vector<uint32_t> su((size_t)P * A);
+    for (int i = 0; i < P; ++i) last[i] = c.alleles(i)[c.len[i] - 1];
+    for (size_t i = 0; i < su.size(); ++i) su[i] = succ[i] < 0 ? NONE : (uint32_t)succ[i];
+    hipError_t e;
+    if (P && ((e = hipMemcpyAsync(t_start.p, c.start.data(), (size_t)P * 4, hipMemcpyHostToDevice, st)) ||
+              (e = hipMemcpyAsync(t_len.p, c.len.data(), (size_t)P * 4, hipMemcpyHostToDevice, st)) ||
+              (e = hipMemcpyAsync(t_node.p, node.data(), (size_t)P * 4, hipMemcpyHostToDevice, st)) ||
+              (e = hipMemcpyAsync(t_freq.p, c.freq.data(), (size_t)P * 8, hipMemcpyHostToDevice, st)) ||
+              (e = hipMemcpyAsync(t_prefix.p, c.prefix.data(), (size_t)P * 8, hipMemcpyHostToDevice, st)) ||
+              (e = hipMemcpyAsync(t_tp.p, c.tp.data(), (size_t)P * 8, hipMemcpyHostToDevice, st)) ||
+              (e = hipMemcpyAsync(t_last.p, last.data(), (size_t)P, hipMemcpyHostToDevice, st)) ||
+              (e = hipMemcpyAsync(t_succ.p, su.data(), su.size() * 4, hipMemcpyHostToDevice, st)) ||
+              (e = hipStreamSynchronize(st))))
+      return hipfail(e, "exact: install table");
+    this->P = P;
+    // head list: start 0, length head_len, id order (PatternManager.cpp:304-306)
+    std::vector<std::pair<uint32_t, uint8_t>> heads;
+    h_head_ids.clear();
+    h_head_al.clear();
+    std::vector<uint8_t> tab;
+    if (head_len > 1) tab.assign((size_t)std::max(P, 1) * head_len, 0);
+    for (int i = 0; i < P; ++i)
+      if (c.start[i] == 0 && c.len[i] == head_len) {
+        heads.push_back({(uint32_t)i, c.alleles(i)[head_len - 1]});
+        if (head_len > 1) {
+          h_head_ids.push_back((uint32_t)i);
+          h_head_al.insert(h_head_al.end(), c.alleles(i), c.alleles(i) + head_len);
+          std::copy(c.alleles(i), c.alleles(i) + head_len, tab.begin() + (size_t)i * head_len);
+        }
+      }
+    if (head_len > 1 && ((e = d_head_al.ensure(tab.size())) ||
+                         (e = hipMemcpyAsync(d_head_al.p, tab.data(), tab.size(), hipMemcpyHostToDevice, st)) ||
+                         (e = hipStreamSynchronize(st))))
+      return hipfail(e, "exact: heads");
+    if ((rc = set_heads(heads))) return rc;
+    ht = c;
+    ht_succ = succ;
+    table_on_host = true;
+    have_model = true;
+    return HMC_OK;
+  }
+
+  // PatternManager::estimatePatterns (PatternManager.cpp:364-410).
+  int estimate_patterns(int *P_out, uint64_t *rm_out) {
+    if (!have_estep) return fail(HMC_EARG, "exact M-step needs an E-step first");
+    if (num_patterns > 0 && model != 1)
+      return fail(HMC_EUNSUPPORTED, "exact M-step after findPatternByNum (num_patterns > 0)");
+    hipEventRecord(ev[4], st);
+    const int L = pan.L;
+    int mxl = max_len <= 0 ? L : max_len;  // m_max_len / m_min_len of the last findPatternByFreq
+    int mnl = std::max(min_len, 1);
+    mxl = std::max(mxl, mnl);
+    double mf = current_min_freq();
+    if (model == 1) {  // findPatternBlock: m_min_freq = -1 (PatternManager.cpp:75-88)
+      mnl = mxl = std::max(1, mc_order + 1);
+      mf = -1.0;
+    }
+    exact_rounds = 0;
+    exact_candidates = 0;
+    ms_walk = 0;
+    Cands cur;
+    std::vector<int32_t> succ;
+    int rc = table_to_host(cur, succ);
+    if (rc) return rc;
+    const int A = pan.amax;
+    if (mf < 0) {  // estimateFrequency() (:347-362): re-estimate in place, ids and successors unchanged
+      if ((rc = estimate_round(cur, 0, cur.size()))) return rc;
+      if ((rc = install_host_table(cur, succ))) return rc;
+    } else {
+      Cands all;
+      std::vector<size_t> seeds;
+      for (size_t i = 0; i < cur.size(); ++i) {
+        all.push(cur.start[i], cur.len[i], cur.alleles(i), 0, false, cur.freq[i], cur.prefix[i], cur.tp[i]);
+        const int s = cur.start[i], e = s + cur.len[i];
+        if (e < L && cur.len[i] < mxl)
+          for (int j = 0; j < h_anum[e]; ++j) {
+            const int32_t sj = succ[i * A + j];
+            if (sj < 0 || cur.start[sj] != s) {  // the extension is not stored: a seed
+              all.push(s, cur.len[i] + 1, cur.alleles(i), (uint8_t)j, true, cur.freq[i]);
+              seeds.push_back(all.size() - 1);
+            }
+          }
+      }
+      size_t rb = 0, re = all.size();
+      std::vector<uint8_t> buf;
+      while (rb < re) {
+        if ((rc = estimate_round(all, rb, re))) return rc;
+        const size_t nb = all.size();
+        for (int level = 0; level < 4; ++level) {  // extendPatterns (:412-438)
+          std::vector<size_t> ns;
+          for (size_t si : seeds) {
+            const int s = all.start[si], ln = all.len[si], e = s + ln;
+            if (e < L && ln < mxl && all.freq[si] >= mf) {
+              buf.assign(all.alleles(si), all.alleles(si) + ln);
+              const double f = all.freq[si];
+              for (int j = 0; j < h_anum[e]; ++j) {
+                all.push(s, ln + 1, buf.data(), (uint8_t)j, true, f);
+                ns.push_back(all.size() - 1);
+              }
+            }
+          }
+          seeds.swap(ns);
+        }
+        rb = nb;
+        re = all.size();
+      }
+      Cands kept;  // (:396-408)
+      for (size_t i = 0; i < all.size(); ++i)
+        if (all.freq[i] >= mf || all.len[i] <= mnl)
+          kept.push(all.start[i], all.len[i], all.alleles(i), 0, false, all.freq[i], all.prefix[i], all.tp[i]);
+      std::vector<int32_t> ksucc;
+      host_successors(kept, ksucc);
+      if ((rc = install_host_table(kept, ksucc))) return rc;
+    }
+    hipEventRecord(ev[5], st);
+    hipError_t e;
+    if ((e = hipStreamSynchronize(st))) return hipfail(e, "exact");
+    float ms = 0;
+    hipEventElapsedTime(&ms, ev[4], ev[5]);
+    ms_m = ms;
+    if (P_out) *P_out = P;
+    if (rm_out) *rm_out = 0;  // no candidate x item scans: the cost is in the trie walks
+    return HMC_OK;
+  }
+
   int mine(int *P_out, uint64_t *rm_out) {
+    // HaploModel.cpp:140-144: after an E-step, --exact-estimate re-estimates
+    // (estimatePatterns) instead of re-mining the samples
+    if (exact_estimate && have_samples && have_model) return estimate_patterns(P_out, rm_out);
+    table_on_host = false;
     if (!(num_patterns > 0 && model != 1)) return mine_impl(P_out, rm_out, 0);
     int k = 8;
     while (true) {
@@ -661,8 +1085,8 @@ struct Ctx {
     while (true) {
       const int cb = lbeg[level], ce = lend[level], nlev = ce - cb;
       const int nxt = cur ^ 1;  // children's lists are written here during the count
-      if ((e = l_idx[nxt].ensure(std::max<unsigned long long>(next_total, 1)))) return hipfail(e, "mine lists");
-      if (genotype && (e = l_val[nxt].ensure(std::max<unsigned long long>(next_total, 1))))
+      if ((e = ensure_or_release(l_idx[nxt], std::max<unsigned long long>(next_total, 1)))) return hipfail(e, "mine lists");
+      if (genotype && (e = ensure_or_release(l_val[nxt], std::max<unsigned long long>(next_total, 1))))
         return hipfail(e, "mine lists");
       MineArgs a = mine_args(genotype);
       a.lout_idx = l_idx[nxt].p;
@@ -806,6 +1230,18 @@ struct Ctx {
       return hipfail(e, "mine");
     hipEventRecord(ev[5], st);
     if ((e = hipStreamSynchronize(st))) return hipfail(e, "mine");
+    // The matching lists of the genotype branch (M0) reach tens of GB at
+    // cfg 3 (R_M ~ 10^11 entries); give them back to the E-step's stores.
+    for (int k = 0; k < 2; ++k) {
+      if (l_idx[k].n * 4 > (4ull << 30)) l_idx[k].release();
+      if (l_val[k].n * 8 > (4ull << 30)) l_val[k].release();
+    }
+    if (getenv("HMC_DEBUG_MEM")) {
+      size_t fb = 0, tb = 0;
+      hipMemGetInfo(&fb, &tb);
+      fprintf(stderr, "[hmc] after mining: free %.1f GB of %.1f; nodes %.1f GB\n", fb / 1e9, tb / 1e9,
+              node_cap * 70.0 / 1e9);
+    }
     unsigned long long rm = 0;
     for (int k = 0; k < RM_SLOTS; ++k) rm += rm_slots[(size_t)k * 16];
     if (bynum_rounds > 0) rm = rm_bynum;  // the scans of the candidates the rounds generated
@@ -1145,10 +1581,15 @@ struct Ctx {
     size_t freeb = 0, totb = 0;
     hipMemGetInfo(&freeb, &totb);
     const double avail = (double)freeb + (double)d_trace.n * 4 + (double)d_rec.n * 4;
-    trace_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.45), 96ull << 30),
+    // (cfg 3's E1 with the M0 model needs ~2x HBM in records + traces; larger
+    // stores (fewer groups) measured no faster and crowd out the next M0)
+    trace_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.35), 96ull << 30),
                                       1ull << 20) / 4;
-    rec_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.25), 48ull << 30),
+    rec_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.25), 64ull << 30),
                                     1ull << 20) / 4;
+    if (getenv("HMC_DEBUG_MEM"))
+      fprintf(stderr, "[hmc] E-step: free %.1f GB, stores %.1f + %.1f GB, budgets trace %.1f rec %.1f GB\n",
+              freeb / 1e9, d_trace.n * 4 / 1e9, d_rec.n * 4 / 1e9, trace_budget * 4 / 1e9, rec_budget * 4 / 1e9);
     h_total.assign(n, 0.0);
     h_ncand.assign(n, 0);
     h_status.assign(n, 0);
@@ -1330,11 +1771,11 @@ struct Ctx {
     return HMC_OK;
   }
 
-  int read_status(const std::vector<int32_t> &ids, int k, bool ncand) {
+  int read_status(const std::vector<int32_t> &ids, int k, bool ncand, const int32_t *dstatus = nullptr) {
     // per-individual status (and candidate counts) of ids[0, k): whole arrays, small
     hipError_t e;
     const int n = nloc();
-    if ((e = hipMemcpyAsync(h_status.data(), d_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
+    if ((e = hipMemcpyAsync(h_status.data(), dstatus ? dstatus : d_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
         (ncand && (e = hipMemcpyAsync(h_ncand.data(), d_ncand.p, (size_t)n * 4, hipMemcpyDeviceToHost, st))) ||
         (e = hipStreamSynchronize(st)))
       return hipfail(e, "estep status");
@@ -1349,7 +1790,7 @@ struct Ctx {
     const int S = this->S(), n = nloc();
     int dev_cu = 256;
     hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, device);
-    const int G = std::max(1, std::min(waves > 0 ? waves : dev_cu * 8, n));
+    const int G = std::max(1, std::min(waves > 0 ? waves : dev_cu * std::max(8, lds_waves_per_cu), n));
     hipError_t e;
     size_t pos = 0;
     int batch = n;
@@ -1405,11 +1846,15 @@ struct Ctx {
 
   // Split E-step (estep_split.hip): structure pass, value pass, fused fallback
   // for individuals whose forward likelihood underflows.
-  int estep_split(const std::vector<int32_t> &order) {
+  // exact = true: the exact M-step's pass over the individuals (structure
+  // records with forward links, then exact_fb + exact_walk per group instead
+  // of the value pass and traceback; E-step outputs are left untouched).
+  int estep_split(const std::vector<int32_t> &order, bool exact = false) {
     const int S = this->S(), n = nloc(), L = pan.L;
+    int32_t *dstatus = exact ? d_xstatus.p : d_status.p;
     int dev_cu = 256;
     hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, device);
-    const int G = std::max(1, std::min(waves > 0 ? waves : dev_cu * 8, n));
+    const int G = std::max(1, std::min(waves > 0 ? waves : dev_cu * std::max(8, lds_waves_per_cu), n));
     hipError_t e;
     float ms = 0;
     std::vector<int32_t> pending(order), sset, rest;
@@ -1440,7 +1885,7 @@ struct Ctx {
           return rc;
       }
       const int hcap1 = next_pow2(2 * fcap), ccap1 = 8 * fcap;
-      const int bpc1 = std::max(lds_waves_per_cu, np > 4 * dev_cu ? 8 : 4);
+      const int bpc1 = np > 4 * dev_cu ? 8 : 4;  // structure pass: one wave per individual
       const int grid1 = std::max(1, std::min(np, dev_cu * bpc1));
       const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1);
       if ((e = d_scr1.ensure(per1 * grid1)) || (e = d_rec_off.ensure((size_t)n * (L + 1))) ||
@@ -1467,17 +1912,18 @@ struct Ctx {
       s1.rec_off = d_rec_off.p;
       s1.rec_need = d_rneed.p;
       s1.trace_need = d_tneed.p;
-      s1.status = d_status.p;
-      s1.re_count = d_re.p;
-      s1.fmax = d_fmax.p;
+      s1.status = dstatus;
+      s1.re_count = exact ? d_xre.p : d_re.p;
+      s1.fmax = exact ? d_xfmax.p : d_fmax.p;
       s1.max_states = d_maxst.p;
+      s1.exact = exact;
       hipEventRecord(ev[0], st);
       if ((e = launch_estep_structure(s1, grid1, st))) return hipfail(e, "estep_structure launch");
       hipEventRecord(ev[1], st);
       if ((e = hipMemcpyAsync(rneed.data(), d_rneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
           (e = hipMemcpyAsync(tneed.data(), d_tneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)))
         return hipfail(e, "estep_structure");
-      if ((rc = read_status(pending, np, false))) return rc;
+      if ((rc = read_status(pending, np, false, dstatus))) return rc;
       hipEventElapsedTime(&ms, ev[0], ev[1]);
       ms_s1 += ms;
       ++n_struct_passes;
@@ -1516,6 +1962,11 @@ struct Ctx {
         if ((e = hipMemcpyAsync(d_tbase.p, tb.data(), (size_t)n * 8, hipMemcpyHostToDevice, st)))
           return hipfail(e, "estep");
         if ((rc = upload_order(d_order2, sset.data() + pos, (int)k))) return rc;
+        if (exact) {
+          if ((rc = exact_group(sset.data() + pos, (int)k))) return rc;
+          pos += k;
+          continue;
+        }
         const int grid2 = std::max(1, std::min<int>(G, (int)k));
         const size_t per2 = estep_s2_scratch_bytes(fcap, S);
         if ((e = d_scr2.ensure(per2 * grid2))) return hipfail(e, "estep pass-2 scratch");
@@ -1879,6 +2330,22 @@ int hmc_ctx_create_comm(int device, void *rccl_comm, hmc_ctx **out) {
   return HMC_OK;
 }
 
+int hmc_rccl_comm_init(int device, int world, int rank, const void *unique_id, void **comm) {
+  if (!comm || !unique_id || world < 1 || rank < 0 || rank >= world) return HMC_EARG;
+  if (hipSetDevice(device) != hipSuccess) return HMC_EHIP;
+  ncclUniqueId id;
+  memcpy(&id, unique_id, sizeof id);
+  ncclComm_t c = nullptr;
+  if (ncclCommInitRank(&c, world, id, rank) != ncclSuccess) return HMC_ERCCL;
+  *comm = c;
+  return HMC_OK;
+}
+
+int hmc_rccl_comm_destroy(void *comm) {
+  if (!comm) return HMC_EARG;
+  return ncclCommDestroy((ncclComm_t)comm) == ncclSuccess ? HMC_OK : HMC_ERCCL;
+}
+
 int hmc_set_reduction(hmc_ctx *h, int mode) {
   if (!h || mode < 0 || mode > 1) return HMC_EARG;
   h->c.reduction = mode;
@@ -1966,6 +2433,20 @@ int hmc_last_estep_split(const hmc_ctx *h, double *structure_ms, double *values_
   if (values_ms) *values_ms = h->c.ms_s2;
   if (fallback_ms) *fallback_ms = h->c.ms_fb;
   if (n_fallback) *n_fallback = h->c.n_fallback;
+  return HMC_OK;
+}
+
+int hmc_set_exact_estimate(hmc_ctx *h, int on) {
+  if (!h) return HMC_EARG;
+  h->c.exact_estimate = on != 0;
+  return HMC_OK;
+}
+
+int hmc_last_exact_stats(const hmc_ctx *h, int *rounds, uint64_t *candidates, double *walk_ms) {
+  if (!h) return HMC_EARG;
+  if (rounds) *rounds = h->c.exact_rounds;
+  if (candidates) *candidates = h->c.exact_candidates;
+  if (walk_ms) *walk_ms = h->c.ms_walk;
   return HMC_OK;
 }
 
@@ -2122,7 +2603,7 @@ int hmc_write_file(hmc_ctx *h, const char *format, const char *path, const char 
 }
 
 int hmc_write_patterns(hmc_ctx *h, const char *path) {
-  if (!h || !path || !h->c.have_model || h->c.node_cap <= 0) return HMC_EARG;
+  if (!h || !path || !h->c.have_model || (h->c.node_cap <= 0 && !h->c.table_on_host)) return HMC_EARG;
   hmc::Ctx &c = h->c;
   const int P = c.P, L = c.pan.L;
   std::vector<int32_t> st(P), ln(P);
@@ -2209,7 +2690,12 @@ int hmc_get_patterns(hmc_ctx *h, int32_t *start, int32_t *len, double *freq, dou
       return c.hipfail(e, "get_patterns");
     for (size_t i = 0; i < s.size(); ++i) succ[i] = s[i] == hmc::NONE ? -1 : (int32_t)s[i];
   }
-  if (alleles && maxlen > 0) {
+  if (alleles && maxlen > 0 && c.table_on_host) {  // the exact M-step's table keeps its alleles on the host
+    for (int i = 0; i < P; ++i) {
+      int32_t *row = alleles + (size_t)i * maxlen;
+      for (int k = 0; k < maxlen; ++k) row[k] = k < ln[i] ? c.pan.symbol(st[i] + k, c.ht.alleles(i)[k]) : -1;
+    }
+  } else if (alleles && maxlen > 0) {
     // Rebuild allele strings from the candidate tree (parent chain) when the
     // table came from the miner; else only the last allele is known.
     std::vector<int32_t> par;
@@ -2278,6 +2764,7 @@ int hmc_set_patterns(hmc_ctx *h, int P, const int32_t *start, const int32_t *len
     return c.hipfail(e, "set_patterns");
   c.P = P;
   c.head_len = hl;
+  c.table_on_host = false;
   c.h_head_ids.clear();  // head alleles unknown: the E-step supports head_len 1 only here
   c.h_head_al.clear();
   c.node_cap = 0;  // allele strings are not known for an injected table

@@ -271,9 +271,9 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
     int fbig = 0;
     wsync();
     if (status == EST_OK) {
-      const unsigned long long words = 4 + 4ull * Fp + 1;
+      const unsigned long long words = 4 + 4ull * Fp + 1 + (a.exact ? 2ull * Fp : 0ull);
       rneed += (words + 1) & ~1ull;
-      tneed += trace_locus_words((unsigned long long)Fp, S);
+      tneed += a.exact ? 4ull * Fp + 2 : trace_locus_words((unsigned long long)Fp, S);
       const unsigned long long o = rec_alloc(a, rcur, rend, words);
       if (o + words > a.rec_cap) {
         counting = true;
@@ -287,6 +287,10 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
           Rtp[t] = a.mod.freq[lo] * a.mod.freq[hi];  // HaploPair.cpp:27
           Rhd[t] = (uint32_t)a.mod.last[lo] | (uint32_t)a.mod.last[hi] << 8 | 1u << 16 | (lo == hi ? 1u << 24 : 0u);
           Rcb[t] = 0;
+          if (a.exact) {  // head pairs' pattern ids (their alleles before head_len)
+            Rcb[Fp + 1 + t] = lo;
+            Rcb[2 * Fp + 1 + t] = hi;
+          }
         }
         if (lane == 0) {
           Rcb[Fp] = 0;
@@ -430,9 +434,10 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
         if (t < Fn) *Y.at(F_CB, t) = (uint32_t)(Cv + incl - m);
         Cv += __shfl(incl, 63);
       }
-      const unsigned long long words = 4 + 4ull * Fn + 1 + (unsigned long long)Cv + Fn;
+      const unsigned long long words =
+          4 + 4ull * Fn + 1 + (unsigned long long)Cv + Fn + (a.exact ? (unsigned long long)C + npairs : 0ull);
       rneed += (words + 1) & ~1ull;
-      tneed += trace_locus_words((unsigned long long)Fn, S);
+      tneed += a.exact ? 4ull * Fn + 2 : trace_locus_words((unsigned long long)Fn, S);
       const unsigned long long o = counting ? 0 : rec_alloc(a, rcur, rend, words);
       if (!counting && o + words > a.rec_cap) counting = true;
       uint32_t *R = a.rec + (counting ? 0 : o);  // not dereferenced while counting
@@ -484,23 +489,27 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
         }
       }
       // contributions of each state in add order
+      uint32_t *Rout = Rct + Cv + nch;  // exact: contributions in extendAll order, then pair orientations
       for (int c0 = 0; c0 < C && !counting; c0 += WAVE) {
         const int c = c0 + lane;
         if (c < C) {
           const uint32_t st = *CT.at(C_ST, c);
+          const uint32_t w = *CT.at(C_SR, c);
           if (st != NONE) {
-            const uint32_t w = *CT.at(C_SR, c);
             const uint32_t ns = *X.at(F_NL, (int)(w & 0xFFFFu));
             Rct[*Y.at(F_CB, (int)st) + *CT.at(C_RK, c)] = w | ns << 24;
           }
+          if (a.exact) Rout[c] = st == NONE ? NONE : (st | (w & (1u << 16)));
         }
       }
+      if (a.exact && !counting)
+        for (int p = lane; p < npairs; p += WAVE) Rout[C + p] = pr_o[p];
       if (lane == 0 && !counting) {
         Rcb[Fn] = (uint32_t)Cv;
         R[0] = (uint32_t)Fn;
         R[1] = (uint32_t)Cv;
         R[2] = (uint32_t)nch;
-        R[3] = 0;
+        R[3] = a.exact ? (uint32_t)C << 10 | (uint32_t)npairs : 0u;  // C < 2^22, npairs <= NP_MAX < 2^10
         roff[i + 1] = o;
       }
       // m_best_pair.clear() for the next locus

@@ -1,0 +1,39 @@
+// exact.hpp — device arguments of the exact M-step kernels (exact.hip).
+#pragma once
+#include "hmc_internal.hpp"
+
+namespace hmc {
+
+// Fixed-point scale of the frequency accumulators: 2^-44 resolution, totals
+// up to 2^19 individuals fit in 63 bits.
+constexpr double EXACT_FIXED_SCALE = 17592186044416.0;  // 2^44
+
+struct ExactArgs {
+  int L, head_len, width;          // loci, head length, alleles per trie node (max alleles per locus)
+  const int32_t *order;            // individuals of this group (batch indices)
+  int n_order;
+  const uint32_t *rec;             // structure records (exact mode)
+  const unsigned long long *rec_off;  // [batch][L+1]
+  int32_t *status;                 // [batch]: EST_OK, or EST_NEEDS_EXACT when a forward likelihood underflows
+  const double *gprob;             // [batch] P(genotype) of the last E-step
+  // fwd/bwd store: per individual a region at x_base, per locus fwd[F] bwd[F]
+  uint32_t *x;
+  const unsigned long long *x_base;   // [batch]
+  unsigned long long *x_off;          // [batch][L+1] (written by exact_fb)
+  // ForwardPatternTree of the round's candidates (host-built)
+  const int32_t *tr_child;         // [nodes][width], -1 = none
+  const int32_t *tr_data;          // [nodes] candidate index or -1
+  const int32_t *tr_root;          // [L] root node of each start locus, -1 = empty
+  int max_depth;                   // longest candidate
+  const uint8_t *head_al;          // [P][head_len] head patterns' alleles (head_len > 1)
+  // per-wave list scratch: [max_depth+1][3][fmax] + [max_depth+2] doubles
+  double *scratch;
+  size_t scratch_stride;           // doubles
+  int fmax;                        // most states of any locus of the group
+  unsigned long long *acc_freq, *acc_prefix;  // [candidates] fixed point
+};
+
+hipError_t launch_exact_fb(const ExactArgs &a, int grid, hipStream_t st);
+hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st);
+
+}  // namespace hmc

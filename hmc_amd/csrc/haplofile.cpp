@@ -326,7 +326,10 @@ bool write_geno_file(const std::string &format, const char *path, const char *pa
           const int32_t a = hap[((size_t)i * 2 + h) * L + k];
           fputc(a < 0 ? '0' : (char)a, fp);
         }
-        fprintf(fp, "   %d 0 %s\n", 2 * i + h, d.ids[i].c_str());
+        std::string id = d.ids[i];  // Haplotype::setID replaces spaces (Haplotype.h:26, Genotype.h:107-113)
+        for (char &ch : id)
+          if (ch == ' ') ch = '_';
+        fprintf(fp, "   %d 0 %s\n", 2 * i + h, id.c_str());
       }
   } else {
     fclose(fp);

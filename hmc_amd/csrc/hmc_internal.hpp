@@ -136,6 +136,12 @@ struct StructArgs {
   // loci without writing them (status EST_OVERFLOW_REC) so both are known.
   unsigned long long *rec_need;   // [batch]
   unsigned long long *trace_need; // [batch]
+  // Exact M-step (--exact-estimate): the records also carry the head pairs'
+  // pattern ids, each locus's contributions in extendAll order (target state |
+  // reversed<<16, NONE when a successor is missing) and its allele pairs'
+  // orientation counts — the forward links of HaploPair (HaploPair.cpp:44,67)
+  // in push order; trace_need then counts the fwd/bwd store (4 words/state).
+  bool exact;
   int32_t *status;                // [batch]
   unsigned long long *re_count;   // [batch]
   int32_t *fmax;                  // [batch]

@@ -118,6 +118,7 @@ class HaploModel:
         self.model = "MV"  # HaploModel::setModel: MV, MC or MA (HMC.cpp:35)
         self.mc_order = 1  # HMC.cpp:41
         self.num_patterns = -1  # HMC.cpp:38: > 0 mines with findPatternByNum
+        self.exact_estimate = False  # HMC.cpp:42 --exact-estimate: M-steps by estimatePatterns
         self.N = self.L = self.amax = 0
         self.iterations = 0
         self.log: list[dict] = []
@@ -133,6 +134,7 @@ class HaploModel:
                                          int(self.sample_size)))
         self._check(lib().hmc_set_model(self._h, str(self.model).encode(), int(self.mc_order)))
         self._check(lib().hmc_set_num_patterns(self._h, int(self.num_patterns)))
+        self._check(lib().hmc_set_exact_estimate(self._h, 1 if self.exact_estimate else 0))
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:
@@ -228,6 +230,11 @@ class HaploModel:
         n, rm = C.c_int(), C.c_uint64()
         self._check(lib().hmc_find_patterns(self._h, C.byref(n), C.byref(rm)))
         return n.value, rm.value
+
+    def exact_stats(self) -> dict:
+        r, c, ms = C.c_int(), C.c_uint64(), C.c_double()
+        self._check(lib().hmc_last_exact_stats(self._h, C.byref(r), C.byref(c), C.byref(ms)))
+        return dict(rounds=r.value, candidates=c.value, walk_ms=ms.value)
 
     def head_len(self) -> int:
         """PatternManager::head_len of the current model (min pattern length)."""

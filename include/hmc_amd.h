@@ -49,6 +49,11 @@ int hmc_ctx_create_dist(int device, int rank, int world, const void *unique_id, 
  * replacing HaploModel's construction (HaploModel.h:29) inside a host that
  * runs its own RCCL. */
 int hmc_ctx_create_comm(int device, void *rccl_comm, hmc_ctx **out);
+/* An RCCL communicator made by the RCCL this library is linked with (for
+ * hosts without their own RCCL binding, and tests: a communicator from a
+ * second copy of librccl in the process would not be usable here). */
+int hmc_rccl_comm_init(int device, int world, int rank, const void *unique_id, void **comm);
+int hmc_rccl_comm_destroy(void *comm);
 /* Same sharding with a caller-supplied collective instead of RCCL: fn must
  * sum `n` doubles element-wise across ranks in place and return 0.  Lets
  * several ranks share one GPU (tests) or run over any host transport. */
@@ -78,6 +83,19 @@ int hmc_set_params(hmc_ctx *ctx, double min_freq_abs, double min_freq, int min_p
  * PatternManager::findPatternBlock(mc_order+1), every candidate of that length,
  * head length mc_order+1), "MA" (MV; its adjustFrequency only range-checks). */
 int hmc_set_model(hmc_ctx *ctx, const char *model, int mc_order);
+/* HaploModel::exact_estimate (--exact-estimate, HMC.cpp:42; HaploModel.cpp:
+ * 140-141): after an E-step, hmc_find_patterns (and hmc_run) re-estimate the
+ * table with PatternManager::estimatePatterns (PatternManager.cpp:364-438):
+ * expected pattern counts under the current model, from a forward-backward
+ * pass and a ForwardPatternTree walk per individual and start locus
+ * (HaploBuilder.cpp:263-450), candidates grown by extendPatterns; M0 still
+ * mines the genotypes.  Model MC re-estimates the table in place.
+ * Frequencies agree with the reference to rounding (its sums run in pointer
+ * order); they are deterministic and independent of the sharding. */
+int hmc_set_exact_estimate(hmc_ctx *ctx, int on);
+/* Last exact M-step: rounds of estimateFrequency, candidates estimated, and
+ * device ms of the trie walks. */
+int hmc_last_exact_stats(const hmc_ctx *ctx, int *rounds, uint64_t *candidates, double *walk_ms);
 /* HaploModel::num_patterns (HMC.cpp:38): > 0 mines with
  * PatternManager::findPatternByNum (PatternManager.cpp:44-70, models MV/MA);
  * <= 0 (default) with findPatternByFreq. */
@@ -212,7 +230,7 @@ int hmc_write_patterns(hmc_ctx *ctx, const char *path);
  * waves: resident E-step waves (0 = automatic). */
 int hmc_set_tuning(hmc_ctx *ctx, int frontier_cap, uint64_t trace_bytes, int waves);
 /* E-step launch shape: wavefronts cooperating on one individual (1..4,
- * default 3) and individuals sharing one CU's LDS (default 4); 0 keeps the
+ * default 2) and individuals sharing one CU's LDS (default 8); 0 keeps the
  * current value.  Results do not depend on the shape. */
 int hmc_set_estep_shape(hmc_ctx *ctx, int waves_per_individual, int individuals_per_cu);
 /* E-step implementation: 0 (default) = two passes, a structure pass that

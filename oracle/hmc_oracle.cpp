@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <atomic>
 #include <string>
 #include <thread>
@@ -275,6 +276,10 @@ struct Pair {
   int alA, alB;  // last alleles of the two patterns
   double tp, fwd;
   std::vector<Link> links;
+  // exact M-step only: m_forward_links[reversed] (HaploPair.cpp:44,67) as
+  // indices into the next locus, and m_backward_likelihood (default 1.0)
+  std::vector<int> fl[2];
+  double bwd = 1.0;
 };
 
 struct Sample {  // one weighted haplotype of HaploData (HaploData.h:57-65)
@@ -297,6 +302,7 @@ struct Params {
   int model = 0;              // HaploModel::setModel (HaploModel.cpp:26-36): 0 MV, 1 MC, 2 MA
   int num_patterns = -1;      // HMC.cpp:38 (findPatternByNum when > 0)
   int mc_order = 1;           // HMC.cpp:41
+  bool exact = false;         // --exact-estimate (HMC.cpp:42, HaploModel.h:26)
 };
 
 struct Timing { double m0 = 0, e = 0, m = 0; };
@@ -618,6 +624,7 @@ struct Model {
   // ------------------------------------------------------------ E-step ----
   static thread_local std::vector<std::vector<Pair>> hp;  // m_haplopairs
   static thread_local int S;
+  static thread_local bool track_links;  // record forward links (exact M-step)
 
   int succOf(int pi, int a, int locus) const {  // HaploPattern.h:36-37
     int j = g.index(locus, a);
@@ -683,6 +690,8 @@ struct Model {
     uint64_t key = ((uint64_t)P[a].id << 32) | P[b].id;
     auto it = best.find(key);
     std::vector<Pair> &nxt = hp[locus + 1];
+    if (track_links)  // hp->m_forward_links[reversed].push_back(this) (HaploPair.cpp:44, 67)
+      hp[locus][predIdx].fl[rev ? 1 : 0].push_back(it == best.end() ? (int)nxt.size() : it->second - 1);
     if (it == best.end()) {
       Pair x;  // extension constructor HaploPair.cpp:35-61
       x.pa = a; x.pb = b;
@@ -769,9 +778,10 @@ struct Model {
   }
 
   // HaploBuilder.cpp:35-126 — returns coverage.
-  double resolve(int gi, std::vector<Candidate> &out, std::vector<int> &resol, double &gprob) {
+  double resolve(int gi, std::vector<Candidate> &out, std::vector<int> &resol, double &gprob, int sample_size = 0) {
     int L = g.L, hl = head_len();
-    S = prm.sample_size > 1 ? prm.sample_size : 1;
+    const int ss = sample_size > 0 ? sample_size : prm.sample_size;
+    S = ss > 1 ? ss : 1;
     hp.assign(L + 1, {});
     tie_cur = 0;
     std::vector<std::unordered_map<uint64_t, int>> best(L + 1);
@@ -880,6 +890,205 @@ struct Model {
     return ll;
   }
 
+  // ------------------------------------------------- exact M-step --------
+  // --exact-estimate: PatternManager::estimatePatterns / extendPatterns
+  // (PatternManager.cpp:347-438) over HaploBuilder::estimateFrequency
+  // (HaploBuilder.cpp:263-450) and the ForwardPatternTree (PatternTree.cpp:179-212).
+  // The reference sums the match lists over std::map<HaploPair*, double> in
+  // pointer (allocation) order; here the maps are keyed by state index
+  // (creation order), so sums agree to rounding, not bit for bit.
+  struct FNode { std::vector<int> ch; int data = -1; };
+  std::vector<FNode> fnodes;
+  std::vector<int> froot;
+  std::vector<Pat> *fpats = nullptr;
+  double cur_gp = 1.0;
+  uint64_t R_X = 0;  // trie-walk match-list entries visited (counter)
+
+  int fnew(int width) { fnodes.push_back(FNode{std::vector<int>(width, -1), -1}); return (int)fnodes.size() - 1; }
+  // ForwardPatternTree::addPattern (PatternTree.cpp:188-212); a missing allele
+  // fans out to every allele of its locus
+  void faddRec(int node, int k, int q, int width) {
+    const Pat &p = (*fpats)[k];
+    const int locus = p.start + q, a = p.al[q];
+    const int i = missing(a) ? -1 : g.index(locus, a);
+    const int lo = i < 0 ? 0 : i, hi = i < 0 ? g.num(locus) : i + 1;
+    for (int j = lo; j < hi; ++j) {
+      if (fnodes[node].ch[j] < 0) { const int c = fnew(width); fnodes[node].ch[j] = c; }
+      const int c = fnodes[node].ch[j];
+      if (q == p.len() - 1) fnodes[c].data = k;
+      else faddRec(c, k, q + 1, width);
+    }
+  }
+  // HaploBuilder::calcBackwardLikelihood (:263-272, HaploPair.cpp:126-136)
+  void calcBackward() {
+    const int L = g.L, hl = head_len();
+    for (int i = L - 1; i >= hl; --i)
+      for (auto &x : hp[i]) {
+        x.bwd = 0;
+        for (int r = 0; r < 2; ++r)
+          for (int t : x.fl[r]) x.bwd += hp[i + 1][t].bwd * hp[i + 1][t].tp;
+      }
+  }
+  typedef std::map<int, double> MList;  // state index -> weight
+  // HaploBuilder::estimateFrequency(node, ...) (:334-450); `locus` is the
+  // trie node's locus, lists hold states after locus-1 (heads while locus < head_len)
+  double fwalk(int node, int locus, int a, double last_freq, const MList last[3]) {
+    const int hl = head_len();
+    MList m[3];
+    if (locus < hl) {
+      const std::vector<Pair> &H = hp[hl];
+      for (auto &e : last[0]) {
+        const Pair &x = H[e.first];
+        const int pa = P[x.pa].al[locus], pb = P[x.pb].al[locus];
+        ++R_X;
+        if (aeq(pa, a)) {
+          if (aeq(pb, a)) m[0][e.first] += e.second;
+          else m[1][e.first] += e.second * 0.5;
+        } else if (aeq(pb, a)) {
+          m[2][e.first] += e.second * 0.5;
+        }
+      }
+      for (auto &e : last[1]) { ++R_X; if (aeq(P[H[e.first].pa].al[locus], a)) m[1][e.first] += e.second; }
+      for (auto &e : last[2]) { ++R_X; if (aeq(P[H[e.first].pb].al[locus], a)) m[2][e.first] += e.second; }
+    } else {
+      const std::vector<Pair> &X = hp[locus], &Y = hp[locus + 1];
+      for (auto &e : last[0])
+        for (int r = 0; r < 2; ++r)
+          for (int t : X[e.first].fl[r]) {
+            const Pair &y = Y[t];
+            ++R_X;
+            if (aeq(y.alA, a)) {
+              if (aeq(y.alB, a)) m[0][t] += e.second * y.tp;
+              else m[1][t] += e.second * y.tp * 0.5;
+            } else if (aeq(y.alB, a)) {
+              m[2][t] += e.second * y.tp * 0.5;
+            }
+          }
+      for (auto &e : last[1]) {
+        for (int t : X[e.first].fl[0]) { ++R_X; if (aeq(Y[t].alA, a)) m[1][t] += e.second * Y[t].tp; }
+        for (int t : X[e.first].fl[1]) { ++R_X; if (aeq(Y[t].alB, a)) m[2][t] += e.second * Y[t].tp; }
+      }
+      for (auto &e : last[2]) {
+        for (int t : X[e.first].fl[0]) { ++R_X; if (aeq(Y[t].alB, a)) m[2][t] += e.second * Y[t].tp; }
+        for (int t : X[e.first].fl[1]) { ++R_X; if (aeq(Y[t].alA, a)) m[1][t] += e.second * Y[t].tp; }
+      }
+    }
+    const std::vector<Pair> &Z = hp[locus < hl ? hl : locus + 1];
+    double freq = 0;
+    for (int k = 0; k < 3; ++k)
+      for (auto &e : m[k]) freq += e.second * Z[e.first].bwd;
+    freq /= cur_gp;
+    if (fnodes[node].data >= 0) {
+      Pat &p = (*fpats)[fnodes[node].data];
+      p.freq += freq;
+      p.prefix += last_freq;
+    }
+    for (int i = 0; i < (int)fnodes[node].ch.size(); ++i)
+      if (fnodes[node].ch[i] >= 0) fwalk(fnodes[node].ch[i], locus + 1, g.symbol(locus + 1, i), freq, m);
+    return freq;
+  }
+  // HaploBuilder::estimateFrequency(patterns) (:274-332) for pats[b, e)
+  void estimateFreqs(std::vector<Pat> &pats, size_t b, size_t e) {
+    const int L = g.L, N = g.N, hl = head_len(), width = g.maxnum();
+    fnodes.clear();
+    froot.assign(L + 1, -1);
+    for (int s = 0; s <= L; ++s) froot[s] = fnew(width);
+    fpats = &pats;
+    for (size_t k = b; k < e; ++k) {
+      faddRec(froot[pats[k].start], (int)k, 0, width);
+      pats[k].freq = 0;
+      pats[k].prefix = 0;
+    }
+    std::vector<Candidate> out;
+    std::vector<int> resol;
+    for (int gi = 0; gi < N; ++gi) {
+      double gprob;
+      track_links = true;
+      resolve(gi, out, resol, gprob, 1);  // HaploBuilder::resolve default sample_size 1 (HaploBuilder.h:49)
+      track_links = false;
+      calcBackward();
+      cur_gp = gp[gi];  // (*m_genos)[geno].genotype_probability(): set by the last resolveAll (HaploModel.cpp:109)
+      for (int start = 0; start < L; ++start) {
+        MList m[3];
+        const int end = std::max(start, hl);
+        for (int i = 0; i < (int)hp[end].size(); ++i) m[0][i] = hp[end][i].fwd;
+        const FNode &r = fnodes[froot[start]];
+        for (int i = 0; i < (int)r.ch.size(); ++i)
+          if (r.ch[i] >= 0) fwalk(r.ch[i], start, g.symbol(start, i), 1.0, m);
+      }
+    }
+    hp.clear();
+    for (size_t k = b; k < e; ++k) {
+      Pat &p = pats[k];
+      double freq = std::min(p.freq, (double)N);
+      double pre = std::min(p.prefix, (double)N);
+      freq = std::min(freq, pre);
+      p.freq = freq / N;
+      p.prefix = pre / N;
+      p.setTp(pre > 0 ? freq / pre : freq / N);
+    }
+  }
+  // PatternManager::estimatePatterns (:364-410) + extendPatterns (:412-438)
+  void estimatePatterns() {
+    const int L = g.L;
+    if (min_freq < 0) {  // estimateFrequency() (:347-362): the same patterns re-estimated
+      std::vector<Pat> pats = P;
+      estimateFreqs(pats, 0, pats.size());
+      for (size_t i = 0; i < P.size(); ++i) {
+        P[i].freq = pats[i].freq;
+        P[i].prefix = pats[i].prefix;
+        P[i].tp = pats[i].tp;
+      }
+      return;
+    }
+    std::vector<Pat> all;
+    std::vector<int> seeds;
+    auto extend = [&](const Pat &hp0, int j) {
+      Pat n;
+      n.start = hp0.start;
+      n.end = hp0.end + 1;
+      n.al = hp0.al;
+      n.al.push_back(g.symbol(hp0.end, j));
+      n.freq = hp0.freq;
+      return n;
+    };
+    for (size_t i = 0; i < P.size(); ++i) {
+      all.push_back(P[i]);
+      const Pat &hp0 = P[i];
+      if (hp0.end < L && hp0.len() < maxlen[hp0.start])
+        for (int j = 0; j < g.num(hp0.end); ++j) {
+          const int s = j < (int)hp0.succ.size() ? hp0.succ[j] : -1;
+          if (s < 0 || P[s].start != hp0.start) {
+            all.push_back(extend(hp0, j));
+            seeds.push_back((int)all.size() - 1);
+          }
+        }
+    }
+    size_t rb = 0, re = all.size();
+    while (rb < re) {
+      estimateFreqs(all, rb, re);
+      const size_t nb = all.size();
+      for (int level = 0; level < 4; ++level) {
+        std::vector<int> ns;
+        for (int si : seeds) {
+          const Pat hp0 = all[si];
+          if (hp0.end < L && hp0.len() < maxlen[hp0.start] && hp0.freq >= min_freq)
+            for (int j = 0; j < g.num(hp0.end); ++j) {
+              all.push_back(extend(hp0, j));
+              ns.push_back((int)all.size() - 1);
+            }
+        }
+        seeds.swap(ns);
+      }
+      rb = nb;
+      re = all.size();
+    }
+    P.clear();
+    for (auto &c : all)
+      if (c.freq >= min_freq || c.len() <= minlen[c.start]) P.push_back(c);
+    initialize();
+  }
+
   // HaploComp (HaploComp.cpp:29-76, 144-155) of the input panel (the "real"
   // phase, as given) against inferred haplotypes infer[i] = [2][L] symbols;
   // m_genos_input == m_genos_real, so no missing error.  out = {switch error,
@@ -972,7 +1181,8 @@ struct Model {
       if (it < prm.max_iter && ll >= old_ll && (old_ll - ll) / old_ll > 0.0001) {
         uint64_t rm0 = R_M;
         auto t2 = clk::now();
-        findPatterns();
+        if (prm.exact) estimatePatterns();  // HaploModel.cpp:140-141
+        else findPatterns();
         t_m_log.push_back(std::chrono::duration<double>(clk::now() - t2).count());
         rm_log.push_back(R_M - rm0);
         npat_log.push_back((int)P.size());
@@ -989,6 +1199,7 @@ thread_local uint64_t Model::tl_rm = 0;
 thread_local std::vector<std::vector<double>> Model::uni;
 thread_local std::vector<std::vector<Pair>> Model::hp;
 thread_local int Model::S = 1;
+thread_local bool Model::track_links = false;
 
 }  // namespace ora
 
@@ -1290,6 +1501,17 @@ void ora_set_model(void *h, int model, int mc_order) {
   Model *m = (Model *)h;
   m->prm.model = model;
   m->prm.mc_order = mc_order;
+}
+// HaploModel::exact_estimate (HMC.cpp:42): M-steps by estimatePatterns
+void ora_set_exact(void *h, int on) { ((Model *)h)->prm.exact = on != 0; }
+// One exact M-step (PatternManager::estimatePatterns) after an E-step; returns
+// the pattern count; *rx = match-list entries visited by the trie walks.
+int ora_estimate_patterns(void *h, uint64_t *rx) {
+  Model *m = (Model *)h;
+  m->R_X = 0;
+  m->estimatePatterns();
+  if (rx) *rx = m->R_X;
+  return (int)m->P.size();
 }
 // GenoData::unphased_num (HaploFile.cpp:475): HaploComp covers [0, n)
 void ora_set_unphased(void *h, int n) { ((Model *)h)->unphased = n; }

@@ -52,6 +52,9 @@ def lib():
         L.ora_tie_flags.argtypes = [vp, P(i)]
         L.ora_set_threads.argtypes = [i]
         L.ora_set_unphased.argtypes = [vp, i]
+        L.ora_set_exact.argtypes = [vp, i]
+        L.ora_estimate_patterns.restype = i
+        L.ora_estimate_patterns.argtypes = [vp, P(u64)]
         L.ora_set_model.argtypes = [vp, i, i]
         L.ora_set_num_patterns.argtypes = [vp, i]
         L.ora_run_comp_log.argtypes = [vp, P(d)]
@@ -191,6 +194,17 @@ class Oracle:
         """HaploModel::setModel: MV (default), MC (Markov chain of order
         mc_order: all patterns of length mc_order+1), MA (MV + range checks)."""
         lib().ora_set_model(self.h, {"MV": 0, "MC": 1, "MA": 2}[model], int(mc_order))
+
+    def set_exact(self, on: bool = True):
+        """HaploModel::exact_estimate (--exact-estimate): M-steps by estimatePatterns."""
+        lib().ora_set_exact(self.h, 1 if on else 0)
+
+    def estimate_patterns(self):
+        """One exact M-step (PatternManager::estimatePatterns) after an E-step;
+        returns (patterns, match-list entries visited)."""
+        rx = C.c_uint64()
+        P = lib().ora_estimate_patterns(self.h, C.byref(rx))
+        return P, rx.value
 
     def set_unphased(self, n: int):
         """GenoData::unphased_num: HaploComp covers individuals [0, n) (BENCH3 parents)."""

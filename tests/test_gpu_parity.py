@@ -524,22 +524,15 @@ def test_two_ranks_one_gpu_host_collective(oracle_mod, tmp_path, variant, reduct
 
 
 def _rccl_comm_one_rank():
-    """A one-rank RCCL communicator made with librccl directly (the caller-owned
-    communicator of hmc_ctx_create_comm)."""
+    """A one-rank RCCL communicator owned by the caller (hmc_ctx_create_comm),
+    made with the RCCL libhmc_amd is linked with (torch may have loaded a
+    second librccl into the process; its communicators are not interchangeable)."""
     import ctypes as C
-
-    class UID(C.Structure):
-        _fields_ = [("internal", C.c_char * 128)]
-
-    hip = C.CDLL("libamdhip64.so")
-    assert hip.hipSetDevice(0) == 0
-    rccl = C.CDLL("/opt/rocm/lib/librccl.so")
-    uid = UID()
-    assert rccl.ncclGetUniqueId(C.byref(uid)) == 0
+    L = hmc_amd.lib()
+    uid = C.create_string_buffer(hmc_amd.HaploModel.unique_id(), 128)
     comm = C.c_void_p()
-    rccl.ncclCommInitRank.argtypes = [C.POINTER(C.c_void_p), C.c_int, UID, C.c_int]
-    assert rccl.ncclCommInitRank(C.byref(comm), 1, uid, 0) == 0
-    return rccl, comm
+    assert L.hmc_rccl_comm_init(0, 1, 0, C.cast(uid, C.c_void_p), C.byref(comm)) == 0
+    return L, comm
 
 
 @pytest.mark.parametrize("how", ["unique_id", "caller_comm"])
@@ -567,7 +560,7 @@ def test_rccl_collectives_one_rank(oracle_mod, monkeypatch, how, reduction):
     np.testing.assert_array_equal(np.array([x["haplocomp"] for x in m.log]), r["haplocomp"])
     m.close()
     if rccl is not None:
-        rccl.ncclCommDestroy(comm)  # the caller's communicator outlives the context
+        assert rccl.hmc_rccl_comm_destroy(comm) == 0  # the caller's communicator outlives the context
 
 
 def test_shard_ranges_balanced_and_tiling():
@@ -681,3 +674,132 @@ def test_segmented_nth_element_matches_libstdcxx(oracle_mod, sw):
         o = off[b]
         _, ref = oracle_mod.std_nth_element(lik[o:o + n], tag[o:o + n].astype(np.int32), nths[b])
         assert np.array_equal(t2[o:o + n].astype(np.int32), ref), (n, nths[b], lik[o:o + n])
+
+
+# ---------------------------------------------------------------- exact M-step
+EXACT_PANELS = ["cfg1", "n60", "a4", "miss2", "a3miss5"]
+
+
+def _rel_close(a, b, rtol=1e-6, atol=1e-12):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.all(np.abs(a - b) <= atol + rtol * np.abs(b))
+
+
+@pytest.mark.parametrize("name", EXACT_PANELS)
+def test_exact_mstep_against_oracle(oracle_mod, name):
+    """--exact-estimate (PatternManager::estimatePatterns, HaploBuilder::
+    estimateFrequency): after M0 and E1, one exact M-step gives the
+    restatement's table — the same patterns in the same (candidate) order,
+    successors equal, frequencies / prefix frequencies / transition
+    probabilities within 1e-6 relative (the north star's bar: the reference
+    sums its match lists in pointer order)."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
+    o.find_patterns()
+    o.resolve_all()
+    P_o, _ = o.estimate_patterns()
+    po = o.patterns()
+    m = gpu_model(p)
+    m.exact_estimate = True
+    m.find_patterns()  # M0 mines the genotypes
+    m.resolve_all()
+    P_g, _ = m.find_patterns()  # after an E-step: estimatePatterns
+    pg = m.patterns()
+    st = m.exact_stats()
+    assert st["rounds"] >= 1 and st["candidates"] >= P_g
+    assert P_g == P_o
+    for k in ("start", "len", "alleles", "succ"):
+        assert np.array_equal(pg[k], po[k]), k
+    for k in ("freq", "prefix", "tp"):
+        assert _rel_close(pg[k], po[k]), (k, np.max(np.abs(pg[k] - po[k]) / np.maximum(np.abs(po[k]), 1e-300)))
+
+
+def test_exact_single_allele_frequencies(oracle_mod):
+    """Known answer: with nothing missing, every phasing carries the same
+    alleles, so the exact frequency of a length-1 pattern is the allele
+    frequency (2 n_aa + n_ab) / 2N of its locus."""
+    p = panel("a4")
+    m = gpu_model(p)
+    m.exact_estimate = True
+    m.find_patterns()
+    m.resolve_all()
+    m.find_patterns()
+    pt = m.patterns()
+    num, sym, fr = m.allele_table()
+    one = np.where(pt["len"] == 1)[0]
+    assert len(one) > 0
+    for i in one:
+        k = pt["start"][i]
+        j = list(sym[k]).index(pt["alleles"][i, 0])
+        assert abs(pt["freq"][i] - fr[k, j]) <= 1e-12
+        assert pt["prefix"][i] == 1.0
+
+
+@pytest.mark.parametrize("name", ["cfg1", "n60", "miss2"])
+def test_exact_em_against_oracle(oracle_mod, name):
+    """HaploModel::run with --exact-estimate: iteration count, per-iteration
+    LL to 1e-9 relative, and the accepted pairs."""
+    p = panel(name)
+    m = gpu_model(p, max_iteration=10)
+    m.exact_estimate = True
+    res = m.run()
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10, max_iter=10)
+    o.set_exact(True)
+    r = o.run()
+    assert m.iterations == r["iterations"]
+    assert np.allclose([x["ll"] for x in m.log], r["ll"], rtol=1e-9, atol=0)
+    assert np.mean(np.all(res == r["resolutions"], axis=(1, 2))) >= 0.99
+
+
+# ------------------------------------------------ full-size chain digests
+def _sha(a, dt):
+    return hashlib.sha256(np.ascontiguousarray(a, dt).tobytes()).hexdigest()
+
+
+def _total_weight(m):
+    import ctypes as C
+    tw = C.c_double()
+    assert hmc_amd.lib().hmc_get_samples(m._h, None, None, C.byref(tw)) == 0
+    return tw.value
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("cfg", [5, 3])
+def test_full_size_chain_against_oracle_digest(cfg):
+    """BASELINE configs 3 (10 000 x 2 000) and 5 (10 000 x 1 000, 8 alleles)
+    at full size against the restatement's digests
+    (tests/golden/cfg{3,5}_chain_digest.json, make_full_digest.py): the EM
+    chain M0, E1, M1, E2, M2, E3 that bench.py times — every pattern table
+    (SHA-256 of ids' start, length, frequency, prefix, tp, successors), R_M,
+    and per E-step the LL, R_E, samples, total weight, and SHA-256 of the
+    per-individual totals, candidate counts and selected pairs.  Tolerance 0."""
+    path = os.path.join(HERE, "golden", f"cfg{cfg}_chain_digest.json")
+    if not os.path.exists(path):
+        pytest.skip(f"{path} not generated")
+    d = json.load(open(path))
+    p = synth.config_panel(cfg)
+    assert (p.N, p.L) == (d["N"], d["L"])
+    m = gpu_model(p)
+
+    def check_m(k):
+        P, rm = m.find_patterns()
+        want = d["m"][k]
+        assert (P, rm) == (want["P"], want["R_M"]), (k, P, rm)
+        assert _digest_patterns(m.patterns(maxlen=1)) == want["table_sha256"], k
+
+    def check_e(k):
+        ll, H, re = m.resolve_all()
+        want = d["e"][k - 1]
+        assert (float(ll).hex(), re, H) == (want["ll_hex"], want["R_E"], want["H"]), k
+        assert float(_total_weight(m)).hex() == want["total_weight_hex"]
+        er = m.estep_results()
+        assert _sha(er["total"], np.float64) == want["totals_sha256"], k
+        assert _sha(er["ncand"], np.int32) == want["ncand_sha256"], k
+        assert [float(er["total"][i]).hex() for i in want["subset"]] == want["subset_totals_hex"]
+        assert _sha(m.resolutions(), np.int32) == want["resolutions_sha256"], k
+
+    check_m(0)
+    for k in range(1, len(d["e"]) + 1):
+        check_e(k)
+        if k < len(d["m"]):
+            check_m(k)

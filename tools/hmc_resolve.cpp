@@ -1,24 +1,31 @@
 // hmc_resolve — C++ drop-in for HMC's resolve mode (HMC.cpp:179-233) built on
-// the C-ABI of libhmc_amd.so.  Reads a PHASE file (HaploFile::readGenoData),
-// runs HaploModel::run on the GPU and writes <input>.reconstructed
-// (HaploFile::writeGenoData).  Options use the reference's names and defaults
-// (HMC.cpp:35-47).
+// the C-ABI of libhmc_amd.so.  Reads the input files in the given format
+// (HaploFile::getHaploFile + readGenoData), runs HaploModel::run on the GPU
+// and writes <first file>.reconstructed in the same format
+// (HaploFile::writeGenoData; BENCH2/3 also rewrite the position file, as
+// HaploFileBench::writeGenoData does), and with --output-patterns the
+// .patterns dump (HMC.cpp:229-232).  Options use the reference's names and
+// defaults (HMC.cpp:17-47).
 //
-//   hmc_resolve [-a 1.5] [-i 1] [--sample-size 10] [--min-pattern-len 1]
-//               [--max-pattern-len 30] [-r min_freq] [-d device] input.phase
+//   hmc_resolve [-f PHASE|HPM|HPM2|BENCH2|BENCH3] [-a 1.5] [-r min_freq] [-n num]
+//               [-m MV|MC|MA] [-o mc_order] [--exact-estimate] [-i 1]
+//               [--sample-size 10] [--min-pattern-len 1] [--max-pattern-len 30]
+//               [--output-patterns x] [--device 0] datafile ...
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../include/hmc_amd.h"
 
 int main(int argc, char **argv) {
   double min_freq_abs = 1.5, min_freq = -1.0;
   int max_iteration = 1, sample_size = 10, min_len = 1, max_len = 30, device = 0;
-  const char *input = nullptr;
-  std::string model = "MV";
+  std::vector<std::string> files;
+  std::string model = "MV", format = "PHASE";
   int mc_order = 1, num_patterns = -1;
+  bool exact = false, output_patterns = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> const char * {
@@ -31,15 +38,19 @@ int main(int argc, char **argv) {
     else if (a == "--sample-size") sample_size = atoi(next());
     else if (a == "--min-pattern-len") min_len = atoi(next());
     else if (a == "--max-pattern-len") max_len = atoi(next());
-    else if (a == "-d" || a == "--device") device = atoi(next());
+    else if (a == "--device") device = atoi(next());
+    else if (a == "-d" || a == "--debug") (void)next();                 // Logger level (HMC.cpp:28)
+    else if (a == "-f" || a == "--input-format") format = next();      // HMC.cpp:29
+    else if (a == "--exact-estimate") exact = true;                      // HMC.cpp:42
+    else if (a == "--output-patterns") { (void)next(); output_patterns = true; }  // HMC.cpp:30, 229-232
     else if (a == "-m" || a == "--model") model = next();             // HMC.cpp:35
     else if (a == "-o" || a == "--mc-order") mc_order = atoi(next());  // HMC.cpp:41
     else if (a == "-n" || a == "--num-patterns") num_patterns = atoi(next());  // HMC.cpp:38
     else if (a[0] == '-') { fprintf(stderr, "unknown option %s\n", a.c_str()); return 1; }
-    else input = argv[i];
+    else files.push_back(argv[i]);
   }
-  if (!input) {
-    fprintf(stderr, "Usage: hmc_resolve [option ...] datafile\n");
+  if (files.empty()) {
+    fprintf(stderr, "Usage: hmc_resolve [option ...] datafiles\n");
     return 1;
   }
   hmc_ctx *ctx = nullptr;
@@ -53,8 +64,11 @@ int main(int argc, char **argv) {
   if ((rc = hmc_set_params(ctx, min_freq_abs, min_freq, min_len, max_len, sample_size))) die("hmc_set_params");
   if ((rc = hmc_set_model(ctx, model.c_str(), mc_order))) die("hmc_set_model");
   if ((rc = hmc_set_num_patterns(ctx, num_patterns))) die("hmc_set_num_patterns");
+  if ((rc = hmc_set_exact_estimate(ctx, exact ? 1 : 0))) die("hmc_set_exact_estimate");
   printf("Reading genotype file ...\n");
-  if ((rc = hmc_load_phase(ctx, input))) die("hmc_load_phase");
+  std::vector<const char *> names;
+  for (auto &f : files) names.push_back(f.c_str());
+  if ((rc = hmc_load_files(ctx, format.c_str(), names.data(), (int)names.size()))) die("hmc_load_files");
   int N = 0, L = 0, A = 0;
   hmc_panel_info(ctx, &N, &L, &A);
   printf("Succesfully read Haplotype file with %d markers and %d genotypes.\n", L, N);
@@ -73,8 +87,16 @@ int main(int argc, char **argv) {
     solve += log[k].t_estep_s + log[k].t_mstep_s;
   }
   printf("Solving Time = %f\n", solve);
-  std::string out = std::string(input) + ".reconstructed";
-  if ((rc = hmc_write_phase(ctx, out.c_str()))) die("hmc_write_phase");
+  // HaploFile::writeGenoData(resolutions, ".reconstructed") on the first file
+  std::vector<std::string> outs{files[0] + ".reconstructed"};
+  if (format == "BENCH2" || format == "BENCH3") outs.push_back(files.size() > 1 ? files[1] : "");
+  std::vector<const char *> onames;
+  for (auto &f : outs) onames.push_back(f.c_str());
+  if ((rc = hmc_write_files(ctx, format.c_str(), onames.data(), (int)onames.size()))) die("hmc_write_files");
+  if (output_patterns) {
+    const std::string pf = files[0] + ".patterns";
+    if ((rc = hmc_write_patterns(ctx, pf.c_str()))) die("hmc_write_patterns");
+  }
   hmc_ctx_destroy(ctx);
   return 0;
 }

@@ -1,5 +1,6 @@
 """Diagnostic build: block-critical-path cycles per phase of the split E-step's
-value pass (estep_values), averaged per individual-locus, for E1..E3 of cfg2."""
+value pass (estep_values), averaged per individual-locus, for E1..E3 of a
+BASELINE config (env CFG, default 2; ITERS E-steps, default 3)."""
 import ctypes as C
 import os
 import sys
@@ -10,18 +11,19 @@ sys.path.insert(0, ROOT)
 import hmc_amd  # noqa: E402
 from hmc_amd import synth  # noqa: E402
 
-p = synth.config_panel(2)
+p = synth.config_panel(int(os.environ.get("CFG", "2")))
 m = hmc_amd.HaploModel()
 nw, ipc = (int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "3:4").split(":"))
 m.set_estep_shape(nw, ipc)
 m.load(hmc_amd.GenoData.from_panel(p))
 m.find_patterns()
 names = ["record hdr", "phase A", "phase B", "trace", "final sync", "final select"]
-for it in range(3):
+for it in range(int(os.environ.get("ITERS", "3"))):
     m.resolve_all()
     st = (C.c_uint64 * 20)()
     hmc_amd.lib().hmc_get_stamps(m._h, st)
     s = m.estep_split_stats()
+    print(f"  passes: structure {s['structure_passes']} value {s['value_passes']}", flush=True)
     nl = p.N * (p.L - 1)
     tot = sum(st[:6])
     print(f"E{it + 1}: structure {s['structure_ms']:.2f} ms values {s['values_ms']:.2f} ms; "
