@@ -1575,7 +1575,7 @@ struct Ctx {
         (e = d_wslot.ensure((size_t)2 * S * n)) || (e = d_trace_cursor.ensure(1)) || (e = d_maxst.ensure(1)) ||
         (e = d_fmax.ensure(n)) || (e = d_loc_off.ensure((size_t)n * (L + 1))) || (e = d_order.ensure(n)) ||
         (e = d_order2.ensure(n)) || (e = d_cost.ensure(n)) || (e = d_tbase.ensure(n)) || (e = d_rbase.ensure(n)) ||
-        (e = d_rneed.ensure(n)) || (e = d_tneed.ensure(n)))
+        (e = d_rneed.ensure(n)) || (e = d_tneed.ensure(n)) || (e = d_recsz.ensure(n)))
       return hipfail(e, "estep alloc");
     // store budgets: trace store and record store grow (never shrink) up to these
     size_t freeb = 0, totb = 0;
@@ -1682,6 +1682,9 @@ struct Ctx {
   }
 
   static constexpr int ESTEP_RESTART = 1;
+  std::vector<unsigned long long> prev_rneed;  // records per individual of the last E-step (estimates)
+  int prev_P = 0;
+  DevBuf<unsigned long long> d_recsz;  // [n] record region size of each individual
   uint64_t trace_budget = 0, rec_budget = 0;  // words
   int n_struct_passes = 0, n_value_passes = 0;
 
@@ -1858,31 +1861,58 @@ struct Ctx {
     hipError_t e;
     float ms = 0;
     std::vector<int32_t> pending(order), sset, rest;
-    std::vector<unsigned long long> rneed(n, 0), tneed(n, 0), base(n, 0);
-    bool known = false;  // rneed / tneed hold the exact needs of `pending`
+    std::vector<unsigned long long> rneed(n, 0), tneed(n, 0), base(n, 0), rsz(n, 0);
+    // Every individual gets its own record region: its exact size once a pass
+    // has measured it (`exact_need`), else an estimate — the previous E-step's
+    // size when the model is of the same scale, or the records-per-cost ratio
+    // of the individuals measured so far.  A region that turns out too small
+    // only defers that individual (it keeps walking without writing and
+    // reports its exact size), so no pass is ever repeated in full.
+    std::vector<char> exact_need(n, 0);
+    std::vector<unsigned long long> est(n, 0);
+    const bool prev_ok = !exact && (int)prev_rneed.size() == n && prev_P > 0 && P < 2 * (int64_t)prev_P &&
+                         2 * (int64_t)P > prev_P;
+    if (prev_ok)
+      for (int i = 0; i < n; ++i) est[i] = prev_rneed[i] + prev_rneed[i] / 4 + 64;
+    bool have_est = prev_ok;
     int rc;
     while (!pending.empty()) {
       // ---- pass 1: structure records --------------------------------------
       int np = (int)pending.size();
-      if (known) {  // the prefix whose records and traces fit the budgets
+      {
         uint64_t r = 0, t = 0;
         int k = 0;
-        while (k < np && (k == 0 || (r + rneed[pending[k]] <= rec_budget && t + tneed[pending[k]] <= trace_budget))) {
-          base[pending[k]] = r;
-          r += rneed[pending[k]];
-          t += tneed[pending[k]];
-          ++k;
+        if (!have_est) {  // nothing measured yet: the heaviest 4 per CU share the store evenly
+          k = std::min(np, 4 * dev_cu);
+          const uint64_t share = rec_budget / (uint64_t)k;
+          for (int q = 0; q < k; ++q) {
+            base[pending[q]] = (uint64_t)q * share;
+            rsz[pending[q]] = share;
+          }
+          r = share * (uint64_t)k;
+        } else {  // the prefix whose regions (and measured traces) fit the budgets
+          while (k < np) {
+            const int bi = pending[k];
+            const uint64_t need = exact_need[bi] ? rneed[bi] : std::min<uint64_t>(est[bi], rec_budget);
+            const uint64_t tn = exact_need[bi] ? tneed[bi] : 0;
+            if (k > 0 && (r + need > rec_budget || t + tn > trace_budget)) break;
+            base[bi] = r;
+            rsz[bi] = need;
+            r += need;
+            t += tn;
+            ++k;
+          }
         }
         np = k;
         if ((rc = ensure_store(d_rec, r, rec_budget, "record store"))) return rc;
-        std::vector<unsigned long long> rb(n, 0);
-        for (int q = 0; q < np; ++q) rb[pending[q]] = base[pending[q]];
-        if ((e = hipMemcpyAsync(d_rbase.p, rb.data(), (size_t)n * 8, hipMemcpyHostToDevice, st)))
+        std::vector<unsigned long long> rb(n, 0), rs(n, 0);
+        for (int q = 0; q < np; ++q) {
+          rb[pending[q]] = base[pending[q]];
+          rs[pending[q]] = rsz[pending[q]];
+        }
+        if ((e = hipMemcpyAsync(d_rbase.p, rb.data(), (size_t)n * 8, hipMemcpyHostToDevice, st)) ||
+            (e = hipMemcpyAsync(d_recsz.p, rs.data(), (size_t)n * 8, hipMemcpyHostToDevice, st)))
           return hipfail(e, "estep");
-      } else if (d_rec.n == 0) {
-        if ((rc = ensure_store(d_rec, std::min<uint64_t>(rec_budget, std::max<uint64_t>((uint64_t)n * L * 640, 16ull << 20)),
-                               rec_budget, "record store")))
-          return rc;
       }
       const int hcap1 = next_pow2(2 * fcap), ccap1 = 8 * fcap;
       const int bpc1 = np > 4 * dev_cu ? 8 : 4;  // structure pass: one wave per individual
@@ -1908,7 +1938,8 @@ struct Ctx {
       s1.rec = d_rec.p;
       s1.rec_cap = d_rec.n;
       s1.rec_cursor = d_rec_cursor.p;
-      s1.rec_base = known ? d_rbase.p : nullptr;
+      s1.rec_base = d_rbase.p;
+      s1.rec_size = d_recsz.p;
       s1.rec_off = d_rec_off.p;
       s1.rec_need = d_rneed.p;
       s1.trace_need = d_tneed.p;
@@ -1938,14 +1969,33 @@ struct Ctx {
           return ESTEP_RESTART;
         }
         if (s == EST_OVERFLOW_REC) {
-          if (known) return fail(HMC_EHIP, "record store overflow with exact sizes");
+          if (exact_need[bi]) return fail(HMC_EHIP, "record store overflow with exact sizes");
           rest.push_back(bi);
         } else {
           sset.push_back(bi);
         }
+        exact_need[bi] = 1;
       }
       for (int q = np; q < (int)pending.size(); ++q) rest.push_back(pending[q]);
-      known = true;  // every individual of `rest` now has its exact needs
+      // estimates for the individuals not measured yet: records per unit of
+      // cost of those measured (after a pass where estimates fell short, or
+      // when there were none)
+      {
+        int deferred = 0;
+        double rs_ = 0, cs = 0;
+        for (int i = 0; i < n; ++i)
+          if (exact_need[i]) {
+            rs_ += (double)rneed[i];
+            cs += (double)std::max(1, h_cost[i]);
+          }
+        for (int q = 0; q < np; ++q) deferred += h_status[pending[q]] == EST_OVERFLOW_REC ? 1 : 0;
+        if (!have_est || deferred * 10 > np) {
+          const double ratio = cs > 0 ? rs_ / cs : 0.0;
+          for (int bi : rest)
+            if (!exact_need[bi]) est[bi] = (uint64_t)(1.25 * ratio * std::max(1, h_cost[bi])) + 64;
+          have_est = true;
+        }
+      }
       // ---- pass 2: values, in groups whose traces fit the store -------------
       size_t pos = 0;
       while (pos < sset.size()) {
@@ -2044,6 +2094,10 @@ struct Ctx {
         pos += k;
       }
       pending.swap(rest);
+    }
+    if (!exact) {
+      prev_rneed = rneed;
+      prev_P = P;
     }
     return HMC_OK;
   }

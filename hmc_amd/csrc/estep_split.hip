@@ -149,10 +149,14 @@ __device__ inline uint32_t ld_acq(uint32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Next record of `words` words, or REC_NONE when it does not fit: the store
+// (bump allocator) or the individual's own region (rec_base / rec_size).
+constexpr unsigned long long REC_NONE = ~0ull;
 __device__ inline unsigned long long rec_alloc(const StructArgs &a, unsigned long long &cur, unsigned long long &end,
                                                unsigned long long words) {
   words = (words + 1) & ~1ull;  // records start on even words (8-byte aligned tpv)
   if (cur + words > end) {
+    if (a.rec_base) return REC_NONE;  // past this individual's region
     const unsigned long long take = words > REC_CHUNK ? words : REC_CHUNK;
     unsigned long long base = 0;
     if (lane_id() == 0) base = atomicAdd(a.rec_cursor, take);
@@ -161,6 +165,7 @@ __device__ inline unsigned long long rec_alloc(const StructArgs &a, unsigned lon
     end = base + take;
   }
   const unsigned long long off = cur;
+  if (off + words > a.rec_cap) return REC_NONE;
   cur += words;
   return off;
 }
@@ -216,7 +221,8 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
     unsigned long long re = 0;
     // records: this individual's reserved region, else the bump allocator; once
     // a record does not fit, `counting` keeps the walk going without writes
-    unsigned long long rcur = a.rec_base ? a.rec_base[bi] : 0, rend = a.rec_base ? ~0ull : 0;
+    unsigned long long rcur = a.rec_base ? a.rec_base[bi] : 0;
+    unsigned long long rend = a.rec_base ? (a.rec_size ? rcur + a.rec_size[bi] : ~0ull) : 0;
     bool counting = false;
     unsigned long long rneed = 0, tneed = 0;  // exact record / trace words (lane-uniform)
     IdFront X = FA, Y = FB;
@@ -275,7 +281,7 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
       rneed += (words + 1) & ~1ull;
       tneed += a.exact ? 4ull * Fp + 2 : trace_locus_words((unsigned long long)Fp, S);
       const unsigned long long o = rec_alloc(a, rcur, rend, words);
-      if (o + words > a.rec_cap) {
+      if (o == REC_NONE) {
         counting = true;
         if (lane == 0) re += (unsigned long long)Fp;
       } else {
@@ -439,7 +445,7 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
       rneed += (words + 1) & ~1ull;
       tneed += a.exact ? 4ull * Fn + 2 : trace_locus_words((unsigned long long)Fn, S);
       const unsigned long long o = counting ? 0 : rec_alloc(a, rcur, rend, words);
-      if (!counting && o + words > a.rec_cap) counting = true;
+      if (o == REC_NONE) counting = true;
       uint32_t *R = a.rec + (counting ? 0 : o);  // not dereferenced while counting
       double *Rtp = (double *)(R + 4);
       uint32_t *Rhd = R + 4 + 2 * Fn, *Rcb = Rhd + Fn, *Rct = Rcb + Fn + 1, *Rch = Rct + Cv;
@@ -702,7 +708,12 @@ __device__ inline bool k2_write_trace(const ValueArgs &a, K2Shared *bs, const VF
 size_t estep_s2_scratch_bytes(int fcap, int S) { return 2 * k2_front_bytes(fcap, S); }
 size_t estep_s2_lds_bytes(int S, int fc, int nw) { return (size_t)k2_plan(S, fc, nw).bytes; }
 
-__global__ __launch_bounds__(256) void estep_values(ValueArgs a) {
+#ifdef HMC_VALUES_WPE  // tuning experiments: force more resident waves per SIMD (fewer VGPRs)
+#define HMC_VALUES_ATTR __attribute__((amdgpu_waves_per_eu(HMC_VALUES_WPE)))
+#else
+#define HMC_VALUES_ATTR
+#endif
+__global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int S = a.S, L = a.L, hl = a.head_len;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;

@@ -130,6 +130,7 @@ struct StructArgs {
   unsigned long long rec_cap;     // words
   unsigned long long *rec_cursor; // bump allocator (when rec_base is null)
   const unsigned long long *rec_base;  // [batch] reserved record region of each individual, or null
+  const unsigned long long *rec_size;  // [batch] its size in words (null: unbounded, the exact need)
   unsigned long long *rec_off;    // [batch][L+1]
   // Exact store needs of each individual (words): its records and its value-pass
   // trace.  An individual whose records do not fit the store keeps walking the
