@@ -1958,6 +1958,8 @@ struct Ctx {
       hipEventElapsedTime(&ms, ev[0], ev[1]);
       ms_s1 += ms;
       ++n_struct_passes;
+      if (getenv("HMC_DEBUG_MEM"))
+        fprintf(stderr, "[hmc] structure pass %d: %d individuals, %.1f ms\n", n_struct_passes, np, ms);
       sset.clear();
       rest.clear();
       for (int q = 0; q < np; ++q) {
@@ -2054,6 +2056,8 @@ struct Ctx {
         hipEventElapsedTime(&ms, ev[0], ev[1]);
         ms_s2 += ms;
         ++n_value_passes;
+        if (getenv("HMC_DEBUG_MEM"))
+          fprintf(stderr, "[hmc] value pass %d: %zu individuals, %.1f ms\n", n_value_passes, k, ms);
         h_redo.clear();
         for (size_t q = 0; q < k; ++q) {
           const int bi = sset[pos + q];
