@@ -265,6 +265,7 @@ struct Ctx {
   int fcap = 2048, waves = 0;
   int lds_waves_per_cu = 8;  // E-step individuals (blocks) sharing one CU's 160 KiB LDS
   int estep_nw = 2;          // E-step waves per individual (shape sweep at cfg 3: 2:8 beats 3:4 by 25%)
+  bool value_fast = false;   // value-only k-best lists first, the exact pass for ties only (hmc_set_value_mode)
   uint64_t trace_bytes = 0;
 
   Panel pan;
@@ -350,11 +351,13 @@ struct Ctx {
   std::vector<int32_t> h_status1, h_redo;
   DevBuf<int32_t> d_redo;
   int n_fallback = 0;  // individuals re-run on the fused kernel by the last E-step
+  int n_order_redo = 0;  // individuals re-run on the exact value pass (ties) by the last E-step
 
   // timings
   hipEvent_t ev[6] = {};
   double ms_fwd = 0, ms_tb = 0, ms_m = 0;
   double ms_s1 = 0, ms_s2 = 0, ms_fb = 0;  // split E-step: structure, values, fused fallback
+  double ms_order = 0;                     // part of ms_s2: exact value pass re-runs
 
   int fail(int code, const char *fmt, ...) {
     char buf[1024];
@@ -1616,8 +1619,8 @@ struct Ctx {
     if ((e = hipMemcpyAsync(d_cost.p, h_cost.data(), (size_t)n * 4, hipMemcpyHostToDevice, st)))
       return hipfail(e, "estep");
     ms_fwd = ms_tb = 0;
-    ms_s1 = ms_s2 = ms_fb = 0;
-    n_fallback = 0;
+    ms_s1 = ms_s2 = ms_fb = ms_order = 0;
+    n_fallback = n_order_redo = 0;
     n_struct_passes = n_value_passes = 0;
     int rc = 0;
     while (true) {  // a frontier overflow (fcap grows) restarts the E-step
@@ -2049,8 +2052,9 @@ struct Ctx {
         v.weight = d_weight.p;
         v.cost = d_cost.p;
         v.stamps = d_stamps.p;
+        const bool fast = value_fast;
         hipEventRecord(ev[0], st);
-        if ((e = launch_estep_values(v, grid2, estep_nw, st))) return hipfail(e, "estep_values launch");
+        if ((e = launch_estep_values(v, grid2, estep_nw, fast, st))) return hipfail(e, "estep_values launch");
         hipEventRecord(ev[1], st);
         if ((rc = read_status(sset, (int)k, true))) return rc;
         hipEventElapsedTime(&ms, ev[0], ev[1]);
@@ -2058,10 +2062,33 @@ struct Ctx {
         ++n_value_passes;
         if (getenv("HMC_DEBUG_MEM"))
           fprintf(stderr, "[hmc] value pass %d: %zu individuals, %.1f ms\n", n_value_passes, k, ms);
+        // ---- ties: individuals whose result would depend on the libstdc++ list
+        // order re-run on the exact value pass, in their own trace regions
+        std::vector<int> h_order;
+        for (size_t q = 0; q < k; ++q)
+          if (h_status[sset[pos + q]] == EST_NEEDS_ORDER) h_order.push_back(sset[pos + q]);
+        n_order_redo += (int)h_order.size();
+        if (!h_order.empty()) {
+          const int nr = (int)h_order.size();
+          if ((e = d_redo.ensure(nr))) return hipfail(e, "estep order re-run");
+          if ((rc = upload_order(d_redo, h_order.data(), nr))) return rc;
+          ValueArgs v2 = v;
+          v2.order = d_redo.p;
+          v2.n_order = nr;
+          hipEventRecord(ev[0], st);
+          if ((e = launch_estep_values(v2, std::max(1, std::min(G, nr)), estep_nw, false, st)))
+            return hipfail(e, "estep_values launch");
+          hipEventRecord(ev[1], st);
+          if ((rc = read_status(sset, (int)k, true))) return rc;
+          hipEventElapsedTime(&ms, ev[0], ev[1]);
+          ms_s2 += ms;
+          ms_order += ms;
+        }
         h_redo.clear();
         for (size_t q = 0; q < k; ++q) {
           const int bi = sset[pos + q];
           if (h_status[bi] == EST_OVERFLOW_TRACE) return fail(HMC_EHIP, "trace store overflow with exact sizes");
+          if (h_status[bi] == EST_NEEDS_ORDER) return fail(HMC_EHIP, "exact value pass reported a tie");
           if (h_status[bi] == EST_NEEDS_EXACT) h_redo.push_back(bi);
         }
         // ---- exact fallback: individuals whose forward likelihood underflowed.
@@ -2505,6 +2532,19 @@ int hmc_last_exact_stats(const hmc_ctx *h, int *rounds, uint64_t *candidates, do
   if (rounds) *rounds = h->c.exact_rounds;
   if (candidates) *candidates = h->c.exact_candidates;
   if (walk_ms) *walk_ms = h->c.ms_walk;
+  return HMC_OK;
+}
+
+int hmc_set_value_mode(hmc_ctx *h, int mode) {
+  if (!h || mode < 0 || mode > 1) return HMC_EARG;  // 0: value-only + re-runs, 1: libstdc++ permutations
+  h->c.value_fast = mode == 0;
+  return HMC_OK;
+}
+
+int hmc_last_estep_order(const hmc_ctx *h, int *n_rerun, double *rerun_ms) {
+  if (!h) return HMC_EARG;
+  if (n_rerun) *n_rerun = h->c.n_order_redo;
+  if (rerun_ms) *rerun_ms = h->c.ms_order;
   return HMC_OK;
 }
 

@@ -234,6 +234,39 @@ __device__ inline void seg_nth_slots(int n, int nth, const Seg &sg, const SegScr
   }
 }
 
+// Value-only top-S of every segment's list (slots [0, n), n <= SW): each
+// element's rank is the number of elements greater than it plus the equal ones
+// in lower slots, and the S best are written to slots [0, S) in rank order.
+// Returns, on the lane that finds one, the non-zero value straddling the
+// S-cut (the element ranked S equals one ranked above it), else 0: only such
+// a tie can make the retained set depend on the order libstdc++ would have
+// left the list in — and only if it is still at the cut when the list is
+// complete (a later, larger cut evicts both tied elements anyway).  Segments
+// with n <= S are left untouched.  Whole-wave call.
+__device__ inline double seg_rank_select(int n, int S, const Seg &sg, const SegScratch &ss) {
+  const int k = sg.k;
+  const double *sl = ss.slik + (sg.mask != 0ull ? sg.base : 0);
+  const bool mine = sg.mask != 0ull && n > S && k < n;
+  const double v = mine ? sl[k] : 0.0;
+  const uint32_t m = mine ? ss.smeta[sg.base + k] : 0u;
+  int gt = 0, eq = 0;
+  for (int q = 0; q < sg.sw; q += 2) {  // two slots per read; segment lanes read the same address
+    const double2 y = *(const double2 *)(sl + q);
+    gt += (q < n && y.x > v) ? 1 : 0;
+    eq += (q < k && y.x == v) ? 1 : 0;
+    gt += (q + 1 < n && y.y > v) ? 1 : 0;
+    eq += (q + 1 < k && y.y == v) ? 1 : 0;
+  }
+  const int rank = gt + eq;
+  wave_lds_sync();
+  if (mine && rank < S) {
+    ss.slik[sg.base + rank] = v;
+    ss.smeta[sg.base + rank] = m;
+  }
+  wave_lds_sync();
+  return mine && rank == S && eq > 0 ? v : 0.0;
+}
+
 // Register interface: lane g*SW+k holds element k of segment g's list.
 __device__ inline void seg_nth_element(double &v, uint32_t &m, int n, int nth, const Seg &sg,
                                        const SegScratch &ss) {

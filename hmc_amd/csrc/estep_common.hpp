@@ -36,10 +36,10 @@ __host__ __device__ inline unsigned long long trace_links(unsigned long long off
 // (HaploPair.cpp:35-61, 63-80): likelihood x tp, link = s, index = position in
 // s's list, reversed flag, and the homozygous rule (a homozygous link entering
 // a pair with different last alleles loses the flag and, when reversed, its
-// likelihood).  Groups of 8 links: the loads of a group issue together.
+// likelihood).  Groups of GRP links: the loads of a group issue together.
+template <int GRP = 8>
 __device__ inline void copy_extended(const double *xl, const uint32_t *xm, double *yl, uint32_t *ym, int k0, int ns,
                                      uint32_t s, double tpv, bool rev, bool differ) {
-  constexpr int GRP = 8;
   for (int k = 0; k < ns; k += GRP) {
     double v[GRP];
     uint32_t m[GRP];

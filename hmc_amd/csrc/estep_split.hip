@@ -600,6 +600,7 @@ struct K2Shared {
   int next;  // chain queue head
   int flag;  // a forward likelihood hit 0 before the last locus
   int iters; // diagnostic build: most chain-loop iterations of any wave this locus
+  int tie;   // FAST: a non-zero likelihood straddles some list's S-cut
 };
 
 struct K2Plan {
@@ -651,30 +652,26 @@ __device__ inline bool k2_write_trace(const ValueArgs &a, K2Shared *bs, const VF
   if (off + words > a.trace_cap) return false;
   uint32_t *hdr = a.trace + off + 1;
   uint32_t *lnk = a.trace + trace_links(off, (uint32_t)F);
+#ifndef HMC_TRACE_PER_STATE
+  for (int t = threadIdx.x; t < F; t += NT) hdr[t] = (Rhd[t] & 0xFFFFu) | *Y.nl(t) << 16;
+  // the link block is the frontier's meta array in state order (LDS tier,
+  // then HBM tier), links past a list's length zeroed: one coalesced word
+  // per thread and step
+  const uint32_t nlw = (uint32_t)F * (uint32_t)S;
+  for (uint32_t w = threadIdx.x; w < nlw; w += (uint32_t)NT) {
+    const uint32_t t = w / (uint32_t)S, k = w - t * (uint32_t)S;
+    const uint32_t n = *Y.nl((int)t);
+    lnk[w] = k < n ? Y.meta((int)t)[k] : 0u;
+  }
+#else  // one thread per state, S words each
   for (int t = threadIdx.x; t < F; t += NT) {
     const uint32_t n = *Y.nl(t);
     hdr[t] = (Rhd[t] & 0xFFFFu) | n << 16;
     const uint32_t *pm = Y.meta(t);
     uint32_t *dst = lnk + (size_t)t * S;
-    if ((S & 1) == 0) {
-      uint2 v[S_MAX / 2];
-#pragma unroll
-      for (int k = 0; k < S_MAX / 2; ++k)
-        if (2 * k < S) v[k] = ((const uint2 *)pm)[k];
-#pragma unroll
-      for (int k = 0; k < S_MAX / 2; ++k)
-        if (2 * k < S)
-          ((uint2 *)dst)[k] = make_uint2((uint32_t)(2 * k) < n ? v[k].x : 0u, (uint32_t)(2 * k + 1) < n ? v[k].y : 0u);
-    } else {
-      uint32_t v[S_MAX];
-#pragma unroll
-      for (int k = 0; k < S_MAX; ++k)
-        if (k < S) v[k] = pm[k];
-#pragma unroll
-      for (int k = 0; k < S_MAX; ++k)
-        if (k < S) dst[k] = (uint32_t)k < n ? v[k] : 0u;
-    }
+    for (int k = 0; k < S; ++k) dst[k] = (uint32_t)k < n ? pm[k] : 0u;
   }
+#endif
   if (threadIdx.x == 0) {
     a.trace[off] = (uint32_t)F;
     a.loc_off[(size_t)bi * (a.L + 1) + j] = off;
@@ -705,14 +702,23 @@ __device__ inline bool k2_write_trace(const ValueArgs &a, K2Shared *bs, const VF
 #define K2_FLUSH
 #endif
 
+#ifndef HMC_PA_UNROLL
+#define HMC_PA_UNROLL 8
+#endif
 size_t estep_s2_scratch_bytes(int fcap, int S) { return 2 * k2_front_bytes(fcap, S); }
 size_t estep_s2_lds_bytes(int S, int fc, int nw) { return (size_t)k2_plan(S, fc, nw).bytes; }
 
 #ifdef HMC_VALUES_WPE  // tuning experiments: force more resident waves per SIMD (fewer VGPRs)
 #define HMC_VALUES_ATTR __attribute__((amdgpu_waves_per_eu(HMC_VALUES_WPE)))
-#else
-#define HMC_VALUES_ATTR
+#else  // 4 waves per SIMD: 2 waves x 8 individuals per CU
+#define HMC_VALUES_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
+// FAST: the k-best lists are kept by value only (seg_rank_select): a list's
+// arrangement differs from the reference's, which changes no result while no
+// non-zero likelihood ties across a list's S-cut and the final candidates are
+// tie-free and non-zero; otherwise the individual reports EST_NEEDS_ORDER and
+// is re-run by the exact instantiation (FAST = false, libstdc++ permutations).
+template <bool FAST>
 __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int S = a.S, L = a.L, hl = a.head_len;
@@ -736,6 +742,7 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
     const int bi = a.order[q];
     const unsigned long long t_indiv = __builtin_amdgcn_s_memtime();
     int status = a.status[bi];
+    if (status == EST_NEEDS_ORDER) status = EST_OK;  // the re-run of a value-only pass
     if (status != EST_OK) {  // pass 1 found no resolution (dead frontier)
       if (tid == 0) {
         a.total[bi] = 0.0;
@@ -778,6 +785,8 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
         bs->next = 0;
         bs->flag = 0;
         bs->iters = 0;
+        bs->tie = 0;
+
       }
       // A: one thread per state — extension constructor (HaploPair.cpp:35-61),
       // the appends that still fit (HaploPair::add without selection,
@@ -788,17 +797,17 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
         const bool differ = (hd & 0xFFu) != ((hd >> 8) & 0xFFu);
         const int cb = (int)Rcb[t], ce = (int)Rcb[t + 1];
         // ordered forward sum (HaploPair.cpp:42, :66): words and predecessor
-        // likelihoods of 8 contributions loaded together, the adds in order
+        // likelihoods of HMC_PA_UNROLL contributions loaded together, the adds in order
         double fwd = 0.0;
-        for (int rb = cb; rb < ce; rb += 8) {
-          uint32_t ws[8];
-          double fs[8];
+        for (int rb = cb; rb < ce; rb += HMC_PA_UNROLL) {
+          uint32_t ws[HMC_PA_UNROLL];
+          double fs[HMC_PA_UNROLL];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) ws[u] = rb + u < ce ? Rct[rb + u] : Rct[cb];
+          for (int u = 0; u < HMC_PA_UNROLL; ++u) ws[u] = rb + u < ce ? Rct[rb + u] : Rct[cb];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) fs[u] = *X.fwd((int)(ws[u] & 0xFFFFu));
+          for (int u = 0; u < HMC_PA_UNROLL; ++u) fs[u] = *X.fwd((int)(ws[u] & 0xFFFFu));
 #pragma unroll
-          for (int u = 0; u < 8; ++u)
+          for (int u = 0; u < HMC_PA_UNROLL; ++u)
             if (rb + u < ce) {
               const double v = fs[u] * tpv;
               fwd = rb + u == cb ? v : fwd + v;
@@ -809,14 +818,14 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
         uint32_t s = w & 0xFFFFu, ns = w >> 24;
         double *yl = Y.lik(t);
         uint32_t *ym = Y.meta(t);
-        copy_extended(X.lik((int)s), X.meta((int)s), yl, ym, 0, (int)ns, s, tpv, (w >> 16) & 1u, differ);
+        copy_extended<HMC_PA_UNROLL>(X.lik((int)s), X.meta((int)s), yl, ym, 0, (int)ns, s, tpv, (w >> 16) & 1u, differ);
         int k = (int)ns, r0 = ce;
         for (int r = cb + 1; r < ce; ++r) {
           w = Rct[r];
           s = w & 0xFFFFu;
           ns = w >> 24;
           if (k + (int)ns <= S) {
-            copy_extended(X.lik((int)s), X.meta((int)s), yl, ym, k, (int)ns, s, tpv, (w >> 16) & 1u, differ);
+            copy_extended<HMC_PA_UNROLL>(X.lik((int)s), X.meta((int)s), yl, ym, k, (int)ns, s, tpv, (w >> 16) & 1u, differ);
             k += (int)ns;
           } else {
             r0 = r;
@@ -827,6 +836,7 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
         *Y.nl(t) = (uint32_t)k;
         *Y.r0(t) = (uint32_t)r0;
         if (!(fwd > 0.0) && j < L) bs->flag = 1;
+
       }
       __syncthreads();
       K2_ST(1);
@@ -847,7 +857,7 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
 #ifdef HMC_STAMPS
         unsigned long long tstep = __builtin_amdgcn_s_memtime();
 #endif
-        double tpv = 0.0;
+        double tpv = 0.0, tie_v = 0.0;
         uint32_t wc = 0, wn = 0;
         bool differ = false, done = sg.g >= G;
         double *slot_l = ss.slik + lane;
@@ -910,7 +920,12 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
           const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
           K2_CNT(14, ts0 - tstep);
 #endif
-          seg_nth_slots(n, S - 1, sg, ss);
+          if (FAST) {
+            const double tv = seg_rank_select(n, S, sg, ss);
+            tie_v = tv > tie_v ? tv : tie_v;
+          } else {
+            seg_nth_slots(n, S - 1, sg, ss);
+          }
 #ifdef HMC_STAMPS
           tstep = __builtin_amdgcn_s_memtime();
           K2_CNT(13, tstep - ts0);
@@ -918,6 +933,9 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
           if (act) {
             k0 = S;
             if (++r == re_) {
+              // FAST: a tie recorded on the way that is still at the final cut
+              if (FAST && tie_v != 0.0 && tie_v == ss.slik[sg.base + S - 1]) bs->tie = 1;
+              tie_v = 0.0;
               if (sg.k < S) {
                 Y.lik(st)[sg.k] = *slot_l;
                 Y.meta(st)[sg.k] = *slot_m;
@@ -934,6 +952,10 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
       __syncthreads();
       K2_ST(2);
       K2_CNT(12, bs->iters);
+      if (FAST && bs->tie) {
+        status = EST_NEEDS_ORDER;
+        break;
+      }
       if (!k2_write_trace(a, bs, Y, Rhd, F, j, bi, tcur, tend)) status = EST_OVERFLOW_TRACE;
       K2_ST(3);
       K2_CNT(11, 1);
@@ -948,10 +970,11 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
     K2_ST(4);
     if (tid == 0) {
       a.cost[bi] = (int32_t)((__builtin_amdgcn_s_memtime() - t_indiv) >> 10);
-      a.status[bi] = status;
       int cnt = 0;
       double total = 0.0;
       if (status == EST_OK) {
+        double out_max = 0.0;  // FAST: best likelihood the selection dropped
+        bool out_any = false;
         for (int t = 0; t < Fp; ++t) {
           total += *X.fwd(t);
           const uint32_t n = *X.nl(t);
@@ -963,10 +986,23 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
           }
           if (cnt > S) {
             nth_element_greater_masks(W, cnt, S - 1, cnt);
+            if (FAST)
+              for (int q = S; q < cnt; ++q) {
+                out_max = out_any && out_max > W.l(q) ? out_max : W.l(q);
+                out_any = true;
+              }
             cnt = S;
           }
         }
         sort_greater_small(W, cnt);
+        if (FAST) {  // the candidates and their order must not depend on list order
+          bool tie = out_any && cnt > 0 && out_max == W.l(cnt - 1);
+          for (int c = 0; c < cnt; ++c) tie = tie || W.l(c) == 0.0 || (c > 0 && W.l(c) == W.l(c - 1));
+          if (tie) status = EST_NEEDS_ORDER;
+        }
+      }
+      a.status[bi] = status;
+      if (status == EST_OK) {
         double coverage = 0.0;
         for (int c = 0; c < cnt; ++c) {
           const uint32_t mm = W.m(c);
@@ -982,6 +1018,8 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
         }
         for (int c = 0; c < cnt; ++c)  // HaploModel.cpp:97-98
           a.weight[(size_t)bi * S_MAX + c] = a.posterior[(size_t)bi * S_MAX + c] / coverage;
+      } else {
+        cnt = 0;
       }
       a.total[bi] = total;
       a.ncand[bi] = cnt;
@@ -1009,16 +1047,21 @@ hipError_t launch_estep_structure(const StructArgs &a, int grid, hipStream_t st)
   return hipGetLastError();
 }
 
-hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, hipStream_t st) {
+hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, hipStream_t st) {
   if (a.S < 1 || a.S > S_MAX || a.fcap > 65535 || a.lds_fc < 0 || nw < 1 || nw > 4) return hipErrorInvalidValue;
   const size_t lds = estep_s2_lds_bytes(a.S, a.lds_fc, nw);
   static size_t lds_attr = 0;
   if (lds > 65536 && lds > lds_attr) {
-    hipError_t e = hipFuncSetAttribute((const void *)estep_values, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
+    for (const void *f : {(const void *)estep_values<true>, (const void *)estep_values<false>}) {
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
     lds_attr = lds;
   }
-  hipLaunchKernelGGL(estep_values, dim3(grid), dim3(WAVE * nw), lds, st, a);
+  if (fast)
+    hipLaunchKernelGGL(estep_values<true>, dim3(grid), dim3(WAVE * nw), lds, st, a);
+  else
+    hipLaunchKernelGGL(estep_values<false>, dim3(grid), dim3(WAVE * nw), lds, st, a);
   return hipGetLastError();
 }
 

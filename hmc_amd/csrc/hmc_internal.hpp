@@ -41,6 +41,8 @@ enum EStatus : int32_t {
   EST_NEEDS_EXACT = 2,         // split E-step: a forward likelihood underflowed to 0 before
                                // the last locus, so extend() would skip that pair
                                // (HaploBuilder.cpp:237) — re-run on the fused kernel
+  EST_NEEDS_ORDER = 3,         // value-only value pass: a tie makes the result depend on
+                               // the libstdc++ list order — re-run on the exact value pass
 };
 
 // Panel resident in HBM.
@@ -202,7 +204,7 @@ size_t estep_s1_lds_bytes(int fc, int hc, int cc);
 size_t estep_s2_scratch_bytes(int fcap, int S);
 size_t estep_s2_lds_bytes(int S, int fc, int nw);
 hipError_t launch_estep_structure(const StructArgs &a, int grid, hipStream_t st);
-hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, hipStream_t st);
+hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, hipStream_t st);
 hipError_t launch_traceback(const TracebackArgs &a, int total_cands, hipStream_t st);
 hipError_t launch_transpose_rows_u8(const uint8_t *in, const int32_t *rowmap, uint8_t *out, int rows, int cols,
                                     hipStream_t st);

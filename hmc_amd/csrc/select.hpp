@@ -24,7 +24,9 @@
 
 namespace hmc {
 
-// A list view: element k lives at lik[k*stride], meta[k*stride].
+// A list view: element k lives at lik[k*stride], meta[k*stride].  The
+// algorithms below take any view with the same members (l, m, set, copy,
+// swap, gt), e.g. one typed for LDS in the value pass.
 struct LinkList {
   double *lik;
   uint32_t *meta;
@@ -49,7 +51,8 @@ struct LinkList {
 HMC_HD int lg2_floor(int n) { return 31 - __builtin_clz((unsigned)n); }
 
 // std::__move_median_to_first (stl_algo.h:79-102)
-HMC_HD void move_median_to_first(const LinkList &v, int result, int a, int b, int c) {
+template <class V>
+HMC_HD void move_median_to_first(const V &v, int result, int a, int b, int c) {
   if (v.gt(a, b)) {
     if (v.gt(b, c)) v.swap(result, b);
     else if (v.gt(a, c)) v.swap(result, c);
@@ -60,7 +63,8 @@ HMC_HD void move_median_to_first(const LinkList &v, int result, int a, int b, in
 }
 
 // std::__unguarded_partition (stl_algo.h:1878-1896); pivot value stays at `pivot`.
-HMC_HD int unguarded_partition(const LinkList &v, int first, int last, int pivot) {
+template <class V>
+HMC_HD int unguarded_partition(const V &v, int first, int last, int pivot) {
   while (true) {
     while (v.gt(first, pivot)) ++first;
     --last;
@@ -72,14 +76,16 @@ HMC_HD int unguarded_partition(const LinkList &v, int first, int last, int pivot
 }
 
 // std::__unguarded_partition_pivot (stl_algo.h:1900-1907)
-HMC_HD int unguarded_partition_pivot(const LinkList &v, int first, int last) {
+template <class V>
+HMC_HD int unguarded_partition_pivot(const V &v, int first, int last) {
   int mid = first + (last - first) / 2;
   move_median_to_first(v, first, first + 1, mid, last - 1);
   return unguarded_partition(v, first + 1, last, first);
 }
 
 // std::__insertion_sort + __unguarded_linear_insert (stl_algo.h:1799-1849)
-HMC_HD void insertion_sort(const LinkList &v, int first, int last) {
+template <class V>
+HMC_HD void insertion_sort(const V &v, int first, int last) {
   if (first == last) return;
   for (int i = first + 1; i != last; ++i) {
     double x = v.l(i);
@@ -100,7 +106,8 @@ HMC_HD void insertion_sort(const LinkList &v, int first, int last) {
 }
 
 // std::__push_heap with a value comparator (stl_heap.h:134-149)
-HMC_HD void push_heap(const LinkList &v, int first, int hole, int top, double x, uint32_t y) {
+template <class V>
+HMC_HD void push_heap(const V &v, int first, int hole, int top, double x, uint32_t y) {
   int parent = (hole - 1) / 2;
   while (hole > top && v.l(first + parent) > x) {
     v.copy(first + hole, first + parent);
@@ -111,7 +118,8 @@ HMC_HD void push_heap(const LinkList &v, int first, int hole, int top, double x,
 }
 
 // std::__adjust_heap (stl_heap.h:223-250)
-HMC_HD void adjust_heap(const LinkList &v, int first, int hole, int len, double x, uint32_t y) {
+template <class V>
+HMC_HD void adjust_heap(const V &v, int first, int hole, int len, double x, uint32_t y) {
   const int top = hole;
   int second = hole;
   while (second < (len - 1) / 2) {
@@ -129,7 +137,8 @@ HMC_HD void adjust_heap(const LinkList &v, int first, int hole, int len, double 
 }
 
 // std::__make_heap (stl_heap.h:339-360)
-HMC_HD void make_heap(const LinkList &v, int first, int last) {
+template <class V>
+HMC_HD void make_heap(const V &v, int first, int last) {
   int len = last - first;
   if (len < 2) return;
   int parent = (len - 2) / 2;
@@ -143,7 +152,8 @@ HMC_HD void make_heap(const LinkList &v, int first, int last) {
 }
 
 // std::__heap_select with std::__pop_heap (stl_algo.h:1642-1651, stl_heap.h:253-266)
-HMC_HD void heap_select(const LinkList &v, int first, int middle, int last) {
+template <class V>
+HMC_HD void heap_select(const V &v, int first, int middle, int last) {
   make_heap(v, first, middle);
   for (int i = middle; i < last; ++i) {
     if (v.gt(i, first)) {
@@ -156,7 +166,8 @@ HMC_HD void heap_select(const LinkList &v, int first, int middle, int last) {
 }
 
 // std::nth_element(first, first+nth, first+n, greater) (stl_algo.h:1964-1986, 4794-4812)
-HMC_HD void nth_element_greater(const LinkList &v, int n, int nth) {
+template <class V>
+HMC_HD void nth_element_greater(const V &v, int n, int nth) {
   if (n == 0 || nth == n) return;
   int first = 0, last = n, depth = lg2_floor(n) * 2;
   while (last - first > 3) {
@@ -189,7 +200,8 @@ HMC_HD uint32_t bit_hi(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
 
 // `span` >= last is the scan bound; on the device it is the same for every
 // lane (2S), so the reads of one partition issue back to back.
-HMC_HD int partition_pivot_masks(const LinkList &v, int first, int last, int span) {
+template <class V>
+HMC_HD int partition_pivot_masks(const V &v, int first, int last, int span) {
   const int a = first + 1, b = first + (last - first) / 2, c = last - 1;
   const double va = v.l(a), vb = v.l(b), vc = v.l(c);
   // the branch tree of move_median_to_first as selects
@@ -219,7 +231,8 @@ HMC_HD int partition_pivot_masks(const LinkList &v, int first, int last, int spa
 }
 
 // nth_element_greater with the mask partition (n <= span <= 32).
-HMC_HD void nth_element_greater_masks(const LinkList &v, int n, int nth, int span) {
+template <class V>
+HMC_HD void nth_element_greater_masks(const V &v, int n, int nth, int span) {
   if (n == 0 || nth == n) return;
   int first = 0, last = n, depth = lg2_floor(n) * 2;
   while (last - first > 3) {
@@ -238,6 +251,7 @@ HMC_HD void nth_element_greater_masks(const LinkList &v, int n, int nth, int spa
 
 // std::sort(first, first+n, greater) for n <= 16 (stl_algo.h:1925-1958):
 // __introsort_loop is a no-op below _S_threshold, leaving __insertion_sort.
-HMC_HD void sort_greater_small(const LinkList &v, int n) { insertion_sort(v, 0, n); }
+template <class V>
+HMC_HD void sort_greater_small(const V &v, int n) { insertion_sort(v, 0, n); }
 
 }  // namespace hmc

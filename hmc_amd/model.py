@@ -176,8 +176,16 @@ class HaploModel:
         self._check(lib().hmc_last_estep_split(self._h, C.byref(s1), C.byref(s2), C.byref(fb), C.byref(nf)))
         ps, pv = C.c_int(), C.c_int()
         self._check(lib().hmc_last_estep_passes(self._h, C.byref(ps), C.byref(pv)))
+        no, om = C.c_int(), C.c_double()
+        self._check(lib().hmc_last_estep_order(self._h, C.byref(no), C.byref(om)))
         return dict(structure_ms=s1.value, values_ms=s2.value, fallback_ms=fb.value, n_fallback=nf.value,
-                    structure_passes=ps.value, value_passes=pv.value)
+                    structure_passes=ps.value, value_passes=pv.value, n_order_rerun=no.value, order_ms=om.value)
+
+    def set_value_mode(self, mode: str):
+        """Value pass of the split E-step: "fast" (value-only k-best lists, the
+        libstdc++ permutations only for individuals with ties) or "exact" (the
+        permutations for everyone; default).  Results are identical."""
+        self._check(lib().hmc_set_value_mode(self._h, {"fast": 0, "exact": 1}[mode]))
 
     # ----------------------------------------------------------------- panel
     def load(self, genos: GenoData):

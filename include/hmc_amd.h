@@ -247,6 +247,19 @@ int hmc_last_estep_split(const hmc_ctx *ctx, double *structure_ms, double *value
 /* Launches of the last hmc_resolve_all: structure passes and value passes
  * (individuals pass in groups when their records / traces exceed the stores). */
 int hmc_last_estep_passes(const hmc_ctx *ctx, int *structure_passes, int *value_passes);
+/* Value pass of the split E-step.  Mode 0: k-best lists are kept by
+ * likelihood value only; an individual for which that could change a result
+ * (a non-zero likelihood tied across some list's S-cut — the set
+ * std::nth_element keeps then depends on the list order, HaploPair.cpp:85-88 —
+ * or final candidates with equal or zero priors, HaploBuilder.cpp:101-105) is
+ * re-run with the libstdc++ permutations.  Mode 1 (default): every individual
+ * with the libstdc++ permutations.  Results are identical; mode 0 pays off
+ * only where few individuals have such ties (at BASELINE config 3 about half
+ * of them have final candidates with equal priors, and mode 1 is faster). */
+int hmc_set_value_mode(hmc_ctx *ctx, int mode);
+/* Individuals the last E-step re-ran with the libstdc++ permutations (mode 0)
+ * and the device time of those re-runs (ms, part of values_ms). */
+int hmc_last_estep_order(const hmc_ctx *ctx, int *n_rerun, double *rerun_ms);
 /* Device time (ms, HIP events on the context stream) of the last E-step
  * forward kernel, traceback and whole M-step. */
 int hmc_last_timings(const hmc_ctx *ctx, double *estep_forward_ms, double *estep_traceback_ms, double *mstep_ms);

@@ -92,6 +92,27 @@ def test_estep_on_reference_model(oracle_mod, name, S, mode):
     assert_estep_equal(m, o, ll_g, ll_o, H, re_g)
 
 
+@pytest.mark.parametrize("name", ["cfg1", "a3miss5", "a8", "n300"])
+@pytest.mark.parametrize("S", [10, 3])
+def test_value_only_mode_with_order_reruns(oracle_mod, name, S):
+    """hmc_set_value_mode(0): value-only k-best lists (seg_rank_select), the
+    libstdc++ permutations only for individuals with ties — same E-step, bit
+    for bit, as HaploModel::resolveAll."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=S)
+    o.find_patterns()
+    pt = o.patterns()
+    m = gpu_model(p, S)
+    m.set_value_mode("fast")
+    m.set_patterns(pt["start"], pt["len"], pt["freq"], pt["tp"], pt["succ"], last_symbols(pt))
+    ll_g, H, re_g = m.resolve_all()
+    o.reset_counters()
+    ll_o = o.resolve_all()
+    assert_estep_equal(m, o, ll_g, ll_o, H, re_g)
+    st = m.estep_split_stats()
+    assert 0 <= st["n_order_rerun"] <= p.N
+
+
 @pytest.mark.parametrize("S", [1, 2, 5, 16])
 def test_estep_sample_sizes(oracle_mod, S):
     p = panel("miss2")

@@ -27,4 +27,5 @@ for shape in sys.argv[1:] or ["3:4"]:
         ref = ref or key
         assert key == ref, (shape, key, ref)
         print(f"shape {shape} run {r}: structure {s['structure_ms']:.1f} ms ({s['structure_passes']} passes) "
-              f"values {s['values_ms']:.1f} ms ({s['value_passes']} passes) ll={ll!r}", flush=True)
+              f"values {s['values_ms']:.1f} ms ({s['value_passes']} passes; re-run {s['n_order_rerun']} individuals "
+              f"{s['order_ms']:.1f} ms) ll={ll!r}", flush=True)
