@@ -265,6 +265,10 @@ struct Ctx {
   int fcap = 2048, waves = 0;
   int lds_waves_per_cu = 8;  // E-step individuals (blocks) sharing one CU's 160 KiB LDS
   int estep_nw = 2;          // E-step waves per individual (shape sweep at cfg 3: 2:8 beats 3:4 by 25%)
+  // value-pass shape (waves per individual : individuals per CU), 0 = by group
+  // size: 1:16 when the group fills 12 individuals per CU (cfg 3 E2: 9% faster
+  // than 2:8), else 2:8 (more segments per individual for small groups)
+  int vp_nw = 0, vp_ipc = 0;
   bool value_fast = false;   // value-only k-best lists first, the exact pass for ties only (hmc_set_value_mode)
   uint64_t trace_bytes = 0;
 
@@ -1585,10 +1589,11 @@ struct Ctx {
     hipMemGetInfo(&freeb, &totb);
     const double avail = (double)freeb + (double)d_trace.n * 4 + (double)d_rec.n * 4;
     // (cfg 3's E1 with the M0 model needs ~2x HBM in records + traces; larger
-    // stores (fewer groups) measured no faster and crowd out the next M0)
-    trace_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.35), 96ull << 30),
+    // stores (fewer groups) measured no faster and crowd out the next M0.  The
+    // trace cap keeps cfg 3's E2.. (~90 GB of traces) in one value pass.)
+    trace_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.42), 120ull << 30),
                                       1ull << 20) / 4;
-    rec_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.25), 64ull << 30),
+    rec_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.28), 80ull << 30),
                                     1ull << 20) / 4;
     if (getenv("HMC_DEBUG_MEM"))
       fprintf(stderr, "[hmc] E-step: free %.1f GB, stores %.1f + %.1f GB, budgets trace %.1f rec %.1f GB\n",
@@ -1876,7 +1881,7 @@ struct Ctx {
     const bool prev_ok = !exact && (int)prev_rneed.size() == n && prev_P > 0 && P < 2 * (int64_t)prev_P &&
                          2 * (int64_t)P > prev_P;
     if (prev_ok)
-      for (int i = 0; i < n; ++i) est[i] = prev_rneed[i] + prev_rneed[i] / 4 + 64;
+      for (int i = 0; i < n; ++i) est[i] = prev_rneed[i] + prev_rneed[i] / 10 + 64;
     bool have_est = prev_ok;
     int rc;
     while (!pending.empty()) {
@@ -1918,7 +1923,8 @@ struct Ctx {
           return hipfail(e, "estep");
       }
       const int hcap1 = next_pow2(2 * fcap), ccap1 = 8 * fcap;
-      const int bpc1 = np > 4 * dev_cu ? 8 : 4;  // structure pass: one wave per individual
+      int bpc1 = np > 4 * dev_cu ? 8 : 4;  // structure pass: one wave per individual
+      if (const char *env = getenv("HMC_S1_BPC")) bpc1 = std::max(1, atoi(env));  // tuning experiments
       const int grid1 = std::max(1, std::min(np, dev_cu * bpc1));
       const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1);
       if ((e = d_scr1.ensure(per1 * grid1)) || (e = d_rec_off.ensure((size_t)n * (L + 1))) ||
@@ -2022,7 +2028,14 @@ struct Ctx {
           pos += k;
           continue;
         }
-        const int grid2 = std::max(1, std::min<int>(G, (int)k));
+        int vnw = vp_nw, vipc = vp_ipc;
+        if (vnw <= 0) {
+          const bool many = (int)k >= 12 * dev_cu;
+          vnw = many ? 1 : 2;
+          vipc = many ? 16 : 8;
+        }
+        const int G2 = std::max(1, std::min(waves > 0 ? waves : dev_cu * vipc, n));
+        const int grid2 = std::max(1, std::min<int>(G2, (int)k));
         const size_t per2 = estep_s2_scratch_bytes(fcap, S);
         if ((e = d_scr2.ensure(per2 * grid2))) return hipfail(e, "estep pass-2 scratch");
         ValueArgs v;
@@ -2036,7 +2049,7 @@ struct Ctx {
         v.scratch = d_scr2.p;
         v.scratch_stride = per2;
         v.fcap = fcap;
-        v.lds_fc = s2_tier(S);
+        v.lds_fc = s2_tier(S, vnw, vipc);
         v.trace = d_trace.p;
         v.trace_cap = d_trace.n;
         v.trace_cursor = d_trace_cursor.p;
@@ -2054,7 +2067,7 @@ struct Ctx {
         v.stamps = d_stamps.p;
         const bool fast = value_fast;
         hipEventRecord(ev[0], st);
-        if ((e = launch_estep_values(v, grid2, estep_nw, fast, st))) return hipfail(e, "estep_values launch");
+        if ((e = launch_estep_values(v, grid2, vnw, fast, st))) return hipfail(e, "estep_values launch");
         hipEventRecord(ev[1], st);
         if ((rc = read_status(sset, (int)k, true))) return rc;
         hipEventElapsedTime(&ms, ev[0], ev[1]);
@@ -2076,7 +2089,7 @@ struct Ctx {
           v2.order = d_redo.p;
           v2.n_order = nr;
           hipEventRecord(ev[0], st);
-          if ((e = launch_estep_values(v2, std::max(1, std::min(G, nr)), estep_nw, false, st)))
+          if ((e = launch_estep_values(v2, std::max(1, std::min(G2, nr)), vnw, false, st)))
             return hipfail(e, "estep_values launch");
           hipEventRecord(ev[1], st);
           if ((rc = read_status(sset, (int)k, true))) return rc;
@@ -2145,10 +2158,10 @@ struct Ctx {
     cc = 0;
   }
   // LDS tier of pass 2: states per frontier for the block's LDS share.
-  int s2_tier(int S) const {
-    const int budget = 160 * 1024 / std::max(1, lds_waves_per_cu) - 256;
+  static int s2_tier(int S, int nw, int ipc) {
+    const int budget = 160 * 1024 / std::max(1, ipc) - 256;
     for (int f = 4096; f >= 4; f -= 4)
-      if ((int)estep_s2_lds_bytes(S, f, estep_nw) <= budget) return f;
+      if ((int)estep_s2_lds_bytes(S, f, nw) <= budget) return f;
     return 0;
   }
 
@@ -2558,8 +2571,9 @@ int hmc_last_estep_passes(const hmc_ctx *h, int *structure_passes, int *value_pa
 int hmc_set_estep_shape(hmc_ctx *h, int waves_per_individual, int individuals_per_cu) {
   if (!h) return HMC_EARG;
   if (waves_per_individual < 0 || waves_per_individual > 4 || individuals_per_cu < 0) return HMC_EARG;
-  if (waves_per_individual > 0) h->c.estep_nw = waves_per_individual;
-  if (individuals_per_cu > 0) h->c.lds_waves_per_cu = individuals_per_cu;
+  if (waves_per_individual > 0) h->c.estep_nw = h->c.vp_nw = waves_per_individual;
+  if (individuals_per_cu > 0) h->c.lds_waves_per_cu = h->c.vp_ipc = individuals_per_cu;
+  if (waves_per_individual == 0 && individuals_per_cu == 0) h->c.vp_nw = h->c.vp_ipc = 0;  // value pass by group size
   return HMC_OK;
 }
 

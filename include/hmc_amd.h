@@ -231,7 +231,9 @@ int hmc_write_patterns(hmc_ctx *ctx, const char *path);
 int hmc_set_tuning(hmc_ctx *ctx, int frontier_cap, uint64_t trace_bytes, int waves);
 /* E-step launch shape: wavefronts cooperating on one individual (1..4,
  * default 2) and individuals sharing one CU's LDS (default 8); 0 keeps the
- * current value.  Results do not depend on the shape. */
+ * current value.  A shape set here applies to every kernel; (0, 0) returns the
+ * split E-step's value pass to its automatic shape (1:16 for groups of at
+ * least 12 individuals per CU, else 2:8).  Results do not depend on the shape. */
 int hmc_set_estep_shape(hmc_ctx *ctx, int waves_per_individual, int individuals_per_cu);
 /* E-step implementation: 0 (default) = two passes, a structure pass that
  * replays extendAll/addHaploPair (HaploBuilder.cpp:226-261) on pattern ids
