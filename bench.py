@@ -16,8 +16,10 @@ the samples are dropped and M0 is mined again so that the timed steps start
 from M0 (E1 included).  --config 2 / 5 select the other single-GPU configs.
 
 Multi-GPU: launched by torch.distributed.run, one process per GPU.  The panel
-is the same (strong scaling): individuals are sharded in contiguous blocks, the
-M-step all-reduces the per-level candidate sums over RCCL inside libhmc_amd.
+is the same (strong scaling): individuals are sharded in contiguous blocks; the
+M-step's per-level candidate sums are reduced in rank order over RCCL inside
+libhmc_amd (chained ncclBroadcast of seeded partial sums: bit-identical to one
+GPU; hmc_set_reduction selects a single ncclAllReduce instead).
 torch.distributed (gloo) only bootstraps the RCCL id, the barriers and the
 max-over-ranks time.
 """
@@ -59,6 +61,8 @@ def parse():
     ap.add_argument("--cpu-indiv", type=int, default=40, help="individuals timed for the CPU E-step sample")
     ap.add_argument("--cpu-roots", type=int, default=0, help="start loci timed for the CPU M-step sample (0: L/40)")
     ap.add_argument("--trace-bytes", type=int, default=0, help="E-step store budget per store (0: automatic)")
+    ap.add_argument("--reduction", default="ordered", choices=["ordered", "allreduce"],
+                    help="cross-rank M-step sums: rank-ordered (bit-identical to one GPU) or one all-reduce")
     a = ap.parse_args()
     c = synth.CONFIGS[a.config]
     a.N = a.individuals or c["N"]
@@ -115,6 +119,7 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         uid = obj[0]
     m = hmc_amd.HaploModel(device=local, rank=rank, world=world, unique_id=uid)
+    m.set_reduction(args.reduction)
     m.sample_size = args.sample_size
     if args.trace_bytes:
         m.set_tuning(trace_bytes=args.trace_bytes)
@@ -202,7 +207,8 @@ def main():
                             f"step = one EM iteration (E_k + M_k) from the genotype-mined model M0",
                 "individuals": N, "loci": L, "sample_size": args.sample_size,
                 "min_freq_abs": 1.5, "pattern_len": [1, 30],
-                "parallelism": f"individual-sharded x{world}, RCCL all-reduce per mining level",
+                "parallelism": f"individual-sharded x{world}, " + ("ordered RCCL reduction (chained broadcasts)" if args.reduction == "ordered"
+                                                                     else "RCCL all-reduce") + " per mining level",
             },
             "roofline": {
                 "bound": "hbm", "kernel": "estep_values",
