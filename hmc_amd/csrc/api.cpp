@@ -2146,6 +2146,65 @@ struct Ctx {
     return HMC_OK;
   }
 
+  // PatternManager::checkFrequency (PatternManager.cpp:146-193) of n given
+  // candidates of one length against the current items (genotypes while no
+  // samples exist, else the weighted samples): the per-level seam of the
+  // reference's DFS (searchPattern, :100-144).  Sums in item order; across
+  // ranks in rank order (or one all-reduce), as the mining levels.
+  DevBuf<int32_t> d_lv_start;
+  DevBuf<uint8_t> d_lv_al;
+  DevBuf<double> d_lv_sum;
+  int mine_level(int level, int n, const int32_t *start, const int32_t *alleles, double *freq, uint64_t *scanned) {
+    if (!have_panel) return fail(HMC_EARG, "no genotypes loaded");
+    if (level < 0 || n < 0 || (n > 0 && (!start || !freq || (level > 0 && !alleles))))
+      return fail(HMC_EARG, "mine_level arguments");
+    const int L = pan.L;
+    if (scanned) *scanned = 0;
+    if (n == 0) return HMC_OK;
+    if (level == 0) {  // HaploPattern of length 0: frequency 1 (checkFrequency :149-150)
+      for (int c = 0; c < n; ++c) freq[c] = 1.0;
+      return HMC_OK;
+    }
+    std::vector<uint8_t> al((size_t)n * level);
+    for (int c = 0; c < n; ++c) {
+      if (start[c] < 0 || start[c] + level > L) return fail(HMC_EARG, "candidate %d outside the loci", c);
+      for (int j = 0; j < level; ++j) {
+        const auto &sy = pan.sym[start[c] + j];
+        const int32_t a = alleles[(size_t)c * level + j];
+        uint8_t ix = 0xFD;  // a symbol the locus does not have: matches only missing alleles
+        for (size_t q = 0; q < sy.size(); ++q)
+          if (sy[q].first == a) ix = (uint8_t)q;
+        al[(size_t)c * level + j] = ix;
+      }
+    }
+    hipError_t e;
+    if ((e = d_lv_start.ensure(n)) || (e = d_lv_al.ensure(al.size())) || (e = d_lv_sum.ensure(n)) ||
+        (e = hipMemcpyAsync(d_lv_start.p, start, (size_t)n * 4, hipMemcpyHostToDevice, st)) ||
+        (e = hipMemcpyAsync(d_lv_al.p, al.data(), al.size(), hipMemcpyHostToDevice, st)))
+      return hipfail(e, "mine_level");
+    const bool genotype = !have_samples;
+    MineArgs a = mine_args(genotype);
+    int rc;
+    if (multi() && reduction == RED_ORDERED) {
+      for (int r = 0; r < world; ++r) {
+        if (r == rank) {
+          a.seeded = r > 0;
+          if ((e = launch_mine_scan(a, level, n, d_lv_start.p, d_lv_al.p, d_lv_sum.p, st))) return hipfail(e, "mine_scan");
+        }
+        if ((rc = bcast(d_lv_sum.p, n, r))) return rc;
+      }
+    } else {
+      if ((e = launch_mine_scan(a, level, n, d_lv_start.p, d_lv_al.p, d_lv_sum.p, st))) return hipfail(e, "mine_scan");
+      if ((rc = allreduce_sum(d_lv_sum.p, n))) return rc;
+    }
+    if ((e = hipMemcpyAsync(freq, d_lv_sum.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+      return hipfail(e, "mine_level");
+    const double denom = genotype ? (double)pan.N : total_weight;  // :178, :190
+    for (int c = 0; c < n; ++c) freq[c] = freq[c] / denom;
+    if (scanned) *scanned = (uint64_t)n * (uint64_t)a.n_items;
+    return HMC_OK;
+  }
+
   // LDS tiers of pass 1 (one wave per individual, `budget` bytes): states per
   // frontier, key slots (2x, power of two), contributions per locus (2x).
   static void s1_tier(int budget, int &fc, int &hc, int &cc) {
@@ -2768,6 +2827,12 @@ int hmc_allele_table(const hmc_ctx *h, int32_t *num, int32_t *sym, double *freq)
 int hmc_find_patterns(hmc_ctx *h, int *n_patterns, uint64_t *r_m) {
   if (!h) return HMC_EARG;
   return h->c.mine(n_patterns, r_m);
+}
+
+int hmc_mine_level(hmc_ctx *h, int level, int n, const int32_t *start, const int32_t *alleles, double *freq,
+                   uint64_t *scanned) {
+  if (!h) return HMC_EARG;
+  return h->c.mine_level(level, n, start, alleles, freq, scanned);
 }
 
 int hmc_model_info(const hmc_ctx *h, int *n_patterns, int *head_len) {

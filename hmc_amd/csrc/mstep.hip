@@ -558,6 +558,63 @@ __global__ void mine_succ(MineArgs a, PatternTable t, int P) {
 }
 
 // ---- host-side launch helpers -----------------------------------------------
+// PatternManager::checkFrequency (PatternManager.cpp:146-193) for arbitrary
+// candidates of one length: one wavefront per candidate scans every item of
+// this rank in order.  Genotype branch: getMatchingFrequency (:267-291), the
+// product taken locus by locus as `total_freq *= 0.5 * freq`; sample branch:
+// the haplotype weight.  Lane 0 adds the matching items' values in item order
+// (non-matching items add nothing), continuing sum[c] when seeded.
+__global__ __launch_bounds__(64) void mine_scan(MineArgs a, int level, int n, const int32_t *cstart,
+                                                const uint8_t *cal, double *sum) {
+  __shared__ double vals[WAVE];
+  const int lane = threadIdx.x;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (int c = blockIdx.x; c < n; c += gridDim.x) {
+    const int st = cstart[c];
+    const uint8_t *al = cal + (size_t)c * level;
+    double s = a.seeded ? sum[c] : 0.0;
+    for (int base = 0; base < a.n_items; base += WAVE) {
+      const int i = base + lane;
+      const uint32_t item = (uint32_t)(a.item_base + (i < a.n_items ? i : a.n_items - 1));
+      bool m = i < a.n_items;
+      double v = 1.0;
+      for (int j = 0; j < level; ++j) {
+        const int e = st + j;
+        const uint8_t pa = al[j];
+        if (a.genotype) {
+          const uchar2 g = a.geno_lm[(size_t)e * a.item_stride + item];
+          const bool m0 = g.x == MISSING, m1 = g.y == MISSING;
+          m = m && (m0 || m1 || g.x == pa || g.y == pa);
+          const double af = pa < a.amax ? a.afreq[(size_t)e * a.amax + pa] : 0.0;
+          const double x0 = m0 ? af : (g.x == pa ? 1.0 : 0.0);
+          const double x1 = m1 ? af : (g.y == pa ? 1.0 : 0.0);
+          v = v * (0.5 * ((0.0 + x0) + x1));
+        } else {
+          m = m && a.samp_lm[(size_t)e * a.item_stride + item] == pa;
+        }
+        if (!__ballot(m)) break;
+      }
+      const uint64_t b = __ballot(m);
+      if (m) vals[__popcll(b & lt)] = a.genotype ? v : a.w[item];
+      wave_sync();
+      if (lane == 0) {
+        const int k = __popcll(b);
+        for (int q = 0; q < k; ++q) s = s + vals[q];
+      }
+      wave_sync();
+    }
+    if (lane == 0) sum[c] = s;
+  }
+}
+
+hipError_t launch_mine_scan(const MineArgs &a, int level, int n, const int32_t *cstart, const uint8_t *cal,
+                            double *sum, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (level < 1 || a.n_items < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mine_scan, dim3(n < 65536 ? n : 65536), dim3(WAVE), 0, st, a, level, n, cstart, cal, sum);
+  return hipGetLastError();
+}
+
 hipError_t launch_mine_count(const MineArgs &a, int level, int pbeg, int pend, hipStream_t st) {
   if (pend <= pbeg) return hipSuccess;
   const size_t lds = (size_t)mine_count_bufs(a.amax) * ((size_t)a.amax * CROW * 8 + (size_t)a.amax * WAVE * 4);

@@ -56,6 +56,11 @@ struct PatternTable {
   uint32_t *succ = nullptr;  // [P][amax]
 };
 
+// checkFrequency of n candidates of length `level` (start[n], allele indices
+// [n][level], 0xFD = a symbol the locus does not have) over this rank's items:
+// sum[c] = ordered sum of the matching items' values (continued when seeded).
+hipError_t launch_mine_scan(const MineArgs &a, int level, int n, const int32_t *cstart, const uint8_t *cal,
+                            double *sum, hipStream_t st);
 hipError_t launch_mine_count(const MineArgs &a, int level, int pbeg, int pend, hipStream_t st);
 hipError_t launch_mine_finalize(const MineArgs &a, int level, int b, int e, unsigned long long *ext_list,
                                 int32_t *next_children, hipStream_t st);

@@ -181,6 +181,17 @@ class HaploModel:
         return dict(structure_ms=s1.value, values_ms=s2.value, fallback_ms=fb.value, n_fallback=nf.value,
                     structure_passes=ps.value, value_passes=pv.value, n_order_rerun=no.value, order_ms=om.value)
 
+    def mine_level(self, start, alleles) -> tuple[np.ndarray, int]:
+        """PatternManager::checkFrequency for candidates of one length: start[n],
+        alleles[n][level] symbols -> (frequencies, items scanned)."""
+        start = np.ascontiguousarray(start, np.int32)
+        alleles = np.ascontiguousarray(alleles, np.int32).reshape(len(start), -1)
+        freq = np.zeros(len(start))
+        sc = C.c_uint64()
+        self._check(lib().hmc_mine_level(self._h, alleles.shape[1], len(start), _p(start, C.c_int32),
+                                         _p(alleles, C.c_int32), _p(freq, C.c_double), C.byref(sc)))
+        return freq, sc.value
+
     def set_value_mode(self, mode: str):
         """Value pass of the split E-step: "fast" (value-only k-best lists, the
         libstdc++ permutations only for individuals with ties) or "exact" (the

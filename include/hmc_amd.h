@@ -121,6 +121,16 @@ int hmc_allele_table(const hmc_ctx *ctx, int32_t *num, int32_t *sym, double *fre
  * successors).  *n_patterns = patterns found; *r_m = candidate x item scan
  * steps (SURVEY.md §8d R_M, local to this rank). */
 int hmc_find_patterns(hmc_ctx *ctx, int *n_patterns, uint64_t *r_m);
+/* Per-level seam of the same search: PatternManager::checkFrequency
+ * (PatternManager.cpp:146-193, called for each candidate by searchPattern
+ * :100-144) for n caller-given candidates of length `level` — start[n],
+ * alleles[n][level] as symbols.  freq[c] = the pattern frequency the reference
+ * assigns: genotype branch (no samples yet) sum over individuals of
+ * getMatchingFrequency (:267-291) / N, sample branch sum of matching sample
+ * weights / total weight; sums in item order and, across ranks, in rank order
+ * (hmc_set_reduction).  *scanned = n x items of this rank. */
+int hmc_mine_level(hmc_ctx *ctx, int level, int n, const int32_t *start, const int32_t *alleles, double *freq,
+                   uint64_t *scanned);
 int hmc_model_info(const hmc_ctx *ctx, int *n_patterns, int *head_len);
 /* Pattern table in id order (HaploPattern.h:16-98).  succ[P][max_alleles]
  * holds pattern ids (-1 = none); alleles[P][maxlen] symbols (-1 padding).

@@ -126,6 +126,70 @@ def test_estep_sample_sizes(oracle_mod, S):
     assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
 
 
+def _check_frequency(p, model, start, alleles, samples=None):
+    """PatternManager::checkFrequency (PatternManager.cpp:146-193), restated
+    in Python floats (sequential IEEE adds in item order)."""
+    num, sym, fr = model.allele_table()
+    out = []
+    for st, al in zip(start, alleles):
+        total = 0.0
+        if samples is None:
+            for i in range(p.N):
+                g = p.alleles[i]
+                ok, f = True, 1.0
+                for j, a in enumerate(al):  # Genotype::isMatch + getMatchingFrequency (:267-291)
+                    k = st + j
+                    b0, b1 = int(g[0, k]), int(g[1, k])
+                    if not (b0 < 0 or b1 < 0 or b0 == a or b1 == a):
+                        ok = False
+                        break
+                    af = 0.0
+                    for q in range(num[k]):
+                        if sym[k, q] == a:
+                            af = fr[k, q]
+                    x = 0.0
+                    x += af if b0 < 0 else (1.0 if b0 == a else 0.0)
+                    x += af if b1 < 0 else (1.0 if b1 == a else 0.0)
+                    f *= 0.5 * x
+                if ok:
+                    total += f
+            out.append(total / p.N)
+        else:
+            sal, w, tw = samples
+            for h in range(len(w)):
+                if all(sal[h, st + j] == a for j, a in enumerate(al)):
+                    total += w[h]
+            out.append(total / tw)
+    return np.array(out)
+
+
+@pytest.mark.parametrize("name", ["cfg1", "a3miss5", "a8"])
+def test_mine_level_seam(oracle_mod, name):
+    """hmc_mine_level (checkFrequency for caller-given candidates, the per-level
+    seam of searchPattern): equals the mined tables' frequencies bit for bit,
+    M0 from the genotypes and M1 from the samples, and a Python restatement of
+    checkFrequency on random (mostly infrequent) candidates."""
+    p = panel(name)
+    m = gpu_model(p)
+    rng = np.random.default_rng(5)
+    num, sym, _ = m.allele_table()
+    for it in range(2):
+        m.find_patterns()
+        pt = m.patterns()
+        for lv in np.unique(pt["len"]):
+            sel = pt["len"] == lv
+            f, sc = m.mine_level(pt["start"][sel], pt["alleles"][sel, :lv])
+            assert np.array_equal(f, pt["freq"][sel]), (it, lv)
+        lv = 4
+        st = rng.integers(0, p.L - lv, 40)
+        al = np.array([[sym[s + j, rng.integers(0, num[s + j])] for j in range(lv)] for s in st], np.int32)
+        f, sc = m.mine_level(st, al)
+        samples = None if it == 0 else m.samples(H)
+        assert np.array_equal(f, _check_frequency(p, m, st, al, samples)), it
+        assert sc == 40 * (p.N if it == 0 else H)
+        _, H, _ = m.resolve_all()
+
+
 @pytest.mark.parametrize("name", sorted(PANELS))
 def test_mine_genotypes_and_samples(oracle_mod, name):
     """M0 (genotype branch) and M1 (sample branch) pattern tables, bit-exact."""
