@@ -350,6 +350,7 @@ struct Ctx {
   enum { ESTEP_SPLIT = 0, ESTEP_FUSED = 1 };
   int estep_mode = ESTEP_SPLIT;
   DevBuf<char> d_scr1, d_scr2;
+  DevBuf<int32_t> d_nextq;  // dynamic-schedule counters of the structure and value passes
   DevBuf<uint32_t> d_rec;
   DevBuf<unsigned long long> d_rec_off, d_rec_cursor;
   std::vector<int32_t> h_status1, h_redo;
@@ -1957,6 +1958,8 @@ struct Ctx {
       s1.fmax = exact ? d_xfmax.p : d_fmax.p;
       s1.max_states = d_maxst.p;
       s1.exact = exact;
+      if ((e = d_nextq.ensure(2)) || (e = hipMemsetAsync(d_nextq.p, 0, 8, st))) return hipfail(e, "estep");
+      s1.next_q = d_nextq.p;
       hipEventRecord(ev[0], st);
       if ((e = launch_estep_structure(s1, grid1, st))) return hipfail(e, "estep_structure launch");
       hipEventRecord(ev[1], st);
@@ -2065,6 +2068,8 @@ struct Ctx {
         v.weight = d_weight.p;
         v.cost = d_cost.p;
         v.stamps = d_stamps.p;
+        v.next_q = d_nextq.p + 1;
+        if ((e = hipMemsetAsync(d_nextq.p + 1, 0, 4, st))) return hipfail(e, "estep");
         const bool fast = value_fast;
         hipEventRecord(ev[0], st);
         if ((e = launch_estep_values(v, grid2, vnw, fast, st))) return hipfail(e, "estep_values launch");
@@ -2088,6 +2093,7 @@ struct Ctx {
           ValueArgs v2 = v;
           v2.order = d_redo.p;
           v2.n_order = nr;
+          if ((e = hipMemsetAsync(d_nextq.p + 1, 0, 4, st))) return hipfail(e, "estep");
           hipEventRecord(ev[0], st);
           if ((e = launch_estep_values(v2, std::max(1, std::min(G2, nr)), vnw, false, st)))
             return hipfail(e, "estep_values launch");

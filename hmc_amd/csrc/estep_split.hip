@@ -212,7 +212,14 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
   };
   reset_tables();
 
-  for (int q = blockIdx.x; q < a.n_order; q += gridDim.x) {
+  // individuals are taken from the heaviest-first order list one at a time as
+  // blocks finish (longest-processing-time-first), not round-robin
+  auto next_q = [&]() -> int {
+    int t = 0;
+    if (lane == 0) t = atomicAdd(a.next_q, 1);
+    return __shfl(t, 0) + (int)gridDim.x;
+  };
+  for (int q = blockIdx.x; q < a.n_order; q = next_q()) {
     const int bi = a.order[q];
     const int gi = a.indiv_begin + bi;
     const uchar2 *g = a.pan.geno_im + (size_t)gi * L;
@@ -601,6 +608,7 @@ struct K2Shared {
   int flag;  // a forward likelihood hit 0 before the last locus
   int iters; // diagnostic build: most chain-loop iterations of any wave this locus
   int tie;   // FAST: a non-zero likelihood straddles some list's S-cut
+  int q;     // next individual of the order list
 };
 
 struct K2Plan {
@@ -738,7 +746,15 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
   const VFront FB{smem + plan.o_front[1], (unsigned char *)sp + k2_front_bytes(a.fcap, S), a.lds_fc, a.fcap, S};
 
   K2_T0
-  for (int q = blockIdx.x; q < a.n_order; q += gridDim.x) {
+  // individuals are taken from the heaviest-first order list one at a time as
+  // blocks finish (longest-processing-time-first), not round-robin
+  auto next_q = [&]() -> int {
+    __syncthreads();
+    if (tid == 0) bs->q = atomicAdd(a.next_q, 1) + (int)gridDim.x;
+    __syncthreads();
+    return bs->q;
+  };
+  for (int q = blockIdx.x; q < a.n_order; q = next_q()) {
     const int bi = a.order[q];
     const unsigned long long t_indiv = __builtin_amdgcn_s_memtime();
     int status = a.status[bi];

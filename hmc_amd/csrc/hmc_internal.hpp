@@ -145,6 +145,7 @@ struct StructArgs {
   // orientation counts — the forward links of HaploPair (HaploPair.cpp:44,67)
   // in push order; trace_need then counts the fwd/bwd store (4 words/state).
   bool exact;
+  int32_t *next_q;                // dynamic schedule: order entries taken after the first gridDim.x (zeroed)
   int32_t *status;                // [batch]
   unsigned long long *re_count;   // [batch]
   int32_t *fmax;                  // [batch]
@@ -166,6 +167,7 @@ struct ValueArgs {
   char *scratch;
   size_t scratch_stride;
   int fcap, lds_fc;
+  int32_t *next_q;  // dynamic schedule: order entries taken after the first gridDim.x (zeroed)
   uint32_t *trace;
   unsigned long long trace_cap;
   unsigned long long *trace_cursor;
