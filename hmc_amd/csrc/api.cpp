@@ -1900,16 +1900,30 @@ struct Ctx {
           }
           r = share * (uint64_t)k;
         } else {  // the prefix whose regions (and measured traces) fit the budgets
+          uint64_t r_est = 0;
           while (k < np) {
             const int bi = pending[k];
             const uint64_t need = exact_need[bi] ? rneed[bi] : std::min<uint64_t>(est[bi], rec_budget);
             const uint64_t tn = exact_need[bi] ? tneed[bi] : 0;
             if (k > 0 && (r + need > rec_budget || t + tn > trace_budget)) break;
-            base[bi] = r;
             rsz[bi] = need;
             r += need;
             t += tn;
+            r_est += exact_need[bi] ? 0 : need;
             ++k;
+          }
+          // the store left over goes to the estimated regions (up to 3x), so
+          // fewer individuals are deferred to a pass of their own
+          const double grow = r_est > 0 && r < rec_budget
+                                  ? std::min(3.0, 1.0 + (double)(rec_budget - r) / (double)r_est)
+                                  : 1.0;
+          r = 0;
+          for (int q = 0; q < k; ++q) {
+            const int bi = pending[q];
+            if (!exact_need[bi]) rsz[bi] = std::min<uint64_t>((uint64_t)((double)rsz[bi] * grow), rec_budget);
+            if (r + rsz[bi] > rec_budget) rsz[bi] = rec_budget - r;
+            base[bi] = r;
+            r += rsz[bi];
           }
         }
         np = k;
@@ -1970,14 +1984,27 @@ struct Ctx {
       hipEventElapsedTime(&ms, ev[0], ev[1]);
       ms_s1 += ms;
       ++n_struct_passes;
-      if (getenv("HMC_DEBUG_MEM"))
-        fprintf(stderr, "[hmc] structure pass %d: %d individuals, %.1f ms\n", n_struct_passes, np, ms);
+      if (getenv("HMC_DEBUG_MEM")) {
+        int ndef = 0;
+        uint64_t rsum = 0, rmax = 0, tsum = 0, rres = 0;
+        for (int q = 0; q < np; ++q) {
+          const int bi = pending[q];
+          ndef += h_status[bi] == EST_OVERFLOW_REC ? 1 : 0;
+          rsum += rneed[bi];
+          rmax = std::max<uint64_t>(rmax, rneed[bi]);
+          tsum += tneed[bi];
+          rres += rsz[bi];
+        }
+        fprintf(stderr, "[hmc] structure pass %d: %d individuals, %.1f ms; deferred %d, records need %.2f GB (max %.1f MB, "
+                "reserved %.2f GB), traces %.2f GB\n", n_struct_passes, np, ms, ndef, rsum * 4e-9, rmax * 4e-6, rres * 4e-9,
+                tsum * 4e-9);
+      }
       sset.clear();
       rest.clear();
       for (int q = 0; q < np; ++q) {
         const int bi = pending[q], s = h_status[bi];
         if (s == EST_NO_HEAD_PATTERN) return fail(HMC_ENOPATTERN, "Can not find matching pattern!");
-        if (s == EST_OVERFLOW_FRONTIER) {
+        if (s == EST_OVERFLOW_FRONTIER) {  // (deferring only these individuals measured slower)
           if (fcap >= 65535) return fail(HMC_EUNSUPPORTED, "frontier exceeds 65535 states");
           fcap = std::min(65535, fcap * 2);
           return ESTEP_RESTART;
