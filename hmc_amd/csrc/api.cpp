@@ -1120,12 +1120,12 @@ struct Ctx {
       }
 #endif
       if (multi() && reduction == RED_ORDERED) {
-        // rank r continues every child's sum from ranks 0..r-1 (items in order)
+        // every rank scans its items and writes the children's lists at once;
+        // then rank r continues every child's sum from ranks 0..r-1 (items in
+        // order) over its lists and passes it on
+        if ((e = launch_mine_count(a, level, pbeg, pend, st))) return hipfail(e, "mine_count");
         for (int r = 0; r < world; ++r) {
-          if (r == rank) {
-            a.seeded = r > 0;
-            if ((e = launch_mine_count(a, level, pbeg, pend, st))) return hipfail(e, "mine_count");
-          }
+          if (r == rank && r > 0 && (e = launch_mine_sum(a, cb, ce, st))) return hipfail(e, "mine_sum");
           if ((rc = bcast(n_sum.p + cb, nlev, r))) return rc;
         }
       } else if ((e = launch_mine_count(a, level, pbeg, pend, st))) {

@@ -615,6 +615,43 @@ hipError_t launch_mine_scan(const MineArgs &a, int level, int n, const int32_t *
   return hipGetLastError();
 }
 
+// Ordered cross-rank reduction, the add chain alone: child c's sum continues
+// from sum[c] (the running sum of the ranks before this one) over the values
+// of its matching list that mine_count just wrote on this rank (genotype
+// branch: the carried products; sample branch: the haplotype weights), in
+// list order.  mine_count itself runs on all ranks at once, so only this
+// cheap pass is sequential across ranks.
+__global__ __launch_bounds__(64) void mine_sum(MineArgs a, int cb, int ce) {
+  __shared__ double vals[WAVE];
+  const int lane = threadIdx.x;
+  for (int c = cb + blockIdx.x; c < ce; c += gridDim.x) {
+    const uint32_t n = a.cnt[c];
+    const unsigned long long off = a.list_off[c];
+    double s = a.sum[c];
+    for (uint32_t base = 0; base < n; base += WAVE) {
+      const uint32_t i = base + lane;
+      double v = 0.0;
+      if (i < n) v = a.genotype ? a.lout_val[off + i] : a.w[a.lout_idx[off + i]];
+      vals[lane] = v;
+      wave_sync();
+      if (lane == 0) {
+        const uint32_t k = n - base < (uint32_t)WAVE ? n - base : (uint32_t)WAVE;
+        for (uint32_t q = 0; q < k; ++q) s = s + vals[q];
+      }
+      wave_sync();
+    }
+    if (lane == 0) a.sum[c] = s;
+  }
+}
+
+hipError_t launch_mine_sum(const MineArgs &a, int cb, int ce, hipStream_t st) {
+  if (ce <= cb) return hipSuccess;
+  if (!a.lout_idx || (a.genotype && !a.lout_val)) return hipErrorInvalidValue;
+  const int n = ce - cb;
+  hipLaunchKernelGGL(mine_sum, dim3(n < 65536 ? n : 65536), dim3(WAVE), 0, st, a, cb, ce);
+  return hipGetLastError();
+}
+
 hipError_t launch_mine_count(const MineArgs &a, int level, int pbeg, int pend, hipStream_t st) {
   if (pend <= pbeg) return hipSuccess;
   const size_t lds = (size_t)mine_count_bufs(a.amax) * ((size_t)a.amax * CROW * 8 + (size_t)a.amax * WAVE * 4);

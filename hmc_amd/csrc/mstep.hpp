@@ -61,6 +61,9 @@ struct PatternTable {
 // sum[c] = ordered sum of the matching items' values (continued when seeded).
 hipError_t launch_mine_scan(const MineArgs &a, int level, int n, const int32_t *cstart, const uint8_t *cal,
                             double *sum, hipStream_t st);
+// Ordered reduction: child sums of [cb, ce) continued over this rank's lists
+// (the ones the level's mine_count wrote to lout_idx / lout_val).
+hipError_t launch_mine_sum(const MineArgs &a, int cb, int ce, hipStream_t st);
 hipError_t launch_mine_count(const MineArgs &a, int level, int pbeg, int pend, hipStream_t st);
 hipError_t launch_mine_finalize(const MineArgs &a, int level, int b, int e, unsigned long long *ext_list,
                                 int32_t *next_children, hipStream_t st);
