@@ -9,7 +9,8 @@ loci (cfg 3, seed 3; the largest configuration quoted for one MI355X), reference
 parameters (min-freq-abs 1.5, pattern length 1..30, sample size 10).  A "step"
 is one EM iteration, E-step (HaploModel::resolveAll) + M-step
 (PatternManager::findPatternByFreq on the weighted samples), continuing the EM
-chain from the genotype-mined model M0: step k = E_k + M_k.  Before the timed
+chain from the genotype-mined model M0: step k = E_k, accept + HaploComp, M_k
+(hmc_em_iteration: one HaploModel::run iteration).  Before the timed
 region the panel is resident in HBM and M0 has been mined (its time is
 reported separately); the warmup steps run the same chain, then
 the samples are dropped and M0 is mined again so that the timed steps start
@@ -147,12 +148,17 @@ def main():
 
     progress(f"M0 {P0} patterns in {t_m0:.1f} s")
 
+    chain = {"it": 0, "old_ll": -float("inf")}
+
     def em_step():
-        ll, H, re = m.resolve_all()
+        # one HaploModel::run iteration (HaploModel.cpp:130-144): E-step, accept,
+        # HaploComp, M-step (always: a fixed number of steps is timed)
+        chain["it"] += 1
+        log, chain["old_ll"], _ = m.em_iteration(chain["it"], chain["old_ll"], always_mstep=True)
+        ll, H, re, rm, P = log["log_likelihood"], log["n_samples"], log["r_e"], log["r_m"], log["n_patterns"]
         t = m.timings()
         sp = m.estep_split_stats()
-        P, rm = m.find_patterns()
-        progress(f"EM step: LL {ll:.6f}, R_E {re}, E {t['estep_forward_ms']:.0f} ms, M {m.timings()['mstep_ms']:.0f} ms")
+        progress(f"EM step: LL {ll:.6f}, R_E {re}, E {t['estep_forward_ms']:.0f} ms, M {t['mstep_ms']:.0f} ms")
         return dict(ll=ll, H=H, r_e=re, r_m=rm, P=P, estep_ms=t["estep_forward_ms"] + t["estep_traceback_ms"],
                     struct_ms=sp["structure_ms"], values_ms=sp["values_ms"], fallback_ms=sp["fallback_ms"],
                     n_fallback=sp["n_fallback"], struct_passes=sp["structure_passes"],
@@ -161,6 +167,7 @@ def main():
     warm = [em_step() for _ in range(args.warmup)]
     m.clear_samples()
     m.find_patterns()  # back to M0 so the timed chain is E1+M1, E2+M2, ...
+    chain.update(it=0, old_ll=-float("inf"))
 
     barrier()
     t0 = time.perf_counter()
@@ -204,7 +211,7 @@ def main():
                     f"missing={args.missing}, seed={args.seed}), generated in-process",
             "config": {
                 "workload": f"{args.tag}: {N} individuals x {L} SNP loci, {args.A} alleles/locus; "
-                            f"step = one EM iteration (E_k + M_k) from the genotype-mined model M0",
+                            f"step = one EM iteration (E_k, accept, HaploComp, M_k) from the genotype-mined model M0",
                 "individuals": N, "loci": L, "sample_size": args.sample_size,
                 "min_freq_abs": 1.5, "pattern_len": [1, 30],
                 "parallelism": f"individual-sharded x{world}, " + ("ordered RCCL reduction (chained broadcasts)" if args.reduction == "ordered"

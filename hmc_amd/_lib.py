@@ -74,6 +74,7 @@ _SIGS = [
     ("hmc_get_resolutions", _i, [_vp, _P(C.c_int32)]),
     ("hmc_clear_samples", _i, [_vp]),
     ("hmc_run", _i, [_vp, _i, _P(IterLog), _i, _P(_i), _P(_d), _P(_u64), _P(_i)]),
+    ("hmc_em_iteration", _i, [_vp, _i, _i, _i, _P(_d), _P(IterLog), _P(_i)]),
     ("hmc_get_best_resolutions", _i, [_vp, _P(C.c_int32)]),
     ("hmc_haplocomp", _i, [_vp, _P(_d), _P(_d), _P(_d)]),
     ("hmc_set_model", _i, [_vp, _cp, _i]),

@@ -2387,6 +2387,58 @@ struct Ctx {
   }
 
   // ------------------------------------------------------------------ run --
+  // resolutions = unphased (HaploModel.cpp:127)
+  void init_best() {
+    const int n = nloc(), L = pan.L;
+    best_res.assign((size_t)n * 2 * L, 0);
+    for (int i = 0; i < n; ++i)
+      for (int h = 0; h < 2; ++h)
+        for (int k = 0; k < L; ++k)
+          best_res[((size_t)i * 2 + h) * L + k] = pan.idx[((size_t)(i0 + i) * 2 + h) * L + k];
+    have_best = true;
+  }
+
+  // One iteration of HaploModel::run (HaploModel.cpp:130-144): E-step, accept
+  // the resolutions if the LL did not drop, HaploComp, the continue rule, and
+  // the M-step when continuing (or always, force_m: a fixed number of steps).
+  int em_iteration(int it, int max_iter, bool force_m, double &old_ll, hmc_iter_log &rec, bool &go) {
+    using clk = std::chrono::steady_clock;
+    if (!have_best) init_best();
+    auto t1 = clk::now();
+    double ll = 0;
+    int Hs = 0;
+    uint64_t re = 0;
+    int rc;
+    if ((rc = estep(&ll, &Hs, &re))) return rc;
+    const double te = std::chrono::duration<double>(clk::now() - t1).count();
+    if (ll >= old_ll) {
+      if ((rc = resolutions_idx(best_res))) return rc;
+    }
+    rec = hmc_iter_log{};
+    double hc[3];
+    if ((rc = haplocomp(best_res, hc))) return rc;  // HaploModel.cpp:134-136
+    rec.switch_error = hc[0];
+    rec.ihp = hc[1];
+    rec.igp = hc[2];
+    rec.log_likelihood = ll;
+    rec.t_estep_s = te;
+    rec.r_e = re;
+    rec.n_samples = Hs;
+    rec.n_patterns = P;
+    go = it < max_iter && ll >= old_ll && (old_ll - ll) / old_ll > 0.0001;  // HaploModel.cpp:139
+    if (go || force_m) {
+      auto t2 = clk::now();
+      int np = 0;
+      uint64_t rm = 0;
+      if ((rc = mine(&np, &rm))) return rc;
+      rec.t_mstep_s = std::chrono::duration<double>(clk::now() - t2).count();
+      rec.r_m = rm;
+      rec.n_patterns = np;
+      old_ll = ll;
+    }
+    return HMC_OK;
+  }
+
   int run(int max_iter, hmc_iter_log *log, int cap, int *iters, double *t_m0, uint64_t *rm0, int *np0) {
     using clk = std::chrono::steady_clock;
     have_samples = false;  // HaploModel::build -> setGenoData clears samples (HaploBuilder.cpp:19-23)
@@ -2398,46 +2450,13 @@ struct Ctx {
     if (t_m0) *t_m0 = std::chrono::duration<double>(clk::now() - t0).count();
     if (rm0) *rm0 = rm;
     if (np0) *np0 = np;
-    // resolutions = unphased (HaploModel.cpp:127)
-    const int n = nloc(), L = pan.L;
-    best_res.assign((size_t)n * 2 * L, 0);
-    for (int i = 0; i < n; ++i)
-      for (int h = 0; h < 2; ++h)
-        for (int k = 0; k < L; ++k)
-          best_res[((size_t)i * 2 + h) * L + k] = pan.idx[((size_t)(i0 + i) * 2 + h) * L + k];
-    have_best = true;
+    init_best();
     double old_ll = -DBL_MAX;
     int it = 0;
     for (it = 1; it <= max_iter; ++it) {
-      auto t1 = clk::now();
-      double ll = 0;
-      int Hs = 0;
-      uint64_t re = 0;
-      if ((rc = estep(&ll, &Hs, &re))) return rc;
-      const double te = std::chrono::duration<double>(clk::now() - t1).count();
-      if (ll >= old_ll) {
-        if ((rc = resolutions_idx(best_res))) return rc;
-      }
       hmc_iter_log rec{};
-      double hc[3];
-      if ((rc = haplocomp(best_res, hc))) return rc;  // HaploModel.cpp:134-136
-      rec.switch_error = hc[0];
-      rec.ihp = hc[1];
-      rec.igp = hc[2];
-      rec.log_likelihood = ll;
-      rec.t_estep_s = te;
-      rec.r_e = re;
-      rec.n_samples = Hs;
-      rec.n_patterns = P;
-      const bool go = it < max_iter && ll >= old_ll && (old_ll - ll) / old_ll > 0.0001;  // HaploModel.cpp:139
-      if (go) {
-        auto t2 = clk::now();
-        if ((rc = mine(&np, &rm))) return rc;
-        rec.t_mstep_s = std::chrono::duration<double>(clk::now() - t2).count();
-        rec.r_m = rm;
-        rec.n_patterns = np;
-        old_ll = ll;
-      }
+      bool go = false;
+      if ((rc = em_iteration(it, max_iter, false, old_ll, rec, go))) return rc;
       if (log && it - 1 < cap) log[it - 1] = rec;
       if (!go) break;
     }
@@ -3081,6 +3100,19 @@ int hmc_clear_samples(hmc_ctx *h) {
   if (!h) return HMC_EARG;
   h->c.have_samples = false;
   h->c.H = 0;
+  return HMC_OK;
+}
+
+int hmc_em_iteration(hmc_ctx *h, int iteration, int max_iter, int always_mstep, double *old_ll, hmc_iter_log *log,
+                     int *go) {
+  if (!h || !old_ll) return HMC_EARG;
+  if (!h->c.have_model) return h->c.fail(HMC_EARG, "no pattern model: hmc_find_patterns first");
+  hmc_iter_log rec{};
+  bool g = false;
+  const int rc = h->c.em_iteration(iteration, max_iter, always_mstep != 0, *old_ll, rec, g);
+  if (rc) return rc;
+  if (log) *log = rec;
+  if (go) *go = g ? 1 : 0;
   return HMC_OK;
 }
 

@@ -357,6 +357,19 @@ class HaploModel:
         self._check(lib().hmc_get_best_resolutions(self._h, _p(out, C.c_int32)))
         return out
 
+    def em_iteration(self, iteration: int, old_ll: float, always_mstep: bool = True,
+                     max_iteration: int = 1 << 30) -> tuple[dict, float, bool]:
+        """One HaploModel::run iteration (HaploModel.cpp:130-144): E-step, accept,
+        HaploComp, continue rule, M-step.  Returns (log, new old_ll, go)."""
+        self._push_params()
+        ol = C.c_double(old_ll)
+        rec = IterLog()
+        go = C.c_int()
+        self._check(lib().hmc_em_iteration(self._h, int(iteration), int(max_iteration), int(bool(always_mstep)),
+                                           C.byref(ol), C.byref(rec), C.byref(go)))
+        log = {f: getattr(rec, f) for f, _ in IterLog._fields_}
+        return log, ol.value, bool(go.value)
+
     def haplocomp(self):
         """HaploComp (switch error, IHP, IGP) of the input panel against the
         accepted resolutions of the last run (HaploComp.cpp:29-155)."""

@@ -188,6 +188,14 @@ typedef struct hmc_iter_log {
  * number run; *t_m0_s, *r_m0, *n_patterns0 describe M0. */
 int hmc_run(hmc_ctx *ctx, int max_iteration, hmc_iter_log *log, int log_cap, int *iterations, double *t_m0_s,
             uint64_t *r_m0, int *n_patterns0);
+/* One iteration of that loop (HaploModel.cpp:130-144) for a host that drives
+ * the EM itself, after a first hmc_find_patterns: E-step, accept the
+ * resolutions if the LL did not drop below *old_ll, HaploComp, the continue
+ * rule (*go), and the M-step when continuing — or always, with always_mstep
+ * (a fixed number of steps, as bench.py times).  *old_ll (start: -DBL_MAX)
+ * becomes the LL when the M-step ran. */
+int hmc_em_iteration(hmc_ctx *ctx, int iteration, int max_iteration, int always_mstep, double *old_ll,
+                     hmc_iter_log *log, int *go);
 /* HaploComp (HaploComp.cpp:29-155) of the input panel, phase as given,
  * against the accepted resolutions: switch error, incorrect-haplotype and
  * incorrect-genotype percentages over all ranks' individuals.  Replaces the

@@ -260,6 +260,34 @@ def test_full_em(oracle_mod, name):
     np.testing.assert_array_equal(np.array(m.haplocomp()), r["haplocomp"][-1])
 
 
+@pytest.mark.parametrize("name", ["cfg1", "miss2"])
+def test_em_iteration_drives_the_same_chain(oracle_mod, name):
+    """hmc_em_iteration (one HaploModel::run iteration, HaploModel.cpp:130-144)
+    driven from the host until the continue rule stops: the same iterations,
+    LL, R_E / R_M, HaploComp lines and accepted pairs as HaploModel::run."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10, max_iter=30)
+    r = o.run()
+    m = gpu_model(p)
+    m.find_patterns()
+    old, logs = -np.finfo(np.float64).max, []
+    for it in range(1, 31):
+        log, old, go = m.em_iteration(it, old, always_mstep=False, max_iteration=30)
+        logs.append(log)
+        if not go:
+            break
+    assert len(logs) == r["iterations"]
+    assert [x["log_likelihood"] for x in logs] == r["ll"].tolist()
+    assert [x["r_e"] for x in logs] == r["R_E"].tolist()
+    for k in range(r["iterations"] - 1):
+        assert logs[k]["r_m"] == r["R_M"][k + 1]
+    np.testing.assert_array_equal(np.array([(x["switch_error"], x["ihp"], x["igp"]) for x in logs]), r["haplocomp"])
+    best = np.zeros((p.N, 2, p.L), np.int32)
+    assert hmc_amd.lib().hmc_get_best_resolutions(m._h, best.ctypes.data_as(__import__("ctypes").POINTER(
+        __import__("ctypes").c_int32))) == 0
+    assert np.array_equal(best, r["resolutions"])
+
+
 @pytest.mark.parametrize("name,model,order,min_len", [
     ("n60", "MC", 1, 1), ("a3miss5", "MC", 1, 1), ("n60", "MC", 2, 1), ("a4", "MC", 1, 1),
     ("miss2", "MA", 1, 1), ("n60", "MV", 1, 2), ("a3miss5", "MV", 1, 3)])
