@@ -95,6 +95,7 @@ _SIGS = [
     ("hmc_last_timings", _i, [_vp, _P(_d), _P(_d), _P(_d)]),
     ("hmc_test_nth_element", None, [_P(_d), _P(C.c_uint32), _i, _i]),
     ("hmc_test_sort_small", None, [_P(_d), _P(C.c_uint32), _i]),
+    ("hmc_test_sort", None, [_P(_d), _P(C.c_uint32), _i]),
     ("hmc_test_nth_element_masks", None, [_P(_d), _P(C.c_uint32), _i, _i]),
     ("hmc_test_coop_nth_element", _i, [_i, _P(_d), _P(C.c_uint32), _P(C.c_int32), _P(C.c_int32), _P(C.c_int32),
                                        _i, _i, _i]),

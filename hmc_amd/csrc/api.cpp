@@ -3224,4 +3224,9 @@ void hmc_test_sort_small(double *lik, uint32_t *tag, int n) {
   hmc::sort_greater_small(v, n);
 }
 
+void hmc_test_sort(double *lik, uint32_t *tag, int n) {
+  hmc::LinkList v{lik, tag, 1};
+  hmc::sort_greater(v, n);
+}
+
 }  // extern "C"

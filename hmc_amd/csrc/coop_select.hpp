@@ -85,7 +85,7 @@ __device__ inline Seg make_seg(int SW) {
   s.mask = s.g < G ? (w << s.base) : 0ull;
   s.lt = s.mask & ((1ull << lane) - 1ull);
   s.wm = s.g < G ? (SW >= 32 ? ~0u : ((1u << SW) - 1u)) : 0u;
-  s.ltk = (1u << s.k) - 1u;
+  s.ltk = s.k < 32 ? (1u << s.k) - 1u : ~0u;
   return s;
 }
 
@@ -108,8 +108,8 @@ struct SegScratch {
 
 // std::nth_element(v, v+nth, v+n, greater) on every segment's list, in
 // place in the LDS slots slik/smeta (segment g's element k in slot
-// g*SW + k; n, nth uniform inside a segment, n <= SW <= 32; n == 0 marks an
-// idle segment).  Whole-wave call, branch-free per lane.
+// g*SW + k; n, nth uniform inside a segment, n <= SW <= 64; n == 0 marks an
+// idle segment).  Whole-wave call, branch-free per lane for SW <= 32.
 //
 // One partition costs two LDS round trips: one batch that reads the median
 // candidates, the value at `first` and every lane's own element, and the stop
@@ -122,6 +122,14 @@ struct SegScratch {
 __device__ inline void seg_nth_slots(int n, int nth, const Seg &sg, const SegScratch &ss) {
   const int lane = (int)(threadIdx.x & 63);
   const int k = sg.k;
+  if (sg.sw > 32) {  // lists of up to 64 (S > 16): one per wave, the sequential algorithm on its first lane
+    if (n > 0 && nth != n && sg.mask != 0ull && k == 0) {
+      const LinkList wl{ss.slik + sg.base, ss.smeta + sg.base, 1};
+      nth_element_greater(wl, n, nth);
+    }
+    wave_lds_sync();
+    return;
+  }
   int first = 0, last = n, depth = n > 0 ? lg2_floor(n) * 2 : 0;
   const bool act = n > 0 && nth != n && sg.mask != 0ull;
   double *sl = ss.slik + sg.base;

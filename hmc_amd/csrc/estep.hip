@@ -209,34 +209,20 @@ __device__ inline bool write_trace(const EstepArgs &a, const Lds &l, BlockShared
   uint32_t *lnk = a.trace + trace_links(off, (uint32_t)Fn);
   for (int t = threadIdx.x; t < Fn; t += NT)
     hdr[t] = hdr_pack(a.mod.last[get_lo(l, F, t)], a.mod.last[get_hi(l, F, t)], get_nl(l, F, t));
-  // one thread per state: its S link words (zero past nl), all loads issued
-  // before the stores (the source may be LDS or HBM); 8-byte pairs for even S
-  if ((S & 1) == 0) {
-    for (int t = threadIdx.x; t < Fn; t += NT) {
-      const uint32_t n = get_nl(l, F, t);
-      const uint2 *pm = (const uint2 *)meta_ptr(l, F, t);
-      uint2 *dst = (uint2 *)(lnk + (size_t)t * S);
-      uint2 v[S_MAX / 2];
+  // one thread per state: its S link words (zero past nl), the loads of each
+  // 16-word chunk issued before its stores (the source may be LDS or HBM)
+  for (int t = threadIdx.x; t < Fn; t += NT) {
+    const uint32_t n = get_nl(l, F, t);
+    const uint32_t *pm = meta_ptr(l, F, t);
+    uint32_t *dst = lnk + (size_t)t * S;
+    for (int k0 = 0; k0 < S; k0 += 16) {
+      uint32_t v[16];
 #pragma unroll
-      for (int k = 0; k < S_MAX / 2; ++k)
-        if (2 * k < S) v[k] = pm[k];
+      for (int k = 0; k < 16; ++k)
+        if (k0 + k < S) v[k] = pm[k0 + k];
 #pragma unroll
-      for (int k = 0; k < S_MAX / 2; ++k)
-        if (2 * k < S)
-          dst[k] = make_uint2((uint32_t)(2 * k) < n ? v[k].x : 0u, (uint32_t)(2 * k + 1) < n ? v[k].y : 0u);
-    }
-  } else {
-    for (int t = threadIdx.x; t < Fn; t += NT) {
-      const uint32_t n = get_nl(l, F, t);
-      const uint32_t *pm = meta_ptr(l, F, t);
-      uint32_t *dst = lnk + (size_t)t * S;
-      uint32_t v[S_MAX];
-#pragma unroll
-      for (int k = 0; k < S_MAX; ++k)
-        if (k < S) v[k] = pm[k];
-#pragma unroll
-      for (int k = 0; k < S_MAX; ++k)
-        if (k < S) dst[k] = (uint32_t)k < n ? v[k] : 0u;
+      for (int k = 0; k < 16; ++k)
+        if (k0 + k < S) dst[k0 + k] = (uint32_t)(k0 + k) < n ? v[k] : 0u;
     }
   }
   if (threadIdx.x == 0) {
@@ -758,11 +744,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void e
             W.set(cnt++, lk, meta_pack((uint32_t)t, k, false, homo, false));
           }
           if (cnt > S) {
-            nth_element_greater_masks(W, cnt, S - 1, cnt);
+            if (cnt <= 32) nth_element_greater_masks(W, cnt, S - 1, cnt);
+            else nth_element_greater(W, cnt, S - 1);
             cnt = S;
           }
         }
-        sort_greater_small(W, cnt);
+        sort_greater(W, cnt, ss.lpos);  // the selection scratch is free here
         double coverage = 0.0;
         for (int c = 0; c < cnt; ++c) {
           const uint32_t m = W.m(c);
@@ -792,8 +779,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void e
 // individual, one per candidate; walks the trace store from locus L back to
 // the head locus and writes both haplotypes as sample rows.
 __global__ __launch_bounds__(256) void estep_traceback(TracebackArgs a) {
-  const int q = blockIdx.x * 16 + threadIdx.x / 16;
-  const int c = threadIdx.x % 16;
+  // one lane per candidate, cw (16 or 32) lanes per individual
+  const int cw = a.S > 16 ? 32 : 16;
+  const int q = blockIdx.x * (256 / cw) + threadIdx.x / cw;
+  const int c = threadIdx.x % cw;
   if (q >= a.nbatch) return;
   const int bi = a.order ? a.order[q] : q;
   if (c >= a.ncand[bi]) return;
@@ -972,7 +961,9 @@ hipError_t launch_estep(const EstepArgs &a, int grid, int nw, hipStream_t st) {
 
 hipError_t launch_traceback(const TracebackArgs &a, int, hipStream_t st) {
   if (a.nbatch <= 0) return hipSuccess;
-  hipLaunchKernelGGL(estep_traceback, dim3((a.nbatch + 15) / 16), dim3(256), 0, st, a);
+  if (a.S < 1 || a.S > S_MAX) return hipErrorInvalidValue;
+  const int per = 256 / (a.S > 16 ? 32 : 16);  // individuals per block
+  hipLaunchKernelGGL(estep_traceback, dim3((a.nbatch + per - 1) / per), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

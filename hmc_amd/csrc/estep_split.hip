@@ -1001,7 +1001,8 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
             W.set(cnt++, lk, meta_pack((uint32_t)t, k, false, homo, false));
           }
           if (cnt > S) {
-            nth_element_greater_masks(W, cnt, S - 1, cnt);
+            if (cnt <= 32) nth_element_greater_masks(W, cnt, S - 1, cnt);
+            else nth_element_greater(W, cnt, S - 1);
             if (FAST)
               for (int q = S; q < cnt; ++q) {
                 out_max = out_any && out_max > W.l(q) ? out_max : W.l(q);
@@ -1010,7 +1011,7 @@ __global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a)
             cnt = S;
           }
         }
-        sort_greater_small(W, cnt);
+        sort_greater(W, cnt, ss.lpos);  // the selection scratch is free here
         if (FAST) {  // the candidates and their order must not depend on list order
           bool tie = out_any && cnt > 0 && out_max == W.l(cnt - 1);
           for (int c = 0; c < cnt; ++c) tie = tie || W.l(c) == 0.0 || (c > 0 && W.l(c) == W.l(c - 1));

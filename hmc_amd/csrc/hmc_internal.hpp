@@ -8,7 +8,7 @@ namespace hmc {
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint8_t MISSING = 0xFF;
-constexpr int S_MAX = 16;    // sample_size limit (std::sort == insertion sort up to 16)
+constexpr int S_MAX = 32;    // sample_size limit (2S-link lists fit one wavefront)
 constexpr int A_MAX = 32;    // alleles per locus limit
 constexpr int WAVE = 64;
 

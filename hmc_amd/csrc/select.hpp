@@ -254,4 +254,69 @@ HMC_HD void nth_element_greater_masks(const V &v, int n, int nth, int span) {
 template <class V>
 HMC_HD void sort_greater_small(const V &v, int n) { insertion_sort(v, 0, n); }
 
+// std::__unguarded_linear_insert / __unguarded_insertion_sort (stl_algo.h:1799-1869)
+template <class V>
+HMC_HD void unguarded_insertion_sort(const V &v, int first, int last) {
+  for (int i = first; i != last; ++i) {
+    const double x = v.l(i);
+    const uint32_t y = v.m(i);
+    int hole = i, next = i - 1;
+    while (x > v.l(next)) {
+      v.copy(hole, next);
+      hole = next;
+      --next;
+    }
+    v.set(hole, x, y);
+  }
+}
+
+// std::sort(first, first+n, greater) for any n (stl_algo.h:1896-1958, 1925-1948):
+// __introsort_loop with _S_threshold 16 (right part first, then the loop
+// continues on the left part), __partial_sort = heap sort at depth 0, then
+// __final_insertion_sort.  The recursion runs on an explicit stack.
+// stk: 48 ints of scratch for the explicit stack (depth <= 2 lg n <= 16 pushes).
+template <class V>
+HMC_HD void sort_greater(const V &v, int n, int *stk) {
+  if (n <= 16) {
+    insertion_sort(v, 0, n);
+    return;
+  }
+  int *sf = stk, *sl = stk + 16, *sd = stk + 32, top = 0;
+  sf[0] = 0;
+  sl[0] = n;
+  sd[0] = lg2_floor(n) * 2;
+  top = 1;
+  while (top > 0) {
+    --top;
+    int first = sf[top], last = sl[top], depth = sd[top];
+    while (last - first > 16) {
+      if (depth == 0) {  // std::__partial_sort(first, last, last): heap select + sort_heap
+        make_heap(v, first, last);
+        for (int e = last; e - first > 1;) {  // std::__sort_heap / __pop_heap (stl_heap.h:253-266, 423-432)
+          --e;
+          const double x = v.l(e);
+          const uint32_t y = v.m(e);
+          v.copy(e, first);
+          adjust_heap(v, first, 0, e - first, x, y);
+        }
+        break;
+      }
+      --depth;
+      const int cut = unguarded_partition_pivot(v, first, last);
+      sf[top] = first;  // the loop's continuation on [first, cut) after the recursive call
+      sl[top] = cut;
+      sd[top] = depth;
+      ++top;
+      first = cut;  // std::__introsort_loop(cut, last, depth)
+    }
+  }
+  insertion_sort(v, 0, 16);  // std::__final_insertion_sort
+  unguarded_insertion_sort(v, 16, n);
+}
+template <class V>
+HMC_HD void sort_greater(const V &v, int n) {
+  int stk[48];
+  sort_greater(v, n, stk);
+}
+
 }  // namespace hmc

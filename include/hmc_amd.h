@@ -290,6 +290,9 @@ int hmc_last_timings(const hmc_ctx *ctx, double *estep_forward_ms, double *estep
  * of (lik, tag) records ordered by lik. */
 void hmc_test_nth_element(double *lik, uint32_t *tag, int n, int nth);
 void hmc_test_sort_small(double *lik, uint32_t *tag, int n);
+/* std::sort(v, v+n, greater) for any n (introsort, heap sort at depth 0,
+ * final insertion sort): the final candidate order for sample_size > 16. */
+void hmc_test_sort(double *lik, uint32_t *tag, int n);
 /* The E-step's mask-partition formulation of the same nth_element (n <= 32). */
 void hmc_test_nth_element_masks(double *lik, uint32_t *tag, int n, int nth);
 /* GPU check of the segmented wave selection the E-step kernel uses

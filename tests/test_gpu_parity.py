@@ -113,7 +113,7 @@ def test_value_only_mode_with_order_reruns(oracle_mod, name, S):
     assert 0 <= st["n_order_rerun"] <= p.N
 
 
-@pytest.mark.parametrize("S", [1, 2, 5, 16])
+@pytest.mark.parametrize("S", [1, 2, 5, 16, 17, 24, 32])
 def test_estep_sample_sizes(oracle_mod, S):
     p = panel("miss2")
     o = oracle_mod.Oracle(p.alleles, p.types, sample_size=S)

@@ -67,3 +67,21 @@ def test_small_sort_matches_libstdcxx(oracle_mod, n):
         _, t1 = _ours(L.hmc_test_sort_small, lik, tag)
         _, t2 = oracle_mod.std_sort(lik, tag)
         assert np.array_equal(t1, t2)
+
+
+@pytest.mark.parametrize("n", list(range(0, 70)) + [100, 257, 1000])
+def test_sort_matches_libstdcxx(oracle_mod, n):
+    """std::sort for any n (select.hpp sort_greater: introsort with the
+    threshold 16, heap sort at depth 0, final insertion sort) — the final
+    candidate order when sample_size > 16."""
+    L = hmc_amd.lib()
+    rng = np.random.default_rng(300 + n)
+    for rep in range(4):
+        for ci, lik in enumerate(_cases(rng, max(n, 1))):
+            if ci == 6:  # NaN: std::sort's unguarded loops need a strict weak order
+                continue
+            lik = lik[:n]
+            tag = np.arange(n, dtype=np.int32)
+            _, t1 = _ours(L.hmc_test_sort, lik, tag)
+            _, t2 = oracle_mod.std_sort(lik, tag)
+            assert np.array_equal(t1, t2), (n, ci)
