@@ -342,8 +342,11 @@ struct Ctx {
   std::vector<int32_t> h_rowmap;                        // dense sample h -> slot row
   std::vector<unsigned long long> h_re;
   bool have_estep = false;
-  std::vector<uint8_t> best_res;  // [n][2][L] accepted resolutions (allele index)
+  std::vector<uint8_t> best_res;  // [n][2][L] accepted resolutions (allele index), host copy
   bool have_best = false;
+  bool best_on_host = false;      // best_res matches d_best
+  DevBuf<uint8_t> d_best;         // the accepted resolutions on the device
+  DevBuf<int32_t> d_hc_cnt, d_hc_bad;
 
   // split E-step (estep_split.hip): structure pass + value pass, fused
   // kernel as the exact fallback for underflowing individuals
@@ -2347,51 +2350,30 @@ struct Ctx {
   // counters, summed over ranks (HaploComp::operator+=, :78-90), then
   // out = {switch error, IHP, IGP}.  m_genos_input == m_genos_real there, so
   // no missing error.
-  int haplocomp(const std::vector<uint8_t> &res, double out[3]) {
+  int haplocomp(double out[3]) {
     const int n = nloc(), L = pan.L;
-    auto am = [](uint8_t x, uint8_t y) { return x == MISSING || y == MISSING || x == y; };  // Allele::isMatch
+    const int ncmp = std::max(0, std::min(n, pan.unphased - i0));  // m_genotype_num = unphased_num() (HaploComp.cpp:40)
+    hipError_t e;
+    std::vector<int32_t> hc((size_t)ncmp * 6), bad(ncmp);
+    if (ncmp > 0) {
+      if ((e = d_hc_cnt.ensure((size_t)ncmp * 6)) || (e = d_hc_bad.ensure(ncmp)) ||
+          (e = launch_haplocomp_counts(d_geno_im.p, i0, ncmp, L, d_best.p, d_hc_cnt.p, d_hc_bad.p, st)) ||
+          (e = hipMemcpyAsync(hc.data(), d_hc_cnt.p, hc.size() * 4, hipMemcpyDeviceToHost, st)) ||
+          (e = hipMemcpyAsync(bad.data(), d_hc_bad.p, bad.size() * 4, hipMemcpyDeviceToHost, st)) ||
+          (e = hipStreamSynchronize(st)))
+        return hipfail(e, "haplocomp");
+    }
     double cnt[6] = {0, 0, 0, 0, 0, 0};  // se_num, se_den, ihp_num, ihp_den, igp_num, igp_den
-    for (int i = 0; i < n; ++i) {
-      if (i0 + i >= pan.unphased) break;  // m_genotype_num = unphased_num() (HaploComp.cpp:40)
-      const uint8_t *r0 = pan.idx.data() + ((size_t)(i0 + i) * 2) * L, *r1 = r0 + L;
-      const uint8_t *f0 = res.data() + ((size_t)i * 2) * L, *f1 = f0 + L;
-      auto hasMissing = [&](int k) { return r0[k] == MISSING || r1[k] == MISSING; };
-      auto match = [&](int k, bool rev) {  // Genotype::isMatch(g, i, reversed) (Genotype.cpp:97-116)
-        return rev ? (am(r0[k], f1[k]) && am(r1[k], f0[k])) : (am(r0[k], f0[k]) && am(r1[k], f1[k]));
-      };
-      int het = 0, miss = 0;  // Genotype::checkGenotype (Genotype.cpp:44-55)
-      for (int k = 0; k < L; ++k) {
-        het += am(r0[k], r1[k]) ? 0 : 1;
-        miss += hasMissing(k) ? 1 : 0;
-      }
-      // getSwitchDistanceIgnoreMissing (Genotype.cpp:224-266)
-      int start = L, sd = 0;
-      for (int k = 0; k < L; ++k)
-        if (!(hasMissing(k) || (match(k, true) && match(k, false)))) { start = k; break; }
-      if (start < L) {
-        bool rev;
-        if (match(start, true)) rev = true;
-        else if (match(start, false)) rev = false;
-        else return fail(HMC_EARG, "Inconsistent genotypes at locus %d!", start);
-        for (int k = start + 1; k < L; ++k) {
-          if (hasMissing(k) || match(k, rev)) continue;
-          if (!match(k, !rev)) return fail(HMC_EARG, "Inconsistent genotypes at locus %d!", k);
-          rev = !rev;
-          ++sd;
-        }
-      }
-      int d1 = 0, d2 = 0;  // getDiffNumIgnoreMissing (Genotype.cpp:160-175)
-      for (int k = 0; k < L; ++k)
-        if (!hasMissing(k)) {
-          d1 += match(k, true) ? 0 : 1;
-          d2 += match(k, false) ? 0 : 1;
-        }
+    for (int i = 0; i < ncmp; ++i) {
+      if (bad[i] >= 0) return fail(HMC_EARG, "Inconsistent genotypes at locus %d!", bad[i]);
+      const int32_t *c = hc.data() + (size_t)i * 6;
+      const int sd = c[0], het = c[1];
       cnt[0] += sd;
       cnt[1] += het - 1;
       cnt[2] += sd > 0 ? 1 : 0;
       cnt[3] += het > 1 ? 1 : 0;
-      cnt[4] += d1 < d2 ? d1 : d2;
-      cnt[5] += L - miss;
+      cnt[4] += c[4];
+      cnt[5] += c[5];
     }
     int rc = allreduce_host(cnt, 6);  // integers < 2^53: exact in any order
     if (rc) return rc;
@@ -2401,16 +2383,45 @@ struct Ctx {
     return HMC_OK;
   }
 
+  // the accepted resolutions on the host (outputs)
+  int sync_best() {
+    if (best_on_host) return HMC_OK;
+    hipError_t e;
+    best_res.resize((size_t)nloc() * 2 * pan.L);
+    if ((e = hipMemcpyAsync(best_res.data(), d_best.p, best_res.size(), hipMemcpyDeviceToHost, st)) ||
+        (e = hipStreamSynchronize(st)))
+      return hipfail(e, "resolutions");
+    best_on_host = true;
+    return HMC_OK;
+  }
+
   // ------------------------------------------------------------------ run --
   // resolutions = unphased (HaploModel.cpp:127)
-  void init_best() {
+  int init_best() {
     const int n = nloc(), L = pan.L;
     best_res.assign((size_t)n * 2 * L, 0);
     for (int i = 0; i < n; ++i)
       for (int h = 0; h < 2; ++h)
         for (int k = 0; k < L; ++k)
           best_res[((size_t)i * 2 + h) * L + k] = pan.idx[((size_t)(i0 + i) * 2 + h) * L + k];
-    have_best = true;
+    hipError_t e;
+    if ((e = d_best.ensure(best_res.size())) ||
+        (e = hipMemcpyAsync(d_best.p, best_res.data(), best_res.size(), hipMemcpyHostToDevice, st)) ||
+        (e = hipStreamSynchronize(st)))
+      return hipfail(e, "resolutions");
+    have_best = best_on_host = true;
+    return HMC_OK;
+  }
+  // HaploModel.cpp:132-133: resolutions = this E-step's best pairs (device copy)
+  int accept_resolutions() {
+    if (!have_estep) return fail(HMC_EARG, "no E-step has run");
+    const int n = nloc(), L = pan.L;
+    hipError_t e;
+    if ((e = d_best.ensure((size_t)n * 2 * L)) ||
+        (e = launch_gather_resolutions(d_rows.p, L, d_sbase.p, d_ncand.p, d_geno_im.p, i0, n, d_best.p, st)))
+      return hipfail(e, "resolutions");
+    best_on_host = false;
+    return HMC_OK;
   }
 
   // One iteration of HaploModel::run (HaploModel.cpp:130-144): E-step, accept
@@ -2418,20 +2429,18 @@ struct Ctx {
   // the M-step when continuing (or always, force_m: a fixed number of steps).
   int em_iteration(int it, int max_iter, bool force_m, double &old_ll, hmc_iter_log &rec, bool &go) {
     using clk = std::chrono::steady_clock;
-    if (!have_best) init_best();
+    int rc;
+    if (!have_best && (rc = init_best())) return rc;
     auto t1 = clk::now();
     double ll = 0;
     int Hs = 0;
     uint64_t re = 0;
-    int rc;
     if ((rc = estep(&ll, &Hs, &re))) return rc;
     const double te = std::chrono::duration<double>(clk::now() - t1).count();
-    if (ll >= old_ll) {
-      if ((rc = resolutions_idx(best_res))) return rc;
-    }
+    if (ll >= old_ll && (rc = accept_resolutions())) return rc;
     rec = hmc_iter_log{};
     double hc[3];
-    if ((rc = haplocomp(best_res, hc))) return rc;  // HaploModel.cpp:134-136
+    if ((rc = haplocomp(hc))) return rc;  // HaploModel.cpp:134-136
     rec.switch_error = hc[0];
     rec.ihp = hc[1];
     rec.igp = hc[2];
@@ -2465,7 +2474,7 @@ struct Ctx {
     if (t_m0) *t_m0 = std::chrono::duration<double>(clk::now() - t0).count();
     if (rm0) *rm0 = rm;
     if (np0) *np0 = np;
-    init_best();
+    if ((rc = init_best())) return rc;
     double old_ll = -DBL_MAX;
     int it = 0;
     for (it = 1; it <= max_iter; ++it) {
@@ -2825,6 +2834,7 @@ int hmc_write_files(hmc_ctx *h, const char *format, const char *const *paths, in
   if (!h || !format || !paths || n_paths <= 0 || !h->c.have_best || h->c.world != 1) return HMC_EARG;
   if (std::string(format) == "PHASE") return hmc_write_phase(h, paths[0]);
   hmc::Ctx &c = h->c;
+  if (const int rc = c.sync_best()) return rc;
   const hmc::FileData d = writer_meta(c);
   std::vector<int32_t> hap((size_t)d.N * 2 * d.L);
   c.to_symbols(c.best_res, hap.data());
@@ -3134,7 +3144,7 @@ int hmc_em_iteration(hmc_ctx *h, int iteration, int max_iter, int always_mstep, 
 int hmc_haplocomp(hmc_ctx *h, double *switch_error, double *ihp, double *igp) {
   if (!h || !h->c.have_best) return HMC_EARG;
   double out[3];
-  const int rc = h->c.haplocomp(h->c.best_res, out);
+  const int rc = h->c.haplocomp(out);
   if (rc) return rc;
   if (switch_error) *switch_error = out[0];
   if (ihp) *ihp = out[1];
@@ -3144,6 +3154,7 @@ int hmc_haplocomp(hmc_ctx *h, double *switch_error, double *ihp, double *igp) {
 
 int hmc_get_best_resolutions(hmc_ctx *h, int32_t *out) {
   if (!h || !out || !h->c.have_best) return HMC_EARG;
+  if (const int rc = h->c.sync_best()) return rc;
   h->c.to_symbols(h->c.best_res, out);
   return HMC_OK;
 }
@@ -3151,6 +3162,7 @@ int hmc_get_best_resolutions(hmc_ctx *h, int32_t *out) {
 int hmc_write_phase(hmc_ctx *h, const char *path) {
   if (!h || !path || !h->c.have_best || h->c.world != 1) return HMC_EARG;
   Ctx &c = h->c;
+  if (const int rc = c.sync_best()) return rc;
   FILE *fp = fopen(path, "w");
   if (!fp) return c.fail(HMC_EIO, "Can not open file %s!", path);
   const int N = c.pan.N, L = c.pan.L;

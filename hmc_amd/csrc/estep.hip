@@ -901,6 +901,67 @@ __global__ void gather_resolutions(const uint8_t *rows, int L, const int32_t *sb
   out[((size_t)i * 2 + 1) * L + l] = b;
 }
 
+// HaploComp counters of one individual (HaploComp.cpp:29-76, Genotype.cpp:
+// 44-55, 97-116, 160-175, 224-266): the input genotypes (phase as given)
+// against the accepted resolution, one thread per individual.  cnt[i][6] =
+// switch distance, heterozygous loci, (unused), -, min mismatches, non-missing
+// loci; bad[i] = first locus where the two are inconsistent, else -1.
+__global__ void haplocomp_counts(const uchar2 *geno_im, int i0, int n, int L, const uint8_t *res, int32_t *cnt,
+                                 int32_t *bad) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uchar2 *g = geno_im + (size_t)(i0 + i) * L;
+  const uint8_t *f0 = res + (size_t)i * 2 * L, *f1 = f0 + L;
+  auto am = [](uint8_t x, uint8_t y) { return x == MISSING || y == MISSING || x == y; };  // Allele::isMatch
+  auto match = [&](int k, bool rev) {
+    const uchar2 r = g[k];
+    return rev ? (am(r.x, f1[k]) && am(r.y, f0[k])) : (am(r.x, f0[k]) && am(r.y, f1[k]));
+  };
+  int het = 0, miss = 0, d1 = 0, d2 = 0, sd = 0, start = -1, bad_at = -1;
+  bool rev = false;
+  for (int k = 0; k < L; ++k) {
+    const uchar2 r = g[k];
+    const bool hm = r.x == MISSING || r.y == MISSING;
+    het += am(r.x, r.y) ? 0 : 1;
+    miss += hm ? 1 : 0;
+    if (hm) continue;
+    const bool mt = match(k, true), mf = match(k, false);
+    d1 += mt ? 0 : 1;
+    d2 += mf ? 0 : 1;
+    if (bad_at >= 0) continue;
+    if (start < 0) {  // getSwitchDistanceIgnoreMissing: the first locus not matching both ways
+      if (mt && mf) continue;
+      start = k;
+      if (mt) rev = true;
+      else if (mf) rev = false;
+      else bad_at = k;
+      continue;
+    }
+    if (rev ? mt : mf) continue;
+    if (!(rev ? mf : mt)) {
+      bad_at = k;
+      continue;
+    }
+    rev = !rev;
+    ++sd;
+  }
+  int32_t *c = cnt + (size_t)i * 6;
+  c[0] = sd;
+  c[1] = het;
+  c[2] = 0;
+  c[3] = 0;
+  c[4] = d1 < d2 ? d1 : d2;
+  c[5] = L - miss;
+  bad[i] = bad_at;
+}
+
+hipError_t launch_haplocomp_counts(const uchar2 *geno_im, int i0, int n, int L, const uint8_t *res, int32_t *cnt,
+                                   int32_t *bad, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(haplocomp_counts, dim3((n + 127) / 128), dim3(128), 0, st, geno_im, i0, n, L, res, cnt, bad);
+  return hipGetLastError();
+}
+
 hipError_t launch_gather_resolutions(const uint8_t *rows, int L, const int32_t *sbase, const int32_t *ncand,
                                      const uchar2 *geno_im, int i0, int n, uint8_t *out, hipStream_t st) {
   const long long tot = (long long)n * L;
