@@ -1695,7 +1695,6 @@ struct Ctx {
 
   static constexpr int ESTEP_RESTART = 1;
   std::vector<unsigned long long> prev_rneed;  // records per individual of the last E-step (estimates)
-  std::vector<unsigned long long> prev_tneed;  // its traces
   int prev_P = 0;
   DevBuf<unsigned long long> d_recsz;  // [n] record region size of each individual
   uint64_t trace_budget = 0, rec_budget = 0;  // words
@@ -1885,14 +1884,8 @@ struct Ctx {
     std::vector<unsigned long long> est(n, 0);
     const bool prev_ok = !exact && (int)prev_rneed.size() == n && prev_P > 0 && P < 2 * (int64_t)prev_P &&
                          2 * (int64_t)P > prev_P;
-    // trace estimates (so that a structure group is also one value group):
-    // the previous E-step's, else traces per record word of those measured
-    std::vector<unsigned long long> est_t(n, 0);
     if (prev_ok)
-      for (int i = 0; i < n; ++i) {
-        est[i] = prev_rneed[i] + prev_rneed[i] / 10 + 64;
-        est_t[i] = (int)prev_tneed.size() == n ? prev_tneed[i] + prev_tneed[i] / 10 + 64 : 0;
-      }
+      for (int i = 0; i < n; ++i) est[i] = prev_rneed[i] + prev_rneed[i] / 10 + 64;
     bool have_est = prev_ok;
     int rc;
     while (!pending.empty()) {
@@ -1914,7 +1907,9 @@ struct Ctx {
           while (k < np) {
             const int bi = pending[k];
             const uint64_t need = exact_need[bi] ? rneed[bi] : std::min<uint64_t>(est[bi], rec_budget);
-            const uint64_t tn = exact_need[bi] ? tneed[bi] : std::min<uint64_t>(est_t[bi], trace_budget);
+            // (estimated traces are not counted: groups cut by records and then
+            // split by exact traces measured faster at cfg 3's E1)
+            const uint64_t tn = exact_need[bi] ? tneed[bi] : 0;
             if (k > 0 && (r + need > rec_budget || t + tn > trace_budget)) break;
             rsz[bi] = need;
             r += need;
@@ -2042,15 +2037,8 @@ struct Ctx {
         for (int q = 0; q < np; ++q) deferred += h_status[pending[q]] == EST_OVERFLOW_REC ? 1 : 0;
         if (!have_est || deferred * 10 > np) {
           const double ratio = cs > 0 ? rs_ / cs : 0.0;
-          double ts = 0;
-          for (int i = 0; i < n; ++i)
-            if (exact_need[i]) ts += (double)tneed[i];
-          const double tr = rs_ > 0 ? ts / rs_ : 0.0;  // trace words per record word
           for (int bi : rest)
-            if (!exact_need[bi]) {
-              est[bi] = (uint64_t)(1.25 * ratio * std::max(1, h_cost[bi])) + 64;
-              est_t[bi] = (uint64_t)(tr * (double)est[bi]);
-            }
+            if (!exact_need[bi]) est[bi] = (uint64_t)(1.25 * ratio * std::max(1, h_cost[bi])) + 64;
           have_est = true;
         }
       }
@@ -2191,7 +2179,6 @@ struct Ctx {
     }
     if (!exact) {
       prev_rneed = rneed;
-      prev_tneed = tneed;
       prev_P = P;
     }
     return HMC_OK;
