@@ -1964,7 +1964,7 @@ struct Ctx {
       s1.fcap = fcap;
       s1.hcap = hcap1;
       s1.ccap = ccap1;
-      s1_tier(160 * 1024 / bpc1 - 256, s1.lds_fc, s1.lds_hc, s1.lds_cc);
+      s1_tier(160 * 1024 / bpc1 - 256, pan.amax, s1.lds_fc, s1.lds_hc, s1.lds_cc);
       s1.rec = d_rec.p;
       s1.rec_cap = d_rec.n;
       s1.rec_cursor = d_rec_cursor.p;
@@ -2246,10 +2246,10 @@ struct Ctx {
 
   // LDS tiers of pass 1 (one wave per individual, `budget` bytes): states per
   // frontier, key slots (2x, power of two), contributions per locus (2x).
-  static void s1_tier(int budget, int &fc, int &hc, int &cc) {
+  static void s1_tier(int budget, int amax, int &fc, int &hc, int &cc) {
     for (int f = 1024; f >= 16; f -= 16) {
       const int h = next_pow2(2 * f), c = 2 * f;
-      if ((int)estep_s1_lds_bytes(f, h, c) <= budget) { fc = f; hc = h; cc = c; return; }
+      if ((int)estep_s1_lds_bytes(f, h, c, amax) <= budget) { fc = f; hc = h; cc = c; return; }
     }
     fc = 0;
     hc = 16;

@@ -109,11 +109,12 @@ struct K1Plan {
   int o_pairs, o_bucket, o_front[2], o_keys, o_contrib, bytes;
 };
 
-__host__ __device__ inline K1Plan k1_plan(int fc, int hc, int cc) {
+// npm: allele pairs of a fully missing locus, amax (amax + 1) / 2 <= NP_MAX
+__host__ __device__ inline K1Plan k1_plan(int fc, int hc, int cc, int npm) {
   K1Plan p;
   int o = 0;
   auto take = [&](int bytes) { int r = o; o += (bytes + 15) & ~15; return r; };
-  p.o_pairs = take((NP_MAX + 2) * 4 + 3 * NP_MAX);
+  p.o_pairs = take((npm + 2) * 4 + 3 * npm);
   p.o_bucket = take(NBUCKET * 4);
   p.o_front[0] = take(F_NARR * fc * 4);
   p.o_front[1] = take(F_NARR * fc * 4);
@@ -177,18 +178,21 @@ __host__ __device__ inline size_t k1_front_words(int fcap) { return al256((size_
 size_t estep_s1_scratch_bytes(int fcap, int hcap, int ccap) {
   return 2 * al256(F_NARR * k1_front_words(fcap) * 4) + al256((size_t)hcap * 24) + al256((size_t)ccap * 12);
 }
-size_t estep_s1_lds_bytes(int fc, int hc, int cc) { return (size_t)k1_plan(fc, hc, cc).bytes; }
+size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax) {
+  return (size_t)k1_plan(fc, hc, cc, amax * (amax + 1) / 2).bytes;
+}
 
 __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const K1Plan plan = k1_plan(a.lds_fc, a.lds_hc, a.lds_cc);
+  const int npm = a.pan.amax * (a.pan.amax + 1) / 2;
+  const K1Plan plan = k1_plan(a.lds_fc, a.lds_hc, a.lds_cc, npm);
   const int lane = lane_id();
   const uint64_t lt = lanemask_lt();
   const int S = a.S, L = a.pan.L, amax = a.pan.amax, hl = a.mod.head_len;
-  int *pr_off = (int *)(smem + plan.o_pairs);  // [NP_MAX+2]; [NP_MAX+1] = npairs
-  uint8_t *pr_x = (uint8_t *)(pr_off + NP_MAX + 2);
-  uint8_t *pr_y = pr_x + NP_MAX;
-  uint8_t *pr_o = pr_y + NP_MAX;
+  int *pr_off = (int *)(smem + plan.o_pairs);  // [npm+2]; [npm+1] = npairs
+  uint8_t *pr_x = (uint8_t *)(pr_off + npm + 2);
+  uint8_t *pr_y = pr_x + npm;
+  uint8_t *pr_o = pr_y + npm;
   int *bucket = (int *)(smem + plan.o_bucket);
 
   char *sp = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
@@ -343,10 +347,10 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
         int off = 0;
         for (int p = 0; p < np; ++p) { pr_off[p] = off; off += Fp * pr_o[p]; }
         pr_off[np] = off;
-        pr_off[NP_MAX + 1] = np;
+        pr_off[npm + 1] = np;
       }
       wsync();
-      const int npairs = pr_off[NP_MAX + 1];
+      const int npairs = pr_off[npm + 1];
       const int C = pr_off[npairs];
       if (C > a.ccap) { status = EST_OVERFLOW_FRONTIER; break; }
       int Fn = 0;
@@ -1052,7 +1056,7 @@ hipError_t launch_estep_structure(const StructArgs &a, int grid, hipStream_t st)
       (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || a.lds_cc < 0 || a.ccap < 1 || a.mod.head_len < 1 ||
       (a.mod.head_len > 1 && (!a.mod.hf_off || !a.mod.hf_pairs || !a.mod.hf_status)))
     return hipErrorInvalidValue;
-  const size_t lds = estep_s1_lds_bytes(a.lds_fc, a.lds_hc, a.lds_cc);
+  const size_t lds = estep_s1_lds_bytes(a.lds_fc, a.lds_hc, a.lds_cc, a.pan.amax);
   static size_t lds_attr = 0;
   if (lds > 65536 && lds > lds_attr) {
     hipError_t e =
