@@ -794,6 +794,7 @@ struct Ctx {
     }
     ++exact_rounds;
     exact_candidates += nc;
+    if (getenv("HMC_DEBUG_MEM")) fprintf(stderr, "[hmc] exact round %d: %zu candidates\n", exact_rounds, nc);
     return HMC_OK;
   }
   size_t xacc_nc = 0;
