@@ -2067,9 +2067,12 @@ struct Ctx {
         }
         int vnw = vp_nw, vipc = vp_ipc;
         if (vnw <= 0) {
-          const bool many = (int)k >= 12 * dev_cu;
-          vnw = many ? 1 : 2;
-          vipc = many ? 16 : 8;
+          // by individuals per CU (cfg 3 and its rank shards, tools/shard_shapes.py,
+          // profiles/r02/shard_shapes/): 1:16 from 32 per CU (10 000: 557 vs 615 ms
+          // at 2:8), 2:8 from 8 (4 994: 290 vs 333 ms at 1:16), else 3:8 (1 239:
+          // 101 vs 112 ms at 2:8)
+          vnw = (int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3);
+          vipc = vnw == 1 ? 16 : 8;
         }
         const int G2 = std::max(1, std::min(waves > 0 ? waves : dev_cu * vipc, n));
         const int grid2 = std::max(1, std::min<int>(G2, (int)k));
