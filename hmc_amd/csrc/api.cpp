@@ -1945,7 +1945,10 @@ struct Ctx {
           return hipfail(e, "estep");
       }
       const int hcap1 = next_pow2(2 * fcap), ccap1 = 8 * fcap;
-      int bpc1 = np > 4 * dev_cu ? 8 : 4;  // structure pass: one wave per individual
+      // structure pass: one wave per individual; 12 per CU (3 per SIMD at 145
+      // VGPRs) above 8 per CU, so cfg 3's E1 groups of 2 200-2 700 run in one
+      // round (profiles/r02/e1_groups/: 603-658 -> 484-586 ms per group)
+      int bpc1 = np > 8 * dev_cu ? 12 : (np > 4 * dev_cu ? 8 : 4);
       if (const char *env = getenv("HMC_S1_BPC")) bpc1 = std::max(1, atoi(env));  // tuning experiments
       const int grid1 = std::max(1, std::min(np, dev_cu * bpc1));
       const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1);
@@ -2054,6 +2057,15 @@ struct Ctx {
           t += tneed[sset[pos + k]];
           ++k;
         }
+        // traces over the budget by a few individuals while structure groups
+        // still follow: those join the next group (re-walked there, exact sizes
+        // known) instead of a value pass of their own, which would cost one
+        // heavy individual's whole latency (cfg 3 E1: 61-78 individuals,
+        // 230-270 ms each, profiles/r02/e1_groups/)
+        if (pos == 0 && !exact && !rest.empty() && k < sset.size() && 4 * (sset.size() - k) <= sset.size()) {
+          rest.insert(rest.begin(), sset.begin() + (std::ptrdiff_t)k, sset.end());
+          sset.resize(k);
+        }
         if ((rc = ensure_store(d_trace, std::max<uint64_t>(t, 1), trace_budget, "trace store"))) return rc;
         std::vector<unsigned long long> tb(n, 0);
         for (size_t q = 0; q < k; ++q) tb[sset[pos + q]] = base[sset[pos + q]];
@@ -2073,6 +2085,12 @@ struct Ctx {
           // 101 vs 112 ms at 2:8)
           vnw = (int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3);
           vipc = vnw == 1 ? 16 : 8;
+          static const char *vp_env = getenv("HMC_VP_SHAPE");  // tuning experiments: "nw:ipc"
+          int a0 = 0, a1 = 0;
+          if (vp_env && sscanf(vp_env, "%d:%d", &a0, &a1) == 2 && a0 >= 1 && a0 <= 4 && a1 >= 1) {
+            vnw = a0;
+            vipc = a1;
+          }
         }
         const int G2 = std::max(1, std::min(waves > 0 ? waves : dev_cu * vipc, n));
         const int grid2 = std::max(1, std::min<int>(G2, (int)k));

@@ -505,7 +505,7 @@ def test_cfg5_full_size_properties():
     assert np.all(nc > 0) and np.isfinite(ll) and H == int(2 * nc.sum())
     k = np.arange(er["prior"].shape[1])
     valid = k[None, :] < nc[:, None]
-    pr = np.where(valid, er["prior"], -np.inf)
+    pr = np.where(valid, er["prior"], 0.0)  # slots past ncand are not compared (valid[:, 1:] implies both valid)
     assert np.all(np.diff(pr, axis=1)[valid[:, 1:]] <= 0)
     assert np.all(np.abs(np.where(valid, er["weight"], 0.0).sum(1) - 1.0) < 1e-12)
     res = m.resolutions()
