@@ -35,6 +35,7 @@ timeout -s KILL 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OU
 cp "$(find "$OUT/trace" -name "*kernel_stats.csv" | head -n 1)" "$DEST/kernel_stats_cfg$CFG.csv"
 tail -1 "$OUT/trace.json" > "$DEST/bench_under_rocprof_cfg$CFG.json"
 SHORT="bench.py --config $CFG --no-cpu-baseline --steps 2 --warmup 0"
+[ -n "${SKIP_SQ:-}" ] && { echo "[profile] done (SQ passes skipped)" >&2; exit 0; }
 for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU" \
          "SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM"; do
   N=$(echo "$P" | awk '{print $1}')
