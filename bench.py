@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--trace-bytes", type=int, default=0, help="E-step store budget per store (0: automatic)")
     ap.add_argument("--reduction", default="ordered", choices=["ordered", "allreduce"],
                     help="cross-rank M-step sums: rank-ordered (bit-identical to one GPU) or one all-reduce")
+    ap.add_argument("--collective", default="rccl", choices=["rccl", "host"],
+                    help="M-step collective: RCCL (the product), or a gloo host all-reduce with every rank on "
+                         "GPU LOCAL_RANK %% device_count (rehearses the multi-rank bench on one GPU; not a measurement)")
     a = ap.parse_args()
     c = synth.CONFIGS[a.config]
     a.N = a.individuals or c["N"]
@@ -89,7 +92,8 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local)
+    dev = local % max(1, torch.cuda.device_count()) if args.collective == "host" else local
+    torch.cuda.set_device(dev)
 
     def barrier():
         if world > 1:
@@ -114,12 +118,18 @@ def main():
     panel = synth.founder_mosaic(N, L, A=args.A, missing=args.missing, seed=args.seed)
     genos = hmc_amd.GenoData.from_panel(panel)
 
-    uid = None
-    if world > 1:
-        obj = [hmc_amd.HaploModel.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        uid = obj[0]
-    m = hmc_amd.HaploModel(device=local, rank=rank, world=world, unique_id=uid)
+    if world > 1 and args.collective == "host":
+        def host_allreduce(arr):  # in place, float64, summed over ranks by gloo
+            dist.all_reduce(torch.from_numpy(arr))
+
+        m = hmc_amd.HaploModel(device=dev, rank=rank, world=world, host_allreduce=host_allreduce)
+    else:
+        uid = None
+        if world > 1:
+            obj = [hmc_amd.HaploModel.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            uid = obj[0]
+        m = hmc_amd.HaploModel(device=local, rank=rank, world=world, unique_id=uid)
     m.set_reduction(args.reduction)
     m.sample_size = args.sample_size
     if args.trace_bytes:
@@ -215,7 +225,9 @@ def main():
                 "individuals": N, "loci": L, "sample_size": args.sample_size,
                 "min_freq_abs": 1.5, "pattern_len": [1, 30],
                 "parallelism": f"individual-sharded x{world}, " + ("ordered RCCL reduction (chained broadcasts)" if args.reduction == "ordered"
-                                                                     else "RCCL all-reduce") + " per mining level",
+                                                                     else "RCCL all-reduce") + " per mining level"
+                               + (" [REHEARSAL: gloo host collective, ranks sharing GPUs - not a measurement]"
+                                  if world > 1 and args.collective == "host" else ""),
             },
             "roofline": {
                 "bound": "hbm", "kernel": "estep_values",
