@@ -1707,7 +1707,12 @@ struct Ctx {
     if (words > budget) return fail(HMC_ENOMEM, "%s: one individual needs %llu words (budget %llu)", what,
                                     (unsigned long long)words, (unsigned long long)budget);
     b.release();  // 1.25x headroom: a store of tens of GB is mapped eagerly, re-allocations are slow
-    hipError_t e = b.ensure(std::min<uint64_t>(budget, words + words / 4));
+    const uint64_t want = std::min<uint64_t>(budget, words + words / 4);
+    hipError_t e = b.ensure(want);
+    if (e == hipErrorOutOfMemory && want > words) {  // the device is shared: no headroom
+      (void)hipGetLastError();
+      e = b.ensure(words);
+    }
     if (e) return hipfail(e, what);
     return HMC_OK;
   }
