@@ -2088,8 +2088,10 @@ struct Ctx {
           // profiles/r02/shard_shapes/): 1:16 from 32 per CU (10 000: 557 vs 615 ms
           // at 2:8), 2:8 from 8 (4 994: 290 vs 333 ms at 1:16), else 3:8 (1 239:
           // 101 vs 112 ms at 2:8)
+          // (1:20 runs the 5-waves-per-SIMD build: 505-514 vs 535-558 ms at
+          // 1:16 for cfg 3's E3, profiles/r02/values_ab/)
           vnw = (int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3);
-          vipc = vnw == 1 ? 16 : 8;
+          vipc = vnw == 1 ? 20 : 8;
           static const char *vp_env = getenv("HMC_VP_SHAPE");  // tuning experiments: "nw:ipc"
           int a0 = 0, a1 = 0;
           if (vp_env && sscanf(vp_env, "%d:%d", &a0, &a1) == 2 && a0 >= 1 && a0 <= 4 && a1 >= 1) {
@@ -2099,6 +2101,8 @@ struct Ctx {
         }
         const int G2 = std::max(1, std::min(waves > 0 ? waves : dev_cu * vipc, n));
         const int grid2 = std::max(1, std::min<int>(G2, (int)k));
+        // register budget: 5 waves per SIMD once the shape asks for more than 16 per CU
+        const int vwpe = vnw * vipc > 16 && vnw * vipc <= 20 ? 5 : 4;
         const size_t per2 = estep_s2_scratch_bytes(fcap, S);
         if ((e = d_scr2.ensure(per2 * grid2))) return hipfail(e, "estep pass-2 scratch");
         ValueArgs v;
@@ -2132,7 +2136,7 @@ struct Ctx {
         if ((e = hipMemsetAsync(d_nextq.p + 1, 0, 4, st))) return hipfail(e, "estep");
         const bool fast = value_fast;
         hipEventRecord(ev[0], st);
-        if ((e = launch_estep_values(v, grid2, vnw, fast, st))) return hipfail(e, "estep_values launch");
+        if ((e = launch_estep_values(v, grid2, vnw, fast, vwpe, st))) return hipfail(e, "estep_values launch");
         hipEventRecord(ev[1], st);
         if ((rc = read_status(sset, (int)k, true))) return rc;
         hipEventElapsedTime(&ms, ev[0], ev[1]);
@@ -2155,7 +2159,7 @@ struct Ctx {
           v2.n_order = nr;
           if ((e = hipMemsetAsync(d_nextq.p + 1, 0, 4, st))) return hipfail(e, "estep");
           hipEventRecord(ev[0], st);
-          if ((e = launch_estep_values(v2, std::max(1, std::min(G2, nr)), vnw, false, st)))
+          if ((e = launch_estep_values(v2, std::max(1, std::min(G2, nr)), vnw, false, vwpe, st)))
             return hipfail(e, "estep_values launch");
           hipEventRecord(ev[1], st);
           if ((rc = read_status(sset, (int)k, true))) return rc;

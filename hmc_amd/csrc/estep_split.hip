@@ -714,24 +714,23 @@ __device__ inline bool k2_write_trace(const ValueArgs &a, K2Shared *bs, const VF
 #define K2_FLUSH
 #endif
 
-#ifndef HMC_PA_UNROLL
-#define HMC_PA_UNROLL 8
+#ifndef HMC_PA_UNROLL  // 4: measured equal to 8 at 4 waves per SIMD, and lets 5 fit in 96 VGPRs
+#define HMC_PA_UNROLL 4
 #endif
 size_t estep_s2_scratch_bytes(int fcap, int S) { return 2 * k2_front_bytes(fcap, S); }
 size_t estep_s2_lds_bytes(int S, int fc, int nw) { return (size_t)k2_plan(S, fc, nw).bytes; }
 
-#ifdef HMC_VALUES_WPE  // tuning experiments: force more resident waves per SIMD (fewer VGPRs)
-#define HMC_VALUES_ATTR __attribute__((amdgpu_waves_per_eu(HMC_VALUES_WPE)))
-#else  // 4 waves per SIMD: 2 waves x 8 individuals per CU
-#define HMC_VALUES_ATTR __attribute__((amdgpu_waves_per_eu(4)))
-#endif
+// WPE: resident waves per SIMD the register allocation targets — 4 (127
+// VGPRs: shapes of up to 16 waves per CU) or 5 (96 VGPRs, a few spills in
+// the per-individual epilogue: the 1 x 20 shape of full groups, 5-6 % faster
+// than 1 x 16 at cfg 3, profiles/r02/values_ab/).
 // FAST: the k-best lists are kept by value only (seg_rank_select): a list's
 // arrangement differs from the reference's, which changes no result while no
 // non-zero likelihood ties across a list's S-cut and the final candidates are
 // tie-free and non-zero; otherwise the individual reports EST_NEEDS_ORDER and
 // is re-run by the exact instantiation (FAST = false, libstdc++ permutations).
-template <bool FAST>
-__global__ __launch_bounds__(256) HMC_VALUES_ATTR void estep_values(ValueArgs a) {
+template <bool FAST, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void estep_values(ValueArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int S = a.S, L = a.L, hl = a.head_len;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;
@@ -1068,21 +1067,27 @@ hipError_t launch_estep_structure(const StructArgs &a, int grid, hipStream_t st)
   return hipGetLastError();
 }
 
-hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, hipStream_t st) {
-  if (a.S < 1 || a.S > S_MAX || a.fcap > 65535 || a.lds_fc < 0 || nw < 1 || nw > 4) return hipErrorInvalidValue;
+hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, int wpe, hipStream_t st) {
+  if (a.S < 1 || a.S > S_MAX || a.fcap > 65535 || a.lds_fc < 0 || nw < 1 || nw > 4 || (wpe != 4 && wpe != 5))
+    return hipErrorInvalidValue;
   const size_t lds = estep_s2_lds_bytes(a.S, a.lds_fc, nw);
   static size_t lds_attr = 0;
   if (lds > 65536 && lds > lds_attr) {
-    for (const void *f : {(const void *)estep_values<true>, (const void *)estep_values<false>}) {
+    for (const void *f : {(const void *)estep_values<true, 4>, (const void *)estep_values<false, 4>,
+                          (const void *)estep_values<true, 5>, (const void *)estep_values<false, 5>}) {
       hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
     }
     lds_attr = lds;
   }
-  if (fast)
-    hipLaunchKernelGGL(estep_values<true>, dim3(grid), dim3(WAVE * nw), lds, st, a);
-  else
-    hipLaunchKernelGGL(estep_values<false>, dim3(grid), dim3(WAVE * nw), lds, st, a);
+  const dim3 g(grid), b(WAVE * nw);
+  if (wpe == 5) {
+    if (fast) hipLaunchKernelGGL((estep_values<true, 5>), g, b, lds, st, a);
+    else hipLaunchKernelGGL((estep_values<false, 5>), g, b, lds, st, a);
+  } else {
+    if (fast) hipLaunchKernelGGL((estep_values<true, 4>), g, b, lds, st, a);
+    else hipLaunchKernelGGL((estep_values<false, 4>), g, b, lds, st, a);
+  }
   return hipGetLastError();
 }
 

@@ -206,7 +206,8 @@ size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax);
 size_t estep_s2_scratch_bytes(int fcap, int S);
 size_t estep_s2_lds_bytes(int S, int fc, int nw);
 hipError_t launch_estep_structure(const StructArgs &a, int grid, hipStream_t st);
-hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, hipStream_t st);
+// wpe: 4 or 5 resident waves per SIMD (register budget of the instantiation)
+hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, int wpe, hipStream_t st);
 hipError_t launch_traceback(const TracebackArgs &a, int total_cands, hipStream_t st);
 hipError_t launch_transpose_rows_u8(const uint8_t *in, const int32_t *rowmap, uint8_t *out, int rows, int cols,
                                     hipStream_t st);
