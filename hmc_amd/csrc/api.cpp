@@ -1900,8 +1900,21 @@ struct Ctx {
       {
         uint64_t r = 0, t = 0;
         int k = 0;
+        // experiment (not measured yet): HMC_EST_STRATIFIED=1 takes the
+        // first pass over the whole cost range and estimates by nearest cost
+        static const bool strat = getenv("HMC_EST_STRATIFIED") != nullptr;
         if (!have_est) {  // nothing measured yet: the heaviest 4 per CU share the store evenly
           k = std::min(np, 4 * dev_cu);
+          if (strat && np > k) {  // every np/k-th of the heaviest-first list
+            std::vector<int32_t> pick, other;
+            pick.reserve(k);
+            other.reserve(np - k);
+            for (int q = 0; q < np; ++q)
+              ((int64_t)q * k / np != (int64_t)(q - 1) * k / np || q == 0 ? pick : other).push_back(pending[q]);
+            pending = pick;
+            pending.insert(pending.end(), other.begin(), other.end());
+            k = (int)pick.size();
+          }
           const uint64_t share = rec_budget / (uint64_t)k;
           for (int q = 0; q < k; ++q) {
             base[pending[q]] = (uint64_t)q * share;
@@ -2047,8 +2060,25 @@ struct Ctx {
         for (int q = 0; q < np; ++q) deferred += h_status[pending[q]] == EST_OVERFLOW_REC ? 1 : 0;
         if (!have_est || deferred * 10 > np) {
           const double ratio = cs > 0 ? rs_ / cs : 0.0;
-          for (int bi : rest)
-            if (!exact_need[bi]) est[bi] = (uint64_t)(1.25 * ratio * std::max(1, h_cost[bi])) + 64;
+          std::vector<std::pair<int, double>> cr;  // HMC_EST_STRATIFIED: (cost, records per cost) measured
+          if (getenv("HMC_EST_STRATIFIED")) {
+            for (int i = 0; i < n; ++i)
+              if (exact_need[i]) cr.emplace_back(std::max(1, h_cost[i]), (double)rneed[i] / std::max(1, h_cost[i]));
+            std::sort(cr.begin(), cr.end());
+          }
+          for (int bi : rest) {
+            if (exact_need[bi]) continue;
+            const int c = std::max(1, h_cost[bi]);
+            if (cr.empty()) {
+              est[bi] = (uint64_t)(1.25 * ratio * c) + 64;
+              continue;
+            }
+            // the largest ratio among the 4 measured nearest in cost on each side
+            const int at = (int)(std::lower_bound(cr.begin(), cr.end(), std::make_pair(c, -1.0)) - cr.begin());
+            double q = 0.0;
+            for (int u = std::max(0, at - 4); u < std::min((int)cr.size(), at + 4); ++u) q = std::max(q, cr[u].second);
+            est[bi] = (uint64_t)(1.1 * q * c) + 64;
+          }
           have_est = true;
         }
       }
