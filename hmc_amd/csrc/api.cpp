@@ -1900,9 +1900,11 @@ struct Ctx {
       {
         uint64_t r = 0, t = 0;
         int k = 0;
-        // experiment (not measured yet): HMC_EST_STRATIFIED=1 takes the
-        // first pass over the whole cost range and estimates by nearest cost
-        static const bool strat = getenv("HMC_EST_STRATIFIED") != nullptr;
+        // the first pass spans the whole cost range and later estimates use the
+        // measured individuals nearest in cost (cfg 3 E1 after E5: 7.1 -> 5.9 s,
+        // deferred 1 713 -> 12 per group, profiles/r02/e1_groups/);
+        // HMC_EST_HEAVIEST=1 restores the heaviest-first sample and one ratio
+        static const bool strat = getenv("HMC_EST_HEAVIEST") == nullptr;
         if (!have_est) {  // nothing measured yet: the heaviest 4 per CU share the store evenly
           k = std::min(np, 4 * dev_cu);
           if (strat && np > k) {  // every np/k-th of the heaviest-first list
@@ -2060,8 +2062,8 @@ struct Ctx {
         for (int q = 0; q < np; ++q) deferred += h_status[pending[q]] == EST_OVERFLOW_REC ? 1 : 0;
         if (!have_est || deferred * 10 > np) {
           const double ratio = cs > 0 ? rs_ / cs : 0.0;
-          std::vector<std::pair<int, double>> cr;  // HMC_EST_STRATIFIED: (cost, records per cost) measured
-          if (getenv("HMC_EST_STRATIFIED")) {
+          std::vector<std::pair<int, double>> cr;  // (cost, records per cost) of the measured
+          if (getenv("HMC_EST_HEAVIEST") == nullptr) {
             for (int i = 0; i < n; ++i)
               if (exact_need[i]) cr.emplace_back(std::max(1, h_cost[i]), (double)rneed[i] / std::max(1, h_cost[i]));
             std::sort(cr.begin(), cr.end());
