@@ -1,34 +1,43 @@
 #!/usr/bin/env python3
 """Benchmark: individual·loci per second per EM iteration of the HaploModel EM
-(BASELINE.json metric) on synthetic founder-mosaic panels.
+(BASELINE.json metric, SURVEY.md §8d) on synthetic founder-mosaic panels.
 
     python bench.py --gpus N --steps K --warmup W
 
 Workload: BASELINE.json configs[2] — 10 000 individuals x 2 000 biallelic SNP
 loci (cfg 3, seed 3; the largest configuration quoted for one MI355X), reference
-parameters (min-freq-abs 1.5, pattern length 1..30, sample size 10).  A "step"
-is one EM iteration, E-step (HaploModel::resolveAll) + M-step
-(PatternManager::findPatternByFreq on the weighted samples), continuing the EM
-chain from the genotype-mined model M0: step k = E_k, accept + HaploComp, M_k
-(hmc_em_iteration: one HaploModel::run iteration).  Before the timed
-region the panel is resident in HBM and M0 has been mined (its time is
-reported separately); the warmup steps run the same chain, then
-the samples are dropped and M0 is mined again so that the timed steps start
-from M0 (E1 included).  --config 2 / 5 select the other single-GPU configs.
+parameters (min-freq-abs 1.5, pattern length 1..30, sample size 10).
 
-Multi-GPU: launched by torch.distributed.run, one process per GPU.  The panel
-is the same (strong scaling): individuals are sharded in contiguous blocks; the
-M-step's per-level candidate sums are reduced in rank order over RCCL inside
-libhmc_amd (chained ncclBroadcast of seeded partial sums: bit-identical to one
-GPU; hmc_set_reduction selects a single ncclAllReduce instead).
-torch.distributed (gloo) only bootstraps the RCCL id, the barriers and the
-max-over-ranks time.
+A step is one EM iteration of the reference's converged chain
+(HaploModel::run, HaploModel.cpp:130-153): E_k, accept + HaploComp, and M_k
+when the chain continues ((old_ll - ll) / old_ll > 1e-4 with ll >= old_ll).
+The iteration that stops the chain has no M-step; the next step starts the
+chain again from the genotype-mined model M0 (hmc_em_rewind: M0's table
+restored, no samples, resolutions = input — inside the timed step).  At cfg 3
+the chain is E1+M1, E2+M2, E3, so the K timed steps cycle through it; M0 is
+mined once before the timed region and reported separately.
+value = N·L·K / timed seconds (K need not be a multiple of the chain length:
+the leftover steps are the chain's first, heaviest ones, so this is the
+conservative figure); `value_chain` is the same over whole chains only, and
+`value_steady` the forced iterations after the chain's end (E4, E5, ...).
+
+Multi-GPU: one process per GPU, launched by torch.distributed.run — or, when
+WORLD_SIZE is not set and --gpus N > 1, by this script itself: it starts N
+fresh worker processes (rank env set, 127.0.0.1 rendezvous) before anything
+touches a GPU and exits with their status.  The panel is the same (strong
+scaling): individuals are sharded in contiguous blocks; the M-step's per-level
+candidate sums are reduced in rank order over RCCL inside libhmc_amd (chained
+ncclBroadcast of seeded partial sums: bit-identical to one GPU;
+hmc_set_reduction selects a single ncclAllReduce instead).  torch.distributed
+(gloo) only bootstraps the RCCL id, the barriers and the max-over-ranks time.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -37,12 +46,13 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import hmc_amd  # noqa: E402
+import hmc_amd  # noqa: E402  (ctypes binding; loads nothing until first use)
 from hmc_amd import synth  # noqa: E402
 
 METRIC = "individuals×loci/sec per EM iter, synthetic panel, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E (spec)
-PMC_DIR = os.path.join(ROOT, "profiles", "r02")
+PMC_DIR = os.path.join(ROOT, "profiles", "r03")
+DBL_MAX = sys.float_info.max
 
 
 def parse():
@@ -58,9 +68,12 @@ def parse():
     ap.add_argument("--missing", type=float, default=0.0, help="missing-allele rate of the synthetic panel")
     ap.add_argument("--seed", type=int, default=0, help="panel seed (default = config index)")
     ap.add_argument("--sample-size", type=int, default=10)
+    ap.add_argument("--steady-steps", type=int, default=8,
+                    help="forced iterations after the chain's end, timed for value_steady (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-indiv", type=int, default=40, help="individuals timed for the CPU E-step sample")
-    ap.add_argument("--cpu-roots", type=int, default=0, help="start loci timed for the CPU M-step sample (0: L/40)")
+    ap.add_argument("--cpu-indiv", type=int, default=20, help="individuals per CPU E-step sample (E_k, k >= 2)")
+    ap.add_argument("--cpu-indiv-e1", type=int, default=6, help="individuals of the CPU E_1 sample (M0 model)")
+    ap.add_argument("--cpu-roots", type=int, default=10, help="start loci per CPU M-step sample")
     ap.add_argument("--trace-bytes", type=int, default=0, help="E-step store budget per store (0: automatic)")
     ap.add_argument("--reduction", default="ordered", choices=["ordered", "allreduce"],
                     help="cross-rank M-step sums: rank-ordered (bit-identical to one GPU) or one all-reduce")
@@ -84,9 +97,45 @@ def dist_env():
     return rank, local, world
 
 
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: N fresh worker processes of this
+    script, one per GPU, with the torch.distributed env a launcher would set.
+    Runs before anything in this process touches a GPU (no exec from here)."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                c = p.poll()
+                if c is None:
+                    continue
+                procs.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c
+                    for q in procs:  # one rank failed: the others would wait forever in a collective
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     rank, local, world = dist_env()
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
@@ -114,6 +163,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return float(t.item())
 
+    def progress(msg):
+        if rank == 0:
+            print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
     N, L = args.N, args.L
     panel = synth.founder_mosaic(N, L, A=args.A, missing=args.missing, seed=args.seed)
     genos = hmc_amd.GenoData.from_panel(panel)
@@ -135,49 +188,60 @@ def main():
     if args.trace_bytes:
         m.set_tuning(trace_bytes=args.trace_bytes)
     m.load(genos)
+    ident = hmc_amd.lib_identity()
+    progress(f"library {ident['path']} sha256 {ident['sha256_16']} ({ident['build']})")
 
-    # M0 on the genotypes (reported separately)
+    # M0 on the genotypes (reported separately), kept for the rewinds
     barrier()
     t0 = time.perf_counter()
     P0, rm0 = m.find_patterns()
     barrier()
     t_m0 = max_over_ranks(time.perf_counter() - t0)
+    m.model_save()
+    progress(f"M0 {P0} patterns in {t_m0:.1f} s")
 
-    # CPU baseline (rank 0, N = 1 only): the oracle restatement on this host
+    # CPU baseline (rank 0, N = 1 only): the oracle restatement on this host,
+    # sampled along the same chain
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(m, panel, args)
         print(f"[bench] cpu baseline {cpu['value']:.4g} {cpu['unit']} ({cpu['t_iter_s']:.0f} s/iteration)",
               file=sys.stderr, flush=True)
-        m.clear_samples()
-        m.find_patterns()
+        m.em_rewind()
 
-    def progress(msg):
-        if rank == 0:
-            print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+    chain = {"it": 0, "old_ll": -DBL_MAX, "ended": False}
 
-    progress(f"M0 {P0} patterns in {t_m0:.1f} s")
-
-    chain = {"it": 0, "old_ll": -float("inf")}
-
-    def em_step():
-        # one HaploModel::run iteration (HaploModel.cpp:130-144): E-step, accept,
-        # HaploComp, M-step (always: a fixed number of steps is timed)
+    def em_step(force_m: bool = False):
+        """One step of the converged chain (or, force_m, an iteration that
+        always runs its M-step: the steady leg)."""
+        t_s = time.perf_counter()
+        if chain["ended"]:  # the previous step stopped the chain: start again from M0
+            m.em_rewind()
+            chain.update(it=0, old_ll=-DBL_MAX, ended=False)
         chain["it"] += 1
-        log, chain["old_ll"], _ = m.em_iteration(chain["it"], chain["old_ll"], always_mstep=True)
-        ll, H, re, rm, P = log["log_likelihood"], log["n_samples"], log["r_e"], log["r_m"], log["n_patterns"]
+        it = chain["it"]
+        log, chain["old_ll"], go = m.em_iteration(it, chain["old_ll"], always_mstep=force_m)
+        if not go and not force_m:
+            chain["ended"] = True
+        wall = time.perf_counter() - t_s
         t = m.timings()
         sp = m.estep_split_stats()
-        progress(f"EM step: LL {ll:.6f}, R_E {re}, E {t['estep_forward_ms']:.0f} ms, M {t['mstep_ms']:.0f} ms")
-        return dict(ll=ll, H=H, r_e=re, r_m=rm, P=P, estep_ms=t["estep_forward_ms"] + t["estep_traceback_ms"],
-                    struct_ms=sp["structure_ms"], values_ms=sp["values_ms"], fallback_ms=sp["fallback_ms"],
-                    n_fallback=sp["n_fallback"], struct_passes=sp["structure_passes"],
-                    value_passes=sp["value_passes"], tb_ms=t["estep_traceback_ms"], mstep_ms=m.timings()["mstep_ms"])
+        progress(f"EM iteration {it}: LL {log['log_likelihood']:.6f}, R_E {log['r_e']}, "
+                 f"E {t['estep_forward_ms'] + t['estep_traceback_ms']:.0f} ms "
+                 f"(structure {sp['structure_ms']:.0f} in {sp['structure_passes']}, values {sp['values_ms']:.0f} in "
+                 f"{sp['value_passes']}), M {t['mstep_ms'] if go or force_m else 0:.0f} ms, step {wall * 1e3:.0f} ms"
+                 + ("" if go or force_m else "  [chain stops]"))
+        return dict(iteration=it, go=bool(go), wall_ms=wall * 1e3, ll=log["log_likelihood"], H=log["n_samples"],
+                    r_e=log["r_e"], r_m=log["r_m"] if go or force_m else 0, P=log["n_patterns"],
+                    estep_ms=t["estep_forward_ms"] + t["estep_traceback_ms"], struct_ms=sp["structure_ms"],
+                    values_ms=sp["values_ms"], fallback_ms=sp["fallback_ms"], n_fallback=sp["n_fallback"],
+                    struct_passes=sp["structure_passes"], value_passes=sp["value_passes"],
+                    tb_ms=t["estep_traceback_ms"], mstep_ms=t["mstep_ms"] if go or force_m else 0.0)
 
-    warm = [em_step() for _ in range(args.warmup)]
-    m.clear_samples()
-    m.find_patterns()  # back to M0 so the timed chain is E1+M1, E2+M2, ...
-    chain.update(it=0, old_ll=-float("inf"))
+    for _ in range(args.warmup):
+        em_step()
+    m.em_rewind()  # the timed region starts a fresh chain at E1
+    chain.update(it=0, old_ll=-DBL_MAX, ended=False)
 
     barrier()
     t0 = time.perf_counter()
@@ -186,6 +250,35 @@ def main():
     elapsed = max_over_ranks(time.perf_counter() - t0)
     ms_per_step = elapsed / args.steps * 1e3
     value = N * L / (elapsed / args.steps)
+
+    # whole chains inside the timed region (per-step walls are this rank's;
+    # every step ends in a collective, so ranks stay in step)
+    chains, cur = [], []
+    for s in steps:
+        cur.append(s)
+        if not s["go"]:
+            chains.append(cur)
+            cur = []
+    chain_iters = sum(len(c) for c in chains)
+    chain_s = max_over_ranks(sum(s["wall_ms"] for c in chains for s in c) / 1e3)
+    value_chain = N * L * chain_iters / chain_s if chain_iters else None
+
+    # steady leg (not the headline): a fresh chain to its end, then forced iterations
+    steady = None
+    if args.steady_steps > 0:
+        m.em_rewind()
+        chain.update(it=0, old_ll=-DBL_MAX, ended=False)
+        while True:
+            s = em_step(force_m=True)
+            if not s["go"]:
+                break
+        barrier()
+        t1 = time.perf_counter()
+        st = [em_step(force_m=True) for _ in range(args.steady_steps)]
+        barrier()
+        el = max_over_ranks(time.perf_counter() - t1)
+        steady = {"value": N * L / (el / args.steady_steps), "ms_per_step": el / args.steady_steps * 1e3,
+                  "iterations": [s["iteration"] for s in st]}
 
     # Roofline of the dominant kernel, the E-step value pass (estep_values):
     # SURVEY.md §8d prices the E-step at 8 B per retained k-best link (R_E); the
@@ -221,7 +314,8 @@ def main():
                     f"missing={args.missing}, seed={args.seed}), generated in-process",
             "config": {
                 "workload": f"{args.tag}: {N} individuals x {L} SNP loci, {args.A} alleles/locus; "
-                            f"step = one EM iteration (E_k, accept, HaploComp, M_k) from the genotype-mined model M0",
+                            f"step = one iteration of the reference's converged EM chain from M0 "
+                            f"(E_k, accept, HaploComp, M_k while continuing; restart from M0 after the stop)",
                 "individuals": N, "loci": L, "sample_size": args.sample_size,
                 "min_freq_abs": 1.5, "pattern_len": [1, 30],
                 "parallelism": f"individual-sharded x{world}, " + ("ordered RCCL reduction (chained broadcasts)" if args.reduction == "ordered"
@@ -229,6 +323,10 @@ def main():
                                + (" [REHEARSAL: gloo host collective, ranks sharing GPUs - not a measurement]"
                                   if world > 1 and args.collective == "host" else ""),
             },
+            "value_chain": value_chain,
+            "chain": {"iterations": [len(c) for c in chains],
+                      "ms_per_iteration": chain_s / chain_iters * 1e3 if chain_iters else None},
+            "value_steady": steady,
             "roofline": {
                 "bound": "hbm", "kernel": "estep_values",
                 "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
@@ -246,6 +344,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "m0": {"seconds": t_m0, "patterns": P0, "r_m": rm0},
+            "library": ident,
             "per_step": [{k: (round(v, 6) if isinstance(v, float) else v) for k, v in s.items()} for s in steps],
         }
         print(json.dumps(line), flush=True)
@@ -256,7 +355,7 @@ def main():
 
 def pmc_summary(tag):
     """rocprofv3 PMC summary (HBM bytes per estep_values launch) of this
-    workload, committed under profiles/r02/ by tools/profile_round.sh; None
+    workload, committed under profiles/r03/ by tools/profile_round.sh; None
     when this configuration has not been profiled."""
     p = os.path.join(PMC_DIR, f"pmc_estep_values_{tag}.json")
     try:
@@ -269,36 +368,57 @@ def pmc_summary(tag):
 
 
 def cpu_baseline(m, panel, args):
-    """Time the CPU restatement (oracle/, 1 thread) on a bounded sample of EM
-    iteration 2 of the same chain: E_2 over the first `cpu_indiv` individuals
-    with the M1 model (scaled to all individuals) + M_2 over `cpu_roots` start
-    loci (each root's DFS subtree is independent, PatternManager.cpp:94-97;
-    scaled to all L roots).  The GPU supplies M1 and the E_2 samples, which are
-    bit-identical to the restatement's (tests/test_gpu_parity.py)."""
+    """Time the CPU restatement (oracle/, 1 thread) on bounded, stratified
+    samples of the same converged chain: each E_k over a sample of individuals
+    spread evenly over the E-step's own cost order (heterozygous-or-missing
+    loci, heaviest first), each M_k over start loci spread evenly over [0, L)
+    (each root's DFS subtree is independent, PatternManager.cpp:94-97), with
+    the GPU's model and samples of that step (bit-identical to the
+    restatement's, tests/test_gpu_parity.py).  Every sample is scaled to the
+    whole panel; t_iter = the chain's scaled time / its iterations."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: timed as the baseline, never as the product
 
-    m.resolve_all()  # E1
-    m.find_patterns()  # M1
-    pt = m.patterns(maxlen=30)
+    N, L = panel.N, panel.L
+    a = panel.alleles
+    het = ((a[:, 0, :] != a[:, 1, :]) | (a[:, 0, :] < 0)).sum(axis=1)
+    order = np.argsort(-het, kind="stable")
+
+    def strat_indiv(k):
+        k = max(1, min(k, N))
+        return np.sort(order[(np.arange(k) * N) // k + N // (2 * k)])
+
+    kr = max(1, min(args.cpu_roots, L))
+    roots = (np.arange(kr) * L) // kr + L // (2 * kr)
     o = oracle.Oracle(panel.alleles, panel.types, sample_size=args.sample_size)
-    o.set_patterns(pt)
-    del pt
-    ns = min(args.cpu_indiv, panel.N)
-    t_e = o.time_resolve_range(0, ns)
-    ll, H, re = m.resolve_all()  # E2 samples on the GPU
-    al, w, _ = m.samples(H)
-    o.set_samples(al, w)
-    del al
-    k = args.cpu_roots or max(1, panel.L // 40)
-    t_m = o.time_find_patterns_roots(panel.L - k, panel.L)
-    t_iter = t_e * panel.N / ns + t_m * panel.L / k
+    old_ll, it, parts = -DBL_MAX, 1, []
+    while True:
+        pt = m.patterns(maxlen=30)
+        o.set_patterns(pt)
+        del pt
+        ids = strat_indiv(args.cpu_indiv_e1 if it == 1 else args.cpu_indiv)
+        te = o.time_resolve_list(ids)
+        parts.append({"step": f"E{it}", "sample": len(ids), "seconds": te, "scale": N / len(ids)})
+        ll, H, _ = m.resolve_all()  # the same E-step on the GPU (its samples feed the next M-step)
+        go = ll >= old_ll and (old_ll - ll) / old_ll > 1e-4  # HaploModel.cpp:139
+        if not go:
+            break
+        al, w, _ = m.samples(H)
+        o.set_samples(al, w)
+        del al
+        tm = o.time_find_patterns_root_list(roots)
+        parts.append({"step": f"M{it}", "sample": int(kr), "seconds": tm, "scale": L / kr})
+        m.find_patterns()
+        old_ll, it = ll, it + 1
+    t_chain = sum(p["seconds"] * p["scale"] for p in parts)
+    t_iter = t_chain / it
     return {
-        "value": panel.N * panel.L / t_iter, "unit": "individual·loci/s", "cores": 1, "kind": "port",
-        "sample": f"EM iteration 2: E_2 over {ns}/{panel.N} individuals (scaled x{panel.N / ns:g}) + M_2 over "
-                  f"start loci [{panel.L - k}, {panel.L}) of {panel.L} (scaled x{panel.L / k:g}), "
+        "value": N * L / t_iter, "unit": "individual·loci/s", "cores": 1, "kind": "port",
+        "sample": f"converged chain of {it} EM iterations ({', '.join(p['step'] for p in parts)}): E_1 over "
+                  f"{min(args.cpu_indiv_e1, N)} and E_k over {min(args.cpu_indiv, N)} individuals spread over the "
+                  f"cost order, M_k over {kr} start loci spread over [0, {L}), each scaled to the panel; "
                   f"oracle/hmc_oracle.cpp g++ -O2, 1 thread",
-        "t_estep_sample_s": t_e, "t_mstep_sample_s": t_m, "t_iter_s": t_iter,
+        "parts": parts, "t_iter_s": t_iter, "sample_seconds": sum(p["seconds"] for p in parts),
     }
 
 

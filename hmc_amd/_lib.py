@@ -92,6 +92,10 @@ _SIGS = [
     ("hmc_write_phase", _i, [_vp, _cp]),
     ("hmc_set_tuning", _i, [_vp, _i, _u64, _i]),
     ("hmc_set_estep_shape", _i, [_vp, _i, _i]),
+    ("hmc_set_pass_shapes", _i, [_vp, _i, _i, _i]),
+    ("hmc_model_save", _i, [_vp]),
+    ("hmc_em_rewind", _i, [_vp]),
+    ("hmc_build_info", _cp, []),
     ("hmc_last_timings", _i, [_vp, _P(_d), _P(_d), _P(_d)]),
     ("hmc_test_nth_element", None, [_P(_d), _P(C.c_uint32), _i, _i]),
     ("hmc_test_sort_small", None, [_P(_d), _P(C.c_uint32), _i]),
@@ -102,6 +106,18 @@ _SIGS = [
 ]
 
 EXPORTED = [s[0] for s in _SIGS]
+
+
+def lib_identity() -> dict:
+    """Which libhmc_amd.so this process loaded: path, SHA-256 prefix of the
+    file and the library's own build string."""
+    import hashlib
+
+    L = lib()
+    with open(LIB_PATH, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    return {"path": os.path.relpath(LIB_PATH, os.path.dirname(_HERE)), "sha256_16": sha,
+            "build": L.hmc_build_info().decode()}
 
 
 def lib():

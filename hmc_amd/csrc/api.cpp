@@ -262,13 +262,18 @@ struct Ctx {
   FileData file_meta;     // ids / marker names / positions of the last hmc_load_file
   int min_len = 1, max_len = 30, sample_size = 10;
   // tuning
-  int fcap = 2048, waves = 0;
+  static constexpr int FCAP_INIT = 2048, FCAP_BIG = 16384;
+  int fcap = FCAP_INIT, fcap_user = FCAP_INIT, waves = 0;
+  bool fcap_user_set = false;  // hmc_set_tuning gave a frontier capacity: no automatic start capacity
   int lds_waves_per_cu = 8;  // E-step individuals (blocks) sharing one CU's 160 KiB LDS
   int estep_nw = 2;          // E-step waves per individual (shape sweep at cfg 3: 2:8 beats 3:4 by 25%)
   // value-pass shape (waves per individual : individuals per CU), 0 = by group
-  // size: 1:16 when the group fills 12 individuals per CU (cfg 3 E2: 9% faster
-  // than 2:8), else 2:8 (more segments per individual for small groups)
-  int vp_nw = 0, vp_ipc = 0;
+  // size (estep_split: 1:20 from 32 individuals per CU, 2:8 from 8, else 3:8);
+  // structure-pass individuals per CU, 0 = by group size (12 / 8 / 4)
+  int vp_nw = 0, vp_ipc = 0, s1_ipc = 0;
+  // diagnostics only (stderr logging, never a change of what runs): read once
+  // at context creation from HMC_DEBUG_MEM / HMC_DIAG_MINE
+  bool debug_mem = false, diag_mine = false;
   bool value_fast = false;   // value-only k-best lists first, the exact pass for ties only (hmc_set_value_mode)
   uint64_t trace_bytes = 0;
 
@@ -301,6 +306,14 @@ struct Ctx {
   DevBuf<uint8_t> t_last;
   DevBuf<uint32_t> t_succ, d_head_ids, d_head_pat0;
   int n_head = 0;
+  // Table generations: every new table gets a new number; the candidate tree
+  // (n_* arrays: the allele strings of a mined table) belongs to tree_gen.
+  uint64_t model_gen = 0, tree_gen = ~0ull, next_gen = 0;
+  bool tree_ok() const { return node_cap > 0 && tree_gen == model_gen; }
+  void new_table(bool with_tree) {
+    model_gen = ++next_gen;
+    if (with_tree) tree_gen = model_gen;
+  }
 
   // mining state
   DevBuf<int32_t> n_parent, n_start, n_child_base, n_link;
@@ -691,7 +704,7 @@ struct Ctx {
         (e = hipMemcpyAsync(su.data(), t_succ.p, su.size() * 4, hipMemcpyDeviceToHost, this->st)) ||
         (e = hipStreamSynchronize(this->st)))
       return hipfail(e, "exact: table");
-    if (node_cap == 0) return fail(HMC_EUNSUPPORTED, "exact M-step needs a mined or estimated table (allele strings)");
+    if (!tree_ok()) return fail(HMC_EUNSUPPORTED, "exact M-step needs a mined or estimated table (allele strings)");
     int nmax = 0;
     for (int i = 0; i < P; ++i) nmax = std::max(nmax, node[i] + 1);
     std::vector<int32_t> par(nmax);
@@ -794,7 +807,7 @@ struct Ctx {
     }
     ++exact_rounds;
     exact_candidates += nc;
-    if (getenv("HMC_DEBUG_MEM")) fprintf(stderr, "[hmc] exact round %d: %zu candidates\n", exact_rounds, nc);
+    if (debug_mem) fprintf(stderr, "[hmc] exact round %d: %zu candidates\n", exact_rounds, nc);
     return HMC_OK;
   }
   size_t xacc_nc = 0;
@@ -948,6 +961,7 @@ struct Ctx {
     ht_succ = succ;
     table_on_host = true;
     have_model = true;
+    new_table(false);
     return HMC_OK;
   }
 
@@ -1109,7 +1123,6 @@ struct Ctx {
       a.max_len = mxl;
       a.lin_idx = level == 1 ? nullptr : l_idx[cur].p;
       a.lin_val = level == 1 ? nullptr : l_val[cur].p;
-      static const bool diag_mine = getenv("HMC_DIAG_MINE") != nullptr;
       hipEvent_t dm0 = nullptr, dm1 = nullptr;
       if (diag_mine) {
         hipEventCreate(&dm0);
@@ -1248,7 +1261,7 @@ struct Ctx {
       if (l_idx[k].n * 4 > (4ull << 30)) l_idx[k].release();
       if (l_val[k].n * 8 > (4ull << 30)) l_val[k].release();
     }
-    if (getenv("HMC_DEBUG_MEM")) {
+    if (debug_mem) {
       size_t fb = 0, tb = 0;
       hipMemGetInfo(&fb, &tb);
       fprintf(stderr, "[hmc] after mining: free %.1f GB of %.1f; nodes %.1f GB\n", fb / 1e9, tb / 1e9,
@@ -1261,6 +1274,7 @@ struct Ctx {
     hipEventElapsedTime(&ms, ev[4], ev[5]);
     ms_m = ms;
     have_model = true;
+    new_table(true);
     (void)ntot;
     if (P_out) *P_out = P;
     if (rm_out) *rm_out = rm;
@@ -1593,6 +1607,11 @@ struct Ctx {
     size_t freeb = 0, totb = 0;
     hipMemGetInfo(&freeb, &totb);
     const double avail = (double)freeb + (double)d_trace.n * 4 + (double)d_rec.n * 4;
+    // Frontier capacity of the structure pass: a frontier past it restarts the
+    // E-step with twice the capacity (cfg 3's E1 on the M0 model needs 2^14:
+    // three restarts from 2^11, ~0.6 s).  With HBM to spare, start there: the
+    // pass's per-block scratch is ~190 B per state (3 GB per 1 000 blocks).
+    if (!fcap_user_set && fcap < FCAP_BIG && avail > 96e9) fcap = FCAP_BIG;
     // (cfg 3's E1 with the M0 model needs ~2x HBM in records + traces; larger
     // stores (fewer groups) measured no faster and crowd out the next M0.  The
     // trace cap keeps cfg 3's E2.. (~90 GB of traces) in one value pass.)
@@ -1600,7 +1619,7 @@ struct Ctx {
                                       1ull << 20) / 4;
     rec_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.28), 80ull << 30),
                                     1ull << 20) / 4;
-    if (getenv("HMC_DEBUG_MEM"))
+    if (debug_mem)
       fprintf(stderr, "[hmc] E-step: free %.1f GB, stores %.1f + %.1f GB, budgets trace %.1f rec %.1f GB\n",
               freeb / 1e9, d_trace.n * 4 / 1e9, d_rec.n * 4 / 1e9, trace_budget * 4 / 1e9, rec_budget * 4 / 1e9);
     h_total.assign(n, 0.0);
@@ -1750,7 +1769,9 @@ struct Ctx {
     a.cost = d_cost.p;
     a.stamps = d_stamps.p;
     a.diag_indiv = -1;
+#ifdef HMC_STAMPS  // diagnostic build only: stamp one batch index
     if (const char *di = getenv("HMC_DIAG_INDIV")) a.diag_indiv = atoi(di);
+#endif
     return a;
   }
 
@@ -1880,6 +1901,7 @@ struct Ctx {
     float ms = 0;
     std::vector<int32_t> pending(order), sset, rest;
     std::vector<unsigned long long> rneed(n, 0), tneed(n, 0), base(n, 0), rsz(n, 0);
+    std::vector<int32_t> fbig(n, 0);  // largest frontier of each individual (structure pass)
     // Every individual gets its own record region: its exact size once a pass
     // has measured it (`exact_need`), else an estimate — the previous E-step's
     // size when the model is of the same scale, or the records-per-cost ratio
@@ -1902,12 +1924,10 @@ struct Ctx {
         int k = 0;
         // the first pass spans the whole cost range and later estimates use the
         // measured individuals nearest in cost (cfg 3 E1 after E5: 7.1 -> 5.9 s,
-        // deferred 1 713 -> 12 per group, profiles/r02/e1_groups/);
-        // HMC_EST_HEAVIEST=1 restores the heaviest-first sample and one ratio
-        static const bool strat = getenv("HMC_EST_HEAVIEST") == nullptr;
-        if (!have_est) {  // nothing measured yet: the heaviest 4 per CU share the store evenly
+        // deferred 1 713 -> 12 per group, profiles/r02/e1_groups/)
+        if (!have_est) {  // nothing measured yet: 4 per CU share the store evenly
           k = std::min(np, 4 * dev_cu);
-          if (strat && np > k) {  // every np/k-th of the heaviest-first list
+          if (np > k) {  // every np/k-th of the heaviest-first list
             std::vector<int32_t> pick, other;
             pick.reserve(k);
             other.reserve(np - k);
@@ -1968,8 +1988,7 @@ struct Ctx {
       // structure pass: one wave per individual; 12 per CU (3 per SIMD at 145
       // VGPRs) above 8 per CU, so cfg 3's E1 groups of 2 200-2 700 run in one
       // round (profiles/r02/e1_groups/: 603-658 -> 484-586 ms per group)
-      int bpc1 = np > 8 * dev_cu ? 12 : (np > 4 * dev_cu ? 8 : 4);
-      if (const char *env = getenv("HMC_S1_BPC")) bpc1 = std::max(1, atoi(env));  // tuning experiments
+      const int bpc1 = s1_ipc > 0 ? s1_ipc : (np > 8 * dev_cu ? 12 : (np > 4 * dev_cu ? 8 : 4));
       const int grid1 = std::max(1, std::min(np, dev_cu * bpc1));
       const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1);
       if ((e = d_scr1.ensure(per1 * grid1)) || (e = d_rec_off.ensure((size_t)n * (L + 1))) ||
@@ -2008,13 +2027,14 @@ struct Ctx {
       if ((e = launch_estep_structure(s1, grid1, st))) return hipfail(e, "estep_structure launch");
       hipEventRecord(ev[1], st);
       if ((e = hipMemcpyAsync(rneed.data(), d_rneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
-          (e = hipMemcpyAsync(tneed.data(), d_tneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)))
+          (e = hipMemcpyAsync(tneed.data(), d_tneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
+          (e = hipMemcpyAsync(fbig.data(), s1.fmax, (size_t)n * 4, hipMemcpyDeviceToHost, st)))
         return hipfail(e, "estep_structure");
       if ((rc = read_status(pending, np, false, dstatus))) return rc;
       hipEventElapsedTime(&ms, ev[0], ev[1]);
       ms_s1 += ms;
       ++n_struct_passes;
-      if (getenv("HMC_DEBUG_MEM")) {
+      if (debug_mem) {
         int ndef = 0;
         uint64_t rsum = 0, rmax = 0, tsum = 0, rres = 0;
         for (int q = 0; q < np; ++q) {
@@ -2063,11 +2083,9 @@ struct Ctx {
         if (!have_est || deferred * 10 > np) {
           const double ratio = cs > 0 ? rs_ / cs : 0.0;
           std::vector<std::pair<int, double>> cr;  // (cost, records per cost) of the measured
-          if (getenv("HMC_EST_HEAVIEST") == nullptr) {
-            for (int i = 0; i < n; ++i)
-              if (exact_need[i]) cr.emplace_back(std::max(1, h_cost[i]), (double)rneed[i] / std::max(1, h_cost[i]));
-            std::sort(cr.begin(), cr.end());
-          }
+          for (int i = 0; i < n; ++i)
+            if (exact_need[i]) cr.emplace_back(std::max(1, h_cost[i]), (double)rneed[i] / std::max(1, h_cost[i]));
+          std::sort(cr.begin(), cr.end());
           for (int bi : rest) {
             if (exact_need[bi]) continue;
             const int c = std::max(1, h_cost[bi]);
@@ -2114,28 +2132,24 @@ struct Ctx {
           pos += k;
           continue;
         }
-        int vnw = vp_nw, vipc = vp_ipc;
-        if (vnw <= 0) {
-          // by individuals per CU (cfg 3 and its rank shards, tools/shard_shapes.py,
-          // profiles/r02/shard_shapes/): 1:16 from 32 per CU (10 000: 557 vs 615 ms
-          // at 2:8), 2:8 from 8 (4 994: 290 vs 333 ms at 1:16), else 3:8 (1 239:
-          // 101 vs 112 ms at 2:8)
-          // (1:20 runs the 5-waves-per-SIMD build: 505-514 vs 535-558 ms at
-          // 1:16 for cfg 3's E3, profiles/r02/values_ab/)
-          vnw = (int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3);
-          vipc = vnw == 1 ? 20 : 8;
-          static const char *vp_env = getenv("HMC_VP_SHAPE");  // tuning experiments: "nw:ipc"
-          int a0 = 0, a1 = 0;
-          if (vp_env && sscanf(vp_env, "%d:%d", &a0, &a1) == 2 && a0 >= 1 && a0 <= 4 && a1 >= 1) {
-            vnw = a0;
-            vipc = a1;
-          }
-        }
+        // by individuals per CU (cfg 3 and its rank shards, tools/shard_shapes.py,
+        // profiles/r02/shard_shapes/): 1:16 from 32 per CU (10 000: 557 vs 615 ms
+        // at 2:8), 2:8 from 8 (4 994: 290 vs 333 ms at 1:16), else 3:8 (1 239:
+        // 101 vs 112 ms at 2:8)
+        // (1:20 runs the 5-waves-per-SIMD build: 505-514 vs 535-558 ms at
+        // 1:16 for cfg 3's E3, profiles/r02/values_ab/)
+        int vnw = vp_nw > 0 ? vp_nw : ((int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3));
+        int vipc = vp_ipc > 0 ? vp_ipc : (vnw == 1 ? 20 : 8);  // a half-given shape completes by the same rule
         const int G2 = std::max(1, std::min(waves > 0 ? waves : dev_cu * vipc, n));
         const int grid2 = std::max(1, std::min<int>(G2, (int)k));
         // register budget: 5 waves per SIMD once the shape asks for more than 16 per CU
         const int vwpe = vnw * vipc > 16 && vnw * vipc <= 20 ? 5 : 4;
-        const size_t per2 = estep_s2_scratch_bytes(fcap, S);
+        // the HBM tier of the value frontiers holds the group's largest
+        // frontier (pass 1 measured it), not the structure pass's capacity
+        int fgrp = 1;
+        for (size_t q = 0; q < k; ++q) fgrp = std::max(fgrp, (int)fbig[sset[pos + q]]);
+        fgrp = std::min(fcap, (fgrp + 63) & ~63);
+        const size_t per2 = estep_s2_scratch_bytes(fgrp, S);
         if ((e = d_scr2.ensure(per2 * grid2))) return hipfail(e, "estep pass-2 scratch");
         ValueArgs v;
         v.S = S;
@@ -2147,7 +2161,7 @@ struct Ctx {
         v.rec_off = d_rec_off.p;
         v.scratch = d_scr2.p;
         v.scratch_stride = per2;
-        v.fcap = fcap;
+        v.fcap = fgrp;
         v.lds_fc = s2_tier(S, vnw, vipc);
         v.trace = d_trace.p;
         v.trace_cap = d_trace.n;
@@ -2174,7 +2188,7 @@ struct Ctx {
         hipEventElapsedTime(&ms, ev[0], ev[1]);
         ms_s2 += ms;
         ++n_value_passes;
-        if (getenv("HMC_DEBUG_MEM"))
+        if (debug_mem)
           fprintf(stderr, "[hmc] value pass %d: %zu individuals, %.1f ms\n", n_value_passes, k, ms);
         // ---- ties: individuals whose result would depend on the libstdc++ list
         // order re-run on the exact value pass, in their own trace regions
@@ -2334,8 +2348,7 @@ struct Ctx {
     const int budget = 160 * 1024 / std::max(1, lds_waves_per_cu) - 256;
     fc = 0;
     hc = 64;
-    int kf = lds_key_factor;
-    if (const char *env = getenv("HMC_KEY_FACTOR")) kf = std::max(1, atoi(env));  // tuning experiments
+    const int kf = lds_key_factor;
     for (int f = 4096; f >= 0; f -= 4) {
       const int h = next_pow2(std::max(64, kf * f));
       if ((int)estep_lds_bytes(S, f, h, estep_nw) <= budget) { fc = f; hc = h; return; }
@@ -2514,6 +2527,96 @@ struct Ctx {
     return HMC_OK;
   }
 
+  // ------------------------------------------------------- model snapshot --
+  // A device copy of one pattern table (hmc_model_save) and the rewind of the
+  // EM to the state right after the M-step that built it (hmc_em_rewind):
+  // HaploModel::run after build() (HaploModel.cpp:121-129) — no samples,
+  // resolutions = the input genotypes, nothing learned from earlier E-steps
+  // (scheduling costs, store-size estimates, frontier capacity).  Lets a host
+  // run the reference's converged chain from M0 repeatedly without mining M0
+  // again (bench.py).
+  struct Snap {
+    bool valid = false, table_on_host = false;
+    int P = 0, head_len = 1, n_head = 0;
+    uint64_t gen = 0;
+    DevBuf<int32_t> start, len, node;
+    DevBuf<double> freq, prefix, tp;
+    DevBuf<uint8_t> last, head_al;
+    DevBuf<uint32_t> succ, head_ids, head_pat0;
+    std::vector<uint32_t> h_head_ids;
+    std::vector<uint8_t> h_head_al;
+    Cands ht;
+    std::vector<int32_t> ht_succ;
+  } snap;
+
+  template <class T>
+  hipError_t dcopy(DevBuf<T> &dst, const DevBuf<T> &src, size_t n) {
+    if (n == 0 || !src.p) return hipSuccess;
+    hipError_t e = dst.ensure(n);
+    if (e) return e;
+    return hipMemcpyAsync(dst.p, src.p, n * sizeof(T), hipMemcpyDeviceToDevice, st);
+  }
+  int model_save() {
+    if (!have_model) return fail(HMC_EARG, "no pattern model to save");
+    const size_t p = (size_t)std::max(P, 1), A = (size_t)pan.amax;
+    hipError_t e;
+    if ((e = dcopy(snap.start, t_start, p)) || (e = dcopy(snap.len, t_len, p)) || (e = dcopy(snap.node, t_node, p)) ||
+        (e = dcopy(snap.freq, t_freq, p)) || (e = dcopy(snap.prefix, t_prefix, p)) || (e = dcopy(snap.tp, t_tp, p)) ||
+        (e = dcopy(snap.last, t_last, p)) || (e = dcopy(snap.succ, t_succ, p * A)) ||
+        (e = dcopy(snap.head_ids, d_head_ids, std::max<size_t>(n_head, 1))) ||
+        (e = dcopy(snap.head_pat0, d_head_pat0, A + 1)) ||
+        (head_len > 1 && (e = dcopy(snap.head_al, d_head_al, p * head_len))) || (e = hipStreamSynchronize(st)))
+      return hipfail(e, "model_save");
+    snap.P = P;
+    snap.head_len = head_len;
+    snap.n_head = n_head;
+    snap.gen = model_gen;
+    snap.h_head_ids = h_head_ids;
+    snap.h_head_al = h_head_al;
+    snap.table_on_host = table_on_host;
+    if (table_on_host) {
+      snap.ht = ht;
+      snap.ht_succ = ht_succ;
+    }
+    snap.valid = true;
+    return HMC_OK;
+  }
+  int em_rewind() {
+    if (!snap.valid) return fail(HMC_EARG, "no saved model (hmc_model_save)");
+    const size_t p = (size_t)std::max(snap.P, 1), A = (size_t)pan.amax;
+    hipError_t e;
+    if ((e = dcopy(t_start, snap.start, p)) || (e = dcopy(t_len, snap.len, p)) || (e = dcopy(t_node, snap.node, p)) ||
+        (e = dcopy(t_freq, snap.freq, p)) || (e = dcopy(t_prefix, snap.prefix, p)) || (e = dcopy(t_tp, snap.tp, p)) ||
+        (e = dcopy(t_last, snap.last, p)) || (e = dcopy(t_succ, snap.succ, p * A)) ||
+        (e = dcopy(d_head_ids, snap.head_ids, std::max<size_t>(snap.n_head, 1))) ||
+        (e = dcopy(d_head_pat0, snap.head_pat0, A + 1)) ||
+        (snap.head_len > 1 && (e = dcopy(d_head_al, snap.head_al, p * snap.head_len))) ||
+        (e = hipStreamSynchronize(st)))
+      return hipfail(e, "em_rewind");
+    P = snap.P;
+    head_len = snap.head_len;
+    n_head = snap.n_head;
+    model_gen = snap.gen;  // the candidate tree is valid again only if nothing was mined since
+    h_head_ids = snap.h_head_ids;
+    h_head_al = snap.h_head_al;
+    table_on_host = snap.table_on_host;
+    if (table_on_host) {
+      ht = snap.ht;
+      ht_succ = snap.ht_succ;
+    }
+    have_model = true;
+    hf_valid = false;
+    // the EM state of a fresh HaploModel::run after this M-step
+    have_samples = have_estep = have_best = best_on_host = false;
+    H = 0;
+    total_weight = 0.0;
+    h_cost.clear();
+    prev_rneed.clear();
+    prev_P = 0;
+    fcap = fcap_user;
+    return HMC_OK;
+  }
+
   int run(int max_iter, hmc_iter_log *log, int cap, int *iters, double *t_m0, uint64_t *rm0, int *np0) {
     using clk = std::chrono::steady_clock;
     have_samples = false;  // HaploModel::build -> setGenoData clears samples (HaploBuilder.cpp:19-23)
@@ -2557,6 +2660,8 @@ static int ctx_init(hmc_ctx *h, int device) {
   hipError_t e = hipSetDevice(device);
   if (e) return h->c.hipfail(e, "hipSetDevice");
   h->c.device = device;
+  h->c.debug_mem = getenv("HMC_DEBUG_MEM") != nullptr;
+  h->c.diag_mine = getenv("HMC_DIAG_MINE") != nullptr;
   if ((e = hipStreamCreateWithFlags(&h->c.st, hipStreamNonBlocking))) return h->c.hipfail(e, "hipStreamCreate");
   for (auto &ev : h->c.ev)
     if ((e = hipEventCreate(&ev))) return h->c.hipfail(e, "hipEventCreate");
@@ -2691,7 +2796,10 @@ int hmc_set_params(hmc_ctx *h, double min_freq_abs, double min_freq, int min_len
 int hmc_set_tuning(hmc_ctx *h, int frontier_cap, uint64_t trace_bytes, int waves) {
   if (!h) return HMC_EARG;
   if (waves < 0) { h->c.lds_waves_per_cu = -waves; waves = 0; }  // negative: E-step waves per CU (LDS split)
-  if (frontier_cap > 0) h->c.fcap = std::min(frontier_cap, 65535);
+  if (frontier_cap > 0) {
+    h->c.fcap = h->c.fcap_user = std::min(frontier_cap, 65535);
+    h->c.fcap_user_set = true;
+  }
   h->c.trace_bytes = trace_bytes;
   h->c.waves = waves;
   return HMC_OK;
@@ -2761,6 +2869,23 @@ int hmc_set_estep_shape(hmc_ctx *h, int waves_per_individual, int individuals_pe
   if (individuals_per_cu > 0) h->c.lds_waves_per_cu = h->c.vp_ipc = individuals_per_cu;
   if (waves_per_individual == 0 && individuals_per_cu == 0) h->c.vp_nw = h->c.vp_ipc = 0;  // value pass by group size
   return HMC_OK;
+}
+
+int hmc_set_pass_shapes(hmc_ctx *h, int structure_ipc, int value_waves, int value_ipc) {
+  if (!h || structure_ipc < 0 || structure_ipc > 32 || value_waves < 0 || value_waves > 4 || value_ipc < 0 ||
+      value_ipc > 32)
+    return HMC_EARG;
+  h->c.s1_ipc = structure_ipc;
+  h->c.vp_nw = value_waves;
+  h->c.vp_ipc = value_ipc;
+  return HMC_OK;
+}
+
+int hmc_model_save(hmc_ctx *h) { return h ? h->c.model_save() : HMC_EARG; }
+int hmc_em_rewind(hmc_ctx *h) { return h ? h->c.em_rewind() : HMC_EARG; }
+
+const char *hmc_build_info(void) {
+  return "hmc_amd 0.3 gfx950 -O3 -ffp-contract=off, built " __DATE__ " " __TIME__;
 }
 
 int hmc_load_phase(hmc_ctx *h, const char *path) {
@@ -2902,7 +3027,7 @@ int hmc_write_file(hmc_ctx *h, const char *format, const char *path, const char 
 }
 
 int hmc_write_patterns(hmc_ctx *h, const char *path) {
-  if (!h || !path || !h->c.have_model || (h->c.node_cap <= 0 && !h->c.table_on_host)) return HMC_EARG;
+  if (!h || !path || !h->c.have_model || (!h->c.tree_ok() && !h->c.table_on_host)) return HMC_EARG;
   hmc::Ctx &c = h->c;
   const int P = c.P, L = c.pan.L;
   std::vector<int32_t> st(P), ln(P);
@@ -3005,7 +3130,7 @@ int hmc_get_patterns(hmc_ctx *h, int32_t *start, int32_t *len, double *freq, dou
     // table came from the miner; else only the last allele is known.
     std::vector<int32_t> par;
     std::vector<uint8_t> al;
-    bool tree = c.node_cap > 0;
+    const bool tree = c.tree_ok();
     if (tree) {
       if ((e = hipMemcpyAsync(node.data(), c.t_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, c.st)) ||
           (e = hipStreamSynchronize(c.st)))
@@ -3072,7 +3197,7 @@ int hmc_set_patterns(hmc_ctx *h, int P, const int32_t *start, const int32_t *len
   c.table_on_host = false;
   c.h_head_ids.clear();  // head alleles unknown: the E-step supports head_len 1 only here
   c.h_head_al.clear();
-  c.node_cap = 0;  // allele strings are not known for an injected table
+  c.new_table(false);  // allele strings are not known for an injected table
   rc = c.set_heads(heads);
   if (rc) return rc;
   c.have_model = true;

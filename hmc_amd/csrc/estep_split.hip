@@ -285,7 +285,7 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
     }
     int Fp = __shfl(Fp0, 0);
     status = __shfl(st0, 0);
-    int fbig = 0;
+    int fbig = Fp;  // the head frontier counts too: the value pass sizes its HBM tier by this
     wsync();
     if (status == EST_OK) {
       const unsigned long long words = 4 + 4ull * Fp + 1 + (a.exact ? 2ull * Fp : 0ull);

@@ -109,7 +109,11 @@ __global__ __launch_bounds__(256) void exact_fb(ExactArgs a) {
       }
       __syncthreads();
     }
-    if (flag) {
+    // every thread reads the flag before any thread can reset it for the next
+    // individual (the reset sits before the barrier at the top of the loop)
+    const bool underflow = flag != 0;
+    __syncthreads();
+    if (underflow) {
       if (tid == 0) a.status[bi] = EST_NEEDS_EXACT;
       continue;
     }

@@ -162,6 +162,19 @@ class HaploModel:
         """E-step launch shape (results are identical for every shape)."""
         self._check(lib().hmc_set_estep_shape(self._h, waves_per_individual, individuals_per_cu))
 
+    def set_pass_shapes(self, structure_ipc: int = 0, value_waves: int = 0, value_ipc: int = 0):
+        """Launch shapes of the split E-step's passes (0 = automatic)."""
+        self._check(lib().hmc_set_pass_shapes(self._h, structure_ipc, value_waves, value_ipc))
+
+    def model_save(self):
+        """Keep a device copy of the current pattern table (hmc_model_save)."""
+        self._check(lib().hmc_model_save(self._h))
+
+    def em_rewind(self):
+        """Restore the saved table and the EM state right after it was built
+        (HaploModel::run after build(), HaploModel.cpp:121-129)."""
+        self._check(lib().hmc_em_rewind(self._h))
+
     def set_reduction(self, mode: str):
         """Cross-rank sums: "ordered" (default, bit-exact with one rank) or
         "allreduce" (one collective per mining level, last-bit drift)."""

@@ -196,6 +196,18 @@ int hmc_run(hmc_ctx *ctx, int max_iteration, hmc_iter_log *log, int log_cap, int
  * becomes the LL when the M-step ran. */
 int hmc_em_iteration(hmc_ctx *ctx, int iteration, int max_iteration, int always_mstep, double *old_ll,
                      hmc_iter_log *log, int *go);
+/* Model snapshot for hosts that repeat the EM from one M-step (bench.py runs
+ * the reference's converged chain from M0 again and again).  hmc_model_save
+ * keeps a device copy of the current pattern table; hmc_em_rewind restores it
+ * and returns the EM to the state HaploModel::run has right after build()
+ * (HaploModel.cpp:121-129): no samples, resolutions = the input genotypes,
+ * nothing carried over from earlier E-steps (their scheduling costs and store
+ * sizes); the next hmc_em_iteration(1, ..., *old_ll = -DBL_MAX) starts a fresh
+ * chain.  Results equal a fresh context's.  After a rewind, hmc_get_patterns
+ * spells whole allele strings only if no table was mined since the save (the
+ * candidate tree that spells them is not kept); otherwise the last allele. */
+int hmc_model_save(hmc_ctx *ctx);
+int hmc_em_rewind(hmc_ctx *ctx);
 /* HaploComp (HaploComp.cpp:29-155) of the input panel, phase as given,
  * against the accepted resolutions: switch error, incorrect-haplotype and
  * incorrect-genotype percentages over all ranks' individuals.  Replaces the
@@ -250,9 +262,16 @@ int hmc_set_tuning(hmc_ctx *ctx, int frontier_cap, uint64_t trace_bytes, int wav
 /* E-step launch shape: wavefronts cooperating on one individual (1..4,
  * default 2) and individuals sharing one CU's LDS (default 8); 0 keeps the
  * current value.  A shape set here applies to every kernel; (0, 0) returns the
- * split E-step's value pass to its automatic shape (1:16 for groups of at
- * least 12 individuals per CU, else 2:8).  Results do not depend on the shape. */
+ * split E-step's value pass to its automatic shape: 1 wave x 20 individuals per
+ * CU for groups of at least 32 individuals per CU, 2 x 8 from 8 per CU, else
+ * 3 x 8; a value-pass shape given by one number only takes the other from the
+ * same rule.  Results do not depend on the shape. */
 int hmc_set_estep_shape(hmc_ctx *ctx, int waves_per_individual, int individuals_per_cu);
+/* Launch shapes of the split E-step's two passes, 0 = automatic for each:
+ * structure pass individuals per CU (automatic: 12 above 8 per CU in the group,
+ * 8 above 4, else 4), value pass waves per individual (1..4) and individuals
+ * per CU (rule of hmc_set_estep_shape).  Results do not depend on them. */
+int hmc_set_pass_shapes(hmc_ctx *ctx, int structure_ipc, int value_waves, int value_ipc);
 /* E-step implementation: 0 (default) = two passes, a structure pass that
  * replays extendAll/addHaploPair (HaploBuilder.cpp:226-261) on pattern ids
  * and a value pass with the k-best lists, falling back to 1 for individuals
@@ -303,6 +322,13 @@ int hmc_test_coop_nth_element(int device, double *lik, uint32_t *tag, const int3
                               const int32_t *nth, int count, int total, int seg_width);
 /* Library version string. */
 const char *hmc_version(void);
+/* Version, target, flags and build time of this libhmc_amd.so (bench.py
+ * prints it with the path of the library it loaded). */
+const char *hmc_build_info(void);
+/* Environment read by the library (diagnostics only; none changes a result
+ * or what runs): HMC_DEBUG_MEM, HMC_DIAG_MINE print E-step group / mining
+ * statistics to stderr; HMC_FORCE_COLLECTIVES makes a one-rank context run
+ * its RCCL collectives anyway (test hook). */
 
 #ifdef __cplusplus
 }

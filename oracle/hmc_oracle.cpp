@@ -1472,6 +1472,44 @@ double ora_time_find_patterns_roots(void *h, int s0, int s1) {
   return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// The same two samples over explicit lists (stratified samples for the bench's
+// CPU baseline): HaploBuilder::resolve of individuals ids[0, n), and the
+// sampling M-step over the start loci roots[0, n) (ascending; each root's DFS
+// subtree is independent, PatternManager.cpp:94-97,106-108).
+double ora_time_resolve_list(void *h, const int *ids, int n) {
+  Model *m = (Model *)h;
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<ora::Candidate> out;
+  std::vector<int> resol;
+  double gp;
+  for (int q = 0; q < n; ++q) m->resolve(ids[q], out, resol, gp);
+  m->hp.clear();
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+double ora_time_find_patterns_root_list(void *h, const int *roots, int n) {
+  Model *m = (Model *)h;
+  ora::Params &pr = m->prm;
+  if (pr.min_freq_abs > 0) pr.min_freq = pr.min_freq_abs / (2.0 * m->g.N);
+  const int L = m->g.L;
+  int mxl = pr.max_len <= 0 ? L : pr.max_len, mnl = std::max(pr.min_len, 1);
+  mxl = std::max(mxl, mnl);
+  m->minlen.resize(L, mnl);
+  m->maxlen.resize(L, mxl);
+  auto t0 = std::chrono::steady_clock::now();
+  m->P.clear();
+  m->min_freq = pr.min_freq;
+  std::vector<ora::Model::Cand *> stack;
+  for (int q = 0; q < n; ++q) {
+    if (roots[q] < 0 || roots[q] >= L) continue;
+    auto *c = new ora::Model::Cand;
+    c->p.start = c->p.end = roots[q];
+    stack.push_back(c);
+  }
+  m->searchPattern(stack, false);
+  m->initialize();
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 // HaploModel::resolveAll restricted to individuals [i0, i1) (the shard one
 // rank of the sharded E-step owns); samples/results cover only that range.
 double ora_resolve_range(void *h, int i0, int i1) {

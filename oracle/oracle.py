@@ -86,6 +86,10 @@ def lib():
         L.ora_time_find_patterns.argtypes = [vp]
         L.ora_time_find_patterns_roots.restype = d
         L.ora_time_find_patterns_roots.argtypes = [vp, i, i]
+        L.ora_time_resolve_list.restype = d
+        L.ora_time_resolve_list.argtypes = [vp, P(i), i]
+        L.ora_time_find_patterns_root_list.restype = d
+        L.ora_time_find_patterns_root_list.argtypes = [vp, P(i), i]
         L.ora_resolve_range.restype = d
         L.ora_resolve_range.argtypes = [vp, i, i]
         _lib = L
@@ -183,6 +187,16 @@ class Oracle:
     def time_find_patterns_roots(self, s0: int, s1: int) -> float:
         """Seconds of searchPattern + initialize over the start loci [s0, s1)."""
         return lib().ora_time_find_patterns_roots(self.h, s0, s1)
+
+    def time_resolve_list(self, ids) -> float:
+        """Seconds of HaploBuilder::resolve over the listed individuals."""
+        a = np.ascontiguousarray(ids, np.int32)
+        return lib().ora_time_resolve_list(self.h, _p(a, C.c_int), len(a))
+
+    def time_find_patterns_root_list(self, roots) -> float:
+        """Seconds of searchPattern + initialize over the listed start loci."""
+        a = np.ascontiguousarray(sorted(roots), np.int32)
+        return lib().ora_time_find_patterns_root_list(self.h, _p(a, C.c_int), len(a))
 
     def resolve_range(self, i0: int, i1: int) -> float:
         return lib().ora_resolve_range(self.h, i0, i1)

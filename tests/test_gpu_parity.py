@@ -288,6 +288,56 @@ def test_em_iteration_drives_the_same_chain(oracle_mod, name):
     assert np.array_equal(best, r["resolutions"])
 
 
+@pytest.mark.parametrize("name", ["n60", "miss2"])
+def test_em_rewind_repeats_the_chain(oracle_mod, name):
+    """hmc_model_save after M0 + hmc_em_rewind (bench.py's restart of the
+    converged chain): the chain run after a rewind — after a whole first chain
+    and extra forced iterations — is the restatement's HaploModel::run chain
+    again (LL, R_E, R_M, HaploComp, accepted pairs), and get_patterns returns
+    M0's table again."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10, max_iter=30)
+    r = o.run()
+    m = gpu_model(p)
+    m.find_patterns()
+    m.model_save()
+    pt0 = m.patterns(maxlen=30)
+
+    def chain(extra=0):
+        old, logs = -np.finfo(np.float64).max, []
+        for it in range(1, 31):
+            log, old, go = m.em_iteration(it, old, always_mstep=False, max_iteration=30)
+            logs.append(log)
+            if not go:
+                break
+        for it in range(extra):  # forced iterations past the stop (the bench's steady leg)
+            m.em_iteration(len(logs) + 1 + it, old, always_mstep=True)
+        return logs
+
+    first = chain(extra=2)
+    m.em_rewind()
+    pt = m.patterns(maxlen=30)
+    for k in pt0:
+        if k != "alleles":
+            np.testing.assert_array_equal(pt[k], pt0[k])
+    # later M-steps replaced the candidate tree that spelled M0's allele
+    # strings: only each pattern's last allele is known after the rewind
+    last = pt0["alleles"][np.arange(len(pt0["len"])), pt0["len"] - 1]
+    np.testing.assert_array_equal(pt["alleles"][np.arange(len(pt["len"])), pt["len"] - 1], last)
+    again = chain()
+    for logs in (first, again):
+        assert [x["log_likelihood"] for x in logs] == r["ll"].tolist()
+        assert [x["r_e"] for x in logs] == r["R_E"].tolist()
+        for k in range(r["iterations"] - 1):
+            assert logs[k]["r_m"] == r["R_M"][k + 1]
+        np.testing.assert_array_equal(np.array([(x["switch_error"], x["ihp"], x["igp"]) for x in logs]),
+                                      r["haplocomp"])
+    best = np.zeros((p.N, 2, p.L), np.int32)
+    assert hmc_amd.lib().hmc_get_best_resolutions(m._h, best.ctypes.data_as(__import__("ctypes").POINTER(
+        __import__("ctypes").c_int32))) == 0
+    assert np.array_equal(best, r["resolutions"])
+
+
 @pytest.mark.parametrize("name,model,order,min_len", [
     ("n60", "MC", 1, 1), ("a3miss5", "MC", 1, 1), ("n60", "MC", 2, 1), ("a4", "MC", 1, 1),
     ("miss2", "MA", 1, 1), ("n60", "MV", 1, 2), ("a3miss5", "MV", 1, 3)])
