@@ -134,7 +134,7 @@ struct Panel {
         }
       for (auto &kv : cnt) sym[k].push_back({kv.first, kv.second / tot});
       if ((int)sym[k].size() > A_MAX) {
-        err = "locus " + std::to_string(k) + " has more than 32 alleles";
+        err = "locus " + std::to_string(k) + " has more than " + std::to_string(A_MAX) + " alleles";
         return false;
       }
       amax = std::max(amax, (int)sym[k].size());
@@ -275,7 +275,7 @@ struct Ctx {
   // at context creation from HMC_DEBUG_MEM / HMC_DIAG_MINE
   bool debug_mem = false, diag_mine = false;
   bool value_fast = false;   // value-only k-best lists first, the exact pass for ties only (hmc_set_value_mode)
-  uint64_t trace_bytes = 0;
+  uint64_t trace_bytes = 0, rec_bytes = 0;  // E-step store budgets (0 = automatic)
 
   Panel pan;
   bool have_panel = false;
@@ -301,7 +301,7 @@ struct Ctx {
   DevBuf<int32_t> d_hf_status;
   bool hf_valid = false;
   bool have_model = false;
-  DevBuf<int32_t> t_start, t_len, t_node;
+  DevBuf<int32_t> t_start, t_len, t_node, t_ppat;
   DevBuf<double> t_freq, t_prefix, t_tp;
   DevBuf<uint8_t> t_last;
   DevBuf<uint32_t> t_succ, d_head_ids, d_head_pat0;
@@ -309,7 +309,7 @@ struct Ctx {
   // Table generations: every new table gets a new number; the candidate tree
   // (n_* arrays: the allele strings of a mined table) belongs to tree_gen.
   uint64_t model_gen = 0, tree_gen = ~0ull, next_gen = 0;
-  bool tree_ok() const { return node_cap > 0 && tree_gen == model_gen; }
+  bool tree_ok() const { return node_cap > 0 && tree_gen == model_gen && tree_complete; }
   void new_table(bool with_tree) {
     model_gen = ++next_gen;
     if (with_tree) tree_gen = model_gen;
@@ -571,7 +571,13 @@ struct Ctx {
     return e;
   }
 
-  int grow_nodes(size_t need, size_t used) {
+  // Node window (blocked mining, mine_impl): the node arrays hold the nodes
+  // with global indices [wbase, wbase + node_cap); kernels see pointers offset
+  // by -wbase and use global indices.
+  long long wbase = 0;
+  bool tree_complete = false;  // the window holds every node of the last mined table (one block)
+  int grow_nodes(size_t need_global, size_t used_global) {
+    const size_t need = need_global - (size_t)wbase, used = used_global - (size_t)wbase;
     if (need <= node_cap) return HMC_OK;
     // doubling (each growth re-maps and copies 15 arrays)
     size_t cap = std::max<size_t>(need, 2 * node_cap);
@@ -588,6 +594,30 @@ struct Ctx {
     G(n_cnt) G(n_size) G(n_pos) G(n_list_off) G(n_region)
 #undef G
     node_cap = cap;
+    return HMC_OK;
+  }
+  // Drop the nodes below global index `keep` (the block before the one just
+  // mined): the rest moves to the front of the arrays, in chunks no longer
+  // than the gap so that no copy overlaps itself.
+  template <class T>
+  hipError_t slide(DevBuf<T> &b, size_t gap, size_t n) {
+    for (size_t o = 0; o < n; o += gap) {
+      const size_t m = std::min(gap, n - o);
+      hipError_t e = hipMemcpyAsync(b.p + o, b.p + gap + o, m * sizeof(T), hipMemcpyDeviceToDevice, st);
+      if (e) return e;
+    }
+    return hipSuccess;
+  }
+  int slide_window(long long keep, long long end) {
+    const size_t gap = (size_t)(keep - wbase), n = (size_t)(end - keep);
+    if (gap == 0) return HMC_OK;
+    hipError_t e = hipSuccess;
+#define SL(b) if (!e) e = slide(b, gap, n);
+    SL(n_parent) SL(n_start) SL(n_child_base) SL(n_link) SL(n_allele) SL(n_flags) SL(n_freq) SL(n_prefix) SL(n_tp)
+    SL(n_sum) SL(n_cnt) SL(n_size) SL(n_pos) SL(n_list_off) SL(n_region)
+#undef SL
+    if (e) return hipfail(e, "mine window");
+    wbase = keep;
     return HMC_OK;
   }
 
@@ -613,21 +643,22 @@ struct Ctx {
     a.npos = d_npos.p;
     a.pos_allele = d_pos_allele.p;
     a.rank_of = d_rank_of.p;
-    a.parent = n_parent.p;
-    a.start = n_start.p;
-    a.allele = n_allele.p;
-    a.flags = n_flags.p;
-    a.freq = n_freq.p;
-    a.prefix = n_prefix.p;
-    a.tp = n_tp.p;
-    a.sum = n_sum.p;
-    a.cnt = n_cnt.p;
-    a.size = n_size.p;
-    a.pos = n_pos.p;
-    a.child_base = n_child_base.p;
-    a.link = n_link.p;
-    a.list_off = n_list_off.p;
-    a.region = n_region.p;
+    const long long w = wbase;  // global node index g lives at [g - wbase]
+    a.parent = n_parent.p - w;
+    a.start = n_start.p - w;
+    a.allele = n_allele.p - w;
+    a.flags = n_flags.p - w;
+    a.freq = n_freq.p - w;
+    a.prefix = n_prefix.p - w;
+    a.tp = n_tp.p - w;
+    a.sum = n_sum.p - w;
+    a.cnt = n_cnt.p - w;
+    a.size = n_size.p - w;
+    a.pos = n_pos.p - w;
+    a.child_base = n_child_base.p - w;
+    a.link = n_link.p - w;
+    a.list_off = n_list_off.p - w;
+    a.region = n_region.p - w;
     a.r_region = d_r_region.p;
     a.r_child_base = d_r_child_base.p;
     a.rm = d_rm.p;
@@ -682,8 +713,62 @@ struct Ctx {
   int exact_rounds = 0;
   uint64_t exact_candidates = 0;
 
-  // The current table with allele strings (mined: from the candidate tree;
-  // exact: the host copy).
+  // Allele-index strings of the current device table, id order: pattern i's
+  // alleles at al[off[i] .. off[i] + len[i]).  Spelled from the prefix ids
+  // (ppat; a prefix precedes its extensions in DFS order), or from the
+  // candidate tree where a prefix is no pattern (min_len > 1).  Fails with
+  // HMC_EUNSUPPORTED when neither can spell the table (an injected table).
+  int spell_table(const std::vector<int32_t> &ln, std::vector<int64_t> &off, std::vector<uint8_t> &al) {
+    const int P = this->P;
+    std::vector<int32_t> pp(P), node;
+    std::vector<uint8_t> last(P);
+    hipError_t e;
+    if ((e = hipMemcpyAsync(pp.data(), t_ppat.p, (size_t)P * 4, hipMemcpyDeviceToHost, st)) ||
+        (e = hipMemcpyAsync(last.data(), t_last.p, (size_t)P, hipMemcpyDeviceToHost, st)) ||
+        (e = hipStreamSynchronize(st)))
+      return hipfail(e, "table strings");
+    off.assign((size_t)P + 1, 0);
+    for (int i = 0; i < P; ++i) off[i + 1] = off[i] + ln[i];
+    al.assign((size_t)off[P], 0);
+    std::vector<int32_t> par;
+    std::vector<uint8_t> alc;
+    bool tree_loaded = false;
+    for (int i = 0; i < P; ++i) {
+      uint8_t *o = al.data() + off[i];
+      o[ln[i] - 1] = last[i];
+      const int32_t q = pp[i];
+      if (ln[i] == 1) continue;
+      if (q >= 0 && q < i && ln[q] == ln[i] - 1) {
+        std::copy(al.data() + off[q], al.data() + off[q] + ln[q], o);
+        continue;
+      }
+      if (!tree_ok()) return fail(HMC_EUNSUPPORTED, "allele strings of this table are unknown (a table set from outside)");
+      if (!tree_loaded) {
+        node.resize(P);
+        if ((e = hipMemcpyAsync(node.data(), t_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st)) ||
+            (e = hipStreamSynchronize(st)))
+          return hipfail(e, "table strings");
+        int nmax = 0;
+        for (int k = 0; k < P; ++k) nmax = std::max(nmax, node[k] + 1);
+        par.resize(nmax);
+        alc.resize(nmax);
+        if (nmax && ((e = hipMemcpyAsync(par.data(), n_parent.p, (size_t)nmax * 4, hipMemcpyDeviceToHost, st)) ||
+                     (e = hipMemcpyAsync(alc.data(), n_allele.p, (size_t)nmax, hipMemcpyDeviceToHost, st)) ||
+                     (e = hipStreamSynchronize(st))))
+          return hipfail(e, "table strings");
+        tree_loaded = true;
+      }
+      int32_t v = node[i];
+      for (int k = ln[i] - 1; k >= 0; --k) {
+        o[k] = alc[v];
+        v = par[v];
+      }
+    }
+    return HMC_OK;
+  }
+
+  // The current table with allele strings (mined: spelled from the prefix
+  // ids; exact: the host copy).
   int table_to_host(Cands &c, std::vector<int32_t> &succ) {
     if (table_on_host) {
       c = ht;
@@ -691,39 +776,24 @@ struct Ctx {
       return HMC_OK;
     }
     const int P = this->P, A = pan.amax;
-    std::vector<int32_t> st(P), ln(P), node(P);
+    std::vector<int32_t> st(P), ln(P);
     std::vector<double> fr(P), pre(P), tp(P);
     std::vector<uint32_t> su((size_t)P * A);
     hipError_t e;
     if ((e = hipMemcpyAsync(st.data(), t_start.p, (size_t)P * 4, hipMemcpyDeviceToHost, this->st)) ||
         (e = hipMemcpyAsync(ln.data(), t_len.p, (size_t)P * 4, hipMemcpyDeviceToHost, this->st)) ||
-        (e = hipMemcpyAsync(node.data(), t_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, this->st)) ||
         (e = hipMemcpyAsync(fr.data(), t_freq.p, (size_t)P * 8, hipMemcpyDeviceToHost, this->st)) ||
         (e = hipMemcpyAsync(pre.data(), t_prefix.p, (size_t)P * 8, hipMemcpyDeviceToHost, this->st)) ||
         (e = hipMemcpyAsync(tp.data(), t_tp.p, (size_t)P * 8, hipMemcpyDeviceToHost, this->st)) ||
         (e = hipMemcpyAsync(su.data(), t_succ.p, su.size() * 4, hipMemcpyDeviceToHost, this->st)) ||
         (e = hipStreamSynchronize(this->st)))
       return hipfail(e, "exact: table");
-    if (!tree_ok()) return fail(HMC_EUNSUPPORTED, "exact M-step needs a mined or estimated table (allele strings)");
-    int nmax = 0;
-    for (int i = 0; i < P; ++i) nmax = std::max(nmax, node[i] + 1);
-    std::vector<int32_t> par(nmax);
-    std::vector<uint8_t> alc(nmax);
-    if (nmax && ((e = hipMemcpyAsync(par.data(), n_parent.p, (size_t)nmax * 4, hipMemcpyDeviceToHost, this->st)) ||
-                 (e = hipMemcpyAsync(alc.data(), n_allele.p, (size_t)nmax, hipMemcpyDeviceToHost, this->st)) ||
-                 (e = hipStreamSynchronize(this->st))))
-      return hipfail(e, "exact: table");
+    std::vector<int64_t> off;
+    std::vector<uint8_t> al;
+    int rc = spell_table(ln, off, al);
+    if (rc) return rc;
     c = Cands();
-    std::vector<uint8_t> buf;
-    for (int i = 0; i < P; ++i) {
-      buf.assign(ln[i], 0);
-      int32_t v = node[i];
-      for (int k = ln[i] - 1; k >= 0; --k) {
-        buf[k] = alc[v];
-        v = par[v];
-      }
-      c.push(st[i], ln[i], buf.data(), 0, false, fr[i], pre[i], tp[i]);
-    }
+    for (int i = 0; i < P; ++i) c.push(st[i], ln[i], al.data() + off[i], 0, false, fr[i], pre[i], tp[i]);
     succ.resize((size_t)P * A);
     for (size_t i = 0; i < su.size(); ++i) succ[i] = su[i] == NONE ? -1 : (int32_t)su[i];
     return HMC_OK;
@@ -852,10 +922,12 @@ struct Ctx {
       fmax = std::max(fmax, fm[ids[q]]);
     }
     x.fmax = fmax;
-    x.scratch_stride = (size_t)(tr_maxd + 1) * 3 * fmax + tr_maxd + 2;
+    x.scratch_stride = exact_walk_scratch_doubles(tr_maxd, fmax);
     const long long items = (long long)k * L;
     const int grid = (int)std::max<long long>(1, std::min<long long>(items, (long long)dev_cu * 16));
-    if ((e = d_xscr.ensure(x.scratch_stride * grid))) return hipfail(e, "exact scratch");
+    if ((e = d_xscr.ensure(x.scratch_stride * grid)) ||
+        (e = hipMemsetAsync(d_xscr.p, 0, x.scratch_stride * grid * 8, st)))  // the walk's zero invariant
+      return hipfail(e, "exact scratch");
     x.scratch = d_xscr.p;
     hipEventRecord(ev[0], st);
     if ((e = launch_exact_walk(x, grid, st))) return hipfail(e, "exact_walk");
@@ -934,6 +1006,7 @@ struct Ctx {
               (e = hipMemcpyAsync(t_tp.p, c.tp.data(), (size_t)P * 8, hipMemcpyHostToDevice, st)) ||
               (e = hipMemcpyAsync(t_last.p, last.data(), (size_t)P, hipMemcpyHostToDevice, st)) ||
               (e = hipMemcpyAsync(t_succ.p, su.data(), su.size() * 4, hipMemcpyHostToDevice, st)) ||
+              (e = hipMemsetAsync(t_ppat.p, 0xFE, (size_t)P * 4, st)) ||  // alleles are kept on the host (ht)
               (e = hipStreamSynchronize(st))))
       return hipfail(e, "exact: install table");
     this->P = P;
@@ -970,6 +1043,8 @@ struct Ctx {
     if (!have_estep) return fail(HMC_EARG, "exact M-step needs an E-step first");
     if (num_patterns > 0 && model != 1)
       return fail(HMC_EUNSUPPORTED, "exact M-step after findPatternByNum (num_patterns > 0)");
+    if (pan.amax > 44)  // the records pack a locus's allele pairs (amax (amax + 1) / 2) in 10 bits
+      return fail(HMC_EUNSUPPORTED, "exact M-step with more than 44 alleles per locus");
     hipEventRecord(ev[4], st);
     const int L = pan.L;
     int mxl = max_len <= 0 ? L : max_len;  // m_max_len / m_min_len of the last findPatternByFreq
@@ -1067,9 +1142,30 @@ struct Ctx {
     return t;
   }
 
+  // Start loci per mining block (hmc_set_mine_block; 0 = automatic).  The
+  // roots of the DFS are independent (PatternManager.cpp:90-108), so the
+  // search can run over blocks of start loci from L-1 down: pattern ids stay
+  // the DFS pre-order (a block's ids follow those of the blocks above it),
+  // and a block's successors need only its own nodes and the block above it
+  // (suffixes start at most max_len loci later), so the node arrays hold two
+  // blocks and the matching lists one.  One block when the panel is small or
+  // the rules need the whole tree (findPatternByNum, heads longer than 1).
+  int mine_block_starts = 0;
+  int block_width(int L, int mxl, int mnl, int bynum_rounds) const {
+    if (bynum_rounds > 0 || mnl > 1) return L;
+    int w = mine_block_starts;
+    if (w <= 0) {  // about 2.5e7 individual-loci of panel per block (cfg 3: one block; cfg 4: 10)
+      const double work = (double)pan.N * (double)L;
+      const int nb = (int)std::ceil(work / 2.5e7);
+      if (nb <= 1) return L;
+      w = (L + nb - 1) / nb;
+    }
+    w = std::max(w, mxl + 1);
+    return w >= L ? L : w;
+  }
+
   int mine_impl(int *P_out, uint64_t *rm_out, int bynum_rounds) {
     if (!have_panel) return fail(HMC_EARG, "no panel loaded");
-    const bool genotype = !have_samples;
     const int L = pan.L;
     hipError_t e;
     hipEventRecord(ev[4], st);
@@ -1084,32 +1180,107 @@ struct Ctx {
     }
     if (bynum_rounds > 0) mf = bynum_theta(bynum_rounds);
     if ((e = d_rm.ensure(RM_SLOTS * 16)) || (e = d_totals.ensure(2)) || (e = h_totals.ensure(2)) ||
+        (e = d_rsize.ensure(L)) || (e = d_rpos.ensure(L)) || (e = d_r_region.ensure(L)) ||
         (e = hipMemsetAsync(d_rm.p, 0, RM_SLOTS * 16 * 8, st)))
       return hipfail(e, "mine");
-    std::vector<int> lbeg{0, 0}, lend{0, 0};  // per level node ranges (index = level)
-    int n1 = 0;
-    for (int k = 0; k < L; ++k) n1 += h_npos[k];
-    int rc = grow_nodes(std::max(n1, 1), 0);
-    if (rc) return rc;
-    lbeg[1] = 0;
-    lend[1] = n1;
-    int level = 1, pbeg = 0, pend = L;  // level-1 parents are the L roots
-    int cur = 0;                        // list buffer holding the parents' lists
-    // child lists of the roots: root r owns npos[r] x n_items slots of the next buffer
+    const int W = block_width(L, mxl, mnl, bynum_rounds);
+    wbase = 0;
+    long long next_node = 0;  // global index of the next node
+    long long id_base = 0;    // patterns of the blocks above
+    uint64_t rm_bynum = 0;
+    int rc, nblocks = 0;
+    for (int hi = L; hi > 0;) {
+      const int lo = std::max(0, hi - W);
+      MineBlock mb;
+      if ((rc = mine_block(lo, hi, mxl, mnl, mf, bynum_rounds, next_node, id_base, mb, rm_bynum))) return rc;
+      // the block above this one is no longer needed
+      if ((rc = slide_window(mb.first_node, mb.end_node))) return rc;
+      next_node = mb.end_node;
+      id_base += mb.patterns;
+      hi = lo;
+      ++nblocks;
+    }
+    tree_complete = nblocks == 1;
+    P = (int)id_base;
+    std::vector<unsigned long long> rm_slots((size_t)RM_SLOTS * 16);
+    if ((e = hipMemcpyAsync(rm_slots.data(), d_rm.p, rm_slots.size() * 8, hipMemcpyDeviceToHost, st)))
+      return hipfail(e, "mine");
+    hipEventRecord(ev[5], st);
+    if ((e = hipStreamSynchronize(st))) return hipfail(e, "mine");
+    // The matching lists of the genotype branch (M0) reach tens of GB at
+    // cfg 3 (R_M ~ 10^11 entries); give them back to the E-step's stores.
+    for (int k = 0; k < 2; ++k) {
+      if (l_idx[k].n * 4 > (4ull << 30)) l_idx[k].release();
+      if (l_val[k].n * 8 > (4ull << 30)) l_val[k].release();
+    }
+    if (debug_mem) {
+      size_t fb = 0, tb = 0;
+      hipMemGetInfo(&fb, &tb);
+      fprintf(stderr, "[hmc] after mining: %d patterns in %d block(s) of %d start loci, %lld nodes; free %.1f GB of %.1f; "
+              "node window %.1f GB\n", P, nblocks, W, next_node, fb / 1e9, tb / 1e9, node_cap * 70.0 / 1e9);
+    }
+    unsigned long long rm = 0;
+    for (int k = 0; k < RM_SLOTS; ++k) rm += rm_slots[(size_t)k * 16];
+    if (bynum_rounds > 0) rm = rm_bynum;  // the scans of the candidates the rounds generated
+    float ms = 0;
+    hipEventElapsedTime(&ms, ev[4], ev[5]);
+    ms_m = ms;
+    have_model = true;
+    new_table(true);
+    last_mine_blocks = nblocks;
+    last_mine_nodes = next_node;
+    if (P_out) *P_out = P;
+    if (rm_out) *rm_out = rm;
+    return HMC_OK;
+  }
+  int last_mine_blocks = 0;
+  long long last_mine_nodes = 0;
+
+  struct MineBlock {
+    long long first_node = 0, end_node = 0;  // global node range of the block
+    long long patterns = 0;
+  };
+
+  // The level-synchronous search for the roots [lo, hi): nodes appended at
+  // global index `node0`, pattern ids from `id_base`; then the block's table
+  // rows, successors and (lo == 0) the head list.
+  int mine_block(int lo, int hi, int mxl, int mnl, double mf, int bynum_rounds, long long node0, long long id_base,
+                 MineBlock &mb, uint64_t &rm_bynum) {
+    const bool genotype = !have_samples;
+    const int L = pan.L;
+    hipError_t e;
+    int rc;
+    std::vector<long long> lbeg{0, 0}, lend{0, 0};  // per level node ranges (index = level), global
+    long long n1 = 0;
+    for (int k = lo; k < hi; ++k) n1 += h_npos[k];
+    if ((rc = grow_nodes((size_t)std::max<long long>(node0 + n1, 1), (size_t)node0))) return rc;
+    if (node0 + n1 > (long long)INT32_MAX) return fail(HMC_EUNSUPPORTED, "candidate tree exceeds 2^31 nodes");
+    // level-1 nodes of the block's roots (r_child_base of root k) and the
+    // roots' child lists: root r owns npos[r] x n_items slots of the next buffer
     unsigned long long next_total = 0;
     {
       const unsigned long long ni = (unsigned long long)mine_args(genotype).n_items;
-      std::vector<unsigned long long> rr(L);
-      for (int k = 0; k < L; ++k) {
-        rr[k] = next_total;
+      std::vector<unsigned long long> rr(hi - lo);
+      std::vector<int32_t> rcb(hi - lo);
+      long long c = node0;
+      for (int k = lo; k < hi; ++k) {
+        rr[k - lo] = next_total;
         next_total += (unsigned long long)h_npos[k] * ni;
+        rcb[k - lo] = (int32_t)c;
+        c += h_npos[k];
       }
-      if ((e = d_r_region.ensure(L)) ||
-          (e = hipMemcpyAsync(d_r_region.p, rr.data(), (size_t)L * 8, hipMemcpyHostToDevice, st)))
+      if ((e = hipMemcpyAsync(d_r_region.p + lo, rr.data(), rr.size() * 8, hipMemcpyHostToDevice, st)) ||
+          (e = hipMemcpyAsync(d_r_child_base.p + lo, rcb.data(), rcb.size() * 4, hipMemcpyHostToDevice, st)))
         return hipfail(e, "mine");
     }
+    lbeg[1] = node0;
+    lend[1] = node0 + n1;
+    int level = 1;
+    long long pbeg = lo, pend = hi;  // level-1 parents are the block's roots
+    int cur = 0;                     // list buffer holding the parents' lists
     while (true) {
-      const int cb = lbeg[level], ce = lend[level], nlev = ce - cb;
+      const long long cb = lbeg[level], ce = lend[level];
+      const int nlev = (int)(ce - cb);
       const int nxt = cur ^ 1;  // children's lists are written here during the count
       if ((e = ensure_or_release(l_idx[nxt], std::max<unsigned long long>(next_total, 1)))) return hipfail(e, "mine lists");
       if (genotype && (e = ensure_or_release(l_val[nxt], std::max<unsigned long long>(next_total, 1))))
@@ -1140,12 +1311,12 @@ struct Ctx {
         // every rank scans its items and writes the children's lists at once;
         // then rank r continues every child's sum from ranks 0..r-1 (items in
         // order) over its lists and passes it on
-        if ((e = launch_mine_count(a, level, pbeg, pend, st))) return hipfail(e, "mine_count");
+        if ((e = launch_mine_count(a, level, (int)pbeg, (int)pend, st))) return hipfail(e, "mine_count");
         for (int r = 0; r < world; ++r) {
-          if (r == rank && r > 0 && (e = launch_mine_sum(a, cb, ce, st))) return hipfail(e, "mine_sum");
-          if ((rc = bcast(n_sum.p + cb, nlev, r))) return rc;
+          if (r == rank && r > 0 && (e = launch_mine_sum(a, (int)cb, (int)ce, st))) return hipfail(e, "mine_sum");
+          if ((rc = bcast(n_sum.p + (cb - wbase), nlev, r))) return rc;
         }
-      } else if ((e = launch_mine_count(a, level, pbeg, pend, st))) {
+      } else if ((e = launch_mine_count(a, level, (int)pbeg, (int)pend, st))) {
         return hipfail(e, "mine_count");
       }
       if (diag_mine) {  // per-level list statistics of the parents (diagnostic)
@@ -1155,14 +1326,14 @@ struct Ctx {
         hipEventElapsedTime(&ms, dm0, dm1);
         size_t tot_n = 0, max_n = 0, npar = 0;
         if (level == 1) {
-          npar = (size_t)L;
-          tot_n = (size_t)L * (size_t)a.n_items;
+          npar = (size_t)(hi - lo);
+          tot_n = npar * (size_t)a.n_items;
           max_n = (size_t)a.n_items;
         } else {
           std::vector<uint32_t> hc((size_t)(pend - pbeg));
           std::vector<uint8_t> hf((size_t)(pend - pbeg));
-          hipMemcpy(hc.data(), n_cnt.p + pbeg, hc.size() * 4, hipMemcpyDeviceToHost);
-          hipMemcpy(hf.data(), n_flags.p + pbeg, hf.size(), hipMemcpyDeviceToHost);
+          hipMemcpy(hc.data(), n_cnt.p + (pbeg - wbase), hc.size() * 4, hipMemcpyDeviceToHost);
+          hipMemcpy(hf.data(), n_flags.p + (pbeg - wbase), hf.size(), hipMemcpyDeviceToHost);
           for (size_t q = 0; q < hc.size(); ++q)
             if (hf[q] & 2) {
               ++npar;
@@ -1170,8 +1341,8 @@ struct Ctx {
               max_n = std::max<size_t>(max_n, hc[q]);
             }
         }
-        fprintf(stderr, "mine level %2d: %7zu ext parents of %7d, entries %9zu, max list %7zu, mine_count %.3f ms\n",
-                level, npar, pend - pbeg, tot_n, max_n, ms);
+        fprintf(stderr, "mine block [%d,%d) level %2d: %7zu ext parents of %7lld, entries %9zu, max list %7zu, "
+                "mine_count %.3f ms\n", lo, hi, level, npar, pend - pbeg, tot_n, max_n, ms);
 #ifdef HMC_STAMPS
         unsigned long long hs[8] = {};
         std::vector<unsigned long long> hv((size_t)(pend - pbeg) * 8);
@@ -1184,14 +1355,12 @@ struct Ctx {
         hipEventDestroy(dm0);
         hipEventDestroy(dm1);
       }
-      if (!(multi() && reduction == RED_ORDERED) && (rc = allreduce_sum(n_sum.p + cb, nlev))) return rc;
-      if ((e = s_ext.ensure(nlev)) || (e = s_child.ensure(nlev)))
-        return hipfail(e, "mine");
+      if (!(multi() && reduction == RED_ORDERED) && (rc = allreduce_sum(n_sum.p + (cb - wbase), nlev))) return rc;
+      if ((e = s_ext.ensure(nlev)) || (e = s_child.ensure(nlev))) return hipfail(e, "mine");
       const size_t tmpb = mine_scan_tmp_bytes(nlev);
       if ((e = s_tmp.ensure(tmpb))) return hipfail(e, "mine");
-      if ((e = launch_mine_finalize(a, level, cb, ce, s_ext.p, s_child.p, st))) return hipfail(e, "mine_finalize");
-      if ((e = launch_mine_offsets(a, cb, ce, s_ext.p, s_child.p, ce, s_tmp.p, s_tmp.n, d_totals.p,
-                                   st)))
+      if ((e = launch_mine_finalize(a, level, (int)cb, (int)ce, s_ext.p, s_child.p, st))) return hipfail(e, "mine_finalize");
+      if ((e = launch_mine_offsets(a, (int)cb, (int)ce, s_ext.p, s_child.p, (int)ce, s_tmp.p, s_tmp.n, d_totals.p, st)))
         return hipfail(e, "mine_offsets");
       const unsigned long long *tot = h_totals.p;
       if ((e = hipMemcpyAsync(h_totals.p, d_totals.p, 16, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
@@ -1199,7 +1368,7 @@ struct Ctx {
       next_total = tot[0];  // list slots the next level's children need
       if (tot[1] > (unsigned long long)INT32_MAX - (unsigned long long)ce)
         return fail(HMC_EUNSUPPORTED, "candidate tree exceeds 2^31 nodes at length %d", level + 1);
-      const int nnext = (int)tot[1];
+      const long long nnext = (long long)tot[1];
       cur = nxt;
       if (nnext == 0) break;
       pbeg = cb;
@@ -1207,77 +1376,55 @@ struct Ctx {
       ++level;
       lbeg.push_back(ce);
       lend.push_back(ce + nnext);
-      if ((rc = grow_nodes((size_t)ce + nnext, ce))) return rc;
+      if ((rc = grow_nodes((size_t)(ce + nnext), (size_t)ce))) return rc;
     }
     const int maxlev = level;
-    const int ntot = lend[maxlev];
     MineArgs a = mine_args(genotype);
-    uint64_t rm_bynum = 0;
-    if (bynum_rounds > 0) {
-      rc = bynum_replay(a, ntot, mnl, mxl, bynum_rounds, rm_bynum);
+    long long Pb = 0;
+    if (bynum_rounds > 0) {  // one block: the node window starts at 0
+      rc = bynum_replay(a, (int)lend[maxlev], mnl, mxl, bynum_rounds, rm_bynum);
       if (rc) return rc;
+      Pb = P;
     } else {
-    // DFS pre-order ids from subtree sizes
-    for (int lv = maxlev; lv >= 1; --lv)
-      if ((e = launch_mine_size(a, lv, lbeg[lv], lend[lv], st))) return hipfail(e, "mine_size");
-    if ((e = d_rsize.ensure(L)) || (e = d_rpos.ensure(L))) return hipfail(e, "mine");
-    if ((e = launch_mine_root_size(a, d_rsize.p, st))) return hipfail(e, "mine_root_size");
-    std::vector<uint32_t> rsize(L), rpos(L);
-    if ((e = hipMemcpyAsync(rsize.data(), d_rsize.p, (size_t)L * 4, hipMemcpyDeviceToHost, st)) ||
-        (e = hipStreamSynchronize(st)))
-      return hipfail(e, "mine");
-    uint64_t acc = 0;
-    for (int s = L - 1; s >= 0; --s) {  // roots popped from the back: start L-1 first
-      rpos[s] = (uint32_t)acc;
-      acc += rsize[s];
+      // DFS pre-order ids from subtree sizes
+      for (int lv = maxlev; lv >= 1; --lv)
+        if ((e = launch_mine_size(a, lv, (int)lbeg[lv], (int)lend[lv], st))) return hipfail(e, "mine_size");
+      if ((e = launch_mine_root_size(a, d_rsize.p, lo, hi, st))) return hipfail(e, "mine_root_size");
+      std::vector<uint32_t> rsize(hi - lo), rpos(hi - lo);
+      if ((e = hipMemcpyAsync(rsize.data(), d_rsize.p + lo, rsize.size() * 4, hipMemcpyDeviceToHost, st)) ||
+          (e = hipStreamSynchronize(st)))
+        return hipfail(e, "mine");
+      uint64_t acc = (uint64_t)id_base;
+      for (int s = hi - 1; s >= lo; --s) {  // roots popped from the back: start L-1 first
+        rpos[s - lo] = (uint32_t)acc;
+        acc += rsize[s - lo];
+      }
+      if (acc > (uint64_t)INT32_MAX) return fail(HMC_EUNSUPPORTED, "too many patterns (%llu)", (unsigned long long)acc);
+      Pb = (long long)acc - id_base;
+      if ((e = hipMemcpyAsync(d_rpos.p + lo, rpos.data(), rpos.size() * 4, hipMemcpyHostToDevice, st)))
+        return hipfail(e, "mine");
+      if ((e = launch_mine_pos(a, 1, lo, hi, d_rpos.p, st))) return hipfail(e, "mine_pos");
+      for (int lv = 2; lv <= maxlev; ++lv)
+        if ((e = launch_mine_pos(a, lv, (int)lbeg[lv - 1], (int)lend[lv - 1], d_rpos.p, st))) return hipfail(e, "mine_pos");
     }
-    if (acc > (uint64_t)INT32_MAX) return fail(HMC_EUNSUPPORTED, "too many patterns (%llu)", (unsigned long long)acc);
-    P = (int)acc;
-    if ((e = hipMemcpyAsync(d_rpos.p, rpos.data(), (size_t)L * 4, hipMemcpyHostToDevice, st)))
-      return hipfail(e, "mine");
-    if ((e = launch_mine_pos(a, 1, 0, L, d_rpos.p, st))) return hipfail(e, "mine_pos");
-    for (int lv = 2; lv <= maxlev; ++lv)
-      if ((e = launch_mine_pos(a, lv, lbeg[lv - 1], lend[lv - 1], d_rpos.p, st))) return hipfail(e, "mine_pos");
-    }
-    if ((rc = alloc_table(P))) return rc;
+    if ((rc = grow_table((size_t)(id_base + Pb), (size_t)id_base))) return rc;
     PatternTable t = table();
-    h_lev_begin.assign(lbeg.begin(), lbeg.begin() + maxlev + 1);
-    h_lev_begin.push_back(lend[maxlev]);
-    if ((e = d_lev_begin.ensure(h_lev_begin.size())) ||
-        (e = hipMemcpyAsync(d_lev_begin.p, h_lev_begin.data(), h_lev_begin.size() * 4, hipMemcpyHostToDevice, st)) ||
-        (e = launch_mine_emit(a, d_lev_begin.p, maxlev, lend[maxlev] - lbeg[1], t, st)))
+    std::vector<int> lb(maxlev + 2);  // the block's level ranges (global node indices < 2^31)
+    for (int lv = 1; lv <= maxlev; ++lv) lb[lv] = (int)lbeg[lv];
+    lb[maxlev + 1] = (int)lend[maxlev];
+    if ((e = d_lev_begin.ensure(lb.size())) ||
+        (e = hipMemcpyAsync(d_lev_begin.p, lb.data(), lb.size() * 4, hipMemcpyHostToDevice, st)) ||
+        (e = launch_mine_emit(a, d_lev_begin.p, maxlev, lb[maxlev + 1] - lb[1], t, st)))
       return hipfail(e, "mine_emit");
-    if ((e = launch_mine_succ(a, t, P, st))) return hipfail(e, "mine_succ");
-    head_len = mnl;
-    if ((rc = build_heads_from_nodes(a, mnl <= maxlev ? lbeg[mnl] : 0, mnl <= maxlev ? lend[mnl] : 0))) return rc;
-    std::vector<unsigned long long> rm_slots((size_t)RM_SLOTS * 16);
-    if ((e = hipMemcpyAsync(rm_slots.data(), d_rm.p, rm_slots.size() * 8, hipMemcpyDeviceToHost, st)))
-      return hipfail(e, "mine");
-    hipEventRecord(ev[5], st);
-    if ((e = hipStreamSynchronize(st))) return hipfail(e, "mine");
-    // The matching lists of the genotype branch (M0) reach tens of GB at
-    // cfg 3 (R_M ~ 10^11 entries); give them back to the E-step's stores.
-    for (int k = 0; k < 2; ++k) {
-      if (l_idx[k].n * 4 > (4ull << 30)) l_idx[k].release();
-      if (l_val[k].n * 8 > (4ull << 30)) l_val[k].release();
+    if ((e = launch_mine_succ(a, t, (int)id_base, (int)Pb, st))) return hipfail(e, "mine_succ");
+    if (lo == 0) {
+      head_len = mnl;
+      P = (int)(id_base + Pb);  // the head pairs' lookups see the whole table
+      if ((rc = build_heads_from_nodes(a, mnl <= maxlev ? (int)lbeg[mnl] : 0, mnl <= maxlev ? (int)lend[mnl] : 0))) return rc;
     }
-    if (debug_mem) {
-      size_t fb = 0, tb = 0;
-      hipMemGetInfo(&fb, &tb);
-      fprintf(stderr, "[hmc] after mining: free %.1f GB of %.1f; nodes %.1f GB\n", fb / 1e9, tb / 1e9,
-              node_cap * 70.0 / 1e9);
-    }
-    unsigned long long rm = 0;
-    for (int k = 0; k < RM_SLOTS; ++k) rm += rm_slots[(size_t)k * 16];
-    if (bynum_rounds > 0) rm = rm_bynum;  // the scans of the candidates the rounds generated
-    float ms = 0;
-    hipEventElapsedTime(&ms, ev[4], ev[5]);
-    ms_m = ms;
-    have_model = true;
-    new_table(true);
-    (void)ntot;
-    if (P_out) *P_out = P;
-    if (rm_out) *rm_out = rm;
+    mb.first_node = node0;
+    mb.end_node = lend[maxlev];
+    mb.patterns = Pb;
     return HMC_OK;
   }
 
@@ -1285,9 +1432,22 @@ struct Ctx {
     hipError_t e;
     const size_t n = std::max(np, 1);
     if ((e = t_start.ensure(n)) || (e = t_len.ensure(n)) || (e = t_node.ensure(n)) || (e = t_freq.ensure(n)) ||
-        (e = t_prefix.ensure(n)) || (e = t_tp.ensure(n)) || (e = t_last.ensure(n)) ||
+        (e = t_prefix.ensure(n)) || (e = t_tp.ensure(n)) || (e = t_last.ensure(n)) || (e = t_ppat.ensure(n)) ||
         (e = t_succ.ensure(n * pan.amax)))
       return hipfail(e, "alloc_table");
+    return HMC_OK;
+  }
+  // Grow the table to n rows keeping the first `used` (blocked mining appends blocks).
+  int grow_table(size_t n, size_t used) {
+    hipError_t e;
+    n = std::max<size_t>(n, 1);
+    const size_t A = (size_t)pan.amax;
+    if ((e = t_start.grow_keep(n, used, st)) || (e = t_len.grow_keep(n, used, st)) ||
+        (e = t_node.grow_keep(n, used, st)) || (e = t_freq.grow_keep(n, used, st)) ||
+        (e = t_prefix.grow_keep(n, used, st)) || (e = t_tp.grow_keep(n, used, st)) ||
+        (e = t_last.grow_keep(n, used, st)) || (e = t_ppat.grow_keep(n, used, st)) ||
+        (e = t_succ.grow_keep(n * A, used * A, st)))
+      return hipfail(e, "grow_table");
     return HMC_OK;
   }
   PatternTable table() const {
@@ -1295,6 +1455,7 @@ struct Ctx {
     t.start = t_start.p;
     t.len = t_len.p;
     t.node = t_node.p;
+    t.ppat = t_ppat.p;
     t.freq = t_freq.p;
     t.prefix = t_prefix.p;
     t.tp = t_tp.p;
@@ -1430,9 +1591,10 @@ struct Ctx {
           (e = hipStreamSynchronize(st)))
         return hipfail(e, "heads");
       if (n0 > 0) {
-        if ((e = hipMemcpyAsync(fl.data(), n_flags.p + rcb[0], n0, hipMemcpyDeviceToHost, st)) ||
-            (e = hipMemcpyAsync(alle.data(), n_allele.p + rcb[0], n0, hipMemcpyDeviceToHost, st)) ||
-            (e = hipMemcpyAsync(pos.data(), n_pos.p + rcb[0], (size_t)n0 * 4, hipMemcpyDeviceToHost, st)) ||
+        const long long r0 = (long long)rcb[0] - wbase;  // physical index of root 0's first child
+        if ((e = hipMemcpyAsync(fl.data(), n_flags.p + r0, n0, hipMemcpyDeviceToHost, st)) ||
+            (e = hipMemcpyAsync(alle.data(), n_allele.p + r0, n0, hipMemcpyDeviceToHost, st)) ||
+            (e = hipMemcpyAsync(pos.data(), n_pos.p + r0, (size_t)n0 * 4, hipMemcpyDeviceToHost, st)) ||
             (e = hipStreamSynchronize(st)))
           return hipfail(e, "heads");
       }
@@ -1617,7 +1779,8 @@ struct Ctx {
     // trace cap keeps cfg 3's E2.. (~90 GB of traces) in one value pass.)
     trace_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.42), 120ull << 30),
                                       1ull << 20) / 4;
-    rec_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.28), 80ull << 30),
+    rec_budget = std::max<uint64_t>(rec_bytes ? rec_bytes : trace_bytes ? trace_bytes
+                                    : std::min<uint64_t>((uint64_t)(avail * 0.28), 80ull << 30),
                                     1ull << 20) / 4;
     if (debug_mem)
       fprintf(stderr, "[hmc] E-step: free %.1f GB, stores %.1f + %.1f GB, budgets trace %.1f rec %.1f GB\n",
@@ -1631,7 +1794,7 @@ struct Ctx {
     if ((e = hipMemcpyAsync(d_sbase.p, h_sbase.data(), (size_t)n * 4, hipMemcpyHostToDevice, st)) ||
         (e = hipMemsetAsync(d_maxst.p, 0, 4, st)) || (e = hipMemsetAsync(d_ncand.p, 0, (size_t)n * 4, st)))
       return hipfail(e, "estep");
-    if ((e = d_stamps.ensure(20)) || (e = hipMemsetAsync(d_stamps.p, 0, 20 * 8, st))) return hipfail(e, "stamps");
+    if ((e = d_stamps.ensure(40)) || (e = hipMemsetAsync(d_stamps.p, 0, 40 * 8, st))) return hipfail(e, "stamps");
     // heaviest individuals first (cost of the previous E-step; before the
     // first one, the number of heterozygous or missing loci)
     if ((int)h_cost.size() != n) {
@@ -2020,6 +2183,7 @@ struct Ctx {
       s1.re_count = exact ? d_xre.p : d_re.p;
       s1.fmax = exact ? d_xfmax.p : d_fmax.p;
       s1.max_states = d_maxst.p;
+      s1.stamps = d_stamps.p + 20;
       s1.exact = exact;
       if ((e = d_nextq.ensure(2)) || (e = hipMemsetAsync(d_nextq.p, 0, 8, st))) return hipfail(e, "estep");
       s1.next_q = d_nextq.p;
@@ -2138,8 +2302,16 @@ struct Ctx {
         // 101 vs 112 ms at 2:8)
         // (1:20 runs the 5-waves-per-SIMD build: 505-514 vs 535-558 ms at
         // 1:16 for cfg 3's E3, profiles/r02/values_ab/)
-        int vnw = vp_nw > 0 ? vp_nw : ((int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3));
-        int vipc = vp_ipc > 0 ? vp_ipc : (vnw == 1 ? 20 : 8);  // a half-given shape completes by the same rule
+        // Heavy individuals (the first E-step on the genotype-mined model: cfg 3's
+        // E1 averages ~3 000 record words per locus against ~650 later) take 4
+        // waves each, 4 per CU: more selection segments per individual and a
+        // 4x larger LDS frontier tier (cfg 3 E1 value passes 3.84 -> 2.99 s,
+        // profiles/r03/e1_shapes/).
+        double rw = 0;
+        for (size_t q = 0; q < k; ++q) rw += (double)rneed[sset[pos + q]];
+        const bool heavy = rw / ((double)k * L) > 1500.0;
+        int vnw = vp_nw > 0 ? vp_nw : (heavy ? 4 : ((int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3)));
+        int vipc = vp_ipc > 0 ? vp_ipc : (vnw == 1 ? 20 : (vnw == 4 ? 4 : 8));  // a half-given shape completes by the same rule
         const int G2 = std::max(1, std::min(waves > 0 ? waves : dev_cu * vipc, n));
         const int grid2 = std::max(1, std::min<int>(G2, (int)k));
         // register budget: 5 waves per SIMD once the shape asks for more than 16 per CU
@@ -2351,7 +2523,7 @@ struct Ctx {
     const int kf = lds_key_factor;
     for (int f = 4096; f >= 0; f -= 4) {
       const int h = next_pow2(std::max(64, kf * f));
-      if ((int)estep_lds_bytes(S, f, h, estep_nw) <= budget) { fc = f; hc = h; return; }
+      if ((int)estep_lds_bytes(S, f, h, estep_nw, pan.amax) <= budget) { fc = f; hc = h; return; }
     }
   }
 
@@ -2539,7 +2711,7 @@ struct Ctx {
     bool valid = false, table_on_host = false;
     int P = 0, head_len = 1, n_head = 0;
     uint64_t gen = 0;
-    DevBuf<int32_t> start, len, node;
+    DevBuf<int32_t> start, len, node, ppat;
     DevBuf<double> freq, prefix, tp;
     DevBuf<uint8_t> last, head_al;
     DevBuf<uint32_t> succ, head_ids, head_pat0;
@@ -2561,6 +2733,7 @@ struct Ctx {
     const size_t p = (size_t)std::max(P, 1), A = (size_t)pan.amax;
     hipError_t e;
     if ((e = dcopy(snap.start, t_start, p)) || (e = dcopy(snap.len, t_len, p)) || (e = dcopy(snap.node, t_node, p)) ||
+        (e = dcopy(snap.ppat, t_ppat, p)) ||
         (e = dcopy(snap.freq, t_freq, p)) || (e = dcopy(snap.prefix, t_prefix, p)) || (e = dcopy(snap.tp, t_tp, p)) ||
         (e = dcopy(snap.last, t_last, p)) || (e = dcopy(snap.succ, t_succ, p * A)) ||
         (e = dcopy(snap.head_ids, d_head_ids, std::max<size_t>(n_head, 1))) ||
@@ -2586,6 +2759,7 @@ struct Ctx {
     const size_t p = (size_t)std::max(snap.P, 1), A = (size_t)pan.amax;
     hipError_t e;
     if ((e = dcopy(t_start, snap.start, p)) || (e = dcopy(t_len, snap.len, p)) || (e = dcopy(t_node, snap.node, p)) ||
+        (e = dcopy(t_ppat, snap.ppat, p)) ||
         (e = dcopy(t_freq, snap.freq, p)) || (e = dcopy(t_prefix, snap.prefix, p)) || (e = dcopy(t_tp, snap.tp, p)) ||
         (e = dcopy(t_last, snap.last, p)) || (e = dcopy(t_succ, snap.succ, p * A)) ||
         (e = dcopy(d_head_ids, snap.head_ids, std::max<size_t>(snap.n_head, 1))) ||
@@ -2881,6 +3055,27 @@ int hmc_set_pass_shapes(hmc_ctx *h, int structure_ipc, int value_waves, int valu
   return HMC_OK;
 }
 
+int hmc_set_store_budgets(hmc_ctx *h, uint64_t trace_bytes, uint64_t record_bytes) {
+  if (!h) return HMC_EARG;
+  h->c.trace_bytes = trace_bytes;
+  h->c.rec_bytes = record_bytes;
+  return HMC_OK;
+}
+
+int hmc_set_mine_block(hmc_ctx *h, int start_loci) {
+  if (!h || start_loci < 0) return HMC_EARG;
+  h->c.mine_block_starts = start_loci;
+  return HMC_OK;
+}
+
+int hmc_last_mine_stats(const hmc_ctx *h, int *blocks, int64_t *nodes, double *node_window_gb) {
+  if (!h) return HMC_EARG;
+  if (blocks) *blocks = h->c.last_mine_blocks;
+  if (nodes) *nodes = h->c.last_mine_nodes;
+  if (node_window_gb) *node_window_gb = (double)h->c.node_cap * 70.0 / 1e9;
+  return HMC_OK;
+}
+
 int hmc_model_save(hmc_ctx *h) { return h ? h->c.model_save() : HMC_EARG; }
 int hmc_em_rewind(hmc_ctx *h) { return h ? h->c.em_rewind() : HMC_EARG; }
 
@@ -3100,7 +3295,7 @@ int hmc_get_patterns(hmc_ctx *h, int32_t *start, int32_t *len, double *freq, dou
   if (!h || !h->c.have_model) return HMC_EARG;
   Ctx &c = h->c;
   const int P = c.P, A = c.pan.amax;
-  std::vector<int32_t> st(P), ln(P), node(P);
+  std::vector<int32_t> st(P), ln(P);
   std::vector<uint8_t> last(P);
   hipError_t e;
   if ((e = hipMemcpyAsync(st.data(), c.t_start.p, (size_t)P * 4, hipMemcpyDeviceToHost, c.st)) ||
@@ -3126,33 +3321,17 @@ int hmc_get_patterns(hmc_ctx *h, int32_t *start, int32_t *len, double *freq, dou
       for (int k = 0; k < maxlen; ++k) row[k] = k < ln[i] ? c.pan.symbol(st[i] + k, c.ht.alleles(i)[k]) : -1;
     }
   } else if (alleles && maxlen > 0) {
-    // Rebuild allele strings from the candidate tree (parent chain) when the
-    // table came from the miner; else only the last allele is known.
-    std::vector<int32_t> par;
+    // allele strings spelled from the prefix ids (or the candidate tree);
+    // a table set from outside knows only each pattern's last allele
+    std::vector<int64_t> off;
     std::vector<uint8_t> al;
-    const bool tree = c.tree_ok();
-    if (tree) {
-      if ((e = hipMemcpyAsync(node.data(), c.t_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, c.st)) ||
-          (e = hipStreamSynchronize(c.st)))
-        return c.hipfail(e, "get_patterns");
-      int nmax = 0;
-      for (int i = 0; i < P; ++i) nmax = std::max(nmax, node[i] + 1);
-      par.resize(nmax);
-      al.resize(nmax);
-      if (nmax && ((e = hipMemcpyAsync(par.data(), c.n_parent.p, (size_t)nmax * 4, hipMemcpyDeviceToHost, c.st)) ||
-                   (e = hipMemcpyAsync(al.data(), c.n_allele.p, (size_t)nmax, hipMemcpyDeviceToHost, c.st)) ||
-                   (e = hipStreamSynchronize(c.st))))
-        return c.hipfail(e, "get_patterns");
-    }
+    const bool spelled = c.spell_table(ln, off, al) == HMC_OK;
+    if (!spelled) c.err.clear();
     for (int i = 0; i < P; ++i) {
       int32_t *row = alleles + (size_t)i * maxlen;
       for (int k = 0; k < maxlen; ++k) row[k] = -1;
-      if (tree) {
-        int32_t v = node[i];
-        for (int k = ln[i] - 1; k >= 0 && v >= 0; --k) {
-          if (k < maxlen) row[k] = c.pan.symbol(st[i] + k, al[v]);
-          v = par[v];
-        }
+      if (spelled) {
+        for (int k = 0; k < ln[i] && k < maxlen; ++k) row[k] = c.pan.symbol(st[i] + k, al[off[i] + k]);
       } else if (ln[i] - 1 < maxlen && ln[i] > 0) {
         row[ln[i] - 1] = c.pan.symbol(st[i] + ln[i] - 1, last[i]);
       }
@@ -3190,6 +3369,7 @@ int hmc_set_patterns(hmc_ctx *h, int P, const int32_t *start, const int32_t *len
       (e = hipMemcpyAsync(c.t_tp.p, tp, (size_t)P * 8, hipMemcpyHostToDevice, c.st)) ||
       (e = hipMemcpyAsync(c.t_last.p, last.data(), (size_t)P, hipMemcpyHostToDevice, c.st)) ||
       (e = hipMemcpyAsync(c.t_succ.p, s.data(), s.size() * 4, hipMemcpyHostToDevice, c.st)) ||
+      (e = hipMemsetAsync(c.t_ppat.p, 0xFE, (size_t)P * 4, c.st)) ||  // prefixes unknown
       (e = hipStreamSynchronize(c.st)))
     return c.hipfail(e, "set_patterns");
   c.P = P;
@@ -3249,10 +3429,10 @@ int hmc_get_estep_cost(hmc_ctx *h, int32_t *cost) {
   return HMC_OK;
 }
 
-int hmc_get_stamps(hmc_ctx *h, uint64_t *out12) {
-  if (!h || !out12 || !h->c.d_stamps.p) return HMC_EARG;
+int hmc_get_stamps(hmc_ctx *h, uint64_t *out40) {
+  if (!h || !out40 || !h->c.d_stamps.p) return HMC_EARG;
   hipError_t e;
-  if ((e = hipMemcpyAsync(out12, h->c.d_stamps.p, 20 * 8, hipMemcpyDeviceToHost, h->c.st)) ||
+  if ((e = hipMemcpyAsync(out40, h->c.d_stamps.p, 40 * 8, hipMemcpyDeviceToHost, h->c.st)) ||
       (e = hipStreamSynchronize(h->c.st)))
     return h->c.hipfail(e, "get_stamps");
   return HMC_OK;

@@ -256,7 +256,7 @@ struct LdsPlan {
       bytes;
 };
 
-__host__ __device__ inline LdsPlan lds_plan(int S, int fc, int hc, int nw) {
+__host__ __device__ inline LdsPlan lds_plan(int S, int fc, int hc, int nw, int npm) {
   LdsPlan p;
   int o = 0;
   auto take = [&](int bytes) { int r = o; o += (bytes + 15) & ~15; return r; };
@@ -267,7 +267,7 @@ __host__ __device__ inline LdsPlan lds_plan(int S, int fc, int hc, int nw) {
   p.o_smeta = take(nw * WAVE * 4);
   p.o_par = take(nw * WAVE * (int)sizeof(AddPar));
   p.o_bs = take((int)sizeof(BlockShared));
-  p.o_pairs = take((NP_MAX + 2) * 4 + 3 * NP_MAX);
+  p.o_pairs = take((npm + 2) * 4 + 3 * npm);
   p.o_key = take(hc * 8);
   p.o_cnt = take(hc * 4);
   p.o_state = take(hc * 4);
@@ -285,7 +285,9 @@ __host__ __device__ inline LdsPlan lds_plan(int S, int fc, int hc, int nw) {
   return p;
 }
 
-size_t estep_lds_bytes(int S, int fc, int hc, int nw) { return (size_t)lds_plan(S, fc, hc, nw).bytes; }
+size_t estep_lds_bytes(int S, int fc, int hc, int nw, int amax) {
+  return (size_t)lds_plan(S, fc, hc, nw, amax * (amax + 1) / 2).bytes;
+}
 
 // Diagnostic build only (-DHMC_STAMPS): per-phase shader-clock shares.  Each
 // stamp drains the wave's memory counters so a phase is charged with the
@@ -330,12 +332,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void e
   const int S = a.S, L = a.pan.L, amax = a.pan.amax;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;
   const int NT = blockDim.x, NW = NT / WAVE;
-  const LdsPlan plan = lds_plan(S, a.lds_fc, a.lds_hc, NW);
+  const int npm = a.pan.amax * (a.pan.amax + 1) / 2;  // allele pairs of a fully missing locus
+  const LdsPlan plan = lds_plan(S, a.lds_fc, a.lds_hc, NW, npm);
   const Lds l{smem};
-  int *pr_off = (int *)(smem + plan.o_pairs);  // [NP_MAX+2]; [NP_MAX+1] = npairs
-  uint8_t *pr_x = (uint8_t *)(pr_off + NP_MAX + 2);
-  uint8_t *pr_y = pr_x + NP_MAX;
-  uint8_t *pr_o = pr_y + NP_MAX;
+  int *pr_off = (int *)(smem + plan.o_pairs);  // [npm+2]; [npm+1] = npairs
+  uint8_t *pr_x = (uint8_t *)(pr_off + npm + 2);
+  uint8_t *pr_y = pr_x + npm;
+  uint8_t *pr_o = pr_y + npm;
   BlockShared *bs = (BlockShared *)(smem + plan.o_bs);
   // this wave's selection scratch
   const SegScratch ss{(int *)(smem + plan.o_lpos) + wv * WAVE, (int *)(smem + plan.o_rpos) + wv * WAVE,
@@ -503,10 +506,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void e
         int off = 0;
         for (int p = 0; p < np; ++p) { pr_off[p] = off; off += Fp * pr_o[p]; }
         pr_off[np] = off;
-        pr_off[NP_MAX + 1] = np;
+        pr_off[npm + 1] = np;
       }
       __syncthreads();
-      const int npairs = pr_off[NP_MAX + 1];
+      const int npairs = pr_off[npm + 1];
       const int C = pr_off[npairs];
       int Fn = 0;
 
@@ -1009,7 +1012,7 @@ hipError_t launch_estep(const EstepArgs &a, int grid, int nw, hipStream_t st) {
   if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > 65535 || (a.hcap & (a.hcap - 1)) ||
       a.lds_hc < 1 || (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || nw < 1 || nw > 4)
     return hipErrorInvalidValue;
-  const size_t lds = estep_lds_bytes(a.S, a.lds_fc, a.lds_hc, nw);
+  const size_t lds = estep_lds_bytes(a.S, a.lds_fc, a.lds_hc, nw, a.pan.amax);
   static size_t lds_attr = 0;
   if (lds > 65536 && lds > lds_attr) {
     hipError_t e = hipFuncSetAttribute((const void *)estep_forward, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -109,7 +109,7 @@ struct K1Plan {
   int o_pairs, o_bucket, o_front[2], o_keys, o_contrib, bytes;
 };
 
-// npm: allele pairs of a fully missing locus, amax (amax + 1) / 2 <= NP_MAX
+// npm: allele pairs of a fully missing locus, amax (amax + 1) / 2
 __host__ __device__ inline K1Plan k1_plan(int fc, int hc, int cc, int npm) {
   K1Plan p;
   int o = 0;
@@ -182,8 +182,32 @@ size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax) {
   return (size_t)k1_plan(fc, hc, cc, amax * (amax + 1) / 2).bytes;
 }
 
+// Diagnostic build only (-DHMC_STAMPS): lane 0's shader cycles per phase of
+// the structure pass (each stamp drains the wave's memory counters), plus
+// counters; summed over individuals into a.stamps[16].
+#ifdef HMC_STAMPS
+#define S1_T0 unsigned long long s1t = __builtin_amdgcn_s_memtime(), s1acc[16] = {};
+#define S1_ST(k)                                                   \
+  do {                                                             \
+    __builtin_amdgcn_s_waitcnt(0);                                 \
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();    \
+    s1acc[k] += t1 - s1t;                                          \
+    s1t = t1;                                                      \
+  } while (0)
+#define S1_CNT(k, v) s1acc[k] += (unsigned long long)(v)
+#define S1_FLUSH                                                   \
+  if (a.stamps && lane == 0)                                       \
+    for (int k = 0; k < 16; ++k) atomicAdd(&a.stamps[k], s1acc[k]);
+#else
+#define S1_T0
+#define S1_ST(k) do { } while (0)
+#define S1_CNT(k, v) do { } while (0)
+#define S1_FLUSH
+#endif
+
 __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
+  S1_T0
   const int npm = a.pan.amax * (a.pan.amax + 1) / 2;
   const K1Plan plan = k1_plan(a.lds_fc, a.lds_hc, a.lds_cc, npm);
   const int lane = lane_id();
@@ -322,6 +346,7 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
     }
 
     // ---- structure of the forward over loci (HaploBuilder.cpp:47-82) -------
+    S1_ST(5);
     for (int i = hl; i < L && status == EST_OK; ++i) {
       if (Fp == 0) { status = EST_UNRESOLVED; break; }
       const uchar2 gg = g[i];
@@ -353,6 +378,10 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
       const int npairs = pr_off[npm + 1];
       const int C = pr_off[npairs];
       if (C > a.ccap) { status = EST_OVERFLOW_FRONTIER; break; }
+      S1_ST(0);
+      S1_CNT(8, C);
+      S1_CNT(9, Fp);
+      S1_CNT(13, 1);
       int Fn = 0;
       // successor gathers of up to GB chunks issued together (one exposed
       // latency per GB*64 contributions), then the chunks' keys in order
@@ -401,6 +430,8 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
           slot = k1_key_slot(K, ((unsigned long long)lo << 32) | hi, key_hash(lo, hi));
           atomicOr(K.lanes(slot), 1ull << lane);
         }
+        S1_CNT(10, 1);
+        S1_CNT(11, __popcll(__ballot(valid && slot >= (uint32_t)K.hc)));
         wsync();
         uint64_t gm = 0;
         uint32_t cnt0 = 0;
@@ -441,6 +472,8 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
       if (Fn == 0) { status = EST_UNRESOLVED; break; }
       fbig = Fn > fbig ? Fn : fbig;
       wsync();
+      S1_ST(1);
+      S1_CNT(12, Fn > X.fc ? Fn - X.fc : 0);
 
       // contributions per state -> first position (exclusive scan, creation order)
       int Cv = 0;
@@ -485,6 +518,7 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
         }
       }
       wsync();
+      S1_ST(2);
       int nch = 0;
       {
         const int b = lane < NBUCKET ? bucket[lane] : 0;
@@ -526,9 +560,10 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
         R[0] = (uint32_t)Fn;
         R[1] = (uint32_t)Cv;
         R[2] = (uint32_t)nch;
-        R[3] = a.exact ? (uint32_t)C << 10 | (uint32_t)npairs : 0u;  // C < 2^22, npairs <= NP_MAX < 2^10
+        R[3] = a.exact ? (uint32_t)C << 10 | (uint32_t)npairs : 0u;  // C < 2^22, npairs < 2^10 (amax <= 44 in exact mode)
         roff[i + 1] = o;
       }
+      S1_ST(3);
       // m_best_pair.clear() for the next locus
       for (int t0 = 0; t0 < Fn; t0 += WAVE) {
         const int t = t0 + lane;
@@ -543,6 +578,7 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
       X = Y;
       Y = T;
       Fp = Fn;
+      S1_ST(4);
     }
     if (status == EST_OK && Fp == 0) status = EST_UNRESOLVED;
     if (counting && status != EST_OVERFLOW_FRONTIER && status != EST_NO_HEAD_PATTERN) status = EST_OVERFLOW_REC;
@@ -558,7 +594,9 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
       a.fmax[bi] = fbig;
       atomicMax(a.max_states, (unsigned)fbig);
     }
+    S1_ST(6);
   }
+  S1_FLUSH
 }
 
 // ============================================================ pass 2 ======

@@ -153,13 +153,31 @@ __global__ __launch_bounds__(256) void exact_fb(ExactArgs a) {
 }
 
 // The ForwardPatternTree walk of HaploBuilder::estimateFrequency (:296-308,
-// :334-450), one wavefront per (individual, start locus).
+// :334-450), one wavefront per (individual, start locus), sparse like the
+// reference's maps: a node's three lists are held densely per state (zero
+// where absent) but only the states listed in the depth's `touched` list are
+// ever written, and a child's states are found by following the forward
+// links (the extendAll contributions of the record) of its parent's non-zero
+// states, as the reference pushes along forward_links (:369-427).  Each
+// reached state then gathers over its incoming contributions in record order
+// (the same terms; zero sources add +0.0), so the sums do not depend on the
+// order the states were reached in.  Scratch invariant: every dense entry not
+// in a touched list is 0.0 (the host zeroes the scratch before the launch and
+// every item clears what it wrote).
 __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
-  extern __shared__ int stk[];  // [maxd+1] node, [maxd+1] next child
+  extern __shared__ int stk[];  // [maxd+1] node, [maxd+1] next child, [maxd+1] touched count, marks
   const int lane = threadIdx.x;
   const int L = a.L, hl = a.head_len, W = a.width, maxd = a.max_depth;
-  int *snode = stk, *snext = stk + maxd + 1;
+  int *snode = stk, *snext = stk + maxd + 1, *tcnt = stk + 2 * (maxd + 1);
+  uint32_t *marks = (uint32_t *)(stk + 3 * (maxd + 1));  // [fmax/32 + 1] reached-state bitmap
+  const int nwords = (a.fmax + 31) >> 5;
   double *lists = a.scratch + (size_t)blockIdx.x * a.scratch_stride;  // [maxd+1][3][fmax]
+  double *nf = lists + (size_t)(maxd + 1) * 3 * a.fmax;                // [maxd+2]
+  uint32_t *touched = (uint32_t *)(nf + maxd + 2);                      // [maxd+1][fmax]
+  for (int d = lane; d <= maxd; d += WAVE) tcnt[d] = 0;
+  for (int w = lane; w < nwords; w += WAVE) marks[w] = 0u;
+  __builtin_amdgcn_wave_barrier();
+  __threadfence_block();
   const long long n_items = (long long)a.n_order * L;
   for (long long it = blockIdx.x; it < n_items; it += gridDim.x) {
     const int q = (int)(it / L), start = (int)(it % L);
@@ -179,17 +197,14 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
       const double *fw = (const double *)(a.x + xo[e0]);
       for (int t = lane; t < F0; t += WAVE) {
         lists[t] = fw[t];
-        lists[a.fmax + t] = 0.0;
-        lists[2 * a.fmax + t] = 0.0;
+        touched[t] = (uint32_t)t;
       }
-    }
-    // per-depth node frequencies: a child's prefix frequency is its parent's
-    // (the root's children get 1.0, HaploBuilder.cpp:305)
-    double *nf = lists + (size_t)(maxd + 1) * 3 * a.fmax;
-    if (lane == 0) {
-      snode[0] = root;
-      snext[0] = 0;
-      nf[0] = 1.0;
+      if (lane == 0) {
+        tcnt[0] = F0;
+        snode[0] = root;
+        snext[0] = 0;
+        nf[0] = 1.0;  // the root's children get prefix frequency 1.0 (HaploBuilder.cpp:305)
+      }
     }
     __builtin_amdgcn_wave_barrier();
     __threadfence_block();
@@ -213,9 +228,22 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
       const double last_freq = nf[d];
       const double *P0 = lists + (size_t)d * 3 * a.fmax, *P1 = P0 + a.fmax, *P2 = P1 + a.fmax;
       double *C0 = lists + (size_t)(d + 1) * 3 * a.fmax, *C1 = C0 + a.fmax, *C2 = C1 + a.fmax;
+      const uint32_t *Tp = touched + (size_t)d * a.fmax;
+      uint32_t *Tc = touched + (size_t)(d + 1) * a.fmax;
+      // the previous sibling's entries at depth d+1 back to zero
+      {
+        const int nc = tcnt[d + 1];
+        for (int j = lane; j < nc; j += WAVE) {
+          const uint32_t t = Tc[j];
+          C0[t] = 0.0;
+          C1[t] = 0.0;
+          C2[t] = 0.0;
+        }
+      }
       double part = 0.0;
       bool any = false;
-      if (locus < hl) {  // head pairs: their patterns' alleles (HaploBuilder.cpp:340-367)
+      int ntc = 0;
+      if (locus < hl) {  // head pairs: their patterns' alleles (HaploBuilder.cpp:340-367), same states
         const RecView R(Rh, true);
         const uint32_t *plo = R.cb + Fh + 1, *phi = plo + Fh;
         const double *bw = (const double *)(a.x + xo[hl]) + Fh;
@@ -242,30 +270,79 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
           C0[t] = n0;
           C1[t] = n1;
           C2[t] = n2;
+          Tc[t] = (uint32_t)t;
           part += ((n0 + n1) + n2) * bw[t];
           any |= (n0 != 0.0) | (n1 != 0.0) | (n2 != 0.0);
         }
+        ntc = Fh;
       } else {  // along the forward links into the states after `locus` (:369-427)
         const RecView R(a.rec + roff[locus + 1], false);
         const double *bw = (const double *)(a.x + xo[locus + 1]) + R.F;
-        for (int t = lane; t < R.F; t += WAVE) {
+        // (1) mark the states the parent's non-zero states link to and whose
+        //     pair carries the child's allele on either side
+        const int np = tcnt[d];
+        const int Fp = (int)a.rec[roff[locus]];  // states the links leave from
+        for (int j = lane; j < np; j += WAVE) {
+          const uint32_t s = Tp[j];
+          if (P0[s] == 0.0 && P1[s] == 0.0 && P2[s] == 0.0) continue;
+          uint32_t off = 0;
+          for (int p = 0; p < R.NP; ++p) {
+            const uint32_t no = R.npo[p];
+            for (uint32_t o = 0; o < no; ++o) {
+              const uint32_t w = R.out[off + s * no + o];
+              if (w != NONE) {
+                const uint32_t t = w & 0xFFFFu;
+                const uint32_t hd = R.hdr[t];
+                if ((hd & 0xFFu) == (uint32_t)i || ((hd >> 8) & 0xFFu) == (uint32_t)i)
+                  atomicOr(&marks[t >> 5], 1u << (t & 31u));
+              }
+            }
+            off += (uint32_t)Fp * no;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __threadfence_block();
+        // (2) the marked states in ascending order; the bitmap back to zero
+        const int nw = (R.F + 31) >> 5;
+        for (int w0 = 0; w0 < nw; w0 += WAVE) {
+          const int w = w0 + lane;
+          uint32_t bits = w < nw ? marks[w] : 0u;
+          const int c = __popc(bits);
+          int incl = c;
+#pragma unroll
+          for (int dd = 1; dd < 64; dd <<= 1) {
+            const int y = __shfl_up(incl, dd);
+            if (lane >= dd) incl += y;
+          }
+          int at = ntc + incl - c;
+          while (bits) {
+            const int b = __builtin_ctz(bits);
+            bits &= bits - 1u;
+            Tc[at++] = (uint32_t)(w * 32 + b);
+          }
+          if (w < nw) marks[w] = 0u;
+          ntc += __shfl(incl, 63);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __threadfence_block();
+        // (3) each reached state gathers over its incoming contributions
+        for (int j = lane; j < ntc; j += WAVE) {
+          const uint32_t t = Tc[j];
           const uint32_t hd = R.hdr[t];
           const bool ma = (hd & 0xFFu) == (uint32_t)i, mb = ((hd >> 8) & 0xFFu) == (uint32_t)i;
           double n0 = 0.0, n1 = 0.0, n2 = 0.0;
-          if (ma || mb) {
-            const double tp = R.tpv[t];
-            for (uint32_t r = R.cb[t]; r < R.cb[t + 1]; ++r) {
-              const uint32_t w = R.ct[r];
-              const uint32_t s = w & 0xFFFFu;
-              const bool rev = (w >> 16) & 1u;
-              const double w0 = P0[s], w1 = P1[s], w2 = P2[s];
-              if (ma && mb) n0 += w0 * tp;
-              else if (ma) n1 += w0 * tp * 0.5;
-              else n2 += w0 * tp * 0.5;
-              // a-side list follows the a haplotype: links[0] keep it on a, links[1] move it to b
-              if (!rev ? ma : mb) (!rev ? n1 : n2) += w1 * tp;
-              if (!rev ? mb : ma) (!rev ? n2 : n1) += w2 * tp;
-            }
+          const double tp = R.tpv[t];
+          for (uint32_t r = R.cb[t]; r < R.cb[t + 1]; ++r) {
+            const uint32_t w = R.ct[r];
+            const uint32_t s = w & 0xFFFFu;
+            const bool rev = (w >> 16) & 1u;
+            const double w0 = P0[s], w1 = P1[s], w2 = P2[s];
+            if (ma && mb) n0 += w0 * tp;
+            else if (ma) n1 += w0 * tp * 0.5;
+            else n2 += w0 * tp * 0.5;
+            // a-side list follows the a haplotype: links[0] keep it on a, links[1] move it to b
+            if (!rev ? ma : mb) (!rev ? n1 : n2) += w1 * tp;
+            if (!rev ? mb : ma) (!rev ? n2 : n1) += w2 * tp;
           }
           C0[t] = n0;
           C1[t] = n1;
@@ -274,6 +351,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
           any |= (n0 != 0.0) | (n1 != 0.0) | (n2 != 0.0);
         }
       }
+      if (lane == 0) tcnt[d + 1] = ntc;
       const double freq = wave_sum_fixed(part) / pg;
       const int pat = a.tr_data[child];
       if (lane == 0 && pat >= 0) {  // hp->setFrequency(+freq), setPrefixFreq(+last_freq) (:437-441)
@@ -292,7 +370,30 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
         ++d;
       }
     }
+    // the item's entries back to zero (scratch invariant)
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
+    for (int dd = 0; dd <= maxd; ++dd) {
+      const int nc = tcnt[dd];
+      double *D0 = lists + (size_t)dd * 3 * a.fmax;
+      const uint32_t *T = touched + (size_t)dd * a.fmax;
+      for (int j = lane; j < nc; j += WAVE) {
+        const uint32_t t = T[j];
+        D0[t] = 0.0;
+        D0[a.fmax + t] = 0.0;
+        D0[2 * a.fmax + t] = 0.0;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
+    for (int dd = lane; dd <= maxd; dd += WAVE) tcnt[dd] = 0;
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
   }
+}
+
+size_t exact_walk_scratch_doubles(int max_depth, int fmax) {
+  return (size_t)(max_depth + 1) * 3 * fmax + max_depth + 2 + ((size_t)(max_depth + 1) * fmax + 1) / 2;
 }
 
 hipError_t launch_exact_fb(const ExactArgs &a, int grid, hipStream_t st) {
@@ -303,7 +404,8 @@ hipError_t launch_exact_fb(const ExactArgs &a, int grid, hipStream_t st) {
 
 hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st) {
   if (a.n_order <= 0) return hipSuccess;
-  const size_t lds = (size_t)2 * (a.max_depth + 1) * sizeof(int);
+  const size_t lds = (size_t)3 * (a.max_depth + 1) * sizeof(int) + (size_t)((a.fmax + 31) / 32 + 1) * 4;
+  if (lds > 65536) return hipErrorInvalidValue;
   hipLaunchKernelGGL(exact_walk, dim3(grid), dim3(WAVE), lds, st, a);
   return hipGetLastError();
 }

@@ -9,7 +9,7 @@ namespace hmc {
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint8_t MISSING = 0xFF;
 constexpr int S_MAX = 32;    // sample_size limit (2S-link lists fit one wavefront)
-constexpr int A_MAX = 32;    // alleles per locus limit
+constexpr int A_MAX = 64;    // alleles per locus limit (allele indices are u8; exact M-step: 44)
 constexpr int WAVE = 64;
 
 // Link metadata word (one k-best entry, HaploPairLink HaploPair.h:14-28):
@@ -150,6 +150,7 @@ struct StructArgs {
   unsigned long long *re_count;   // [batch]
   int32_t *fmax;                  // [batch]
   unsigned int *max_states;
+  unsigned long long *stamps;     // diagnostic build: [16] shader cycles per phase / counters
 };
 
 // Trace words one locus with F states takes (header, F header words, pad, F x S
@@ -198,7 +199,7 @@ struct TracebackArgs {
 };
 
 size_t estep_scratch_bytes(int fcap, int hcap, int S, int nw);
-size_t estep_lds_bytes(int S, int fc, int hc, int nw);
+size_t estep_lds_bytes(int S, int fc, int hc, int nw, int amax);
 hipError_t launch_test_coop_nth(double *lik, uint32_t *tag, const int *off, const int *n, const int *nth, int count, int sw, hipStream_t st);
 hipError_t launch_estep(const EstepArgs &a, int grid, int nw, hipStream_t st);
 size_t estep_s1_scratch_bytes(int fcap, int hcap, int ccap);

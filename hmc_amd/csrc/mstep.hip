@@ -430,9 +430,9 @@ __global__ void mine_size(MineArgs a, int level, int b, int e) {
   a.size[c] = s;
 }
 
-__global__ void mine_root_size(MineArgs a, uint32_t *rsize) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= a.L) return;
+__global__ void mine_root_size(MineArgs a, uint32_t *rsize, int lo, int hi) {
+  const int s = lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= hi) return;
   uint32_t t = 0;
   const int cb = a.r_child_base[s];
   for (int k = 0; k < a.npos[s]; ++k) t += a.size[cb + k];
@@ -474,6 +474,8 @@ __global__ void mine_emit(MineArgs a, const int *lev_begin, int maxlev, PatternT
     else hi = mid - 1;
   }
   const uint32_t id = a.pos[c];
+  const int32_t par = a.parent[c];
+  t.ppat[id] = is_root(par) ? -1 : ((a.flags[par] & NODE_ACC) ? (int32_t)a.pos[par] : -2);
   t.start[id] = a.start[c];
   t.len[id] = lo;
   t.freq[id] = a.freq[c];
@@ -484,9 +486,9 @@ __global__ void mine_emit(MineArgs a, const int *lev_begin, int maxlev, PatternT
 }
 
 // successor[j] = longest stored suffix of (pattern + allele j) (PatternManager.cpp:308-317).
-__global__ void mine_succ(MineArgs a, PatternTable t, int P) {
-  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (long long)P * a.amax) return;
+__global__ void mine_succ(MineArgs a, PatternTable t, int id0, int P) {
+  const long long gid = (long long)id0 * a.amax + (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= ((long long)id0 + P) * a.amax) return;
   const int id = (int)(gid / a.amax), j = (int)(gid % a.amax);
   const int e = t.start[id] + t.len[id];
   uint32_t res = NONE;
@@ -701,8 +703,9 @@ hipError_t launch_mine_size(const MineArgs &a, int level, int b, int e, hipStrea
   hipLaunchKernelGGL(mine_size, dim3((e - b + 255) / 256), dim3(256), 0, st, a, level, b, e);
   return hipGetLastError();
 }
-hipError_t launch_mine_root_size(const MineArgs &a, uint32_t *rsize, hipStream_t st) {
-  hipLaunchKernelGGL(mine_root_size, dim3((a.L + 255) / 256), dim3(256), 0, st, a, rsize);
+hipError_t launch_mine_root_size(const MineArgs &a, uint32_t *rsize, int lo, int hi, hipStream_t st) {
+  if (hi <= lo) return hipSuccess;
+  hipLaunchKernelGGL(mine_root_size, dim3((hi - lo + 255) / 256), dim3(256), 0, st, a, rsize, lo, hi);
   return hipGetLastError();
 }
 hipError_t launch_mine_pos(const MineArgs &a, int level, int pbeg, int pend, const uint32_t *rpos, hipStream_t st) {
@@ -716,10 +719,10 @@ hipError_t launch_mine_emit(const MineArgs &a, const int *lev_begin, int maxlev,
   hipLaunchKernelGGL(mine_emit, dim3((n + 255) / 256), dim3(256), 0, st, a, lev_begin, maxlev, t);
   return hipGetLastError();
 }
-hipError_t launch_mine_succ(const MineArgs &a, const PatternTable &t, int P, hipStream_t st) {
+hipError_t launch_mine_succ(const MineArgs &a, const PatternTable &t, int id0, int P, hipStream_t st) {
   const long long n = (long long)P * a.amax;
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mine_succ, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, t, P);
+  hipLaunchKernelGGL(mine_succ, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, t, id0, P);
   return hipGetLastError();
 }
 

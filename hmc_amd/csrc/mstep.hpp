@@ -8,7 +8,10 @@ constexpr uint8_t NODE_ACC = 1;  // accepted into m_patterns (PatternManager.cpp
 constexpr uint8_t NODE_EXT = 2;  // extended by one allele   (PatternManager.cpp:110-111)
 
 // Candidate nodes of all levels live in flat arrays; roots (the empty pattern
-// at each start) are virtual and encoded as -(start + 2); -1 = none.
+// at each start) are virtual and encoded as -(start + 2); -1 = none.  Node
+// indices are global over the whole search; when the search runs in blocks
+// of start loci, the arrays hold a window of them and the MineArgs node
+// pointers are offset so that kernels index them globally.
 constexpr int RM_SLOTS = 64;  // R_M counters, 16 words (128 B) apart
 
 struct MineArgs {
@@ -51,6 +54,10 @@ struct MineArgs {
 // Pattern table in id (= DFS pre-order) order.
 struct PatternTable {
   int32_t *start = nullptr, *len = nullptr, *node = nullptr;
+  // prefix pattern (the pattern without its last allele): its id, -1 for
+  // length-1 patterns, -2 when the prefix is no pattern (below min_len, or a
+  // table installed from outside); spells allele strings without the tree
+  int32_t *ppat = nullptr;
   double *freq = nullptr, *prefix = nullptr, *tp = nullptr;
   uint8_t *last = nullptr;
   uint32_t *succ = nullptr;  // [P][amax]
@@ -72,10 +79,12 @@ hipError_t launch_mine_offsets(const MineArgs &a, int b, int e, unsigned long lo
                                hipStream_t st);
 size_t mine_scan_tmp_bytes(int n);
 hipError_t launch_mine_size(const MineArgs &a, int level, int b, int e, hipStream_t st);
-hipError_t launch_mine_root_size(const MineArgs &a, uint32_t *rsize, hipStream_t st);
+// roots [lo, hi) (a block of start loci, see Ctx::mine_impl)
+hipError_t launch_mine_root_size(const MineArgs &a, uint32_t *rsize, int lo, int hi, hipStream_t st);
 hipError_t launch_mine_pos(const MineArgs &a, int level, int pbeg, int pend, const uint32_t *rpos, hipStream_t st);
 hipError_t launch_mine_emit(const MineArgs &a, const int *lev_begin, int maxlev, int n, const PatternTable &t,
                             hipStream_t st);
-hipError_t launch_mine_succ(const MineArgs &a, const PatternTable &t, int P, hipStream_t st);
+// successors of the patterns [id0, id0 + n)
+hipError_t launch_mine_succ(const MineArgs &a, const PatternTable &t, int id0, int n, hipStream_t st);
 
 }  // namespace hmc

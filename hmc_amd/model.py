@@ -166,6 +166,19 @@ class HaploModel:
         """Launch shapes of the split E-step's passes (0 = automatic)."""
         self._check(lib().hmc_set_pass_shapes(self._h, structure_ipc, value_waves, value_ipc))
 
+    def set_store_budgets(self, trace_bytes: int = 0, record_bytes: int = 0):
+        """E-step store budgets in bytes (0 = automatic)."""
+        self._check(lib().hmc_set_store_budgets(self._h, int(trace_bytes), int(record_bytes)))
+
+    def set_mine_block(self, start_loci: int = 0):
+        """Start loci per block of the pattern search (0 = automatic)."""
+        self._check(lib().hmc_set_mine_block(self._h, int(start_loci)))
+
+    def mine_stats(self) -> dict:
+        b, n, g = C.c_int(), C.c_int64(), C.c_double()
+        self._check(lib().hmc_last_mine_stats(self._h, C.byref(b), C.byref(n), C.byref(g)))
+        return dict(blocks=b.value, nodes=n.value, node_window_gb=g.value)
+
     def model_save(self):
         """Keep a device copy of the current pattern table (hmc_model_save)."""
         self._check(lib().hmc_model_save(self._h))

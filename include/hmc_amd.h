@@ -132,6 +132,17 @@ int hmc_find_patterns(hmc_ctx *ctx, int *n_patterns, uint64_t *r_m);
 int hmc_mine_level(hmc_ctx *ctx, int level, int n, const int32_t *start, const int32_t *alleles, double *freq,
                    uint64_t *scanned);
 int hmc_model_info(const hmc_ctx *ctx, int *n_patterns, int *head_len);
+/* Blocks of start loci for the search (0 = automatic: one block up to about
+ * 2.5e7 individual-loci of panel, else blocks of about that size; always one
+ * block for findPatternByNum, heads longer than 1 locus or patterns as long
+ * as half the panel).  The roots of searchPattern's DFS are independent
+ * (PatternManager.cpp:90-108): blocks from locus L-1 down give the same table,
+ * ids and successors, with the candidate-node memory of two blocks and the
+ * matching lists of one.  Values below max_pattern_len + 1 are raised to it. */
+int hmc_set_mine_block(hmc_ctx *ctx, int start_loci);
+/* Last search: blocks, candidate nodes created (all blocks) and the size of
+ * the node arrays kept (GB, ~70 B per node). */
+int hmc_last_mine_stats(const hmc_ctx *ctx, int *blocks, int64_t *nodes, double *node_window_gb);
 /* Pattern table in id order (HaploPattern.h:16-98).  succ[P][max_alleles]
  * holds pattern ids (-1 = none); alleles[P][maxlen] symbols (-1 padding).
  * Any output pointer may be NULL. */
@@ -160,9 +171,10 @@ int hmc_get_estep_stats(hmc_ctx *ctx, int32_t *fmax);
 /* Per individual of the shard: E-step time of the last E-step in units of
  * 1024 shader clocks (value pass; the scheduling key of the next E-step). */
 int hmc_get_estep_cost(hmc_ctx *ctx, int32_t *cost);
-/* Diagnostic build (libhmc_amd_diag.so) only: 20 shader-cycle / event
- * counters of the E-step phases summed over waves; zeros in the product build. */
-int hmc_get_stamps(hmc_ctx *ctx, uint64_t *out20);
+/* Diagnostic build (libhmc_amd_diag.so) only: shader-cycle / event counters
+ * of the last E-step summed over waves, out40[0, 20) the value pass (or fused
+ * kernel), out40[20, 36) the structure pass; zeros in the product build. */
+int hmc_get_stamps(hmc_ctx *ctx, uint64_t *out40);
 /* HaploData samples of this rank: alleles[H][L] symbols, weights[H]. */
 int hmc_get_samples(hmc_ctx *ctx, int32_t *alleles, double *weights, double *total_weight);
 /* Drop the samples so the next hmc_find_patterns mines the genotypes again
@@ -272,6 +284,11 @@ int hmc_set_estep_shape(hmc_ctx *ctx, int waves_per_individual, int individuals_
  * 8 above 4, else 4), value pass waves per individual (1..4) and individuals
  * per CU (rule of hmc_set_estep_shape).  Results do not depend on them. */
 int hmc_set_pass_shapes(hmc_ctx *ctx, int structure_ipc, int value_waves, int value_ipc);
+/* Budgets of the split E-step's two stores in bytes, 0 = automatic: the
+ * k-best trace store (min(42 % of free HBM, 120 GiB)) and the structure-record
+ * store (min(28 %, 80 GiB); 0 with a trace budget given = the same number).
+ * Individuals pass in groups whose records and traces fit them. */
+int hmc_set_store_budgets(hmc_ctx *ctx, uint64_t trace_bytes, uint64_t record_bytes);
 /* E-step implementation: 0 (default) = two passes, a structure pass that
  * replays extendAll/addHaploPair (HaploBuilder.cpp:226-261) on pattern ids
  * and a value pass with the k-best lists, falling back to 1 for individuals

@@ -9,7 +9,7 @@ wpc = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 m = hmc_amd.HaploModel(); m.set_estep_shape(int(os.environ.get('HMC_NW', '3')), wpc); m.load(hmc_amd.GenoData.from_panel(p)); m.find_patterns()
 for it in range(2):
     ll, H, re = m.resolve_all()
-    st = (C.c_uint64 * 20)()
+    st = (C.c_uint64 * 40)()
     hmc_amd.lib().hmc_get_stamps(m._h, st)
     tot = sum(st)
     print(f"E{it+1} fwd {m.timings()['estep_forward_ms']:.1f} ms; cycles per wave-locus (divide by N_waves):")

@@ -20,7 +20,7 @@ m.find_patterns()
 names = ["record hdr", "phase A", "phase B", "trace", "final sync", "final select"]
 for it in range(int(os.environ.get("ITERS", "3"))):
     m.resolve_all()
-    st = (C.c_uint64 * 20)()
+    st = (C.c_uint64 * 40)()
     hmc_amd.lib().hmc_get_stamps(m._h, st)
     s = m.estep_split_stats()
     print(f"  passes: structure {s['structure_passes']} value {s['value_passes']}", flush=True)
