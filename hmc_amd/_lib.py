@@ -92,7 +92,7 @@ _SIGS = [
     ("hmc_write_phase", _i, [_vp, _cp]),
     ("hmc_set_tuning", _i, [_vp, _i, _u64, _i]),
     ("hmc_set_estep_shape", _i, [_vp, _i, _i]),
-    ("hmc_set_pass_shapes", _i, [_vp, _i, _i, _i]),
+    ("hmc_set_pass_shapes", _i, [_vp, _i, _i, _i, _i]),
     ("hmc_set_store_budgets", _i, [_vp, _u64, _u64]),
     ("hmc_set_mine_block", _i, [_vp, _i]),
     ("hmc_last_mine_stats", _i, [_vp, _P(_i), _P(C.c_int64), _P(_d)]),

@@ -270,7 +270,7 @@ struct Ctx {
   // value-pass shape (waves per individual : individuals per CU), 0 = by group
   // size (estep_split: 1:20 from 32 individuals per CU, 2:8 from 8, else 3:8);
   // structure-pass individuals per CU, 0 = by group size (12 / 8 / 4)
-  int vp_nw = 0, vp_ipc = 0, s1_ipc = 0;
+  int vp_nw = 0, vp_ipc = 0, s1_ipc = 0, s1_nw = 0;
   // diagnostics only (stderr logging, never a change of what runs): read once
   // at context creation from HMC_DEBUG_MEM / HMC_DIAG_MINE
   bool debug_mem = false, diag_mine = false;
@@ -2150,10 +2150,16 @@ struct Ctx {
       const int hcap1 = next_pow2(2 * fcap), ccap1 = 8 * fcap;
       // structure pass: one wave per individual; 12 per CU (3 per SIMD at 145
       // VGPRs) above 8 per CU, so cfg 3's E1 groups of 2 200-2 700 run in one
-      // round (profiles/r02/e1_groups/: 603-658 -> 484-586 ms per group)
-      const int bpc1 = s1_ipc > 0 ? s1_ipc : (np > 8 * dev_cu ? 12 : (np > 4 * dev_cu ? 8 : 4));
+      // round (profiles/r02/e1_groups/: 603-658 -> 484-586 ms per group).  On a
+      // model larger than the panel (the genotype-mined M0: 2.5 patterns per
+      // individual-locus at cfg 3, 0.3 later) frontiers are large (cfg 3 E1:
+      // 470 states per locus, 80 % of them past a one-wave block's LDS tier):
+      // four waves per individual, three per CU
+      const bool heavy_model = (double)P > (double)pan.N * (double)pan.L;
+      const int nw1 = s1_nw > 0 ? s1_nw : (heavy_model ? 4 : 1);
+      const int bpc1 = s1_ipc > 0 ? s1_ipc : (nw1 == 4 ? 3 : (np > 8 * dev_cu ? 12 : (np > 4 * dev_cu ? 8 : 4)));
       const int grid1 = std::max(1, std::min(np, dev_cu * bpc1));
-      const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1);
+      const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1, nw1);
       if ((e = d_scr1.ensure(per1 * grid1)) || (e = d_rec_off.ensure((size_t)n * (L + 1))) ||
           (e = d_rec_cursor.ensure(1)) || (e = hipMemsetAsync(d_rec_cursor.p, 0, 8, st)))
         return hipfail(e, "estep pass-1 alloc");
@@ -2170,7 +2176,7 @@ struct Ctx {
       s1.fcap = fcap;
       s1.hcap = hcap1;
       s1.ccap = ccap1;
-      s1_tier(160 * 1024 / bpc1 - 256, pan.amax, s1.lds_fc, s1.lds_hc, s1.lds_cc);
+      s1_tier(160 * 1024 / bpc1 - 256, pan.amax, nw1, s1.lds_fc, s1.lds_hc, s1.lds_cc);
       s1.rec = d_rec.p;
       s1.rec_cap = d_rec.n;
       s1.rec_cursor = d_rec_cursor.p;
@@ -2188,7 +2194,7 @@ struct Ctx {
       if ((e = d_nextq.ensure(2)) || (e = hipMemsetAsync(d_nextq.p, 0, 8, st))) return hipfail(e, "estep");
       s1.next_q = d_nextq.p;
       hipEventRecord(ev[0], st);
-      if ((e = launch_estep_structure(s1, grid1, st))) return hipfail(e, "estep_structure launch");
+      if ((e = launch_estep_structure(s1, grid1, nw1, st))) return hipfail(e, "estep_structure launch");
       hipEventRecord(ev[1], st);
       if ((e = hipMemcpyAsync(rneed.data(), d_rneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
           (e = hipMemcpyAsync(tneed.data(), d_tneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
@@ -2495,10 +2501,10 @@ struct Ctx {
 
   // LDS tiers of pass 1 (one wave per individual, `budget` bytes): states per
   // frontier, key slots (2x, power of two), contributions per locus (2x).
-  static void s1_tier(int budget, int amax, int &fc, int &hc, int &cc) {
-    for (int f = 1024; f >= 16; f -= 16) {
+  static void s1_tier(int budget, int amax, int nw, int &fc, int &hc, int &cc) {
+    for (int f = 2048; f >= 16; f -= 16) {
       const int h = next_pow2(2 * f), c = 2 * f;
-      if ((int)estep_s1_lds_bytes(f, h, c, amax) <= budget) { fc = f; hc = h; cc = c; return; }
+      if ((int)estep_s1_lds_bytes(f, h, c, amax, nw) <= budget) { fc = f; hc = h; cc = c; return; }
     }
     fc = 0;
     hc = 16;
@@ -3045,10 +3051,11 @@ int hmc_set_estep_shape(hmc_ctx *h, int waves_per_individual, int individuals_pe
   return HMC_OK;
 }
 
-int hmc_set_pass_shapes(hmc_ctx *h, int structure_ipc, int value_waves, int value_ipc) {
-  if (!h || structure_ipc < 0 || structure_ipc > 32 || value_waves < 0 || value_waves > 4 || value_ipc < 0 ||
-      value_ipc > 32)
+int hmc_set_pass_shapes(hmc_ctx *h, int structure_waves, int structure_ipc, int value_waves, int value_ipc) {
+  if (!h || (structure_waves != 0 && structure_waves != 1 && structure_waves != 4) || structure_ipc < 0 ||
+      structure_ipc > 32 || value_waves < 0 || value_waves > 4 || value_ipc < 0 || value_ipc > 32)
     return HMC_EARG;
+  h->c.s1_nw = structure_waves;
   h->c.s1_ipc = structure_ipc;
   h->c.vp_nw = value_waves;
   h->c.vp_ipc = value_ipc;

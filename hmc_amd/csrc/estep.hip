@@ -440,19 +440,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void e
         const uint32_t head = a.mod.head_ids[hix];
         const uint8_t ah = a.mod.last[head];
         if (!(m0 || m1 || g0.x == ah || g0.y == ah)) continue;  // head->isMatch(genotype)
-        uint8_t xs[A_MAX];
-        int nx = 0;
+        // the complementary alleles in order (no private array: it would take
+        // registers from the whole kernel)
         const bool hasAllele = g0.x == ah || g0.y == ah;
-        if ((m0 && m1) || ((m0 || m1) && hasAllele)) {
-          for (int x = 0; x < a.pan.anum[0]; ++x)
-            if (a.pan.afreq[x] > 0) xs[nx++] = (uint8_t)x;
-        } else if (!m0 && !m1 && g0.x != g0.y) {
-          xs[nx++] = (ah == g0.x) ? g0.y : g0.x;
-        } else {
-          xs[nx++] = g0.x;  // may be missing: resolved like findLongestMatchPattern
-        }
+        const bool expand = (m0 && m1) || ((m0 || m1) && hasAllele);
+        const int nx = expand ? (int)a.pan.anum[0] : 1;
         for (int k = 0; k < nx; ++k) {
-          uint32_t q = xs[k] == MISSING ? a.mod.head_pat0[amax] : a.mod.head_pat0[xs[k]];
+          uint32_t xk;
+          if (expand) {
+            if (!(a.pan.afreq[k] > 0)) continue;
+            xk = (uint32_t)k;
+          } else {
+            xk = (!m0 && !m1 && g0.x != g0.y) ? ((ah == g0.x) ? g0.y : g0.x)
+                                              : g0.x;  // may be missing: resolved like findLongestMatchPattern
+          }
+          const uint32_t q = xk == MISSING ? a.mod.head_pat0[amax] : a.mod.head_pat0[xk];
           if (q == NONE) { st0 = EST_NO_HEAD_PATTERN; break; }
           if (q < head) continue;  // hp->id() >= head->id()
           if (Fp0 >= a.fcap) { st0 = EST_OVERFLOW_FRONTIER; break; }

@@ -76,22 +76,28 @@ struct IdFront {
   __device__ uint32_t *at(int k, int t) const { return t < fc ? l + k * fc + t : g + (size_t)k * gs + (t - fc); }
 };
 
-// m_best_pair: slots < hc in LDS, the rest in the HBM table.
+// m_best_pair: slots < hc in LDS, the rest in the HBM table.  Per slot the
+// key, one 64-bit lane mask per wavefront of the block (the contributions of
+// the current chunk that carry the key), the count of contributions so far
+// and the state the key created.
+__host__ __device__ inline int k1_slot_bytes(int nw) { return 16 + 8 * nw; }
 struct K1Keys {
   unsigned char *l, *g;
-  int hc, hcap;
+  int hc, hcap, nw;
   __device__ unsigned long long *key(uint32_t s) const {
     return s < (uint32_t)hc ? (unsigned long long *)l + s : (unsigned long long *)g + (s - hc);
   }
-  __device__ unsigned long long *lanes(uint32_t s) const {
-    return s < (uint32_t)hc ? (unsigned long long *)(l + (size_t)hc * 8) + s
-                            : (unsigned long long *)(g + (size_t)hcap * 8) + (s - hc);
+  __device__ unsigned long long *lanes(uint32_t s) const {  // [nw] words
+    return s < (uint32_t)hc ? (unsigned long long *)(l + (size_t)hc * 8) + (size_t)s * nw
+                            : (unsigned long long *)(g + (size_t)hcap * 8) + (size_t)(s - hc) * nw;
   }
   __device__ uint32_t *cnt(uint32_t s) const {
-    return s < (uint32_t)hc ? (uint32_t *)(l + (size_t)hc * 16) + s : (uint32_t *)(g + (size_t)hcap * 16) + (s - hc);
+    return s < (uint32_t)hc ? (uint32_t *)(l + (size_t)hc * (8 + 8 * nw)) + s
+                            : (uint32_t *)(g + (size_t)hcap * (8 + 8 * nw)) + (s - hc);
   }
   __device__ uint32_t *state(uint32_t s) const {
-    return s < (uint32_t)hc ? (uint32_t *)(l + (size_t)hc * 20) + s : (uint32_t *)(g + (size_t)hcap * 20) + (s - hc);
+    return s < (uint32_t)hc ? (uint32_t *)(l + (size_t)hc * (12 + 8 * nw)) + s
+                            : (uint32_t *)(g + (size_t)hcap * (12 + 8 * nw)) + (s - hc);
   }
 };
 
@@ -106,19 +112,20 @@ struct CTier {
 };
 
 struct K1Plan {
-  int o_pairs, o_bucket, o_front[2], o_keys, o_contrib, bytes;
+  int o_pairs, o_bucket, o_red, o_front[2], o_keys, o_contrib, bytes;
 };
 
 // npm: allele pairs of a fully missing locus, amax (amax + 1) / 2
-__host__ __device__ inline K1Plan k1_plan(int fc, int hc, int cc, int npm) {
+__host__ __device__ inline K1Plan k1_plan(int fc, int hc, int cc, int npm, int nw) {
   K1Plan p;
   int o = 0;
   auto take = [&](int bytes) { int r = o; o += (bytes + 15) & ~15; return r; };
   p.o_pairs = take((npm + 2) * 4 + 3 * npm);
   p.o_bucket = take(NBUCKET * 4);
+  p.o_red = take((2 * nw + 4) * 8);
   p.o_front[0] = take(F_NARR * fc * 4);
   p.o_front[1] = take(F_NARR * fc * 4);
-  p.o_keys = take(hc * 24);
+  p.o_keys = take(hc * k1_slot_bytes(nw));
   p.o_contrib = take(3 * cc * 4);
   p.bytes = o;
   return p;
@@ -150,18 +157,79 @@ __device__ inline uint32_t ld_acq(uint32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+constexpr unsigned long long REC_NONE = ~0ull;
+
+// Block-wide helpers of pass 1 (NW wavefronts per individual; NW == 1 keeps
+// the single-wave hand-offs: LDS order within a wave, lane shuffles).
+template <int NW>
+struct Blk {
+  int *red;  // LDS: [NW] wave totals, [NW] second, [8] broadcast words
+  int tid, lane, wv;
+  __device__ void sync() const {
+    if (NW == 1) wsync();
+    else __syncthreads();
+  }
+  // exclusive scan of x over the block in thread order; *total = the sum
+  __device__ int scan(int x, int *total) const {
+    const int incl = wave_incl_scan(x);
+    if (NW == 1) {
+      *total = __shfl(incl, 63);
+      return incl - x;
+    }
+    if (lane == 63) red[wv] = incl;
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int v = red[w];
+      off += w < wv ? v : 0;
+      tot += v;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + incl - x;
+  }
+  __device__ unsigned long long reduce_u64(unsigned long long x) const {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if (NW == 1) return x;
+    unsigned long long *r = (unsigned long long *)(red + 2 * NW + 8);
+    if (lane == 0) r[wv] = x;
+    __syncthreads();
+    unsigned long long t = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += r[w];
+    __syncthreads();
+    return t;
+  }
+  // thread 0's value, to every thread
+  __device__ int bcast(int v) const {
+    if (NW == 1) return __shfl(v, 0);
+    if (tid == 0) red[2 * NW] = v;
+    __syncthreads();
+    const int r = red[2 * NW];
+    __syncthreads();
+    return r;
+  }
+  __device__ unsigned long long bcast64(unsigned long long v) const {
+    const unsigned lo = (unsigned)bcast((int)(uint32_t)v), hi = (unsigned)bcast((int)(uint32_t)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+  }
+};
+
 // Next record of `words` words, or REC_NONE when it does not fit: the store
 // (bump allocator) or the individual's own region (rec_base / rec_size).
-constexpr unsigned long long REC_NONE = ~0ull;
-__device__ inline unsigned long long rec_alloc(const StructArgs &a, unsigned long long &cur, unsigned long long &end,
-                                               unsigned long long words) {
+// Block-uniform call.
+template <int NW>
+__device__ inline unsigned long long rec_alloc(const StructArgs &a, const Blk<NW> &B, unsigned long long &cur,
+                                               unsigned long long &end, unsigned long long words) {
   words = (words + 1) & ~1ull;  // records start on even words (8-byte aligned tpv)
   if (cur + words > end) {
     if (a.rec_base) return REC_NONE;  // past this individual's region
     const unsigned long long take = words > REC_CHUNK ? words : REC_CHUNK;
     unsigned long long base = 0;
-    if (lane_id() == 0) base = atomicAdd(a.rec_cursor, take);
-    base = __shfl(base, 0);
+    if (B.tid == 0) base = atomicAdd(a.rec_cursor, take);
+    base = B.bcast64(base);
     cur = base;
     end = base + take;
   }
@@ -175,14 +243,15 @@ __device__ inline unsigned long long rec_alloc(const StructArgs &a, unsigned lon
 
 __host__ __device__ inline size_t k1_front_words(int fcap) { return al256((size_t)fcap * 4) / 4; }
 
-size_t estep_s1_scratch_bytes(int fcap, int hcap, int ccap) {
-  return 2 * al256(F_NARR * k1_front_words(fcap) * 4) + al256((size_t)hcap * 24) + al256((size_t)ccap * 12);
+size_t estep_s1_scratch_bytes(int fcap, int hcap, int ccap, int nw) {
+  return 2 * al256(F_NARR * k1_front_words(fcap) * 4) + al256((size_t)hcap * k1_slot_bytes(nw)) +
+         al256((size_t)ccap * 12);
 }
-size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax) {
-  return (size_t)k1_plan(fc, hc, cc, amax * (amax + 1) / 2).bytes;
+size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax, int nw) {
+  return (size_t)k1_plan(fc, hc, cc, amax * (amax + 1) / 2, nw).bytes;
 }
 
-// Diagnostic build only (-DHMC_STAMPS): lane 0's shader cycles per phase of
+// Diagnostic build only (-DHMC_STAMPS): thread 0's shader cycles per phase of
 // the structure pass (each stamp drains the wave's memory counters), plus
 // counters; summed over individuals into a.stamps[16].
 #ifdef HMC_STAMPS
@@ -196,7 +265,7 @@ size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax) {
   } while (0)
 #define S1_CNT(k, v) s1acc[k] += (unsigned long long)(v)
 #define S1_FLUSH                                                   \
-  if (a.stamps && lane == 0)                                       \
+  if (a.stamps && tid == 0)                                        \
     for (int k = 0; k < 16; ++k) atomicAdd(&a.stamps[k], s1acc[k]);
 #else
 #define S1_T0
@@ -205,13 +274,19 @@ size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax) {
 #define S1_FLUSH
 #endif
 
-__global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
+// NW wavefronts per individual: one wave (many individuals per CU) or four
+// (the first E-step's large frontiers: 4x the LDS tier and 4x the
+// contributions per step of the extendAll scan).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) void estep_structure(StructArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
+  constexpr int NT = 64 * NW;
   S1_T0
   const int npm = a.pan.amax * (a.pan.amax + 1) / 2;
-  const K1Plan plan = k1_plan(a.lds_fc, a.lds_hc, a.lds_cc, npm);
-  const int lane = lane_id();
+  const K1Plan plan = k1_plan(a.lds_fc, a.lds_hc, a.lds_cc, npm, NW);
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;
   const uint64_t lt = lanemask_lt();
+  const Blk<NW> B{(int *)(smem + plan.o_red), tid, lane, wv};
   const int S = a.S, L = a.pan.L, amax = a.pan.amax, hl = a.mod.head_len;
   int *pr_off = (int *)(smem + plan.o_pairs);  // [npm+2]; [npm+1] = npairs
   uint8_t *pr_x = (uint8_t *)(pr_off + npm + 2);
@@ -225,18 +300,26 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
   sp += al256(F_NARR * (size_t)gs * 4);
   const IdFront FB{(uint32_t *)(smem + plan.o_front[1]), (uint32_t *)sp, a.lds_fc, gs};
   sp += al256(F_NARR * (size_t)gs * 4);
-  const K1Keys K{smem + plan.o_keys, (unsigned char *)sp, a.lds_hc, a.hcap};
-  sp += al256((size_t)a.hcap * 24);
+  const K1Keys K{smem + plan.o_keys, (unsigned char *)sp, a.lds_hc, a.hcap, NW};
+  sp += al256((size_t)a.hcap * k1_slot_bytes(NW));
   const CTier CT{(uint32_t *)(smem + plan.o_contrib), (uint32_t *)sp, a.lds_cc, a.ccap};
+  // the key table's plainly stored fields; with several waves the HBM tier is
+  // read past the vector L1 (another wave of the block may have written it)
+  auto kcnt = [&](uint32_t sl) -> uint32_t {
+    return (NW == 1 || sl < (uint32_t)K.hc) ? *K.cnt(sl) : ld_acq(K.cnt(sl));
+  };
+  auto kstate = [&](uint32_t sl) -> uint32_t {
+    return (NW == 1 || sl < (uint32_t)K.hc) ? *K.state(sl) : ld_acq(K.state(sl));
+  };
 
   auto reset_tables = [&]() {
-    for (int h = lane; h < K.hc + a.hcap; h += WAVE) {
+    for (int h = tid; h < K.hc + a.hcap; h += NT) {
       *K.key(h) = KEY_EMPTY;
-      *K.lanes(h) = 0ull;
+      for (int w = 0; w < NW; ++w) K.lanes(h)[w] = 0ull;
       *K.cnt(h) = 0;
     }
     __threadfence();
-    wsync();
+    B.sync();
   };
   reset_tables();
 
@@ -244,8 +327,8 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
   // blocks finish (longest-processing-time-first), not round-robin
   auto next_q = [&]() -> int {
     int t = 0;
-    if (lane == 0) t = atomicAdd(a.next_q, 1);
-    return __shfl(t, 0) + (int)gridDim.x;
+    if (tid == 0) t = atomicAdd(a.next_q, 1);
+    return B.bcast(t) + (int)gridDim.x;
   };
   for (int q = blockIdx.x; q < a.n_order; q = next_q()) {
     const int bi = a.order[q];
@@ -253,19 +336,19 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
     const uchar2 *g = a.pan.geno_im + (size_t)gi * L;
     unsigned long long *roff = a.rec_off + (size_t)bi * (L + 1);
     int status = EST_OK;
-    unsigned long long re = 0;
+    unsigned long long re = 0;  // per thread; summed at the end
     // records: this individual's reserved region, else the bump allocator; once
     // a record does not fit, `counting` keeps the walk going without writes
     unsigned long long rcur = a.rec_base ? a.rec_base[bi] : 0;
     unsigned long long rend = a.rec_base ? (a.rec_size ? rcur + a.rec_size[bi] : ~0ull) : 0;
     bool counting = false;
-    unsigned long long rneed = 0, tneed = 0;  // exact record / trace words (lane-uniform)
+    unsigned long long rneed = 0, tneed = 0;  // exact record / trace words (block-uniform)
     IdFront X = FA, Y = FB;
 
     // ---- initHeadList (HaploBuilder.cpp:153-224) ----------------------------
     // head_len == 1 on the device; longer heads from the host's list
     int Fp0 = 0, st0 = EST_OK;
-    if (lane == 0 && hl > 1) {
+    if (tid == 0 && hl > 1) {
       const int li = gi - a.mod.hf_base;
       st0 = a.mod.hf_status[li];
       for (uint32_t t = a.mod.hf_off[li]; t < a.mod.hf_off[li + 1] && st0 == EST_OK; ++t) {
@@ -276,26 +359,28 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
         ++Fp0;
       }
     }
-    if (lane == 0 && hl == 1) {
+    if (tid == 0 && hl == 1) {
       const uchar2 g0 = g[0];
       const bool m0 = g0.x == MISSING, m1 = g0.y == MISSING;
       for (int hix = 0; hix < a.mod.n_head; ++hix) {
         const uint32_t head = a.mod.head_ids[hix];
         const uint8_t ah = a.mod.last[head];
         if (!(m0 || m1 || g0.x == ah || g0.y == ah)) continue;  // head->isMatch(genotype)
-        uint8_t xs[A_MAX];
-        int nx = 0;
+        // the complementary alleles in order (no private array: it would take
+        // registers from the whole kernel)
         const bool hasAllele = g0.x == ah || g0.y == ah;
-        if ((m0 && m1) || ((m0 || m1) && hasAllele)) {
-          for (int x = 0; x < a.pan.anum[0]; ++x)
-            if (a.pan.afreq[x] > 0) xs[nx++] = (uint8_t)x;
-        } else if (!m0 && !m1 && g0.x != g0.y) {
-          xs[nx++] = (ah == g0.x) ? g0.y : g0.x;
-        } else {
-          xs[nx++] = g0.x;  // may be missing: resolved like findLongestMatchPattern
-        }
+        const bool expand = (m0 && m1) || ((m0 || m1) && hasAllele);
+        const int nx = expand ? (int)a.pan.anum[0] : 1;
         for (int k = 0; k < nx; ++k) {
-          const uint32_t hq = xs[k] == MISSING ? a.mod.head_pat0[amax] : a.mod.head_pat0[xs[k]];
+          uint32_t xk;
+          if (expand) {
+            if (!(a.pan.afreq[k] > 0)) continue;
+            xk = (uint32_t)k;
+          } else {
+            xk = (!m0 && !m1 && g0.x != g0.y) ? ((ah == g0.x) ? g0.y : g0.x)
+                                              : g0.x;  // may be missing: resolved like findLongestMatchPattern
+          }
+          const uint32_t hq = xk == MISSING ? a.mod.head_pat0[amax] : a.mod.head_pat0[xk];
           if (hq == NONE) { st0 = EST_NO_HEAD_PATTERN; break; }
           if (hq < head) continue;  // hp->id() >= head->id()
           if (Fp0 >= a.fcap) { st0 = EST_OVERFLOW_FRONTIER; break; }
@@ -307,23 +392,23 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
         if (st0 != EST_OK) break;
       }
     }
-    int Fp = __shfl(Fp0, 0);
-    status = __shfl(st0, 0);
+    int Fp = B.bcast(Fp0);
+    status = B.bcast(st0);
     int fbig = Fp;  // the head frontier counts too: the value pass sizes its HBM tier by this
-    wsync();
+    B.sync();
     if (status == EST_OK) {
       const unsigned long long words = 4 + 4ull * Fp + 1 + (a.exact ? 2ull * Fp : 0ull);
       rneed += (words + 1) & ~1ull;
       tneed += a.exact ? 4ull * Fp + 2 : trace_locus_words((unsigned long long)Fp, S);
-      const unsigned long long o = rec_alloc(a, rcur, rend, words);
+      const unsigned long long o = rec_alloc<NW>(a, B, rcur, rend, words);
       if (o == REC_NONE) {
         counting = true;
-        if (lane == 0) re += (unsigned long long)Fp;
+        if (tid == 0) re += (unsigned long long)Fp;
       } else {
         uint32_t *R = a.rec + o;
         double *Rtp = (double *)(R + 4);
         uint32_t *Rhd = R + 4 + 2 * Fp, *Rcb = Rhd + Fp;
-        for (int t = lane; t < Fp; t += WAVE) {
+        for (int t = tid; t < Fp; t += NT) {
           const uint32_t lo = *X.at(F_LO, t), hi = *X.at(F_HI, t);
           Rtp[t] = a.mod.freq[lo] * a.mod.freq[hi];  // HaploPair.cpp:27
           Rhd[t] = (uint32_t)a.mod.last[lo] | (uint32_t)a.mod.last[hi] << 8 | 1u << 16 | (lo == hi ? 1u << 24 : 0u);
@@ -333,15 +418,15 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
             Rcb[2 * Fp + 1 + t] = hi;
           }
         }
-        if (lane == 0) {
+        if (tid == 0) {
           Rcb[Fp] = 0;
           R[0] = (uint32_t)Fp;
           R[1] = 0;
           R[2] = 0;
           R[3] = 0;
           roff[hl] = o;
+          re += (unsigned long long)Fp;
         }
-        if (lane == 0) re += (unsigned long long)Fp;
       }
     }
 
@@ -350,7 +435,7 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
     for (int i = hl; i < L && status == EST_OK; ++i) {
       if (Fp == 0) { status = EST_UNRESOLVED; break; }
       const uchar2 gg = g[i];
-      if (lane == 0) {  // allele-pair list in extendAll call order
+      if (tid == 0) {  // allele-pair list in extendAll call order
         const double *af = a.pan.afreq + (size_t)i * amax;
         const int an = a.pan.anum[i];
         int np = 0;
@@ -374,7 +459,7 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
         pr_off[np] = off;
         pr_off[npm + 1] = np;
       }
-      wsync();
+      B.sync();
       const int npairs = pr_off[npm + 1];
       const int C = pr_off[npairs];
       if (C > a.ccap) { status = EST_OVERFLOW_FRONTIER; break; }
@@ -384,16 +469,16 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
       S1_CNT(13, 1);
       int Fn = 0;
       // successor gathers of up to GB chunks issued together (one exposed
-      // latency per GB*64 contributions), then the chunks' keys in order
+      // latency per GB*NT contributions), then the chunks' keys in order
       constexpr int GB = 4;
       uint32_t g_sa[GB], g_sb[GB], g_s[GB];
-      for (int c0 = 0; c0 < C; c0 += WAVE) {
-        const int c = c0 + lane;
-        const int gq = (c0 / WAVE) % GB;
+      for (int c0 = 0; c0 < C; c0 += NT) {
+        const int c = c0 + tid;
+        const int gq = (c0 / NT) % GB;
         if (gq == 0) {
 #pragma unroll
           for (int q = 0; q < GB; ++q) {
-            const int cq = c + q * WAVE;
+            const int cq = c + q * NT;
             g_sa[q] = g_sb[q] = NONE;
             g_s[q] = 0;
             if (cq < C) {
@@ -428,30 +513,37 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
         }
         if (valid) {
           slot = k1_key_slot(K, ((unsigned long long)lo << 32) | hi, key_hash(lo, hi));
-          atomicOr(K.lanes(slot), 1ull << lane);
+          atomicOr(K.lanes(slot) + wv, 1ull << lane);
         }
         S1_CNT(10, 1);
         S1_CNT(11, __popcll(__ballot(valid && slot >= (uint32_t)K.hc)));
-        wsync();
-        uint64_t gm = 0;
+        B.sync();
+        // this contribution's rank among the chunk's ones with the same key
+        // (waves before it, then lanes below it) and the chunk's count
+        int li = 0, gsz = 0;
         uint32_t cnt0 = 0;
         if (valid) {
-          gm = slot < (uint32_t)K.hc ? *K.lanes(slot) : ld_acq(K.lanes(slot));
-          cnt0 = *K.cnt(slot);
+#pragma unroll
+          for (int w = 0; w < NW; ++w) {
+            const uint64_t m = slot < (uint32_t)K.hc ? K.lanes(slot)[w] : ld_acq(K.lanes(slot) + w);
+            li += w < wv ? __popcll(m) : (w == wv ? __popcll(m & lt) : 0);
+            gsz += __popcll(m);
+          }
+          cnt0 = kcnt(slot);
         }
-        const int li = __popcll(gm & lt), gsz = __popcll(gm);
-        wsync();
+        B.sync();
         if (valid && li == 0) {
           *K.cnt(slot) = cnt0 + (uint32_t)gsz;
-          *K.lanes(slot) = 0ull;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) K.lanes(slot)[w] = 0ull;
         }
         const bool is_new = valid && cnt0 == 0 && li == 0;
-        const uint64_t nm = __ballot(is_new);
-        const int nnew = __popcll(nm);
+        int nnew = 0;
+        const int rk_new = B.scan(is_new ? 1 : 0, &nnew);
         if (Fn + nnew > a.fcap) { status = EST_OVERFLOW_FRONTIER; break; }
         uint32_t st = 0;
         if (is_new) {
-          st = (uint32_t)(Fn + __popcll(nm & lt));
+          st = (uint32_t)(Fn + rk_new);
           *K.state(slot) = st;
           *Y.at(F_LO, (int)st) = lo;
           *Y.at(F_HI, (int)st) = hi;
@@ -459,8 +551,8 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
           *Y.at(F_NS, (int)st) = 0;
         }
         Fn += nnew;
-        wsync();
-        if (valid && !is_new) st = *K.state(slot);
+        B.sync();
+        if (valid && !is_new) st = kstate(slot);
         if (valid) atomicAdd(Y.at(F_NS, (int)st), *X.at(F_NL, (int)s));
         if (c < C) {
           *CT.at(C_SR, c) = s | (rev ? 1u << 16 : 0u);
@@ -471,35 +563,36 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
       if (status != EST_OK) break;
       if (Fn == 0) { status = EST_UNRESOLVED; break; }
       fbig = Fn > fbig ? Fn : fbig;
-      wsync();
+      B.sync();
       S1_ST(1);
       S1_CNT(12, Fn > X.fc ? Fn - X.fc : 0);
 
       // contributions per state -> first position (exclusive scan, creation order)
       int Cv = 0;
-      for (int t0 = 0; t0 < Fn; t0 += WAVE) {
-        const int t = t0 + lane;
-        const int m = t < Fn ? (int)*K.cnt(*Y.at(F_SLOT, t)) : 0;
-        const int incl = wave_incl_scan(m);
-        if (t < Fn) *Y.at(F_CB, t) = (uint32_t)(Cv + incl - m);
-        Cv += __shfl(incl, 63);
+      for (int t0 = 0; t0 < Fn; t0 += NT) {
+        const int t = t0 + tid;
+        const int m = t < Fn ? (int)kcnt(*Y.at(F_SLOT, t)) : 0;
+        int tot = 0;
+        const int ex = B.scan(m, &tot);
+        if (t < Fn) *Y.at(F_CB, t) = (uint32_t)(Cv + ex);
+        Cv += tot;
       }
       const unsigned long long words =
           4 + 4ull * Fn + 1 + (unsigned long long)Cv + Fn + (a.exact ? (unsigned long long)C + npairs : 0ull);
       rneed += (words + 1) & ~1ull;
       tneed += a.exact ? 4ull * Fn + 2 : trace_locus_words((unsigned long long)Fn, S);
-      const unsigned long long o = counting ? 0 : rec_alloc(a, rcur, rend, words);
+      const unsigned long long o = counting ? 0 : rec_alloc<NW>(a, B, rcur, rend, words);
       if (o == REC_NONE) counting = true;
       uint32_t *R = a.rec + (counting ? 0 : o);  // not dereferenced while counting
       double *Rtp = (double *)(R + 4);
       uint32_t *Rhd = R + 4 + 2 * Fn, *Rcb = Rhd + Fn, *Rct = Rcb + Fn + 1, *Rch = Rct + Cv;
-      if (lane < NBUCKET) bucket[lane] = 0;
-      wsync();
+      if (tid < NBUCKET) bucket[tid] = 0;
+      B.sync();
       // per state: k-best list length min(S, sum of predecessor lengths) (the
       // adds keep S once they overflow, HaploPair.cpp:85-88), tp product, last
       // alleles; states whose lists overflow get a chain entry
-      for (int t0 = 0; t0 < Fn; t0 += WAVE) {
-        const int t = t0 + lane;
+      for (int t0 = 0; t0 < Fn; t0 += NT) {
+        const int t = t0 + tid;
         if (t < Fn) {
           const uint32_t lo = *Y.at(F_LO, t), hi = *Y.at(F_HI, t);
           const uint32_t nsum = t < Y.fc ? *Y.at(F_NS, t) : ld_acq(Y.at(F_NS, t));
@@ -512,28 +605,28 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
             Rcb[t] = *Y.at(F_CB, t);
           }
           if (!counting && nsum > (uint32_t)S) {  // bucket 0 = most contributions
-            const int m = (int)*K.cnt(*Y.at(F_SLOT, t));
+            const int m = (int)kcnt(*Y.at(F_SLOT, t));
             atomicAdd(&bucket[NBUCKET - 1 - (m - 1 < NBUCKET - 1 ? m - 1 : NBUCKET - 1)], 1);
           }
         }
       }
-      wsync();
+      B.sync();
       S1_ST(2);
       int nch = 0;
-      {
+      {  // every wave scans the 32 bucket counts; wave 0 writes the offsets
         const int b = lane < NBUCKET ? bucket[lane] : 0;
         const int incl = wave_incl_scan(b);
         nch = __shfl(incl, 63);
-        wsync();
-        if (lane < NBUCKET) bucket[lane] = incl - b;
+        B.sync();
+        if (wv == 0 && lane < NBUCKET) bucket[lane] = incl - b;
       }
-      wsync();
-      for (int t0 = 0; t0 < Fn && !counting; t0 += WAVE) {
-        const int t = t0 + lane;
+      B.sync();
+      for (int t0 = 0; t0 < Fn && !counting; t0 += NT) {
+        const int t = t0 + tid;
         if (t < Fn) {
           const uint32_t nsum = t < Y.fc ? *Y.at(F_NS, t) : ld_acq(Y.at(F_NS, t));
           if (nsum > (uint32_t)S) {
-            const int m = (int)*K.cnt(*Y.at(F_SLOT, t));
+            const int m = (int)kcnt(*Y.at(F_SLOT, t));
             const int pos = atomicAdd(&bucket[NBUCKET - 1 - (m - 1 < NBUCKET - 1 ? m - 1 : NBUCKET - 1)], 1);
             Rch[pos] = (uint32_t)t;
           }
@@ -541,8 +634,8 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
       }
       // contributions of each state in add order
       uint32_t *Rout = Rct + Cv + nch;  // exact: contributions in extendAll order, then pair orientations
-      for (int c0 = 0; c0 < C && !counting; c0 += WAVE) {
-        const int c = c0 + lane;
+      for (int c0 = 0; c0 < C && !counting; c0 += NT) {
+        const int c = c0 + tid;
         if (c < C) {
           const uint32_t st = *CT.at(C_ST, c);
           const uint32_t w = *CT.at(C_SR, c);
@@ -554,8 +647,8 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
         }
       }
       if (a.exact && !counting)
-        for (int p = lane; p < npairs; p += WAVE) Rout[C + p] = pr_o[p];
-      if (lane == 0 && !counting) {
+        for (int p = tid; p < npairs; p += NT) Rout[C + p] = pr_o[p];
+      if (tid == 0 && !counting) {
         Rcb[Fn] = (uint32_t)Cv;
         R[0] = (uint32_t)Fn;
         R[1] = (uint32_t)Cv;
@@ -565,15 +658,15 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
       }
       S1_ST(3);
       // m_best_pair.clear() for the next locus
-      for (int t0 = 0; t0 < Fn; t0 += WAVE) {
-        const int t = t0 + lane;
+      for (int t0 = 0; t0 < Fn; t0 += NT) {
+        const int t = t0 + tid;
         if (t < Fn) {
           const uint32_t sl = *Y.at(F_SLOT, t);
           *K.key(sl) = KEY_EMPTY;
           *K.cnt(sl) = 0;
         }
       }
-      wsync();
+      B.sync();
       const IdFront T = X;
       X = Y;
       Y = T;
@@ -584,9 +677,8 @@ __global__ __launch_bounds__(64) void estep_structure(StructArgs a) {
     if (counting && status != EST_OVERFLOW_FRONTIER && status != EST_NO_HEAD_PATTERN) status = EST_OVERFLOW_REC;
     fbig = Fp > fbig ? Fp : fbig;
     if (status < 0) reset_tables();  // aborted mid-locus: keys may be left
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) re += __shfl_xor(re, o);
-    if (lane == 0) {
+    re = B.reduce_u64(re);
+    if (tid == 0) {
       a.rec_need[bi] = rneed;
       a.trace_need[bi] = tneed;
       a.status[bi] = status;
@@ -1088,20 +1180,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   K2_FLUSH
 }
 
-hipError_t launch_estep_structure(const StructArgs &a, int grid, hipStream_t st) {
+hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStream_t st) {
   if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > 65535 || (a.hcap & (a.hcap - 1)) || a.lds_hc < 1 ||
       (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || a.lds_cc < 0 || a.ccap < 1 || a.mod.head_len < 1 ||
-      (a.mod.head_len > 1 && (!a.mod.hf_off || !a.mod.hf_pairs || !a.mod.hf_status)))
+      (a.mod.head_len > 1 && (!a.mod.hf_off || !a.mod.hf_pairs || !a.mod.hf_status)) || (nw != 1 && nw != 4))
     return hipErrorInvalidValue;
-  const size_t lds = estep_s1_lds_bytes(a.lds_fc, a.lds_hc, a.lds_cc, a.pan.amax);
-  static size_t lds_attr = 0;
-  if (lds > 65536 && lds > lds_attr) {
-    hipError_t e =
-        hipFuncSetAttribute((const void *)estep_structure, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const size_t lds = estep_s1_lds_bytes(a.lds_fc, a.lds_hc, a.lds_cc, a.pan.amax, nw);
+  static size_t lds_attr[2] = {0, 0};
+  const void *f = nw == 4 ? (const void *)estep_structure<4> : (const void *)estep_structure<1>;
+  if (lds > 65536 && lds > lds_attr[nw == 4]) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    lds_attr = lds;
+    lds_attr[nw == 4] = lds;
   }
-  hipLaunchKernelGGL(estep_structure, dim3(grid), dim3(WAVE), lds, st, a);
+  if (nw == 4) hipLaunchKernelGGL(estep_structure<4>, dim3(grid), dim3(4 * WAVE), lds, st, a);
+  else hipLaunchKernelGGL(estep_structure<1>, dim3(grid), dim3(WAVE), lds, st, a);
   return hipGetLastError();
 }
 

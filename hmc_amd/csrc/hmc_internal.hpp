@@ -202,11 +202,12 @@ size_t estep_scratch_bytes(int fcap, int hcap, int S, int nw);
 size_t estep_lds_bytes(int S, int fc, int hc, int nw, int amax);
 hipError_t launch_test_coop_nth(double *lik, uint32_t *tag, const int *off, const int *n, const int *nth, int count, int sw, hipStream_t st);
 hipError_t launch_estep(const EstepArgs &a, int grid, int nw, hipStream_t st);
-size_t estep_s1_scratch_bytes(int fcap, int hcap, int ccap);
-size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax);
+size_t estep_s1_scratch_bytes(int fcap, int hcap, int ccap, int nw);
+size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax, int nw);
 size_t estep_s2_scratch_bytes(int fcap, int S);
 size_t estep_s2_lds_bytes(int S, int fc, int nw);
-hipError_t launch_estep_structure(const StructArgs &a, int grid, hipStream_t st);
+// nw: wavefronts per individual, 1 or 4
+hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStream_t st);
 // wpe: 4 or 5 resident waves per SIMD (register budget of the instantiation)
 hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, int wpe, hipStream_t st);
 hipError_t launch_traceback(const TracebackArgs &a, int total_cands, hipStream_t st);

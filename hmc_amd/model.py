@@ -162,9 +162,10 @@ class HaploModel:
         """E-step launch shape (results are identical for every shape)."""
         self._check(lib().hmc_set_estep_shape(self._h, waves_per_individual, individuals_per_cu))
 
-    def set_pass_shapes(self, structure_ipc: int = 0, value_waves: int = 0, value_ipc: int = 0):
+    def set_pass_shapes(self, structure_waves: int = 0, structure_ipc: int = 0, value_waves: int = 0,
+                        value_ipc: int = 0):
         """Launch shapes of the split E-step's passes (0 = automatic)."""
-        self._check(lib().hmc_set_pass_shapes(self._h, structure_ipc, value_waves, value_ipc))
+        self._check(lib().hmc_set_pass_shapes(self._h, structure_waves, structure_ipc, value_waves, value_ipc))
 
     def set_store_budgets(self, trace_bytes: int = 0, record_bytes: int = 0):
         """E-step store budgets in bytes (0 = automatic)."""

@@ -280,10 +280,13 @@ int hmc_set_tuning(hmc_ctx *ctx, int frontier_cap, uint64_t trace_bytes, int wav
  * same rule.  Results do not depend on the shape. */
 int hmc_set_estep_shape(hmc_ctx *ctx, int waves_per_individual, int individuals_per_cu);
 /* Launch shapes of the split E-step's two passes, 0 = automatic for each:
- * structure pass individuals per CU (automatic: 12 above 8 per CU in the group,
- * 8 above 4, else 4), value pass waves per individual (1..4) and individuals
- * per CU (rule of hmc_set_estep_shape).  Results do not depend on them. */
-int hmc_set_pass_shapes(hmc_ctx *ctx, int structure_ipc, int value_waves, int value_ipc);
+ * structure pass waves per individual (1 or 4; automatic: 4 on a model with
+ * more patterns than the panel has individual-loci, the genotype-mined M0)
+ * and individuals per CU (automatic: 3 at 4 waves; else 12 above 8 per CU in
+ * the group, 8 above 4, else 4), value pass waves per individual (1..4) and
+ * individuals per CU (rule of hmc_set_estep_shape; groups averaging more than
+ * 1 500 record words per locus take 4 x 4).  Results do not depend on them. */
+int hmc_set_pass_shapes(hmc_ctx *ctx, int structure_waves, int structure_ipc, int value_waves, int value_ipc);
 /* Budgets of the split E-step's two stores in bytes, 0 = automatic: the
  * k-best trace store (min(42 % of free HBM, 120 GiB)) and the structure-record
  * store (min(28 %, 80 GiB); 0 with a trace budget given = the same number).

@@ -92,6 +92,24 @@ def test_estep_on_reference_model(oracle_mod, name, S, mode):
     assert_estep_equal(m, o, ll_g, ll_o, H, re_g)
 
 
+@pytest.mark.parametrize("name", ["n60", "a3miss5", "a8", "n300"])
+@pytest.mark.parametrize("shape", [(1, 12, 1, 20), (4, 3, 4, 4), (4, 1, 2, 8), (1, 4, 3, 8)])
+def test_estep_pass_shapes(oracle_mod, name, shape):
+    """Launch shapes of the split E-step's passes (hmc_set_pass_shapes:
+    structure waves per individual 1 or 4, individuals per CU, value-pass
+    shape) change nothing: the E-step on the M0 model equals
+    HaploModel::resolveAll bit for bit."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
+    o.find_patterns()
+    m = gpu_model(p)
+    m.set_pass_shapes(*shape)
+    m.find_patterns()
+    ll_g, H, re_g = m.resolve_all()
+    o.reset_counters()
+    assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
+
+
 @pytest.mark.parametrize("name", ["cfg1", "a3miss5", "a8", "n300"])
 @pytest.mark.parametrize("S", [10, 3])
 def test_value_only_mode_with_order_reruns(oracle_mod, name, S):

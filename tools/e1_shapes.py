@@ -2,7 +2,7 @@
 shapes: M0 once, then per shape hmc_em_rewind + one E-step.  Results must not
 change with the shape (LL printed); times are device ms of the passes.
 
-    python tools/e1_shapes.py CFG "s1ipc:vnw:vipc[:traceGB:recGB]" ...   (0 = automatic)
+    python tools/e1_shapes.py CFG "s1nw:s1ipc:vnw:vipc[:traceGB:recGB]" ...   (0 = automatic)
 """
 import os
 import sys
@@ -24,8 +24,8 @@ print(f"M0 {P} patterns {time.perf_counter() - t0:.1f} s", flush=True)
 m.model_save()
 for sh in shapes:
     f = [int(x) for x in sh.split(":")] + [0, 0]
-    m.set_pass_shapes(f[0], f[1], f[2])
-    m.set_store_budgets(f[3] * 10**9, f[4] * 10**9)
+    m.set_pass_shapes(f[0], f[1], f[2], f[3])
+    m.set_store_budgets(f[4] * 10**9, f[5] * 10**9)
     m.em_rewind()
     t0 = time.perf_counter()
     ll, H, re = m.resolve_all()
