@@ -95,6 +95,8 @@ _SIGS = [
     ("hmc_set_pass_shapes", _i, [_vp, _i, _i, _i, _i]),
     ("hmc_set_store_budgets", _i, [_vp, _u64, _u64]),
     ("hmc_set_mine_block", _i, [_vp, _i]),
+    ("hmc_set_mine_memory", _i, [_vp, C.c_uint64]),
+    ("hmc_last_estep_frontier", _i, [_vp, _P(C.c_int), _P(C.c_int)]),
     ("hmc_last_mine_stats", _i, [_vp, _P(_i), _P(C.c_int64), _P(_d)]),
     ("hmc_model_save", _i, [_vp]),
     ("hmc_em_rewind", _i, [_vp]),

@@ -264,6 +264,7 @@ struct Ctx {
   // tuning
   static constexpr int FCAP_INIT = 2048, FCAP_BIG = 16384;
   int fcap = FCAP_INIT, fcap_user = FCAP_INIT, waves = 0;
+  int ccap_mult = 8;  // structure-pass contributions per locus = ccap_mult * fcap (grows on overflow)
   bool fcap_user_set = false;  // hmc_set_tuning gave a frontier capacity: no automatic start capacity
   int lds_waves_per_cu = 8;  // E-step individuals (blocks) sharing one CU's 160 KiB LDS
   int estep_nw = 2;          // E-step waves per individual (shape sweep at cfg 3: 2:8 beats 3:4 by 25%)
@@ -325,13 +326,16 @@ struct Ctx {
   size_t node_cap = 0;
   DevBuf<uint32_t> l_idx[2];
   DevBuf<double> l_val[2];
-  DevBuf<unsigned long long> s_ext, d_totals, d_rm;
+  DevBuf<unsigned long long> s_ext, d_totals, d_rm, d_rm_save;
   PinnedBuf<unsigned long long> h_totals;  // fixed 2 slots (next list slots, next nodes)
   DevBuf<int32_t> s_child;
   DevBuf<int> d_lev_begin;  // node offset of each mining level (1..maxlev) + end
   std::vector<int> h_lev_begin;
   DevBuf<char> s_tmp;
   DevBuf<uint32_t> d_rsize, d_rpos;
+  DevBuf<int> d_mine_err;
+  DevBuf<double> d_flag;
+  unsigned long long mine_list_cap = 0;  // bytes of one level's matching lists (0 = device memory)  // set when a successor walk needed a node outside the window
 
   // samples (HaploData) and E-step buffers
   int H = 0;
@@ -576,6 +580,7 @@ struct Ctx {
   // by -wbase and use global indices.
   long long wbase = 0;
   bool tree_complete = false;  // the window holds every node of the last mined table (one block)
+  bool nodes_oom = false;  // the last grow_nodes failure was an out-of-memory
   int grow_nodes(size_t need_global, size_t used_global) {
     const size_t need = need_global - (size_t)wbase, used = used_global - (size_t)wbase;
     if (need <= node_cap) return HMC_OK;
@@ -589,7 +594,7 @@ struct Ctx {
     d_rec.release();                                                           \
     e = b.grow_keep(cap, used, st);                                            \
   }                                                                            \
-  if (e) return hipfail(e, "grow_nodes");
+  if (e) { nodes_oom = e == hipErrorOutOfMemory; return hipfail(e, "grow_nodes"); }
     G(n_parent) G(n_start) G(n_child_base) G(n_link) G(n_allele) G(n_flags) G(n_freq) G(n_prefix) G(n_tp) G(n_sum)
     G(n_cnt) G(n_size) G(n_pos) G(n_list_off) G(n_region)
 #undef G
@@ -677,7 +682,9 @@ struct Ctx {
   // threshold, so the tree is mined on the GPU at theta_k and the rounds are
   // replayed on the host over it (bynum_replay); when a round needs an
   // extension the tree does not have, the tree is mined again deeper.
+  static constexpr size_t SCRATCH_MAX = 48ull << 30;  // per-block E-step scratch of one launch, all blocks
   static constexpr int MINE_RETRY = 1000;
+  static constexpr int MINE_SPLIT = 1001;  // a block ran out of device memory: re-run it narrower
   int bynum_need = 0;  // round the replay needed beyond the mined tree
   // ------------------------------------------------------- exact M-step --
   // PatternManager::estimatePatterns (PatternManager.cpp:364-410) and
@@ -847,12 +854,20 @@ struct Ctx {
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return h_cost[x] > h_cost[y]; });
     xacc_nc = nc;
     int rc;
-    while (true) {
-      rc = estep_split(order, true);
-      if (rc != ESTEP_RESTART) break;
-      if ((er = hipMemsetAsync(d_xacc.p, 0, 2 * nc * 8, st))) return hipfail(er, "exact");
+    if (xc_reuse) {
+      if ((rc = exact_group(nullptr, xc_k))) return rc;
+    } else {
+      const int passes0 = n_struct_passes;
+      while (true) {
+        xc_groups = 0;
+        rc = estep_split(order, true);
+        if (rc != ESTEP_RESTART) break;
+        if ((er = hipMemsetAsync(d_xacc.p, 0, 2 * nc * 8, st))) return hipfail(er, "exact");
+      }
+      if (rc) return rc;
+      // one structure pass and one walk group: the stores hold every individual
+      xc_reuse = n_struct_passes == passes0 + 1 && xc_groups == 1;
     }
-    if (rc) return rc;
     std::vector<unsigned long long> acc(2 * nc);
     if ((er = hipMemcpyAsync(acc.data(), d_xacc.p, acc.size() * 8, hipMemcpyDeviceToHost, st)) ||
         (er = hipStreamSynchronize(st)))
@@ -908,6 +923,10 @@ struct Ctx {
     x.head_al = d_head_al.p;
     x.acc_freq = d_xacc.p;
     x.acc_prefix = d_xacc.p + xacc_nc;
+    if (xc_reuse) {  // a later round over the same group: records and fwd/bwd sums are still in place
+      x.fmax = xc_fmax;
+      return exact_walk_group(x, k, dev_cu);
+    }
     if ((e = launch_exact_fb(x, std::max(1, std::min(k, dev_cu * 8)), st))) return hipfail(e, "exact_fb");
     const int n = nloc();
     std::vector<int32_t> xs(n), fm(n);
@@ -922,7 +941,16 @@ struct Ctx {
       fmax = std::max(fmax, fm[ids[q]]);
     }
     x.fmax = fmax;
-    x.scratch_stride = exact_walk_scratch_doubles(tr_maxd, fmax);
+    xc_fmax = fmax;
+    xc_k = k;
+    ++xc_groups;
+    return exact_walk_group(x, k, dev_cu);
+  }
+  // The trie walk of one group (the current round's trie).
+  int exact_walk_group(ExactArgs &x, int k, int dev_cu) {
+    const int L = pan.L;
+    hipError_t e;
+    x.scratch_stride = exact_walk_scratch_doubles(tr_maxd, x.fmax);
     const long long items = (long long)k * L;
     const int grid = (int)std::max<long long>(1, std::min<long long>(items, (long long)dev_cu * 16));
     if ((e = d_xscr.ensure(x.scratch_stride * grid)) ||
@@ -939,6 +967,11 @@ struct Ctx {
     return HMC_OK;
   }
   double ms_walk = 0;
+  // Rounds of one exact M-step share the E-step model: when a round's
+  // individuals ran as one structure pass and one group, the next rounds walk
+  // their new tries over the same records and fwd/bwd sums (exact_walk only).
+  bool xc_reuse = false;
+  int xc_groups = 0, xc_fmax = 1, xc_k = 0;
 
   // Successors of a pattern set (PatternManager::initialize, :308-317):
   // successor[j] = the longest stored suffix of (pattern + allele j) with start
@@ -1058,6 +1091,7 @@ struct Ctx {
     exact_rounds = 0;
     exact_candidates = 0;
     ms_walk = 0;
+    xc_reuse = false;
     Cands cur;
     std::vector<int32_t> succ;
     int rc = table_to_host(cur, succ);
@@ -1112,6 +1146,7 @@ struct Ctx {
       host_successors(kept, ksucc);
       if ((rc = install_host_table(kept, ksucc))) return rc;
     }
+    xc_reuse = false;
     hipEventRecord(ev[5], st);
     hipError_t e;
     if ((e = hipStreamSynchronize(st))) return hipfail(e, "exact");
@@ -1145,11 +1180,13 @@ struct Ctx {
   // Start loci per mining block (hmc_set_mine_block; 0 = automatic).  The
   // roots of the DFS are independent (PatternManager.cpp:90-108), so the
   // search can run over blocks of start loci from L-1 down: pattern ids stay
-  // the DFS pre-order (a block's ids follow those of the blocks above it),
-  // and a block's successors need only its own nodes and the block above it
-  // (suffixes start at most max_len loci later), so the node arrays hold two
-  // blocks and the matching lists one.  One block when the panel is small or
-  // the rules need the whole tree (findPatternByNum, heads longer than 1).
+  // the DFS pre-order (a block's ids follow those of the blocks above it).  A
+  // node's suffix link starts one locus later, so it lies in its own block or
+  // the one above; successors are taken level by level from the first suffix
+  // that is a pattern (mine_succ_level), so the node arrays hold two blocks
+  // and the matching lists one, whatever the pattern lengths.  One block when
+  // the panel is small or the rules need the whole tree (findPatternByNum,
+  // heads longer than 1, whose patterns are not suffix-closed).
   int mine_block_starts = 0;
   int block_width(int L, int mxl, int mnl, int bynum_rounds) const {
     if (bynum_rounds > 0 || mnl > 1) return L;
@@ -1160,8 +1197,7 @@ struct Ctx {
       if (nb <= 1) return L;
       w = (L + nb - 1) / nb;
     }
-    w = std::max(w, mxl + 1);
-    return w >= L ? L : w;
+    return w >= L ? L : std::max(w, 1);
   }
 
   int mine_impl(int *P_out, uint64_t *rm_out, int bynum_rounds) {
@@ -1183,7 +1219,8 @@ struct Ctx {
         (e = d_rsize.ensure(L)) || (e = d_rpos.ensure(L)) || (e = d_r_region.ensure(L)) ||
         (e = hipMemsetAsync(d_rm.p, 0, RM_SLOTS * 16 * 8, st)))
       return hipfail(e, "mine");
-    const int W = block_width(L, mxl, mnl, bynum_rounds);
+    int W = block_width(L, mxl, mnl, bynum_rounds);
+    if ((e = d_mine_err.ensure(1)) || (e = hipMemsetAsync(d_mine_err.p, 0, 4, st))) return hipfail(e, "mine");
     wbase = 0;
     long long next_node = 0;  // global index of the next node
     long long id_base = 0;    // patterns of the blocks above
@@ -1192,16 +1229,38 @@ struct Ctx {
     for (int hi = L; hi > 0;) {
       const int lo = std::max(0, hi - W);
       MineBlock mb;
-      if ((rc = mine_block(lo, hi, mxl, mnl, mf, bynum_rounds, next_node, id_base, mb, rm_bynum))) return rc;
+      if ((e = d_rm_save.ensure(RM_SLOTS * 16)) ||
+          (e = hipMemcpyAsync(d_rm_save.p, d_rm.p, RM_SLOTS * 16 * 8, hipMemcpyDeviceToDevice, st)))
+        return hipfail(e, "mine");
+      rc = mine_block(lo, hi, mxl, mnl, mf, bynum_rounds, next_node, id_base, mb, rm_bynum);
+      if (rc == MINE_SPLIT) {  // nothing of the block is kept: its R_M counts go, its nodes are overwritten
+        if (bynum_rounds > 0 || mnl > 1 || hi - lo <= 1)
+          return fail(HMC_ENOMEM, "pattern search: out of device memory (blocks of %d start loci)", hi - lo);
+        if ((e = hipMemcpyAsync(d_rm.p, d_rm_save.p, RM_SLOTS * 16 * 8, hipMemcpyDeviceToDevice, st)))
+          return hipfail(e, "mine");
+        W = std::max(1, (hi - lo + 1) / 2);
+        if (debug_mem) fprintf(stderr, "[hmc] mine block [%d, %d): out of memory, %d start loci per block from here\n", lo, hi, W);
+        continue;
+      }
+      if (rc) return rc;
       // the block above this one is no longer needed
       if ((rc = slide_window(mb.first_node, mb.end_node))) return rc;
       next_node = mb.end_node;
       id_base += mb.patterns;
-      hi = lo;
       ++nblocks;
+      if (debug_mem && W < L)
+        fprintf(stderr, "[hmc] mine block %d: start loci [%d, %d), %lld patterns so far, node window %lld..%lld\n",
+                nblocks, lo, hi, id_base, (long long)mb.first_node, (long long)mb.end_node);
+      hi = lo;
     }
     tree_complete = nblocks == 1;
     P = (int)id_base;
+    {
+      int merr = 0;
+      if ((e = hipMemcpyAsync(&merr, d_mine_err.p, 4, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+        return hipfail(e, "mine");
+      if (merr) return fail(HMC_EUNSUPPORTED, "successor walk left the node window (blocks of %d start loci)", W);
+    }
     std::vector<unsigned long long> rm_slots((size_t)RM_SLOTS * 16);
     if ((e = hipMemcpyAsync(rm_slots.data(), d_rm.p, rm_slots.size() * 8, hipMemcpyDeviceToHost, st)))
       return hipfail(e, "mine");
@@ -1253,7 +1312,29 @@ struct Ctx {
     std::vector<long long> lbeg{0, 0}, lend{0, 0};  // per level node ranges (index = level), global
     long long n1 = 0;
     for (int k = lo; k < hi; ++k) n1 += h_npos[k];
-    if ((rc = grow_nodes((size_t)std::max<long long>(node0 + n1, 1), (size_t)node0))) return rc;
+    // Out of device memory for the block's nodes or lists: the block is
+    // re-run with half the width (mine_impl).  Ranks agree on it (one flag
+    // all-reduced per level), so that all of them split the same block.
+    auto oom_split = [&](int rc_in, bool oom) -> int {
+      if (multi()) {
+        double f = oom ? 1.0 : 0.0;
+        hipError_t e2;
+        if ((e2 = d_flag.ensure(1)) || (e2 = hipMemcpyAsync(d_flag.p, &f, 8, hipMemcpyHostToDevice, st)))
+          return hipfail(e2, "mine");
+        if (int r2 = allreduce_sum(d_flag.p, 1)) return r2;
+        if ((e2 = hipMemcpyAsync(&f, d_flag.p, 8, hipMemcpyDeviceToHost, st)) || (e2 = hipStreamSynchronize(st)))
+          return hipfail(e2, "mine");
+        oom = f > 0.0;
+      }
+      if (oom) {
+        (void)hipGetLastError();
+        return MINE_SPLIT;
+      }
+      return rc_in;
+    };
+    nodes_oom = false;
+    rc = grow_nodes((size_t)std::max<long long>(node0 + n1, 1), (size_t)node0);
+    if ((rc = oom_split(rc, rc && nodes_oom))) return rc;
     if (node0 + n1 > (long long)INT32_MAX) return fail(HMC_EUNSUPPORTED, "candidate tree exceeds 2^31 nodes");
     // level-1 nodes of the block's roots (r_child_base of root k) and the
     // roots' child lists: root r owns npos[r] x n_items slots of the next buffer
@@ -1282,9 +1363,13 @@ struct Ctx {
       const long long cb = lbeg[level], ce = lend[level];
       const int nlev = (int)(ce - cb);
       const int nxt = cur ^ 1;  // children's lists are written here during the count
-      if ((e = ensure_or_release(l_idx[nxt], std::max<unsigned long long>(next_total, 1)))) return hipfail(e, "mine lists");
-      if (genotype && (e = ensure_or_release(l_val[nxt], std::max<unsigned long long>(next_total, 1))))
-        return hipfail(e, "mine lists");
+      const unsigned long long list_bytes = next_total * (genotype ? 12ull : 4ull);
+      if (mine_list_cap && list_bytes > mine_list_cap) {
+        if ((rc = oom_split(HMC_OK, true))) return rc;
+      }
+      e = ensure_or_release(l_idx[nxt], std::max<unsigned long long>(next_total, 1));
+      if (!e && genotype) e = ensure_or_release(l_val[nxt], std::max<unsigned long long>(next_total, 1));
+      if ((rc = oom_split(e ? hipfail(e, "mine lists") : HMC_OK, e == hipErrorOutOfMemory))) return rc;
       MineArgs a = mine_args(genotype);
       a.lout_idx = l_idx[nxt].p;
       a.lout_val = genotype ? l_val[nxt].p : nullptr;
@@ -1376,7 +1461,9 @@ struct Ctx {
       ++level;
       lbeg.push_back(ce);
       lend.push_back(ce + nnext);
-      if ((rc = grow_nodes((size_t)(ce + nnext), (size_t)ce))) return rc;
+      nodes_oom = false;
+      rc = grow_nodes((size_t)(ce + nnext), (size_t)ce);
+      if ((rc = oom_split(rc, rc && nodes_oom))) return rc;
     }
     const int maxlev = level;
     MineArgs a = mine_args(genotype);
@@ -1416,7 +1503,9 @@ struct Ctx {
         (e = hipMemcpyAsync(d_lev_begin.p, lb.data(), lb.size() * 4, hipMemcpyHostToDevice, st)) ||
         (e = launch_mine_emit(a, d_lev_begin.p, maxlev, lb[maxlev + 1] - lb[1], t, st)))
       return hipfail(e, "mine_emit");
-    if ((e = launch_mine_succ(a, t, (int)id_base, (int)Pb, st))) return hipfail(e, "mine_succ");
+    for (int lv = 1; lv <= maxlev; ++lv)
+      if ((e = launch_mine_succ_level(a, t, lv, (int)lbeg[lv], (int)lend[lv], (int32_t)wbase, d_mine_err.p, st)))
+        return hipfail(e, "mine_succ");
     if (lo == 0) {
       head_len = mnl;
       P = (int)(id_base + Pb);  // the head pairs' lookups see the whole table
@@ -1442,12 +1531,29 @@ struct Ctx {
     hipError_t e;
     n = std::max<size_t>(n, 1);
     const size_t A = (size_t)pan.amax;
-    if ((e = t_start.grow_keep(n, used, st)) || (e = t_len.grow_keep(n, used, st)) ||
-        (e = t_node.grow_keep(n, used, st)) || (e = t_freq.grow_keep(n, used, st)) ||
-        (e = t_prefix.grow_keep(n, used, st)) || (e = t_tp.grow_keep(n, used, st)) ||
-        (e = t_last.grow_keep(n, used, st)) || (e = t_ppat.grow_keep(n, used, st)) ||
-        (e = t_succ.grow_keep(n * A, used * A, st)))
-      return hipfail(e, "grow_table");
+    auto grow = [&]() -> hipError_t {
+      hipError_t r;
+      if ((r = t_start.grow_keep(n, used, st)) || (r = t_len.grow_keep(n, used, st)) ||
+          (r = t_node.grow_keep(n, used, st)) || (r = t_freq.grow_keep(n, used, st)) ||
+          (r = t_prefix.grow_keep(n, used, st)) || (r = t_tp.grow_keep(n, used, st)) ||
+          (r = t_last.grow_keep(n, used, st)) || (r = t_ppat.grow_keep(n, used, st)) ||
+          (r = t_succ.grow_keep(n * A, used * A, st)))
+        return r;
+      return hipSuccess;
+    };
+    if ((e = grow()) == hipErrorOutOfMemory) {
+      // the table grows after a block's search: its matching lists (sized by
+      // the block's largest level) and the E-step stores can go
+      (void)hipGetLastError();
+      for (int k = 0; k < 2; ++k) {
+        l_idx[k].release();
+        l_val[k].release();
+      }
+      d_trace.release();
+      d_rec.release();
+      e = grow();
+    }
+    if (e) return hipfail(e, "grow_table");
     return HMC_OK;
   }
   PatternTable table() const {
@@ -1755,6 +1861,8 @@ struct Ctx {
     }
     const int L = pan.L, S = this->S(), n = nloc();
     if (S > S_MAX) return fail(HMC_EUNSUPPORTED, "sample_size > %d", S_MAX);
+    if (S > 32 && estep_mode != ESTEP_SPLIT)
+      return fail(HMC_EUNSUPPORTED, "sample_size > 32 needs the split E-step (hmc_set_estep_mode 0)");
     hipError_t e;
     if ((e = d_total.ensure(n)) || (e = d_ncand.ensure(n)) || (e = d_status.ensure(n)) || (e = d_re.ensure(n)) ||
         (e = d_sbase.ensure(n)) || (e = d_prior.ensure((size_t)n * S_MAX)) || (e = d_post.ensure((size_t)n * S_MAX)) ||
@@ -2027,8 +2135,8 @@ struct Ctx {
         const int s = h_status[order[pos + q]];
         if (s == EST_NO_HEAD_PATTERN) return fail(HMC_ENOPATTERN, "Can not find matching pattern!");
         if (s == EST_OVERFLOW_FRONTIER) {
-          if (fcap >= 65535) return fail(HMC_EUNSUPPORTED, "frontier exceeds 65535 states");
-          fcap = std::min(65535, fcap * 2);
+          if (fcap >= F_MAX) return fail(HMC_EUNSUPPORTED, "frontier exceeds %d states", F_MAX);
+          fcap = std::min(F_MAX, fcap * 2);
           return ESTEP_RESTART;
         }
         if (s == EST_OVERFLOW_TRACE) ovf_trace = true;
@@ -2147,7 +2255,8 @@ struct Ctx {
             (e = hipMemcpyAsync(d_recsz.p, rs.data(), (size_t)n * 8, hipMemcpyHostToDevice, st)))
           return hipfail(e, "estep");
       }
-      const int hcap1 = next_pow2(2 * fcap), ccap1 = 8 * fcap;
+      const int hcap1 = next_pow2(2 * fcap);
+      const int ccap1 = (int)std::min<int64_t>(INT32_MAX / 2, (int64_t)ccap_mult * fcap);
       // structure pass: one wave per individual; 12 per CU (3 per SIMD at 145
       // VGPRs) above 8 per CU, so cfg 3's E1 groups of 2 200-2 700 run in one
       // round (profiles/r02/e1_groups/: 603-658 -> 484-586 ms per group).  On a
@@ -2158,8 +2267,9 @@ struct Ctx {
       const bool heavy_model = (double)P > (double)pan.N * (double)pan.L;
       const int nw1 = s1_nw > 0 ? s1_nw : (heavy_model ? 4 : 1);
       const int bpc1 = s1_ipc > 0 ? s1_ipc : (nw1 == 4 ? 3 : (np > 8 * dev_cu ? 12 : (np > 4 * dev_cu ? 8 : 4)));
-      const int grid1 = std::max(1, std::min(np, dev_cu * bpc1));
       const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1, nw1);
+      // (huge frontiers: fewer resident individuals rather than scratch past SCRATCH_MAX)
+      const int grid1 = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::min(np, dev_cu * bpc1), SCRATCH_MAX / per1));
       if ((e = d_scr1.ensure(per1 * grid1)) || (e = d_rec_off.ensure((size_t)n * (L + 1))) ||
           (e = d_rec_cursor.ensure(1)) || (e = hipMemsetAsync(d_rec_cursor.p, 0, 8, st)))
         return hipfail(e, "estep pass-1 alloc");
@@ -2224,9 +2334,14 @@ struct Ctx {
       for (int q = 0; q < np; ++q) {
         const int bi = pending[q], s = h_status[bi];
         if (s == EST_NO_HEAD_PATTERN) return fail(HMC_ENOPATTERN, "Can not find matching pattern!");
+        if (s == EST_OVERFLOW_CONTRIB) {  // missing genotypes: up to amax^2 contributions per state
+          if ((int64_t)ccap_mult * fcap >= INT32_MAX / 2) return fail(HMC_EUNSUPPORTED, "too many contributions at a locus");
+          ccap_mult *= 2;
+          return ESTEP_RESTART;
+        }
         if (s == EST_OVERFLOW_FRONTIER) {  // (deferring only these individuals measured slower)
-          if (fcap >= 65535) return fail(HMC_EUNSUPPORTED, "frontier exceeds 65535 states");
-          fcap = std::min(65535, fcap * 2);
+          if (fcap >= F_MAX) return fail(HMC_EUNSUPPORTED, "frontier exceeds %d states", F_MAX);
+          fcap = std::min(F_MAX, fcap * 2);
           return ESTEP_RESTART;
         }
         if (s == EST_OVERFLOW_REC) {
@@ -2319,7 +2434,6 @@ struct Ctx {
         int vnw = vp_nw > 0 ? vp_nw : (heavy ? 4 : ((int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3)));
         int vipc = vp_ipc > 0 ? vp_ipc : (vnw == 1 ? 20 : (vnw == 4 ? 4 : 8));  // a half-given shape completes by the same rule
         const int G2 = std::max(1, std::min(waves > 0 ? waves : dev_cu * vipc, n));
-        const int grid2 = std::max(1, std::min<int>(G2, (int)k));
         // register budget: 5 waves per SIMD once the shape asks for more than 16 per CU
         const int vwpe = vnw * vipc > 16 && vnw * vipc <= 20 ? 5 : 4;
         // the HBM tier of the value frontiers holds the group's largest
@@ -2328,6 +2442,7 @@ struct Ctx {
         for (size_t q = 0; q < k; ++q) fgrp = std::max(fgrp, (int)fbig[sset[pos + q]]);
         fgrp = std::min(fcap, (fgrp + 63) & ~63);
         const size_t per2 = estep_s2_scratch_bytes(fgrp, S);
+        const int grid2 = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::min<int>(G2, (int)k), SCRATCH_MAX / per2));
         if ((e = d_scr2.ensure(per2 * grid2))) return hipfail(e, "estep pass-2 scratch");
         ValueArgs v;
         v.S = S;
@@ -2358,7 +2473,7 @@ struct Ctx {
         v.stamps = d_stamps.p;
         v.next_q = d_nextq.p + 1;
         if ((e = hipMemsetAsync(d_nextq.p + 1, 0, 4, st))) return hipfail(e, "estep");
-        const bool fast = value_fast;
+        const bool fast = value_fast && S <= 32;  // lists longer than a wavefront: exact order only
         hipEventRecord(ev[0], st);
         if ((e = launch_estep_values(v, grid2, vnw, fast, vwpe, st))) return hipfail(e, "estep_values launch");
         hipEventRecord(ev[1], st);
@@ -2402,6 +2517,9 @@ struct Ctx {
         // The fused kernel's frontiers are subsets of pass 1's (it skips pairs
         // with fwd <= 0, HaploBuilder.cpp:237), so it fits the same region.
         n_fallback += (int)h_redo.size();
+        if (!h_redo.empty() && S > 32)
+          return fail(HMC_EUNSUPPORTED, "forward likelihood underflow with sample_size > 32 (%d individuals)",
+                      (int)h_redo.size());
         if (!h_redo.empty()) {
           const int nr = (int)h_redo.size();
           EstepArgs f = estep_args(S);
@@ -2421,8 +2539,8 @@ struct Ctx {
           for (int r : h_redo) {
             const int s = h_status[r];
             if (s == EST_OVERFLOW_FRONTIER) {
-              if (fcap >= 65535) return fail(HMC_EUNSUPPORTED, "frontier exceeds 65535 states");
-              fcap = std::min(65535, fcap * 2);
+              if (fcap >= F_MAX) return fail(HMC_EUNSUPPORTED, "frontier exceeds %d states", F_MAX);
+              fcap = std::min(F_MAX, fcap * 2);
               return ESTEP_RESTART;
             }
             if (s == EST_OVERFLOW_TRACE) return fail(HMC_EHIP, "fallback trace exceeds its region");
@@ -2977,7 +3095,7 @@ int hmc_set_tuning(hmc_ctx *h, int frontier_cap, uint64_t trace_bytes, int waves
   if (!h) return HMC_EARG;
   if (waves < 0) { h->c.lds_waves_per_cu = -waves; waves = 0; }  // negative: E-step waves per CU (LDS split)
   if (frontier_cap > 0) {
-    h->c.fcap = h->c.fcap_user = std::min(frontier_cap, 65535);
+    h->c.fcap = h->c.fcap_user = std::min(frontier_cap, hmc::F_MAX);
     h->c.fcap_user_set = true;
   }
   h->c.trace_bytes = trace_bytes;
@@ -3072,6 +3190,24 @@ int hmc_set_store_budgets(hmc_ctx *h, uint64_t trace_bytes, uint64_t record_byte
 int hmc_set_mine_block(hmc_ctx *h, int start_loci) {
   if (!h || start_loci < 0) return HMC_EARG;
   h->c.mine_block_starts = start_loci;
+  return HMC_OK;
+}
+
+int hmc_last_estep_frontier(hmc_ctx *h, int *max_states, int *frontier_cap) {
+  if (!h) return HMC_EARG;
+  uint32_t m = 0;
+  if (h->c.d_maxst.p) {
+    hipError_t e = hipMemcpy(&m, h->c.d_maxst.p, 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return h->c.hipfail(e, "frontier stats");
+  }
+  if (max_states) *max_states = (int)m;
+  if (frontier_cap) *frontier_cap = h->c.fcap;
+  return HMC_OK;
+}
+
+int hmc_set_mine_memory(hmc_ctx *h, uint64_t list_bytes) {
+  if (!h) return HMC_EARG;
+  h->c.mine_list_cap = list_bytes;
   return HMC_OK;
 }
 

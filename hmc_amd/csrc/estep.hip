@@ -780,12 +780,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void e
   STAMP_FLUSH
 }
 
-// Traceback (HaploPair::getGenotype, HaploPair.cpp:91-124): 16 lanes per
-// individual, one per candidate; walks the trace store from locus L back to
+// Traceback (HaploPair::getGenotype, HaploPair.cpp:91-124): 16, 32 or 64
+// lanes per individual, one per candidate; walks the trace store from locus L back to
 // the head locus and writes both haplotypes as sample rows.
 __global__ __launch_bounds__(256) void estep_traceback(TracebackArgs a) {
-  // one lane per candidate, cw (16 or 32) lanes per individual
-  const int cw = a.S > 16 ? 32 : 16;
+  // one lane per candidate, cw (16, 32 or 64) lanes per individual
+  const int cw = a.S > 32 ? 64 : (a.S > 16 ? 32 : 16);
   const int q = blockIdx.x * (256 / cw) + threadIdx.x / cw;
   const int c = threadIdx.x % cw;
   if (q >= a.nbatch) return;
@@ -1011,7 +1011,7 @@ hipError_t launch_test_coop_nth(double *lik, uint32_t *tag, const int *off, cons
 }
 
 hipError_t launch_estep(const EstepArgs &a, int grid, int nw, hipStream_t st) {
-  if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > 65535 || (a.hcap & (a.hcap - 1)) ||
+  if (a.S < 1 || a.S > 32 || a.pan.amax > A_MAX || a.fcap > F_MAX || (a.hcap & (a.hcap - 1)) ||
       a.lds_hc < 1 || (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || nw < 1 || nw > 4)
     return hipErrorInvalidValue;
   const size_t lds = estep_lds_bytes(a.S, a.lds_fc, a.lds_hc, nw, a.pan.amax);
@@ -1028,7 +1028,7 @@ hipError_t launch_estep(const EstepArgs &a, int grid, int nw, hipStream_t st) {
 hipError_t launch_traceback(const TracebackArgs &a, int, hipStream_t st) {
   if (a.nbatch <= 0) return hipSuccess;
   if (a.S < 1 || a.S > S_MAX) return hipErrorInvalidValue;
-  const int per = 256 / (a.S > 16 ? 32 : 16);  // individuals per block
+  const int per = 256 / (a.S > 32 ? 64 : (a.S > 16 ? 32 : 16));  // individuals per block
   hipLaunchKernelGGL(estep_traceback, dim3((a.nbatch + per - 1) / per), dim3(256), 0, st, a);
   return hipGetLastError();
 }

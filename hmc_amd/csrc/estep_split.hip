@@ -462,7 +462,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
       B.sync();
       const int npairs = pr_off[npm + 1];
       const int C = pr_off[npairs];
-      if (C > a.ccap) { status = EST_OVERFLOW_FRONTIER; break; }
+      if (C > a.ccap) { status = EST_OVERFLOW_CONTRIB; break; }
       S1_ST(0);
       S1_CNT(8, C);
       S1_CNT(9, Fp);
@@ -555,7 +555,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         if (valid && !is_new) st = kstate(slot);
         if (valid) atomicAdd(Y.at(F_NS, (int)st), *X.at(F_NL, (int)s));
         if (c < C) {
-          *CT.at(C_SR, c) = s | (rev ? 1u << 16 : 0u);
+          *CT.at(C_SR, c) = cw_pack(s, rev);
           *CT.at(C_ST, c) = valid ? st : NONE;
           *CT.at(C_RK, c) = cnt0 + (uint32_t)li;
         }
@@ -640,10 +640,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
           const uint32_t st = *CT.at(C_ST, c);
           const uint32_t w = *CT.at(C_SR, c);
           if (st != NONE) {
-            const uint32_t ns = *X.at(F_NL, (int)(w & 0xFFFFu));
+            const uint32_t ns = *X.at(F_NL, (int)cw_state(w));
             Rct[*Y.at(F_CB, (int)st) + *CT.at(C_RK, c)] = w | ns << 24;
           }
-          if (a.exact) Rout[c] = st == NONE ? NONE : (st | (w & (1u << 16)));
+          if (a.exact) Rout[c] = st == NONE ? NONE : (st | (w & CW_REV));
         }
       }
       if (a.exact && !counting)
@@ -674,7 +674,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
       S1_ST(4);
     }
     if (status == EST_OK && Fp == 0) status = EST_UNRESOLVED;
-    if (counting && status != EST_OVERFLOW_FRONTIER && status != EST_NO_HEAD_PATTERN) status = EST_OVERFLOW_REC;
+    if (counting && status != EST_OVERFLOW_FRONTIER && status != EST_OVERFLOW_CONTRIB && status != EST_NO_HEAD_PATTERN)
+      status = EST_OVERFLOW_REC;
     fbig = Fp > fbig ? Fp : fbig;
     if (status < 0) reset_tables();  // aborted mid-locus: keys may be left
     re = B.reduce_u64(re);
@@ -749,6 +750,10 @@ struct K2Plan {
   int o_lpos, o_rpos, o_junk, o_slik, o_smeta, o_bs, o_front[2], bytes;
 };
 
+// Selection slots per wave: one wavefront of lists of 2S links (S <= 32), or
+// one list of 2S links (S > 32).
+__host__ __device__ inline int k2_slots(int S) { return 2 * S > WAVE ? 2 * S : WAVE; }
+
 __host__ __device__ inline K2Plan k2_plan(int S, int fc, int nw) {
   K2Plan p;
   int o = 0;
@@ -756,8 +761,8 @@ __host__ __device__ inline K2Plan k2_plan(int S, int fc, int nw) {
   p.o_lpos = take(nw * WAVE * 4);
   p.o_rpos = take(nw * WAVE * 4);
   p.o_junk = take(nw * 2 * WAVE * 4);
-  p.o_slik = take(nw * WAVE * 8);
-  p.o_smeta = take(nw * WAVE * 4);
+  p.o_slik = take(nw * k2_slots(S) * 8);
+  p.o_smeta = take(nw * k2_slots(S) * 4);
   p.o_bs = take((int)sizeof(K2Shared));
   p.o_front[0] = take(fc * (16 + 12 * S));
   p.o_front[1] = take(fc * (16 + 12 * S));
@@ -859,7 +864,10 @@ size_t estep_s2_lds_bytes(int S, int fc, int nw) { return (size_t)k2_plan(S, fc,
 // non-zero likelihood ties across a list's S-cut and the final candidates are
 // tie-free and non-zero; otherwise the individual reports EST_NEEDS_ORDER and
 // is re-run by the exact instantiation (FAST = false, libstdc++ permutations).
-template <bool FAST, int WPE>
+// WIDE: sample sizes 33..64 — lists of up to 2S = 128 links, one per wave,
+// each lane holding positions k and k + 64, selection by the sequential
+// libstdc++ code on the wave's first lane (the sw > 32 path of seg_nth_slots).
+template <bool FAST, int WPE, bool WIDE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void estep_values(ValueArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int S = a.S, L = a.L, hl = a.head_len;
@@ -867,11 +875,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const int NT = blockDim.x, NW = NT / WAVE;
   const K2Plan plan = k2_plan(S, a.lds_fc, NW);
   K2Shared *bs = (K2Shared *)(smem + plan.o_bs);
+  const int sws = k2_slots(S);  // selection slots per wave
   const SegScratch ss{(int *)(smem + plan.o_lpos) + wv * WAVE, (int *)(smem + plan.o_rpos) + wv * WAVE,
-                      (int *)(smem + plan.o_junk) + wv * 2 * WAVE, (double *)(smem + plan.o_slik) + wv * WAVE,
-                      (uint32_t *)(smem + plan.o_smeta) + wv * WAVE};
-  const Seg sg = make_seg(2 * S);
-  const int G = WAVE / (2 * S);
+                      (int *)(smem + plan.o_junk) + wv * 2 * WAVE, (double *)(smem + plan.o_slik) + wv * sws,
+                      (uint32_t *)(smem + plan.o_smeta) + wv * sws};
+  const Seg sg = make_seg(WIDE ? WAVE : 2 * S);
+  const int G = WIDE ? 1 : WAVE / (2 * S);
   const LinkList W{(double *)(smem + plan.o_slik), (uint32_t *)(smem + plan.o_smeta), 1};  // final selection
 
   char *sp = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
@@ -954,7 +963,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
           for (int u = 0; u < HMC_PA_UNROLL; ++u) ws[u] = rb + u < ce ? Rct[rb + u] : Rct[cb];
 #pragma unroll
-          for (int u = 0; u < HMC_PA_UNROLL; ++u) fs[u] = *X.fwd((int)(ws[u] & 0xFFFFu));
+          for (int u = 0; u < HMC_PA_UNROLL; ++u) fs[u] = *X.fwd((int)cw_state(ws[u]));
 #pragma unroll
           for (int u = 0; u < HMC_PA_UNROLL; ++u)
             if (rb + u < ce) {
@@ -964,17 +973,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         // extension constructor + the appends that still fit
         uint32_t w = Rct[cb];
-        uint32_t s = w & 0xFFFFu, ns = w >> 24;
+        uint32_t s = cw_state(w), ns = cw_ns(w);
         double *yl = Y.lik(t);
         uint32_t *ym = Y.meta(t);
-        copy_extended<HMC_PA_UNROLL>(X.lik((int)s), X.meta((int)s), yl, ym, 0, (int)ns, s, tpv, (w >> 16) & 1u, differ);
+        copy_extended<HMC_PA_UNROLL>(X.lik((int)s), X.meta((int)s), yl, ym, 0, (int)ns, s, tpv, cw_rev(w), differ);
         int k = (int)ns, r0 = ce;
         for (int r = cb + 1; r < ce; ++r) {
           w = Rct[r];
-          s = w & 0xFFFFu;
-          ns = w >> 24;
+          s = cw_state(w);
+          ns = cw_ns(w);
           if (k + (int)ns <= S) {
-            copy_extended<HMC_PA_UNROLL>(X.lik((int)s), X.meta((int)s), yl, ym, k, (int)ns, s, tpv, (w >> 16) & 1u, differ);
+            copy_extended<HMC_PA_UNROLL>(X.lik((int)s), X.meta((int)s), yl, ym, k, (int)ns, s, tpv, cw_rev(w), differ);
             k += (int)ns;
           } else {
             r0 = r;
@@ -1029,7 +1038,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 k0 = (int)*Y.nl(st);
                 wc = Rct[r];
                 wn = r + 1 < re_ ? Rct[r + 1] : 0u;
-                if (sg.k < k0) {
+                if constexpr (WIDE) {
+                  for (int kk = sg.k; kk < k0; kk += WAVE) {
+                    slot_l[kk - sg.k] = Y.lik(st)[kk];
+                    slot_m[kk - sg.k] = Y.meta(st)[kk];
+                  }
+                } else if (sg.k < k0) {
                   *slot_l = Y.lik(st)[sg.k];
                   *slot_m = Y.meta(st)[sg.k];
                 }
@@ -1042,11 +1056,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           if (!wave_ballot(act)) break;
           int n = 0;
           if (act) {
-            const uint32_t s = wc & 0xFFFFu, ns = wc >> 24;
-            const bool rev = (wc >> 16) & 1u;
+            const uint32_t s = cw_state(wc), ns = cw_ns(wc);
+            const bool rev = cw_rev(wc);
             n = k0 + (int)ns;
-            if (sg.k >= k0 && sg.k < n) {  // HaploPair::add transformation (HaploPair.cpp:63-80)
-              const int qk = sg.k - k0;
+            // HaploPair::add transformation (HaploPair.cpp:63-80)
+            auto extend = [&](int kk) {
+              const int qk = kk - k0;
               double lk;
               uint32_t pm;
               X.ld_link((int)s, qk, lk, pm);
@@ -1056,8 +1071,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 if (rev) lk = 0.0;
                 homo = false;
               }
-              *slot_l = lk;
-              *slot_m = meta_pack(s, (uint32_t)qk, rev, homo, false);
+              slot_l[kk - sg.k] = lk;
+              slot_m[kk - sg.k] = meta_pack(s, (uint32_t)qk, rev, homo, false);
+            };
+            if constexpr (WIDE) {
+              for (int kk = sg.k; kk < n; kk += WAVE)
+                if (kk >= k0) extend(kk);
+            } else if (sg.k >= k0 && sg.k < n) {
+              extend(sg.k);
             }
             wc = wn;
             wn = r + 2 < re_ ? Rct[r + 2] : 0u;
@@ -1085,7 +1106,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
               // FAST: a tie recorded on the way that is still at the final cut
               if (FAST && tie_v != 0.0 && tie_v == ss.slik[sg.base + S - 1]) bs->tie = 1;
               tie_v = 0.0;
-              if (sg.k < S) {
+              if constexpr (WIDE) {
+                for (int kk = sg.k; kk < S; kk += WAVE) {
+                  Y.lik(st)[kk] = slot_l[kk - sg.k];
+                  Y.meta(st)[kk] = slot_m[kk - sg.k];
+                }
+              } else if (sg.k < S) {
                 Y.lik(st)[sg.k] = *slot_l;
                 Y.meta(st)[sg.k] = *slot_m;
               }
@@ -1181,7 +1207,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 }
 
 hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStream_t st) {
-  if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > 65535 || (a.hcap & (a.hcap - 1)) || a.lds_hc < 1 ||
+  if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > F_MAX || (a.hcap & (a.hcap - 1)) || a.lds_hc < 1 ||
       (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || a.lds_cc < 0 || a.ccap < 1 || a.mod.head_len < 1 ||
       (a.mod.head_len > 1 && (!a.mod.hf_off || !a.mod.hf_pairs || !a.mod.hf_status)) || (nw != 1 && nw != 4))
     return hipErrorInvalidValue;
@@ -1199,20 +1225,24 @@ hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStre
 }
 
 hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, int wpe, hipStream_t st) {
-  if (a.S < 1 || a.S > S_MAX || a.fcap > 65535 || a.lds_fc < 0 || nw < 1 || nw > 4 || (wpe != 4 && wpe != 5))
+  if (a.S < 1 || a.S > S_MAX || a.fcap > F_MAX || a.lds_fc < 0 || nw < 1 || nw > 4 || (wpe != 4 && wpe != 5) ||
+      (a.S > 32 && fast))
     return hipErrorInvalidValue;
   const size_t lds = estep_s2_lds_bytes(a.S, a.lds_fc, nw);
   static size_t lds_attr = 0;
   if (lds > 65536 && lds > lds_attr) {
     for (const void *f : {(const void *)estep_values<true, 4>, (const void *)estep_values<false, 4>,
-                          (const void *)estep_values<true, 5>, (const void *)estep_values<false, 5>}) {
+                          (const void *)estep_values<true, 5>, (const void *)estep_values<false, 5>,
+                          (const void *)estep_values<false, 4, true>}) {
       hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
     }
     lds_attr = lds;
   }
   const dim3 g(grid), b(WAVE * nw);
-  if (wpe == 5) {
+  if (a.S > 32) {  // lists of more than one wavefront: exact order only
+    hipLaunchKernelGGL((estep_values<false, 4, true>), g, b, lds, st, a);
+  } else if (wpe == 5) {
     if (fast) hipLaunchKernelGGL((estep_values<true, 5>), g, b, lds, st, a);
     else hipLaunchKernelGGL((estep_values<false, 5>), g, b, lds, st, a);
   } else {

@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void exact_fb(ExactArgs a) {
         const double tpv = R.tpv[t];
         double f = 0.0;
         for (uint32_t r = R.cb[t]; r < R.cb[t + 1]; ++r) {
-          const double v = fp[R.ct[r] & 0xFFFFu] * tpv;
+          const double v = fp[cw_state(R.ct[r])] * tpv;
           f = r == R.cb[t] ? v : f + v;
         }
         fw[t] = f;
@@ -137,8 +137,8 @@ __global__ __launch_bounds__(256) void exact_fb(ExactArgs a) {
             const uint32_t no = N.npo[p];
             for (uint32_t o = 0; o < no; ++o) {
               const uint32_t w = N.out[off + (uint32_t)s * no + o];
-              if (w != NONE && ((w >> 16) & 1u) == (uint32_t)pass) {
-                const uint32_t t = w & 0xFFFFu;
+              if (w != NONE && (uint32_t)cw_rev(w) == (uint32_t)pass) {
+                const uint32_t t = cw_state(w);
                 b += bn[t] * N.tpv[t];
               }
             }
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
             for (uint32_t o = 0; o < no; ++o) {
               const uint32_t w = R.out[off + s * no + o];
               if (w != NONE) {
-                const uint32_t t = w & 0xFFFFu;
+                const uint32_t t = cw_state(w);
                 const uint32_t hd = R.hdr[t];
                 if ((hd & 0xFFu) == (uint32_t)i || ((hd >> 8) & 0xFFu) == (uint32_t)i)
                   atomicOr(&marks[t >> 5], 1u << (t & 31u));
@@ -334,8 +334,8 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
           const double tp = R.tpv[t];
           for (uint32_t r = R.cb[t]; r < R.cb[t + 1]; ++r) {
             const uint32_t w = R.ct[r];
-            const uint32_t s = w & 0xFFFFu;
-            const bool rev = (w >> 16) & 1u;
+            const uint32_t s = cw_state(w);
+            const bool rev = cw_rev(w);
             const double w0 = P0[s], w1 = P1[s], w2 = P2[s];
             if (ma && mb) n0 += w0 * tp;
             else if (ma) n1 += w0 * tp * 0.5;

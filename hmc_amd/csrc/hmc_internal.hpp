@@ -8,22 +8,37 @@ namespace hmc {
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint8_t MISSING = 0xFF;
-constexpr int S_MAX = 32;    // sample_size limit (2S-link lists fit one wavefront)
+constexpr int S_MAX = 64;    // sample_size limit (lists of 2S links: segments of one wavefront up to
+                             // S = 32, one list per wave over two lanes' slots above; fused kernel: 32)
 constexpr int A_MAX = 64;    // alleles per locus limit (allele indices are u8; exact M-step: 44)
 constexpr int WAVE = 64;
 
 // Link metadata word (one k-best entry, HaploPairLink HaploPair.h:14-28):
 //   bits 0-15 predecessor state, 16-23 index in the predecessor's list,
 //   bit 24 reversed, bit 25 homozygous, bit 26 head (link == NULL).
+// State ids (positions in a locus's frontier) take F_BITS bits: frontiers of
+// up to F_MAX states per individual and locus.
+constexpr int F_BITS = 21;
+constexpr uint32_t F_MASK = (1u << F_BITS) - 1u;
+constexpr int F_MAX = (int)F_MASK;  // 2 097 151
+// Link word (a k-best list entry, also the trace store's): predecessor state,
+// index in its list, and the reversed / homozygous / head flags.
 __host__ __device__ inline uint32_t meta_pack(uint32_t pred, uint32_t idx, bool rev, bool homo, bool head) {
-  return (pred & 0xFFFFu) | ((idx & 0xFFu) << 16) | (rev ? 1u << 24 : 0u) | (homo ? 1u << 25 : 0u) |
-         (head ? 1u << 26 : 0u);
+  return (pred & F_MASK) | ((idx & 0xFFu) << F_BITS) | (rev ? 1u << 29 : 0u) | (homo ? 1u << 30 : 0u) |
+         (head ? 1u << 31 : 0u);
 }
-__host__ __device__ inline uint32_t meta_pred(uint32_t m) { return m & 0xFFFFu; }
-__host__ __device__ inline uint32_t meta_idx(uint32_t m) { return (m >> 16) & 0xFFu; }
-__host__ __device__ inline bool meta_rev(uint32_t m) { return (m >> 24) & 1u; }
-__host__ __device__ inline bool meta_homo(uint32_t m) { return (m >> 25) & 1u; }
-__host__ __device__ inline bool meta_head(uint32_t m) { return (m >> 26) & 1u; }
+__host__ __device__ inline uint32_t meta_pred(uint32_t m) { return m & F_MASK; }
+__host__ __device__ inline uint32_t meta_idx(uint32_t m) { return (m >> F_BITS) & 0xFFu; }
+__host__ __device__ inline bool meta_rev(uint32_t m) { return (m >> 29) & 1u; }
+__host__ __device__ inline bool meta_homo(uint32_t m) { return (m >> 30) & 1u; }
+__host__ __device__ inline bool meta_head(uint32_t m) { return (m >> 31) & 1u; }
+// Contribution word of the structure records: predecessor state, reversed
+// flag, and (bits 24..31) the predecessor's list length.
+constexpr uint32_t CW_REV = 1u << F_BITS;
+__host__ __device__ inline uint32_t cw_pack(uint32_t s, bool rev) { return s | (rev ? CW_REV : 0u); }
+__host__ __device__ inline uint32_t cw_state(uint32_t w) { return w & F_MASK; }
+__host__ __device__ inline bool cw_rev(uint32_t w) { return (w >> F_BITS) & 1u; }
+__host__ __device__ inline uint32_t cw_ns(uint32_t w) { return w >> 24; }
 
 // Per-state trace header word: last allele of pattern a / b, link count.
 __host__ __device__ inline uint32_t hdr_pack(uint32_t al_a, uint32_t al_b, uint32_t n) {
@@ -38,6 +53,7 @@ enum EStatus : int32_t {
   EST_OVERFLOW_TRACE = -2,     // trace buffer exhausted
   EST_NO_HEAD_PATTERN = -3,    // "Can not find matching pattern!" (HaploBuilder.cpp:215-217)
   EST_OVERFLOW_REC = -4,       // structure-record store exhausted (split E-step)
+  EST_OVERFLOW_CONTRIB = -5,   // more contributions at a locus than the structure pass's capacity
   EST_NEEDS_EXACT = 2,         // split E-step: a forward likelihood underflowed to 0 before
                                // the last locus, so extend() would skip that pair
                                // (HaploBuilder.cpp:237) — re-run on the fused kernel

@@ -485,40 +485,54 @@ __global__ void mine_emit(MineArgs a, const int *lev_begin, int maxlev, PatternT
   t.node[id] = c;
 }
 
-// successor[j] = longest stored suffix of (pattern + allele j) (PatternManager.cpp:308-317).
-__global__ void mine_succ(MineArgs a, PatternTable t, int id0, int P) {
-  const long long gid = (long long)id0 * a.amax + (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= ((long long)id0 + P) * a.amax) return;
-  const int id = (int)(gid / a.amax), j = (int)(gid % a.amax);
-  const int e = t.start[id] + t.len[id];
+// successor[j] = longest stored suffix of (pattern + allele j)
+// (PatternManager.cpp:308-317), for the patterns of one level (length
+// `level`, nodes [cb, ce)).  The walk goes down the suffix links; the first
+// suffix that is itself a pattern is shorter, so its successor for the same
+// extension locus is already in the table (an earlier level, or a block of
+// higher start loci), and the rest of the walk would be exactly its walk: the
+// answer is taken from there.  Frequent patterns' suffixes are frequent, so
+// this is normally one step, and it never leaves the node window (a suffix
+// link reaches at most one block up).  Nodes below `node_lo` (slid out of the
+// window) are never read: a walk that would need one sets *err.
+__global__ void mine_succ_level(MineArgs a, PatternTable t, int level, int cb, int ce, int32_t node_lo, int *err) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long long)(ce - cb) * a.amax) return;
+  const int c = cb + (int)(gid / a.amax), j = (int)(gid % a.amax);
+  if (!(a.flags[c] & NODE_ACC)) return;
+  const uint32_t id = a.pos[c];
+  const int e = a.start[c] + level;
   uint32_t res = NONE;
+  bool lost = false;
   if (e < a.L && j < a.anum[e]) {
     const uint8_t rk = a.rank_of[(size_t)e * a.amax + j];
-    int32_t u = t.node[id];
-    int depth = 0;  // number of leading alleles dropped so far
+    int32_t u = c;
+    int depth = 0;  // leading alleles dropped so far
     while (true) {
       if (is_root(u)) {
         if (rk != 0xFF) {
-          const int c = a.r_child_base[root_start(u)] + rk;
-          if (a.flags[c] & NODE_ACC) res = a.pos[c];
+          const int ch = a.r_child_base[root_start(u)] + rk;
+          if (ch < node_lo) { lost = true; break; }
+          if (a.flags[ch] & NODE_ACC) res = a.pos[ch];
         }
         break;
       }
       if (u == -1) {
-        // Chain broken: the suffix dropped `depth` alleles is no candidate.
-        // Navigate the shorter suffixes from their roots (rare; exact walk).
-        // The pattern's alleles are read through a window of AW positions,
-        // refilled by walking the parent chain, so any pattern length works.
+        // Chain broken: the suffix dropped so far is no candidate (models
+        // whose patterns are not suffix-closed: min_len > 1, findPatternByNum
+        // — searched in one block).  Navigate the shorter suffixes from their
+        // roots.  The pattern's alleles are read through a window of AW
+        // positions, refilled by walking the parent chain.
         constexpr int AW = 128;
-        const int vs = t.start[id];
-        const int L0 = t.len[id];
+        const int vs = a.start[c];
+        const int L0 = level;
         uint8_t al[AW];
         int w0 = -1;  // first position held in the window (-1: empty)
         auto allele_at = [&](int q) -> uint8_t {
           if (w0 < 0 || q < w0 || q >= w0 + AW) {
             w0 = q;
             const int hi = min(q + AW, L0) - 1;
-            int32_t w = t.node[id];
+            int32_t w = c;
             for (int r = L0 - 1; r > hi; --r) w = a.parent[w];
             for (int r = hi; r >= q; --r) {
               al[r - q] = a.allele[w];
@@ -527,7 +541,7 @@ __global__ void mine_succ(MineArgs a, PatternTable t, int id0, int P) {
           }
           return al[q - w0];
         };
-        for (int d = depth + 1; d <= L0 && res == NONE; ++d) {
+        for (int d = depth + 1; d <= L0 && res == NONE && !lost; ++d) {
           const int ks = vs + d;  // suffix start
           int32_t nd = root_code(ks);
           bool ok = true;
@@ -538,25 +552,34 @@ __global__ void mine_succ(MineArgs a, PatternTable t, int id0, int P) {
             if (is_root(nd)) nd = a.r_child_base[root_start(nd)] + r;
             else if (a.flags[nd] & NODE_EXT) nd = a.child_base[nd] + r;
             else ok = false;
+            if (ok && nd < node_lo) lost = true;
+            ok = ok && !lost;
           }
           if (!ok || rk == 0xFF) continue;
-          int c;
-          if (is_root(nd)) c = a.r_child_base[root_start(nd)] + rk;
-          else if (a.flags[nd] & NODE_EXT) c = a.child_base[nd] + rk;
+          int ch;
+          if (is_root(nd)) ch = a.r_child_base[root_start(nd)] + rk;
+          else if (a.flags[nd] & NODE_EXT) ch = a.child_base[nd] + rk;
           else continue;
-          if (a.flags[c] & NODE_ACC) res = a.pos[c];
+          if (ch < node_lo) { lost = true; break; }
+          if (a.flags[ch] & NODE_ACC) res = a.pos[ch];
         }
         break;
       }
+      if (u < node_lo) { lost = true; break; }
+      if (depth > 0 && (a.flags[u] & NODE_ACC)) {  // a shorter pattern: its successor is known
+        res = t.succ[(size_t)a.pos[u] * a.amax + j];
+        break;
+      }
       if ((a.flags[u] & NODE_EXT) && rk != 0xFF) {
-        const int c = a.child_base[u] + rk;
-        if (a.flags[c] & NODE_ACC) { res = a.pos[c]; break; }
+        const int ch = a.child_base[u] + rk;
+        if (a.flags[ch] & NODE_ACC) { res = a.pos[ch]; break; }
       }
       u = a.link[u];
       ++depth;
     }
   }
-  t.succ[gid] = res;
+  if (lost) atomicOr(err, 1);
+  t.succ[(size_t)id * a.amax + j] = res;
 }
 
 // ---- host-side launch helpers -----------------------------------------------
@@ -719,10 +742,12 @@ hipError_t launch_mine_emit(const MineArgs &a, const int *lev_begin, int maxlev,
   hipLaunchKernelGGL(mine_emit, dim3((n + 255) / 256), dim3(256), 0, st, a, lev_begin, maxlev, t);
   return hipGetLastError();
 }
-hipError_t launch_mine_succ(const MineArgs &a, const PatternTable &t, int id0, int P, hipStream_t st) {
-  const long long n = (long long)P * a.amax;
+hipError_t launch_mine_succ_level(const MineArgs &a, const PatternTable &t, int level, int cb, int ce, int32_t node_lo,
+                                  int *err, hipStream_t st) {
+  const long long n = (long long)(ce - cb) * a.amax;
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mine_succ, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, t, id0, P);
+  hipLaunchKernelGGL(mine_succ_level, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, t, level, cb, ce, node_lo,
+                     err);
   return hipGetLastError();
 }
 

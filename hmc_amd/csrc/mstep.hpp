@@ -85,6 +85,9 @@ hipError_t launch_mine_pos(const MineArgs &a, int level, int pbeg, int pend, con
 hipError_t launch_mine_emit(const MineArgs &a, const int *lev_begin, int maxlev, int n, const PatternTable &t,
                             hipStream_t st);
 // successors of the patterns [id0, id0 + n)
-hipError_t launch_mine_succ(const MineArgs &a, const PatternTable &t, int id0, int n, hipStream_t st);
+// Successors of the patterns of one level (nodes [cb, ce) of length `level`),
+// levels in increasing length; *err |= 1 if a walk needed a node below node_lo.
+hipError_t launch_mine_succ_level(const MineArgs &a, const PatternTable &t, int level, int cb, int ce, int32_t node_lo,
+                                  int *err, hipStream_t st);
 
 }  // namespace hmc

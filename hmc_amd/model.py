@@ -175,6 +175,17 @@ class HaploModel:
         """Start loci per block of the pattern search (0 = automatic)."""
         self._check(lib().hmc_set_mine_block(self._h, int(start_loci)))
 
+    def estep_frontier(self) -> dict:
+        """Largest frontier of the last E-step and the state capacity it ran with."""
+        ms, fc = C.c_int(), C.c_int()
+        self._check(lib().hmc_last_estep_frontier(self._h, C.byref(ms), C.byref(fc)))
+        return dict(max_states=ms.value, capacity=fc.value)
+
+    def set_mine_memory(self, list_bytes: int = 0):
+        """Cap one search level's matching lists (bytes; 0 = device memory):
+        a block over it is re-run with half the width."""
+        self._check(lib().hmc_set_mine_memory(self._h, int(list_bytes)))
+
     def mine_stats(self) -> dict:
         b, n, g = C.c_int(), C.c_int64(), C.c_double()
         self._check(lib().hmc_last_mine_stats(self._h, C.byref(b), C.byref(n), C.byref(g)))

@@ -134,12 +134,22 @@ int hmc_mine_level(hmc_ctx *ctx, int level, int n, const int32_t *start, const i
 int hmc_model_info(const hmc_ctx *ctx, int *n_patterns, int *head_len);
 /* Blocks of start loci for the search (0 = automatic: one block up to about
  * 2.5e7 individual-loci of panel, else blocks of about that size; always one
- * block for findPatternByNum, heads longer than 1 locus or patterns as long
- * as half the panel).  The roots of searchPattern's DFS are independent
- * (PatternManager.cpp:90-108): blocks from locus L-1 down give the same table,
- * ids and successors, with the candidate-node memory of two blocks and the
- * matching lists of one.  Values below max_pattern_len + 1 are raised to it. */
+ * block for findPatternByNum and heads longer than 1 locus).  The roots of
+ * searchPattern's DFS are independent (PatternManager.cpp:90-108): blocks
+ * from locus L-1 down give the same table, ids and successors, with the
+ * candidate-node memory of two blocks and the matching lists of one, for any
+ * pattern length.  A block whose nodes or lists do not fit in device memory
+ * (or in hmc_set_mine_memory's cap) is re-run with half the width, and the
+ * blocks below it keep that width. */
 int hmc_set_mine_block(hmc_ctx *ctx, int start_loci);
+/* Last E-step: the largest frontier (states at one locus of one individual)
+ * and the state capacity it ran with (grows by doubling on overflow, up to
+ * 2 097 151 states: 21-bit state ids in the records and list links). */
+int hmc_last_estep_frontier(hmc_ctx *ctx, int *max_states, int *frontier_cap);
+/* Cap on one search level's matching lists, in bytes (0 = device memory
+ * only; 12 B per entry of the genotype branch, 4 B of the sample branch):
+ * a level over the cap splits its block as if memory had run out. */
+int hmc_set_mine_memory(hmc_ctx *ctx, uint64_t list_bytes);
 /* Last search: blocks, candidate nodes created (all blocks) and the size of
  * the node arrays kept (GB, ~70 B per node). */
 int hmc_last_mine_stats(const hmc_ctx *ctx, int *blocks, int64_t *nodes, double *node_window_gb);

@@ -131,7 +131,7 @@ def test_value_only_mode_with_order_reruns(oracle_mod, name, S):
     assert 0 <= st["n_order_rerun"] <= p.N
 
 
-@pytest.mark.parametrize("S", [1, 2, 5, 16, 17, 24, 32])
+@pytest.mark.parametrize("S", [1, 2, 5, 16, 17, 24, 32, 33, 40, 64])
 def test_estep_sample_sizes(oracle_mod, S):
     p = panel("miss2")
     o = oracle_mod.Oracle(p.alleles, p.types, sample_size=S)
@@ -278,6 +278,51 @@ def test_full_em(oracle_mod, name):
     np.testing.assert_array_equal(np.array(m.haplocomp()), r["haplocomp"][-1])
 
 
+@pytest.mark.parametrize("name,S", [("n60", 40), ("a3miss5", 64)])
+def test_full_em_large_sample_size(oracle_mod, name, S):
+    """sample_size above one wavefront's lists (S = 40, 64: lists of up to 2S
+    links over two lanes' selection slots, HaploPair.cpp:63-89): whole-EM
+    parity with the restatement (LL, R_E, R_M, HaploComp, accepted pairs)."""
+    p = panel(name)
+    m = gpu_model(p, S, max_iteration=30)
+    res = m.run()
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=S, max_iter=30)
+    r = o.run()
+    assert m.iterations == r["iterations"]
+    assert [x["ll"] for x in m.log] == r["ll"].tolist()
+    assert [x["r_e"] for x in m.log] == r["R_E"].tolist()
+    for k in range(r["iterations"] - 1):
+        assert m.log[k]["r_m"] == r["R_M"][k + 1]
+    assert np.array_equal(res, r["resolutions"])
+    np.testing.assert_array_equal(np.array([x["haplocomp"] for x in m.log]), r["haplocomp"])
+
+
+@pytest.mark.timeout(600)
+def test_wide_frontier_over_65535_states(oracle_mod):
+    """An individual whose frontier passes 65 535 states at a locus (no
+    genotype at all on a panel of 8 alleles per locus, patterns mined down to
+    a low threshold: pairs of ~400 patterns per locus): state ids take 21 bits
+    in the structure records and list links, the state capacity grows by
+    doubling, the contribution capacity too (amax^2 contributions per state
+    where both alleles are missing).  The E-step equals
+    HaploModel::resolveAll bit for bit."""
+    rng = np.random.default_rng(1)
+    N, L, A = 100, 6, 8
+    al = (rng.integers(0, A, size=(N, 2, L)) + ord("1")).astype(np.int32)
+    al[0] = -1
+    p = synth.Panel(al, "S" * L)
+    o = oracle_mod.Oracle(p.alleles, p.types, min_freq_abs=0.3, max_len=L, sample_size=10)
+    o.find_patterns()
+    m = gpu_model(p, min_freq_abs=0.3, max_pattern_len=L)
+    m.find_patterns()
+    assert_tables_equal(m.patterns(), o.patterns())
+    ll_g, H, re_g = m.resolve_all()
+    fr = m.estep_frontier()
+    assert fr["max_states"] > 65535, fr
+    o.reset_counters()
+    assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
+
+
 @pytest.mark.parametrize("missing", [0.0, 0.03])
 def test_many_alleles(oracle_mod, missing):
     """Loci with 40 alleles (microsatellite 'M' loci; GenoData's allele tables
@@ -332,13 +377,16 @@ def test_em_iteration_drives_the_same_chain(oracle_mod, name):
     assert np.array_equal(best, r["resolutions"])
 
 
-@pytest.mark.parametrize("name,width", [("n300", 31), ("n300", 77), ("a4", 31), ("a3miss5", 45), ("miss2", 60)])
+@pytest.mark.parametrize("name,width", [("n300", 31), ("n300", 77), ("n300", 5), ("a4", 31), ("a4", 13),
+                                        ("a3miss5", 45), ("miss2", 60), ("miss2", 1)])
 def test_mining_in_start_blocks(oracle_mod, name, width):
     """hmc_set_mine_block: the search by blocks of start loci from L-1 down
     (roots of searchPattern's DFS are independent, PatternManager.cpp:90-108)
     gives the restatement's table exactly — ids, allele strings, frequencies,
     prefix frequencies, transition probabilities, successors, R_M — for M0 and
-    for the M-step on the samples, and the E-step in between agrees too."""
+    for the M-step on the samples, and the E-step in between agrees too.
+    Blocks narrower than the patterns are long (widths 1, 5, 13) need the
+    successors of the block above (mine_succ_level)."""
     p = panel(name)
     o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
     m = gpu_model(p)
@@ -357,6 +405,28 @@ def test_mining_in_start_blocks(oracle_mod, name, width):
         ll_o = o.resolve_all()
         ll, H, re = m.resolve_all()
         assert ll == ll_o
+
+
+@pytest.mark.parametrize("name,cap", [("n300", 2 << 20), ("a3miss5", 1 << 20)])
+def test_mining_splits_blocks_over_memory_cap(oracle_mod, name, cap):
+    """A block whose matching lists exceed the cap (hmc_set_mine_memory, the
+    path taken when device memory runs out) is re-run with half the width:
+    several blocks, and still the restatement's table, R_M and E-step."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
+    m = gpu_model(p)
+    m.set_mine_memory(cap)
+    for step in range(2):
+        o.reset_counters()
+        P = o.find_patterns()
+        Pg, rm = m.find_patterns()
+        assert m.mine_stats()["blocks"] >= 2
+        ref, got = o.patterns(maxlen=30), m.patterns(maxlen=30)
+        assert Pg == P
+        for k in ref:
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+        assert rm == o.counters()[1]
+        assert m.resolve_all()[0] == o.resolve_all()
 
 
 @pytest.mark.parametrize("name", ["n60", "miss2"])
@@ -1032,3 +1102,78 @@ def test_full_size_chain_against_oracle_digest(cfg):
         check_e(k)
         if k < len(d["m"]):
             check_m(k)
+
+
+def _estep_properties(m, p, ll, H):
+    """Samples phase the genotypes (both haplotypes of each candidate, every
+    non-missing locus), candidates' priors are sorted, each individual's
+    weights sum to 1, total weight = 2N — vectorised over all candidates."""
+    er = m.estep_results()
+    n = er["ncand"]
+    assert np.all(n > 0) and np.isfinite(ll) and ll < 0
+    S = er["prior"].shape[1]
+    live = np.arange(S)[None, :] < n[:, None]
+    pr = np.where(live, er["prior"], -np.inf)
+    assert np.all(np.diff(pr, axis=1)[live[:, 1:]] <= 0)
+    assert np.all(np.abs(np.where(live, er["weight"], 0.0).sum(axis=1) - 1.0) < 1e-12)
+    al, w, tw = m.samples(H)
+    assert H == 2 * int(n.sum()) and abs(tw - 2 * p.N) < 1e-6
+    owner = np.repeat(np.arange(p.N), n)  # individual of each candidate (samples in individual order)
+    h0, h1 = al[0::2], al[1::2]
+    g0, g1 = p.alleles[owner, 0], p.alleles[owner, 1]
+    ok = ((h0 == g0) & (h1 == g1)) | ((h0 == g1) & (h1 == g0))
+    assert ok.all()
+
+
+def _table_properties(m, L):
+    pt = m.patterns(maxlen=1)
+    assert np.all(pt["freq"] > 0) and np.all(pt["freq"] <= 1) and np.all(pt["tp"] <= 1)
+    e = pt["start"] + pt["len"]
+    assert np.all(pt["len"] >= 1) and np.all(e <= L)
+    s = pt["succ"]
+    has = s >= 0
+    rows = np.nonzero(has)[0]
+    assert np.all(e[s[has]] == e[rows] + 1)  # a successor ends one locus further
+    return _digest_patterns(pt)
+
+
+@pytest.mark.timeout(1100)
+def test_cfg4_rank_slice_properties():
+    """cfg 4's per-rank workload (6 250 x 5 000, seed 4: one GPU's share of the
+    8-GPU run): M0 mined in blocks of start loci (the automatic width: several
+    blocks here) equals M0 mined in one block (pattern count, R_M and table
+    digest); E1, M1 and E2 keep the full-size properties (samples phase the
+    genotypes, weights sum to 1, priors sorted, frequencies in (0, 1],
+    successors end one locus further); a fresh context repeats M0 and E1 bit
+    for bit (table digest, LL, R_E, resolutions)."""
+    p = synth.founder_mosaic(6250, 5000, A=2, seed=4)
+    one = gpu_model(p)
+    one.set_mine_block(p.L)
+    P1, rm1 = one.find_patterns()
+    assert one.mine_stats()["blocks"] == 1
+    d1 = _digest_patterns(one.patterns(maxlen=1))
+    one.close()
+
+    m = gpu_model(p)
+    P, rm = m.find_patterns()
+    st = m.mine_stats()
+    assert st["blocks"] >= 2, st
+    assert (P, rm) == (P1, rm1)
+    d0 = _table_properties(m, p.L)
+    assert d0 == d1
+    ll1, H1, re1 = m.resolve_all()
+    _estep_properties(m, p, ll1, H1)
+    res1 = m.resolutions()
+    m.find_patterns()
+    _table_properties(m, p.L)
+    ll2, H2, _ = m.resolve_all()
+    _estep_properties(m, p, ll2, H2)
+    m.close()
+
+    r = gpu_model(p)
+    assert r.find_patterns() == (P, rm)
+    assert _digest_patterns(r.patterns(maxlen=1)) == d0
+    ll, H, re = r.resolve_all()
+    assert (float(ll).hex(), H, re) == (float(ll1).hex(), H1, re1)
+    assert np.array_equal(r.resolutions(), res1)
+    r.close()

@@ -1,0 +1,34 @@
+"""A/B of library builds over cfg 3's converged chain: M0 once, then twice
+(hmc_em_rewind) E1, M1, E2, M2, E3 with device ms of every E-step's passes.
+Pick the build with HMC_AMD_LIB; LL and R_E must not change between builds.
+
+    HMC_AMD_LIB=... python tools/chain_ab.py TAG [CFG]
+"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import hmc_amd  # noqa: E402
+from hmc_amd import synth  # noqa: E402
+
+tag = sys.argv[1] if len(sys.argv) > 1 else "run"
+cfg = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+m = hmc_amd.HaploModel()
+m.load(hmc_amd.GenoData.from_panel(synth.config_panel(cfg)))
+t0 = time.perf_counter()
+P, _ = m.find_patterns()
+print(f"{tag}: M0 {P} patterns {time.perf_counter() - t0:.1f} s lib {hmc_amd.lib_identity()}", flush=True)
+m.model_save()
+for rep in range(2):
+    m.em_rewind()
+    for k in range(1, 4):
+        t0 = time.perf_counter()
+        ll, H, re = m.resolve_all()
+        wall = time.perf_counter() - t0
+        s = m.estep_split_stats()
+        print(f"{tag} chain {rep} E{k}: wall {wall * 1e3:.0f} ms structure {s['structure_ms']:.0f} ms "
+              f"({s['structure_passes']}) values {s['values_ms']:.0f} ms ({s['value_passes']}) "
+              f"ll={ll!r} R_E={re}", flush=True)
+        if k < 3:
+            m.find_patterns()

@@ -13,8 +13,8 @@ from hmc_amd import synth  # noqa: E402
 
 p = synth.config_panel(int(os.environ.get("CFG", "2")))
 m = hmc_amd.HaploModel()
-nw, ipc = (int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "3:4").split(":"))
-m.set_estep_shape(nw, ipc)
+nw, ipc = (int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0:0").split(":"))
+m.set_pass_shapes(0, 0, nw, ipc)  # value-pass shape (0 = automatic)
 m.load(hmc_amd.GenoData.from_panel(p))
 m.find_patterns()
 names = ["record hdr", "phase A", "phase B", "trace", "final sync", "final select"]
