@@ -37,14 +37,22 @@ template <class T>
 struct DevBuf {
   T *p = nullptr;
   size_t n = 0;
+  bool host = false;  // pinned host memory instead (model snapshots of very large tables)
   DevBuf() = default;
   DevBuf(const DevBuf &) = delete;
   DevBuf &operator=(const DevBuf &) = delete;
   ~DevBuf() { release(); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) (void)(host ? hipHostFree(p) : hipFree(p));
     p = nullptr;
     n = 0;
+  }
+  void set_host(bool h) {
+    if (h != host) release();
+    host = h;
+  }
+  hipError_t alloc(T **q, size_t bytes) {
+    return host ? hipHostMalloc((void **)q, bytes, hipHostMallocDefault) : hipMalloc((void **)q, bytes);
   }
   // Contents not preserved.  A buffer that has to grow takes 1.5x headroom:
   // large allocations are mapped eagerly by the HIP runtime (~1 s per 10-20 GB),
@@ -54,11 +62,11 @@ struct DevBuf {
     const size_t want = std::max<size_t>(m, 1), grown = n ? std::max(want, n + n / 2) : want;
     release();
     size_t got = grown;
-    hipError_t e = hipMalloc((void **)&p, got * sizeof(T));
+    hipError_t e = alloc(&p, got * sizeof(T));
     if (e != hipSuccess && grown > want) {
       (void)hipGetLastError();
       got = want;
-      e = hipMalloc((void **)&p, got * sizeof(T));
+      e = alloc(&p, got * sizeof(T));
     }
     if (e != hipSuccess) { p = nullptr; return e; }
     n = got;
@@ -812,6 +820,9 @@ struct Ctx {
   // sums over ranks; freq / prefix / tp as at HaploBuilder.cpp:317-331.
   int estimate_round(Cands &c, size_t b, size_t e) {
     const int L = pan.L, A = pan.amax, N = pan.N;
+    const auto t_round = std::chrono::steady_clock::now();
+    const double walk0 = ms_walk;
+    const bool reused = xc_reuse;
     std::vector<int32_t> child, data, root(L, -1);
     int maxd = 0;
     auto new_node = [&]() {
@@ -892,7 +903,11 @@ struct Ctx {
     }
     ++exact_rounds;
     exact_candidates += nc;
-    if (debug_mem) fprintf(stderr, "[hmc] exact round %d: %zu candidates\n", exact_rounds, nc);
+    if (debug_mem)
+      fprintf(stderr, "[hmc] exact round %d: %zu candidates, trie depth %d, walk %.1f ms, round %.1f ms%s\n", exact_rounds,
+              nc, maxd, ms_walk - walk0,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_round).count(),
+              reused ? " (E-step data reused)" : "");
     return HMC_OK;
   }
   size_t xacc_nc = 0;
@@ -957,13 +972,22 @@ struct Ctx {
         (e = hipMemsetAsync(d_xscr.p, 0, x.scratch_stride * grid * 8, st)))  // the walk's zero invariant
       return hipfail(e, "exact scratch");
     x.scratch = d_xscr.p;
-    hipEventRecord(ev[0], st);
-    if ((e = launch_exact_walk(x, grid, st))) return hipfail(e, "exact_walk");
-    hipEventRecord(ev[1], st);
-    if ((e = hipStreamSynchronize(st))) return hipfail(e, "exact_walk");
-    float ms = 0;
-    hipEventElapsedTime(&ms, ev[0], ev[1]);
-    ms_walk += ms;
+    // in slices of the items, so that a long walk reports progress (and the
+    // scratch returns to zero between slices: every item clears its entries)
+    const long long slice = std::max<long long>(grid, (items + 15) / 16);
+    for (long long i0 = 0; i0 < items; i0 += slice) {
+      x.item0 = i0;
+      x.item1 = std::min(items, i0 + slice);
+      hipEventRecord(ev[0], st);
+      if ((e = launch_exact_walk(x, grid, st))) return hipfail(e, "exact_walk");
+      hipEventRecord(ev[1], st);
+      if ((e = hipStreamSynchronize(st))) return hipfail(e, "exact_walk");
+      float ms = 0;
+      hipEventElapsedTime(&ms, ev[0], ev[1]);
+      ms_walk += ms;
+      if (debug_mem && items > 16 * (long long)grid)
+        fprintf(stderr, "[hmc] exact walk: items %lld..%lld of %lld (%d individuals), %.1f ms\n", i0, x.item1, items, k, ms);
+    }
     return HMC_OK;
   }
   double ms_walk = 0;
@@ -1092,10 +1116,15 @@ struct Ctx {
     exact_candidates = 0;
     ms_walk = 0;
     xc_reuse = false;
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+    auto t0 = clk::now();
     Cands cur;
     std::vector<int32_t> succ;
     int rc = table_to_host(cur, succ);
     if (rc) return rc;
+    const double ms_to_host = ms_since(t0);
+    t0 = clk::now();
     const int A = pan.amax;
     if (mf < 0) {  // estimateFrequency() (:347-362): re-estimate in place, ids and successors unchanged
       if ((rc = estimate_round(cur, 0, cur.size()))) return rc;
@@ -1138,13 +1167,20 @@ struct Ctx {
         rb = nb;
         re = all.size();
       }
+      const double ms_rounds = ms_since(t0);
+      t0 = clk::now();
       Cands kept;  // (:396-408)
       for (size_t i = 0; i < all.size(); ++i)
         if (all.freq[i] >= mf || all.len[i] <= mnl)
           kept.push(all.start[i], all.len[i], all.alleles(i), 0, false, all.freq[i], all.prefix[i], all.tp[i]);
       std::vector<int32_t> ksucc;
       host_successors(kept, ksucc);
+      const double ms_succ = ms_since(t0);
+      t0 = clk::now();
       if ((rc = install_host_table(kept, ksucc))) return rc;
+      if (debug_mem)
+        fprintf(stderr, "[hmc] exact M-step: table to host %.1f ms, rounds %.1f ms (walks %.1f), kept + successors %.1f ms, "
+                "install %.1f ms\n", ms_to_host, ms_rounds, ms_walk, ms_succ, ms_since(t0));
     }
     xc_reuse = false;
     hipEventRecord(ev[5], st);
@@ -1188,6 +1224,7 @@ struct Ctx {
   // the panel is small or the rules need the whole tree (findPatternByNum,
   // heads longer than 1, whose patterns are not suffix-closed).
   int mine_block_starts = 0;
+  double last_mine_window_gb = 0;  // node arrays' size at the end of the last search
   int block_width(int L, int mxl, int mnl, int bynum_rounds) const {
     if (bynum_rounds > 0 || mnl > 1) return L;
     int w = mine_block_starts;
@@ -1255,6 +1292,16 @@ struct Ctx {
     }
     tree_complete = nblocks == 1;
     P = (int)id_base;
+    if (!tree_complete) {  // a partial tree is of no further use (strings come from ppat): give its memory back
+      n_parent.release(); n_start.release(); n_child_base.release(); n_link.release(); n_allele.release();
+      n_flags.release(); n_freq.release(); n_prefix.release(); n_tp.release(); n_sum.release(); n_cnt.release();
+      n_size.release(); n_pos.release(); n_list_off.release(); n_region.release();
+      last_mine_window_gb = (double)node_cap * 70.0 / 1e9;
+      node_cap = 0;
+      wbase = 0;
+    } else {
+      last_mine_window_gb = (double)node_cap * 70.0 / 1e9;
+    }
     {
       int merr = 0;
       if ((e = hipMemcpyAsync(&merr, d_mine_err.p, 4, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
@@ -1276,7 +1323,7 @@ struct Ctx {
       size_t fb = 0, tb = 0;
       hipMemGetInfo(&fb, &tb);
       fprintf(stderr, "[hmc] after mining: %d patterns in %d block(s) of %d start loci, %lld nodes; free %.1f GB of %.1f; "
-              "node window %.1f GB\n", P, nblocks, W, next_node, fb / 1e9, tb / 1e9, node_cap * 70.0 / 1e9);
+              "node window %.1f GB\n", P, nblocks, W, next_node, fb / 1e9, tb / 1e9, last_mine_window_gb);
     }
     unsigned long long rm = 0;
     for (int k = 0; k < RM_SLOTS; ++k) rm += rm_slots[(size_t)k * 16];
@@ -2263,10 +2310,15 @@ struct Ctx {
       // model larger than the panel (the genotype-mined M0: 2.5 patterns per
       // individual-locus at cfg 3, 0.3 later) frontiers are large (cfg 3 E1:
       // 470 states per locus, 80 % of them past a one-wave block's LDS tier):
-      // four waves per individual, three per CU
+      // four waves per individual, two per CU (each block's LDS tier holds
+      // more of the frontier: cfg 3 E1 structure 1.65 -> 1.32 s against three
+      // per CU, profiles/r03/e1/e1_s1shapes.log)
       const bool heavy_model = (double)P > (double)pan.N * (double)pan.L;
-      const int nw1 = s1_nw > 0 ? s1_nw : (heavy_model ? 4 : 1);
-      const int bpc1 = s1_ipc > 0 ? s1_ipc : (nw1 == 4 ? 3 : (np > 8 * dev_cu ? 12 : (np > 4 * dev_cu ? 8 : 4)));
+      // (a heavy group of at most one individual per CU — cfg 4's per-rank E1,
+      // records of ~250 MB per individual — takes the whole CU: 16 waves)
+      const int nw1 = s1_nw > 0 ? s1_nw : (heavy_model ? (np <= dev_cu ? 16 : 4) : 1);
+      const int bpc1 = s1_ipc > 0 ? s1_ipc
+                                  : (nw1 == 16 ? 1 : (nw1 == 4 ? 2 : (np > 8 * dev_cu ? 12 : (np > 4 * dev_cu ? 8 : 4))));
       const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1, nw1);
       // (huge frontiers: fewer resident individuals rather than scratch past SCRATCH_MAX)
       const int grid1 = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::min(np, dev_cu * bpc1), SCRATCH_MAX / per1));
@@ -2431,8 +2483,18 @@ struct Ctx {
         double rw = 0;
         for (size_t q = 0; q < k; ++q) rw += (double)rneed[sset[pos + q]];
         const bool heavy = rw / ((double)k * L) > 1500.0;
-        int vnw = vp_nw > 0 ? vp_nw : (heavy ? 4 : ((int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3)));
-        int vipc = vp_ipc > 0 ? vp_ipc : (vnw == 1 ? 20 : (vnw == 4 ? 4 : 8));  // a half-given shape completes by the same rule
+        // Heavy groups too small to give every CU four individuals (records and
+        // traces of hundreds of MB each: cfg 4's per-rank E1 on the 720 M-pattern
+        // M0 runs in groups of ~200) spread the CU's 16 waves over fewer
+        // individuals: more selection segments and LDS per individual.
+        const int per_cu = (int)((k + dev_cu - 1) / dev_cu);
+        const bool small_heavy = heavy && per_cu < 4;
+        int vnw = vp_nw > 0 ? vp_nw
+                            : (small_heavy ? 16 / per_cu
+                                           : (heavy ? 4 : ((int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3))));
+        int vipc = vp_ipc > 0 ? vp_ipc
+                              : (small_heavy ? per_cu
+                                             : (vnw == 1 ? 20 : (vnw >= 4 ? 4 : 8)));  // a half-given shape completes by the same rule
         const int G2 = std::max(1, std::min(waves > 0 ? waves : dev_cu * vipc, n));
         // register budget: 5 waves per SIMD once the shape asks for more than 16 per CU
         const int vwpe = vnw * vipc > 16 && vnw * vipc <= 20 ? 5 : 4;
@@ -2850,11 +2912,23 @@ struct Ctx {
     if (n == 0 || !src.p) return hipSuccess;
     hipError_t e = dst.ensure(n);
     if (e) return e;
-    return hipMemcpyAsync(dst.p, src.p, n * sizeof(T), hipMemcpyDeviceToDevice, st);
+    return hipMemcpyAsync(dst.p, src.p, n * sizeof(T), hipMemcpyDefault, st);
   }
   int model_save() {
     if (!have_model) return fail(HMC_EARG, "no pattern model to save");
     const size_t p = (size_t)std::max(P, 1), A = (size_t)pan.amax;
+    // a table over 8 GB (cfg 4's M0: 720 M patterns, 35 GB) is kept in pinned
+    // host memory: HBM is the E-step stores'; a rewind then reads it over PCIe
+    const bool on_host = (double)p * (41.0 + 4.0 * (double)A) > 8e9;
+    snap.start.set_host(on_host);
+    snap.len.set_host(on_host);
+    snap.node.set_host(on_host);
+    snap.ppat.set_host(on_host);
+    snap.freq.set_host(on_host);
+    snap.prefix.set_host(on_host);
+    snap.tp.set_host(on_host);
+    snap.last.set_host(on_host);
+    snap.succ.set_host(on_host);
     hipError_t e;
     if ((e = dcopy(snap.start, t_start, p)) || (e = dcopy(snap.len, t_len, p)) || (e = dcopy(snap.node, t_node, p)) ||
         (e = dcopy(snap.ppat, t_ppat, p)) ||
@@ -3170,8 +3244,9 @@ int hmc_set_estep_shape(hmc_ctx *h, int waves_per_individual, int individuals_pe
 }
 
 int hmc_set_pass_shapes(hmc_ctx *h, int structure_waves, int structure_ipc, int value_waves, int value_ipc) {
-  if (!h || (structure_waves != 0 && structure_waves != 1 && structure_waves != 4) || structure_ipc < 0 ||
-      structure_ipc > 32 || value_waves < 0 || value_waves > 4 || value_ipc < 0 || value_ipc > 32)
+  if (!h || (structure_waves != 0 && structure_waves != 1 && structure_waves != 4 && structure_waves != 16) ||
+      structure_ipc < 0 ||
+      structure_ipc > 32 || value_waves < 0 || value_waves > 16 || value_ipc < 0 || value_ipc > 32)
     return HMC_EARG;
   h->c.s1_nw = structure_waves;
   h->c.s1_ipc = structure_ipc;
@@ -3215,7 +3290,7 @@ int hmc_last_mine_stats(const hmc_ctx *h, int *blocks, int64_t *nodes, double *n
   if (!h) return HMC_EARG;
   if (blocks) *blocks = h->c.last_mine_blocks;
   if (nodes) *nodes = h->c.last_mine_nodes;
-  if (node_window_gb) *node_window_gb = (double)h->c.node_cap * 70.0 / 1e9;
+  if (node_window_gb) *node_window_gb = h->c.last_mine_window_gb;
   return HMC_OK;
 }
 

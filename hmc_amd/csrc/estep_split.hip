@@ -523,7 +523,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         int li = 0, gsz = 0;
         uint32_t cnt0 = 0;
         if (valid) {
-#pragma unroll
+#pragma unroll 4
           for (int w = 0; w < NW; ++w) {
             const uint64_t m = slot < (uint32_t)K.hc ? K.lanes(slot)[w] : ld_acq(K.lanes(slot) + w);
             li += w < wv ? __popcll(m) : (w == wv ? __popcll(m & lt) : 0);
@@ -534,7 +534,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         B.sync();
         if (valid && li == 0) {
           *K.cnt(slot) = cnt0 + (uint32_t)gsz;
-#pragma unroll
+#pragma unroll 4
           for (int w = 0; w < NW; ++w) K.lanes(slot)[w] = 0ull;
         }
         const bool is_new = valid && cnt0 == 0 && li == 0;
@@ -868,7 +868,7 @@ size_t estep_s2_lds_bytes(int S, int fc, int nw) { return (size_t)k2_plan(S, fc,
 // each lane holding positions k and k + 64, selection by the sequential
 // libstdc++ code on the wave's first lane (the sw > 32 path of seg_nth_slots).
 template <bool FAST, int WPE, bool WIDE = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void estep_values(ValueArgs a) {
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) void estep_values(ValueArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int S = a.S, L = a.L, hl = a.head_len;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;
@@ -1209,23 +1209,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStream_t st) {
   if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > F_MAX || (a.hcap & (a.hcap - 1)) || a.lds_hc < 1 ||
       (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || a.lds_cc < 0 || a.ccap < 1 || a.mod.head_len < 1 ||
-      (a.mod.head_len > 1 && (!a.mod.hf_off || !a.mod.hf_pairs || !a.mod.hf_status)) || (nw != 1 && nw != 4))
+      (a.mod.head_len > 1 && (!a.mod.hf_off || !a.mod.hf_pairs || !a.mod.hf_status)) || (nw != 1 && nw != 4 && nw != 16))
     return hipErrorInvalidValue;
   const size_t lds = estep_s1_lds_bytes(a.lds_fc, a.lds_hc, a.lds_cc, a.pan.amax, nw);
-  static size_t lds_attr[2] = {0, 0};
-  const void *f = nw == 4 ? (const void *)estep_structure<4> : (const void *)estep_structure<1>;
-  if (lds > 65536 && lds > lds_attr[nw == 4]) {
+  static size_t lds_attr[3] = {0, 0, 0};
+  const int ix = nw == 16 ? 2 : (nw == 4 ? 1 : 0);
+  const void *f = nw == 16 ? (const void *)estep_structure<16>
+                           : (nw == 4 ? (const void *)estep_structure<4> : (const void *)estep_structure<1>);
+  if (lds > 65536 && lds > lds_attr[ix]) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    lds_attr[nw == 4] = lds;
+    lds_attr[ix] = lds;
   }
-  if (nw == 4) hipLaunchKernelGGL(estep_structure<4>, dim3(grid), dim3(4 * WAVE), lds, st, a);
+  if (nw == 16) hipLaunchKernelGGL(estep_structure<16>, dim3(grid), dim3(16 * WAVE), lds, st, a);
+  else if (nw == 4) hipLaunchKernelGGL(estep_structure<4>, dim3(grid), dim3(4 * WAVE), lds, st, a);
   else hipLaunchKernelGGL(estep_structure<1>, dim3(grid), dim3(WAVE), lds, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, int wpe, hipStream_t st) {
-  if (a.S < 1 || a.S > S_MAX || a.fcap > F_MAX || a.lds_fc < 0 || nw < 1 || nw > 4 || (wpe != 4 && wpe != 5) ||
+  if (a.S < 1 || a.S > S_MAX || a.fcap > F_MAX || a.lds_fc < 0 || nw < 1 || nw > 16 || (wpe != 4 && wpe != 5) ||
       (a.S > 32 && fast))
     return hipErrorInvalidValue;
   const size_t lds = estep_s2_lds_bytes(a.S, a.lds_fc, nw);

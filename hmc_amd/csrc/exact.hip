@@ -178,8 +178,8 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
   for (int w = lane; w < nwords; w += WAVE) marks[w] = 0u;
   __builtin_amdgcn_wave_barrier();
   __threadfence_block();
-  const long long n_items = (long long)a.n_order * L;
-  for (long long it = blockIdx.x; it < n_items; it += gridDim.x) {
+  const long long n_items = a.item1 < 0 ? (long long)a.n_order * L : a.item1;
+  for (long long it = a.item0 + blockIdx.x; it < n_items; it += gridDim.x) {
     const int q = (int)(it / L), start = (int)(it % L);
     const int bi = a.order[q];
     const int root = a.tr_root[start];

@@ -33,6 +33,7 @@ struct ExactArgs {
   size_t scratch_stride;           // doubles
   int fmax;                        // most states of any locus of the group
   unsigned long long *acc_freq, *acc_prefix;  // [candidates] fixed point
+  long long item0 = 0, item1 = -1;  // walk items [item0, item1) of n_order x L (individual-major); -1 = all
 };
 
 hipError_t launch_exact_fb(const ExactArgs &a, int grid, hipStream_t st);

@@ -74,7 +74,10 @@ int hmc_set_reduction(hmc_ctx *ctx, int mode);
 
 /* HaploModel public parameters (HaploModel.h:15-26; CLI defaults HMC.cpp:35-47).
  * min_freq_abs > 0 overrides min_freq exactly as HaploModel::findPatterns does
- * (HaploModel.cpp:54-56). */
+ * (HaploModel.cpp:54-56).  sample_size 1..64 (HaploPair's k-best lists,
+ * HaploBuilder.cpp:44, HaploPair.cpp:85-88; above 32 the split E-step only,
+ * and an individual whose forward likelihood underflows returns
+ * HMC_EUNSUPPORTED); larger values fail the E-step with HMC_EUNSUPPORTED. */
 int hmc_set_params(hmc_ctx *ctx, double min_freq_abs, double min_freq, int min_pattern_len, int max_pattern_len,
                    int sample_size);
 
@@ -277,9 +280,9 @@ int hmc_write_file(hmc_ctx *ctx, const char *format, const char *path, const cha
 int hmc_write_patterns(hmc_ctx *ctx, const char *path);
 
 /* ---- tuning -------------------------------------------------------------- */
-/* frontier_cap: states per locus per wave before a batch is re-run with a
- * larger capacity; trace_bytes: trace-store budget (0 = automatic);
- * waves: resident E-step waves (0 = automatic). */
+/* frontier_cap: initial states per locus and individual (doubles on
+ * overflow, at most 2 097 151); trace_bytes: trace-store budget (0 =
+ * automatic); waves: resident E-step waves (0 = automatic). */
 int hmc_set_tuning(hmc_ctx *ctx, int frontier_cap, uint64_t trace_bytes, int waves);
 /* E-step launch shape: wavefronts cooperating on one individual (1..4,
  * default 2) and individuals sharing one CU's LDS (default 8); 0 keeps the
@@ -290,12 +293,15 @@ int hmc_set_tuning(hmc_ctx *ctx, int frontier_cap, uint64_t trace_bytes, int wav
  * same rule.  Results do not depend on the shape. */
 int hmc_set_estep_shape(hmc_ctx *ctx, int waves_per_individual, int individuals_per_cu);
 /* Launch shapes of the split E-step's two passes, 0 = automatic for each:
- * structure pass waves per individual (1 or 4; automatic: 4 on a model with
- * more patterns than the panel has individual-loci, the genotype-mined M0)
- * and individuals per CU (automatic: 3 at 4 waves; else 12 above 8 per CU in
+ * structure pass waves per individual (1, 4 or 16; automatic: 4 on a model
+ * with more patterns than the panel has individual-loci, the genotype-mined
+ * M0, 16 when such a group has at most one individual per CU)
+ * and individuals per CU (automatic: 1 at 16 waves, 2 at 4; else 12 above 8 per CU in
  * the group, 8 above 4, else 4), value pass waves per individual (1..4) and
  * individuals per CU (rule of hmc_set_estep_shape; groups averaging more than
- * 1 500 record words per locus take 4 x 4).  Results do not depend on them. */
+ * 1 500 record words per locus take 4 x 4, or 16 / c waves x c per CU when
+ * they have c < 4 individuals per CU).  Value-pass waves per individual 1..16.
+ * Results do not depend on them. */
 int hmc_set_pass_shapes(hmc_ctx *ctx, int structure_waves, int structure_ipc, int value_waves, int value_ipc);
 /* Budgets of the split E-step's two stores in bytes, 0 = automatic: the
  * k-best trace store (min(42 % of free HBM, 120 GiB)) and the structure-record
