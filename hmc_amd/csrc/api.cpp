@@ -2183,7 +2183,7 @@ struct Ctx {
         if (s == EST_NO_HEAD_PATTERN) return fail(HMC_ENOPATTERN, "Can not find matching pattern!");
         if (s == EST_OVERFLOW_FRONTIER) {
           if (fcap >= F_MAX) return fail(HMC_EUNSUPPORTED, "frontier exceeds %d states", F_MAX);
-          fcap = std::min(F_MAX, fcap * 2);
+          fcap = (int)std::min<int64_t>(F_MAX, (int64_t)fcap * 4);  // x4: each overflow costs a whole pass
           return ESTEP_RESTART;
         }
         if (s == EST_OVERFLOW_TRACE) ovf_trace = true;
@@ -2393,7 +2393,8 @@ struct Ctx {
         }
         if (s == EST_OVERFLOW_FRONTIER) {  // (deferring only these individuals measured slower)
           if (fcap >= F_MAX) return fail(HMC_EUNSUPPORTED, "frontier exceeds %d states", F_MAX);
-          fcap = std::min(F_MAX, fcap * 2);
+          if (debug_mem) fprintf(stderr, "[hmc] frontier over %d states: capacity x4, E-step restarts\n", fcap);
+          fcap = (int)std::min<int64_t>(F_MAX, (int64_t)fcap * 4);  // x4: each overflow costs a whole pass
           return ESTEP_RESTART;
         }
         if (s == EST_OVERFLOW_REC) {
@@ -2602,7 +2603,7 @@ struct Ctx {
             const int s = h_status[r];
             if (s == EST_OVERFLOW_FRONTIER) {
               if (fcap >= F_MAX) return fail(HMC_EUNSUPPORTED, "frontier exceeds %d states", F_MAX);
-              fcap = std::min(F_MAX, fcap * 2);
+              fcap = (int)std::min<int64_t>(F_MAX, (int64_t)fcap * 4);  // x4: each overflow costs a whole pass
               return ESTEP_RESTART;
             }
             if (s == EST_OVERFLOW_TRACE) return fail(HMC_EHIP, "fallback trace exceeds its region");
