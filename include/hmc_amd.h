@@ -299,7 +299,7 @@ int hmc_set_estep_shape(hmc_ctx *ctx, int waves_per_individual, int individuals_
  * and individuals per CU (automatic: 1 at 16 waves, 2 at 4; else 12 above 8 per CU in
  * the group, 8 above 4, else 4), value pass waves per individual (1..4) and
  * individuals per CU (rule of hmc_set_estep_shape; groups averaging more than
- * 1 500 record words per locus take 4 x 4, or 16 / c waves x c per CU when
+ * 1 500 record words per locus take 8 x 2, or 16 / c waves x c per CU when
  * they have c < 4 individuals per CU).  Value-pass waves per individual 1..16.
  * Results do not depend on them. */
 int hmc_set_pass_shapes(hmc_ctx *ctx, int structure_waves, int structure_ipc, int value_waves, int value_ipc);
