@@ -3247,7 +3247,8 @@ int hmc_set_estep_shape(hmc_ctx *h, int waves_per_individual, int individuals_pe
 }
 
 int hmc_set_pass_shapes(hmc_ctx *h, int structure_waves, int structure_ipc, int value_waves, int value_ipc) {
-  if (!h || (structure_waves != 0 && structure_waves != 1 && structure_waves != 4 && structure_waves != 16) ||
+  if (!h || (structure_waves != 0 && structure_waves != 1 && structure_waves != 4 && structure_waves != 8 &&
+             structure_waves != 16) ||
       structure_ipc < 0 ||
       structure_ipc > 32 || value_waves < 0 || value_waves > 16 || value_ipc < 0 || value_ipc > 32)
     return HMC_EARG;

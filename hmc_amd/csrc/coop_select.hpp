@@ -94,22 +94,6 @@ __device__ inline int seg_lowest(uint32_t bits) {
   return bits ? __builtin_ctz(bits) : 64;
 }
 
-// Position of the r-th (0-based) set bit of m (r < popcount(m)): a binary
-// search on popcounts, all in registers.
-__device__ inline int sel_bit(uint32_t m, int r) {
-  int pos = 0;
-  int c = __popc(m & 0xFFFFu);
-  if (r >= c) { r -= c; m >>= 16; pos += 16; }
-  c = __popc(m & 0xFFu);
-  if (r >= c) { r -= c; m >>= 8; pos += 8; }
-  c = __popc(m & 0xFu);
-  if (r >= c) { r -= c; m >>= 4; pos += 4; }
-  c = __popc(m & 0x3u);
-  if (r >= c) { r -= c; m >>= 2; pos += 2; }
-  if (r >= (int)(m & 1u)) pos += 1;
-  return pos;
-}
-
 // LDS scratch of the segmented selection, one entry per lane (segment g uses
 // [base, base+SW)): left-stop and right-stop positions, a per-lane junk slot
 // pair that absorbs the writes of lanes that are not stops, and a spill list
@@ -188,20 +172,11 @@ __device__ inline void seg_nth_slots(int n, int nth, const Seg &sg, const SegScr
     const bool isL = part && ((Lw >> x) & 1u), isR = part && ((Rw >> x) & 1u);
     const int kL = __popc(Lw & xb);
     const int kR = nR - 1 - __popc(Rw & xb);
-#ifdef HMC_SEL_REG
-    // the partners from the stop masks in registers: r_kL is the
-    // (nR-1-kL)-th lowest right stop, l_kR the kR-th lowest left stop
-    const int r1 = nR - 1 - kL;
-    const int qR = sel_bit(Rw, r1 >= 0 && r1 < nR ? r1 : 0);
-    const int qL = sel_bit(Lw, kR >= 0 && kR < nL ? kR : 0);
-    (void)lp; (void)rp; (void)jl; (void)jr; (void)kmax;
-#else
     *(isL ? lp + kL : jl) = x;
     *(isR ? rp + kR : jr) = x;
     wave_lds_sync();
     const int qR = rp[kL < kmax ? kL : kmax];
     const int qL = lp[kR < 0 ? 0 : (kR < kmax ? kR : kmax)];
-#endif
     // pair k swaps iff l_k < r_k; both roles are checked, a position swaps at most once
     const bool lsw = isL && kL < nR && x < qR;
     const bool rsw = isR && kR < nL && qL < x;

@@ -1209,19 +1209,22 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
 hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStream_t st) {
   if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > F_MAX || (a.hcap & (a.hcap - 1)) || a.lds_hc < 1 ||
       (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || a.lds_cc < 0 || a.ccap < 1 || a.mod.head_len < 1 ||
-      (a.mod.head_len > 1 && (!a.mod.hf_off || !a.mod.hf_pairs || !a.mod.hf_status)) || (nw != 1 && nw != 4 && nw != 16))
+      (a.mod.head_len > 1 && (!a.mod.hf_off || !a.mod.hf_pairs || !a.mod.hf_status)) ||
+      (nw != 1 && nw != 4 && nw != 8 && nw != 16))
     return hipErrorInvalidValue;
   const size_t lds = estep_s1_lds_bytes(a.lds_fc, a.lds_hc, a.lds_cc, a.pan.amax, nw);
-  static size_t lds_attr[3] = {0, 0, 0};
-  const int ix = nw == 16 ? 2 : (nw == 4 ? 1 : 0);
+  static size_t lds_attr[4] = {0, 0, 0, 0};
+  const int ix = nw == 16 ? 3 : (nw == 8 ? 2 : (nw == 4 ? 1 : 0));
   const void *f = nw == 16 ? (const void *)estep_structure<16>
-                           : (nw == 4 ? (const void *)estep_structure<4> : (const void *)estep_structure<1>);
+                           : (nw == 8 ? (const void *)estep_structure<8>
+                                      : (nw == 4 ? (const void *)estep_structure<4> : (const void *)estep_structure<1>));
   if (lds > 65536 && lds > lds_attr[ix]) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     lds_attr[ix] = lds;
   }
   if (nw == 16) hipLaunchKernelGGL(estep_structure<16>, dim3(grid), dim3(16 * WAVE), lds, st, a);
+  else if (nw == 8) hipLaunchKernelGGL(estep_structure<8>, dim3(grid), dim3(8 * WAVE), lds, st, a);
   else if (nw == 4) hipLaunchKernelGGL(estep_structure<4>, dim3(grid), dim3(4 * WAVE), lds, st, a);
   else hipLaunchKernelGGL(estep_structure<1>, dim3(grid), dim3(WAVE), lds, st, a);
   return hipGetLastError();

@@ -293,7 +293,7 @@ int hmc_set_tuning(hmc_ctx *ctx, int frontier_cap, uint64_t trace_bytes, int wav
  * same rule.  Results do not depend on the shape. */
 int hmc_set_estep_shape(hmc_ctx *ctx, int waves_per_individual, int individuals_per_cu);
 /* Launch shapes of the split E-step's two passes, 0 = automatic for each:
- * structure pass waves per individual (1, 4 or 16; automatic: 4 on a model
+ * structure pass waves per individual (1, 4, 8 or 16; automatic: 4 on a model
  * with more patterns than the panel has individual-loci, the genotype-mined
  * M0, 16 when such a group has at most one individual per CU)
  * and individuals per CU (automatic: 1 at 16 waves, 2 at 4; else 12 above 8 per CU in
