@@ -965,12 +965,23 @@ struct Ctx {
   int exact_walk_group(ExactArgs &x, int k, int dev_cu) {
     const int L = pan.L;
     hipError_t e;
-    x.scratch_stride = exact_walk_scratch_doubles(tr_maxd, x.fmax);
+    x.scratch_stride = exact_walk_scratch_doubles(tr_maxd, x.fmax, x.width);
     const long long items = (long long)k * L;
-    const int grid = (int)std::max<long long>(1, std::min<long long>(items, (long long)dev_cu * 16));
-    if ((e = d_xscr.ensure(x.scratch_stride * grid)) ||
-        (e = hipMemsetAsync(d_xscr.p, 0, x.scratch_stride * grid * 8, st)))  // the walk's zero invariant
-      return hipfail(e, "exact scratch");
+    // 28 waves per CU (7 per SIMD at 64 VGPRs), fewer when the per-wave lists
+    // would pass SCRATCH_MAX
+    const long long by_mem = std::max<long long>(1, (long long)(SCRATCH_MAX / (x.scratch_stride * 8)));
+    const int grid = (int)std::max<long long>(1, std::min<long long>(std::min<long long>(items, (long long)dev_cu * 28), by_mem));
+    // the walk's zero invariant: every item clears what it wrote, so the
+    // scratch is all zero after every complete launch whatever its layout;
+    // only memory not zeroed since its allocation needs a memset
+    const size_t need = x.scratch_stride * grid;
+    const bool fresh = !d_xscr.p || need > d_xscr.n || !xscr_zeroed;  // (re)allocated, or a launch failed
+    if ((e = d_xscr.ensure(need))) return hipfail(e, "exact scratch");
+    if (fresh || need > xscr_zero_n) {
+      if ((e = hipMemsetAsync(d_xscr.p, 0, d_xscr.n * 8, st))) return hipfail(e, "exact scratch");
+      xscr_zero_n = d_xscr.n;
+    }
+    xscr_zeroed = false;  // until the walk below completes
     x.scratch = d_xscr.p;
     // in slices of the items, so that a long walk reports progress (and the
     // scratch returns to zero between slices: every item clears its entries)
@@ -988,9 +999,12 @@ struct Ctx {
       if (debug_mem && items > 16 * (long long)grid)
         fprintf(stderr, "[hmc] exact walk: items %lld..%lld of %lld (%d individuals), %.1f ms\n", i0, x.item1, items, k, ms);
     }
+    xscr_zeroed = true;
     return HMC_OK;
   }
   double ms_walk = 0;
+  bool xscr_zeroed = false;  // d_xscr is all zero (up to xscr_zero_n doubles) since the last complete walk
+  size_t xscr_zero_n = 0;
   // Rounds of one exact M-step share the E-step model: when a round's
   // individuals ran as one structure pass and one group, the next rounds walk
   // their new tries over the same records and fwd/bwd sums (exact_walk only).

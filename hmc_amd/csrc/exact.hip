@@ -152,29 +152,49 @@ __global__ __launch_bounds__(256) void exact_fb(ExactArgs a) {
   }
 }
 
+// One contribution's terms into a child list set (HaploBuilder.cpp:375-427):
+// ma / mb = the child's allele is the pair's a / b allele at this locus.
+__device__ inline void walk_terms(bool ma, bool mb, bool rev, double w0, double w1, double w2, double tp, double &n0,
+                                  double &n1, double &n2) {
+  if (ma && mb) n0 += w0 * tp;
+  else if (ma) n1 += w0 * tp * 0.5;
+  else n2 += w0 * tp * 0.5;
+  // a-side list follows the a haplotype: links[0] keep it on a, links[1] move it to b
+  if (!rev ? ma : mb) (!rev ? n1 : n2) += w1 * tp;
+  if (!rev ? mb : ma) (!rev ? n2 : n1) += w2 * tp;
+}
+
 // The ForwardPatternTree walk of HaploBuilder::estimateFrequency (:296-308,
 // :334-450), one wavefront per (individual, start locus), sparse like the
-// reference's maps: a node's three lists are held densely per state (zero
-// where absent) but only the states listed in the depth's `touched` list are
-// ever written, and a child's states are found by following the forward
-// links (the extendAll contributions of the record) of its parent's non-zero
-// states, as the reference pushes along forward_links (:369-427).  Each
-// reached state then gathers over its incoming contributions in record order
-// (the same terms; zero sources add +0.0), so the sums do not depend on the
-// order the states were reached in.  Scratch invariant: every dense entry not
-// in a touched list is 0.0 (the host zeroes the scratch before the launch and
-// every item clears what it wrote).
+// reference's maps.  A node's children are computed together: the states
+// its non-zero states link to (forward links of the record, marked in an
+// LDS bitmap and compacted in state order) gather, over their incoming
+// contributions in record order, the three lists of every child whose allele
+// their pair carries — a heterozygous state feeds two children from one pass
+// over its contributions.  The children's lists are kept per depth, one slot
+// per allele, so the walk descends into them in allele order without
+// recomputing.  Each child's frequency is sum(weight * backward) over the
+// union of reached states in state order (zero entries add +0.0).  Scratch
+// invariant: every dense entry not in a touched list is 0.0 (the host zeroes
+// the scratch before the launch and every item clears what it wrote).
 __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
-  extern __shared__ int stk[];  // [maxd+1] node, [maxd+1] next child, [maxd+1] touched count, marks
+  extern __shared__ unsigned long long stk64[];  // per depth: descend mask, written-slot mask; then ints; marks
   const int lane = threadIdx.x;
   const int L = a.L, hl = a.head_len, W = a.width, maxd = a.max_depth;
-  int *snode = stk, *snext = stk + maxd + 1, *tcnt = stk + 2 * (maxd + 1);
-  uint32_t *marks = (uint32_t *)(stk + 3 * (maxd + 1));  // [fmax/32 + 1] reached-state bitmap
+  const int D = maxd + 2;
+  unsigned long long *sdesc = stk64, *smask = stk64 + D;
+  int *snode = (int *)(stk64 + 2 * D), *snext = snode + D, *sslot = snext + D, *tcnt = sslot + D;
+  uint32_t *marks = (uint32_t *)(tcnt + D);  // [fmax/32 + 1] reached-state bitmap
   const int nwords = (a.fmax + 31) >> 5;
-  double *lists = a.scratch + (size_t)blockIdx.x * a.scratch_stride;  // [maxd+1][3][fmax]
-  double *nf = lists + (size_t)(maxd + 1) * 3 * a.fmax;                // [maxd+2]
-  uint32_t *touched = (uint32_t *)(nf + maxd + 2);                      // [maxd+1][fmax]
-  for (int d = lane; d <= maxd; d += WAVE) tcnt[d] = 0;
+  const size_t slot_doubles = (size_t)3 * a.fmax;
+  double *lists = a.scratch + (size_t)blockIdx.x * a.scratch_stride;      // [maxd+1][W][3][fmax]
+  double *cfreq = lists + (size_t)(maxd + 1) * W * slot_doubles;          // [maxd+2][W]
+  uint32_t *touched = (uint32_t *)(cfreq + (size_t)(maxd + 2) * W);       // [maxd+1][fmax]
+  auto slot = [&](int d, int i) { return lists + ((size_t)d * W + i) * slot_doubles; };
+  for (int d = lane; d < D; d += WAVE) {
+    tcnt[d] = 0;
+    smask[d] = 0ull;
+  }
   for (int w = lane; w < nwords; w += WAVE) marks[w] = 0u;
   __builtin_amdgcn_wave_barrier();
   __threadfence_block();
@@ -195,15 +215,17 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
       const int e0 = start > hl ? start : hl;
       const int F0 = (int)a.rec[roff[e0]];
       const double *fw = (const double *)(a.x + xo[e0]);
+      double *S0 = slot(0, 0);
       for (int t = lane; t < F0; t += WAVE) {
-        lists[t] = fw[t];
+        S0[t] = fw[t];
         touched[t] = (uint32_t)t;
       }
       if (lane == 0) {
         tcnt[0] = F0;
+        smask[0] = 1ull;
         snode[0] = root;
-        snext[0] = 0;
-        nf[0] = 1.0;  // the root's children get prefix frequency 1.0 (HaploBuilder.cpp:305)
+        snext[0] = -1;  // children not computed yet
+        sslot[0] = 0;
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -213,187 +235,241 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
       __builtin_amdgcn_wave_barrier();
       __threadfence_block();
       const int node = snode[d];
-      int i = snext[d];
-      int child = -1;
-      while (i < W && child < 0) {
-        child = a.tr_child[(size_t)node * W + i];
-        if (child < 0) ++i;
+      if (snext[d] < 0) {  // ---- all children of this node, into depth d+1 ----
+        unsigned long long cm = 0ull;  // alleles with a child
+        if (d < maxd)
+          for (int i0 = 0; i0 < W; i0 += WAVE) {
+            const int i = i0 + lane;
+            cm |= __ballot(i < W && a.tr_child[(size_t)node * W + i] >= 0) << i0;
+          }
+        if (cm == 0ull) {  // node done
+          --d;
+          continue;
+        }
+        const int locus = start + d;  // the children's allele is at this locus
+        const double last_freq = d == 0 ? 1.0 : cfreq[(size_t)d * W + sslot[d]];  // prefix freq (HaploBuilder.cpp:305)
+        const double *P0 = slot(d, sslot[d]), *P1 = P0 + a.fmax, *P2 = P1 + a.fmax;
+        const uint32_t *Tp = touched + (size_t)d * a.fmax;
+        uint32_t *Tc = touched + (size_t)(d + 1) * a.fmax;
+        {  // the previous sibling's children at depth d+1 back to zero
+          const int nc = tcnt[d + 1];
+          const unsigned long long wm = smask[d + 1];
+          for (int j = lane; j < nc; j += WAVE) {
+            const uint32_t t = Tc[j];
+            for (unsigned long long m = wm; m; m &= m - 1) {
+              double *C0 = slot(d + 1, __builtin_ctzll(m));
+              C0[t] = 0.0;
+              C0[a.fmax + t] = 0.0;
+              C0[2 * a.fmax + t] = 0.0;
+            }
+          }
+        }
+        int ntc = 0;
+        const double *bw;
+        if (locus < hl) {  // head pairs: their patterns' alleles (HaploBuilder.cpp:340-367), same states
+          const RecView R(Rh, true);
+          const uint32_t *plo = R.cb + Fh + 1, *phi = plo + Fh;
+          bw = (const double *)(a.x + xo[hl]) + Fh;
+          for (int t = lane; t < Fh; t += WAVE) {
+            uint32_t xa, xb;
+            if (hl == 1) {
+              xa = R.hdr[t] & 0xFFu;
+              xb = (R.hdr[t] >> 8) & 0xFFu;
+            } else {
+              xa = a.head_al[(size_t)plo[t] * hl + locus];
+              xb = a.head_al[(size_t)phi[t] * hl + locus];
+            }
+            const double w0 = P0[t], w1 = P1[t], w2 = P2[t];
+            for (unsigned long long m = cm; m; m &= m - 1) {
+              const uint32_t i = (uint32_t)__builtin_ctzll(m);
+              const bool ma = xa == i, mb = xb == i;
+              double n0 = 0.0, n1 = 0.0, n2 = 0.0;
+              if (ma) {
+                if (mb) n0 = w0;
+                else n1 = w0 * 0.5;
+              } else if (mb) {
+                n2 = w0 * 0.5;
+              }
+              if (ma) n1 += w1;
+              if (mb) n2 += w2;
+              double *C0 = slot(d + 1, (int)i);
+              C0[t] = n0;
+              C0[a.fmax + t] = n1;
+              C0[2 * a.fmax + t] = n2;
+            }
+            Tc[t] = (uint32_t)t;
+          }
+          ntc = Fh;
+        } else {  // along the forward links into the states after `locus` (:369-427)
+          const RecView R(a.rec + roff[locus + 1], false);
+          bw = (const double *)(a.x + xo[locus + 1]) + R.F;
+          // (1) mark the states the parent's non-zero states link to and whose
+          //     pair carries the allele of some child on either side
+          const int np = tcnt[d];
+          const int Fp = (int)a.rec[roff[locus]];  // states the links leave from
+          for (int j = lane; j < np; j += WAVE) {
+            const uint32_t s = Tp[j];
+            if (P0[s] == 0.0 && P1[s] == 0.0 && P2[s] == 0.0) continue;
+            uint32_t off = 0;
+            for (int p = 0; p < R.NP; ++p) {
+              const uint32_t no = R.npo[p];
+              for (uint32_t o = 0; o < no; ++o) {
+                const uint32_t w = R.out[off + s * no + o];
+                if (w != NONE) {
+                  const uint32_t t = cw_state(w);
+                  const uint32_t hd = R.hdr[t];
+                  if (((cm >> (hd & 0xFFu)) & 1ull) || ((cm >> ((hd >> 8) & 0xFFu)) & 1ull))
+                    atomicOr(&marks[t >> 5], 1u << (t & 31u));
+                }
+              }
+              off += (uint32_t)Fp * no;
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+          __threadfence_block();
+          // (2) the marked states in ascending order; the bitmap back to zero
+          const int nw = (R.F + 31) >> 5;
+          for (int w0 = 0; w0 < nw; w0 += WAVE) {
+            const int w = w0 + lane;
+            uint32_t bits = w < nw ? marks[w] : 0u;
+            const int c = __popc(bits);
+            int incl = c;
+#pragma unroll
+            for (int dd = 1; dd < 64; dd <<= 1) {
+              const int y = __shfl_up(incl, dd);
+              if (lane >= dd) incl += y;
+            }
+            int at = ntc + incl - c;
+            while (bits) {
+              const int b = __builtin_ctz(bits);
+              bits &= bits - 1u;
+              Tc[at++] = (uint32_t)(w * 32 + b);
+            }
+            if (w < nw) marks[w] = 0u;
+            ntc += __shfl(incl, 63);
+          }
+          __builtin_amdgcn_wave_barrier();
+          __threadfence_block();
+          // (3) each reached state gathers over its incoming contributions, for
+          //     the children of its a allele and of its b allele in one pass
+          for (int j = lane; j < ntc; j += WAVE) {
+            const uint32_t t = Tc[j];
+            const uint32_t hd = R.hdr[t];
+            const uint32_t xa = hd & 0xFFu, xb = (hd >> 8) & 0xFFu;
+            const bool ca = (cm >> xa) & 1ull, cb = xb != xa && ((cm >> xb) & 1ull);
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0, b0 = 0.0, b1 = 0.0, b2 = 0.0;
+            const double tp = R.tpv[t];
+            for (uint32_t r = R.cb[t]; r < R.cb[t + 1]; ++r) {
+              const uint32_t w = R.ct[r];
+              const uint32_t s = cw_state(w);
+              const bool rev = cw_rev(w);
+              const double w0 = P0[s], w1 = P1[s], w2 = P2[s];
+              if (ca) walk_terms(true, xb == xa, rev, w0, w1, w2, tp, a0, a1, a2);
+              if (cb) walk_terms(false, true, rev, w0, w1, w2, tp, b0, b1, b2);
+            }
+            if (ca) {
+              double *C0 = slot(d + 1, (int)xa);
+              C0[t] = a0;
+              C0[a.fmax + t] = a1;
+              C0[2 * a.fmax + t] = a2;
+            }
+            if (cb) {
+              double *C0 = slot(d + 1, (int)xb);
+              C0[t] = b0;
+              C0[a.fmax + t] = b1;
+              C0[2 * a.fmax + t] = b2;
+            }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __threadfence_block();
+        // (4) every child's frequency: hp->setFrequency(+freq), setPrefixFreq(+last_freq) (:437-441)
+        unsigned long long desc = 0ull;
+        for (unsigned long long m = cm; m; m &= m - 1) {
+          const int i = __builtin_ctzll(m);
+          const double *C0 = slot(d + 1, i);
+          double part = 0.0;
+          bool any = false;
+          for (int j = lane; j < ntc; j += WAVE) {
+            const uint32_t t = Tc[j];
+            const double n0 = C0[t], n1 = C0[a.fmax + t], n2 = C0[2 * a.fmax + t];
+            part += ((n0 + n1) + n2) * bw[t];
+            any |= (n0 != 0.0) | (n1 != 0.0) | (n2 != 0.0);
+          }
+          const double freq = wave_sum_fixed(part) / pg;
+          const int child = a.tr_child[(size_t)node * W + i];
+          const int pat = a.tr_data[child];
+          if (lane == 0) {
+            cfreq[(size_t)(d + 1) * W + i] = freq;
+            if (pat >= 0) {
+              atomicAdd(&a.acc_freq[pat], (unsigned long long)__double2ll_rn(freq * EXACT_FIXED_SCALE));
+              atomicAdd(&a.acc_prefix[pat], (unsigned long long)__double2ll_rn(last_freq * EXACT_FIXED_SCALE));
+            }
+          }
+          if (__ballot(any) != 0ull && d + 1 <= maxd) desc |= 1ull << i;
+        }
+        if (lane == 0) {
+          tcnt[d + 1] = ntc;
+          smask[d + 1] = cm;
+          sdesc[d] = desc;
+          snext[d] = 0;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __threadfence_block();
       }
-      if (child < 0 || d >= maxd) {  // node done
+      // ---- descend into the next child whose lists are not all zero ----
+      const unsigned long long left = sdesc[d] & ~((1ull << snext[d]) - 1ull);
+      if (left == 0ull) {  // node done
         --d;
         continue;
       }
-      if (lane == 0) snext[d] = i + 1;
-      const int locus = start + d;       // the child's allele is at this locus
-      const double last_freq = nf[d];
-      const double *P0 = lists + (size_t)d * 3 * a.fmax, *P1 = P0 + a.fmax, *P2 = P1 + a.fmax;
-      double *C0 = lists + (size_t)(d + 1) * 3 * a.fmax, *C1 = C0 + a.fmax, *C2 = C1 + a.fmax;
-      const uint32_t *Tp = touched + (size_t)d * a.fmax;
-      uint32_t *Tc = touched + (size_t)(d + 1) * a.fmax;
-      // the previous sibling's entries at depth d+1 back to zero
-      {
-        const int nc = tcnt[d + 1];
-        for (int j = lane; j < nc; j += WAVE) {
-          const uint32_t t = Tc[j];
-          C0[t] = 0.0;
-          C1[t] = 0.0;
-          C2[t] = 0.0;
-        }
-      }
-      double part = 0.0;
-      bool any = false;
-      int ntc = 0;
-      if (locus < hl) {  // head pairs: their patterns' alleles (HaploBuilder.cpp:340-367), same states
-        const RecView R(Rh, true);
-        const uint32_t *plo = R.cb + Fh + 1, *phi = plo + Fh;
-        const double *bw = (const double *)(a.x + xo[hl]) + Fh;
-        for (int t = lane; t < Fh; t += WAVE) {
-          uint32_t xa, xb;
-          if (hl == 1) {
-            xa = R.hdr[t] & 0xFFu;
-            xb = (R.hdr[t] >> 8) & 0xFFu;
-          } else {
-            xa = a.head_al[(size_t)plo[t] * hl + locus];
-            xb = a.head_al[(size_t)phi[t] * hl + locus];
-          }
-          const bool ma = xa == (uint32_t)i, mb = xb == (uint32_t)i;
-          const double w0 = P0[t], w1 = P1[t], w2 = P2[t];
-          double n0 = 0.0, n1 = 0.0, n2 = 0.0;
-          if (ma) {
-            if (mb) n0 = w0;
-            else n1 = w0 * 0.5;
-          } else if (mb) {
-            n2 = w0 * 0.5;
-          }
-          if (ma) n1 += w1;
-          if (mb) n2 += w2;
-          C0[t] = n0;
-          C1[t] = n1;
-          C2[t] = n2;
-          Tc[t] = (uint32_t)t;
-          part += ((n0 + n1) + n2) * bw[t];
-          any |= (n0 != 0.0) | (n1 != 0.0) | (n2 != 0.0);
-        }
-        ntc = Fh;
-      } else {  // along the forward links into the states after `locus` (:369-427)
-        const RecView R(a.rec + roff[locus + 1], false);
-        const double *bw = (const double *)(a.x + xo[locus + 1]) + R.F;
-        // (1) mark the states the parent's non-zero states link to and whose
-        //     pair carries the child's allele on either side
-        const int np = tcnt[d];
-        const int Fp = (int)a.rec[roff[locus]];  // states the links leave from
-        for (int j = lane; j < np; j += WAVE) {
-          const uint32_t s = Tp[j];
-          if (P0[s] == 0.0 && P1[s] == 0.0 && P2[s] == 0.0) continue;
-          uint32_t off = 0;
-          for (int p = 0; p < R.NP; ++p) {
-            const uint32_t no = R.npo[p];
-            for (uint32_t o = 0; o < no; ++o) {
-              const uint32_t w = R.out[off + s * no + o];
-              if (w != NONE) {
-                const uint32_t t = cw_state(w);
-                const uint32_t hd = R.hdr[t];
-                if ((hd & 0xFFu) == (uint32_t)i || ((hd >> 8) & 0xFFu) == (uint32_t)i)
-                  atomicOr(&marks[t >> 5], 1u << (t & 31u));
-              }
-            }
-            off += (uint32_t)Fp * no;
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-        __threadfence_block();
-        // (2) the marked states in ascending order; the bitmap back to zero
-        const int nw = (R.F + 31) >> 5;
-        for (int w0 = 0; w0 < nw; w0 += WAVE) {
-          const int w = w0 + lane;
-          uint32_t bits = w < nw ? marks[w] : 0u;
-          const int c = __popc(bits);
-          int incl = c;
-#pragma unroll
-          for (int dd = 1; dd < 64; dd <<= 1) {
-            const int y = __shfl_up(incl, dd);
-            if (lane >= dd) incl += y;
-          }
-          int at = ntc + incl - c;
-          while (bits) {
-            const int b = __builtin_ctz(bits);
-            bits &= bits - 1u;
-            Tc[at++] = (uint32_t)(w * 32 + b);
-          }
-          if (w < nw) marks[w] = 0u;
-          ntc += __shfl(incl, 63);
-        }
-        __builtin_amdgcn_wave_barrier();
-        __threadfence_block();
-        // (3) each reached state gathers over its incoming contributions
-        for (int j = lane; j < ntc; j += WAVE) {
-          const uint32_t t = Tc[j];
-          const uint32_t hd = R.hdr[t];
-          const bool ma = (hd & 0xFFu) == (uint32_t)i, mb = ((hd >> 8) & 0xFFu) == (uint32_t)i;
-          double n0 = 0.0, n1 = 0.0, n2 = 0.0;
-          const double tp = R.tpv[t];
-          for (uint32_t r = R.cb[t]; r < R.cb[t + 1]; ++r) {
-            const uint32_t w = R.ct[r];
-            const uint32_t s = cw_state(w);
-            const bool rev = cw_rev(w);
-            const double w0 = P0[s], w1 = P1[s], w2 = P2[s];
-            if (ma && mb) n0 += w0 * tp;
-            else if (ma) n1 += w0 * tp * 0.5;
-            else n2 += w0 * tp * 0.5;
-            // a-side list follows the a haplotype: links[0] keep it on a, links[1] move it to b
-            if (!rev ? ma : mb) (!rev ? n1 : n2) += w1 * tp;
-            if (!rev ? mb : ma) (!rev ? n2 : n1) += w2 * tp;
-          }
-          C0[t] = n0;
-          C1[t] = n1;
-          C2[t] = n2;
-          part += ((n0 + n1) + n2) * bw[t];
-          any |= (n0 != 0.0) | (n1 != 0.0) | (n2 != 0.0);
-        }
-      }
-      if (lane == 0) tcnt[d + 1] = ntc;
-      const double freq = wave_sum_fixed(part) / pg;
-      const int pat = a.tr_data[child];
-      if (lane == 0 && pat >= 0) {  // hp->setFrequency(+freq), setPrefixFreq(+last_freq) (:437-441)
-        atomicAdd(&a.acc_freq[pat], (unsigned long long)__double2ll_rn(freq * EXACT_FIXED_SCALE));
-        atomicAdd(&a.acc_prefix[pat], (unsigned long long)__double2ll_rn(last_freq * EXACT_FIXED_SCALE));
-      }
-      const bool descend = __ballot(any) != 0ull && d + 1 <= maxd;
+      const int i = __builtin_ctzll(left);
+      const int child = a.tr_child[(size_t)node * W + i];
       __builtin_amdgcn_wave_barrier();
-      __threadfence_block();
-      if (descend) {
-        if (lane == 0) {
-          snode[d + 1] = child;
-          snext[d + 1] = 0;
-          nf[d + 1] = freq;
-        }
-        ++d;
+      if (lane == 0) {
+        snext[d] = i + 1;
+        snode[d + 1] = child;
+        snext[d + 1] = -1;
+        sslot[d + 1] = i;
       }
+      ++d;
     }
     // the item's entries back to zero (scratch invariant)
     __builtin_amdgcn_wave_barrier();
     __threadfence_block();
     for (int dd = 0; dd <= maxd; ++dd) {
       const int nc = tcnt[dd];
-      double *D0 = lists + (size_t)dd * 3 * a.fmax;
+      const unsigned long long wm = smask[dd];
       const uint32_t *T = touched + (size_t)dd * a.fmax;
       for (int j = lane; j < nc; j += WAVE) {
         const uint32_t t = T[j];
-        D0[t] = 0.0;
-        D0[a.fmax + t] = 0.0;
-        D0[2 * a.fmax + t] = 0.0;
+        for (unsigned long long m = wm; m; m &= m - 1) {
+          double *D0 = slot(dd, __builtin_ctzll(m));
+          D0[t] = 0.0;
+          D0[a.fmax + t] = 0.0;
+          D0[2 * a.fmax + t] = 0.0;
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();
     __threadfence_block();
-    for (int dd = lane; dd <= maxd; dd += WAVE) tcnt[dd] = 0;
+    for (int dd = lane; dd < D; dd += WAVE) {
+      tcnt[dd] = 0;
+      smask[dd] = 0ull;
+    }
     __builtin_amdgcn_wave_barrier();
     __threadfence_block();
   }
 }
 
-size_t exact_walk_scratch_doubles(int max_depth, int fmax) {
-  return (size_t)(max_depth + 1) * 3 * fmax + max_depth + 2 + ((size_t)(max_depth + 1) * fmax + 1) / 2;
+size_t exact_walk_scratch_doubles(int max_depth, int fmax, int width) {
+  return (size_t)(max_depth + 1) * width * 3 * fmax + (size_t)(max_depth + 2) * width +
+         ((size_t)(max_depth + 1) * fmax + 1) / 2;
+}
+
+size_t exact_walk_lds_bytes(int max_depth, int fmax) {
+  const size_t D = (size_t)max_depth + 2;
+  return D * 16 + D * 16 + (size_t)((fmax + 31) / 32 + 1) * 4;
 }
 
 hipError_t launch_exact_fb(const ExactArgs &a, int grid, hipStream_t st) {
@@ -404,7 +480,8 @@ hipError_t launch_exact_fb(const ExactArgs &a, int grid, hipStream_t st) {
 
 hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st) {
   if (a.n_order <= 0) return hipSuccess;
-  const size_t lds = (size_t)3 * (a.max_depth + 1) * sizeof(int) + (size_t)((a.fmax + 31) / 32 + 1) * 4;
+  if (a.width < 1 || a.width > 64) return hipErrorInvalidValue;
+  const size_t lds = exact_walk_lds_bytes(a.max_depth, a.fmax);
   if (lds > 65536) return hipErrorInvalidValue;
   hipLaunchKernelGGL(exact_walk, dim3(grid), dim3(WAVE), lds, st, a);
   return hipGetLastError();

@@ -26,9 +26,9 @@ struct ExactArgs {
   const int32_t *tr_root;          // [L] root node of each start locus, -1 = empty
   int max_depth;                   // longest candidate
   const uint8_t *head_al;          // [P][head_len] head patterns' alleles (head_len > 1)
-  // per-wave scratch (exact_walk_scratch_doubles): lists [max_depth+1][3][fmax],
-  // node frequencies [max_depth+2] (doubles), touched states [max_depth+1][fmax]
-  // (u32); zero before the launch
+  // per-wave scratch (exact_walk_scratch_doubles): lists [max_depth+1][width][3][fmax],
+  // children's frequencies [max_depth+2][width] (doubles), touched states
+  // [max_depth+1][fmax] (u32); zero before the launch
   double *scratch;
   size_t scratch_stride;           // doubles
   int fmax;                        // most states of any locus of the group
@@ -38,6 +38,7 @@ struct ExactArgs {
 
 hipError_t launch_exact_fb(const ExactArgs &a, int grid, hipStream_t st);
 hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st);
-size_t exact_walk_scratch_doubles(int max_depth, int fmax);
+size_t exact_walk_scratch_doubles(int max_depth, int fmax, int width);
+size_t exact_walk_lds_bytes(int max_depth, int fmax);
 
 }  // namespace hmc
