@@ -971,21 +971,16 @@ struct Ctx {
     // would pass SCRATCH_MAX
     const long long by_mem = std::max<long long>(1, (long long)(SCRATCH_MAX / (x.scratch_stride * 8)));
     const int grid = (int)std::max<long long>(1, std::min<long long>(std::min<long long>(items, (long long)dev_cu * 28), by_mem));
-    // the walk's zero invariant: every item clears what it wrote, so the
-    // scratch is all zero after every complete launch whatever its layout;
-    // only memory not zeroed since its allocation needs a memset
+    // the walk's zero invariant (its lists; the child frequencies and touched
+    // lists are left behind by each item and would land inside the lists of
+    // a group whose depth or frontier differs): zeroed for every group
     const size_t need = x.scratch_stride * grid;
-    const bool fresh = !d_xscr.p || need > d_xscr.n || !xscr_zeroed;  // (re)allocated, or a launch failed
-    if ((e = d_xscr.ensure(need))) return hipfail(e, "exact scratch");
-    if (fresh || need > xscr_zero_n) {
-      if ((e = hipMemsetAsync(d_xscr.p, 0, d_xscr.n * 8, st))) return hipfail(e, "exact scratch");
-      xscr_zero_n = d_xscr.n;
-    }
-    xscr_zeroed = false;  // until the walk below completes
+    if ((e = d_xscr.ensure(need)) || (e = hipMemsetAsync(d_xscr.p, 0, need * 8, st)))
+      return hipfail(e, "exact scratch");
     x.scratch = d_xscr.p;
-    // in slices of the items, so that a long walk reports progress (and the
-    // scratch returns to zero between slices: every item clears its entries)
-    const long long slice = std::max<long long>(grid, (items + 15) / 16);
+    // long walks (over 4 M items) in 16 slices, so that they report progress
+    // (the lists return to zero between slices: every item clears its entries)
+    const long long slice = items > (4ll << 20) ? std::max<long long>(grid, (items + 15) / 16) : items;
     for (long long i0 = 0; i0 < items; i0 += slice) {
       x.item0 = i0;
       x.item1 = std::min(items, i0 + slice);
@@ -999,12 +994,9 @@ struct Ctx {
       if (debug_mem && items > 16 * (long long)grid)
         fprintf(stderr, "[hmc] exact walk: items %lld..%lld of %lld (%d individuals), %.1f ms\n", i0, x.item1, items, k, ms);
     }
-    xscr_zeroed = true;
     return HMC_OK;
   }
   double ms_walk = 0;
-  bool xscr_zeroed = false;  // d_xscr is all zero (up to xscr_zero_n doubles) since the last complete walk
-  size_t xscr_zero_n = 0;
   // Rounds of one exact M-step share the E-step model: when a round's
   // individuals ran as one structure pass and one group, the next rounds walk
   // their new tries over the same records and fwd/bwd sums (exact_walk only).
@@ -1200,6 +1192,10 @@ struct Ctx {
     hipEventRecord(ev[5], st);
     hipError_t e;
     if ((e = hipStreamSynchronize(st))) return hipfail(e, "exact");
+    // the walk's scratch (up to SCRATCH_MAX) and the tries go back to the E-step
+    d_xscr.release();
+    d_tr_child.release();
+    d_tr_data.release();
     float ms = 0;
     hipEventElapsedTime(&ms, ev[4], ev[5]);
     ms_m = ms;
