@@ -802,15 +802,14 @@ __device__ inline bool k2_write_trace(const ValueArgs &a, K2Shared *bs, const VF
 #ifndef HMC_TRACE_PER_STATE
   for (int t = threadIdx.x; t < F; t += NT) hdr[t] = (Rhd[t] & 0xFFFFu) | *Y.nl(t) << 16;
   // the link block is the frontier's meta array in state order (LDS tier,
-  // then HBM tier), links past a list's length zeroed: thread (tt, kk) of a
-  // sweep writes word t*S + kk of state t = tt, tt + per, ... — one coalesced
-  // word per thread and step, and one division per thread, not per word
-  const int per = NT / S, tt = (int)threadIdx.x / S, kk = (int)threadIdx.x - tt * S;
-  if (tt < per)
-    for (int t = tt; t < F; t += per) {
-      const uint32_t n = *Y.nl(t);
-      lnk[(size_t)t * S + kk] = (uint32_t)kk < n ? Y.meta(t)[kk] : 0u;
-    }
+  // then HBM tier), links past a list's length zeroed: one coalesced word
+  // per thread and step
+  const uint32_t nlw = (uint32_t)F * (uint32_t)S;
+  for (uint32_t w = threadIdx.x; w < nlw; w += (uint32_t)NT) {
+    const uint32_t t = w / (uint32_t)S, k = w - t * (uint32_t)S;
+    const uint32_t n = *Y.nl((int)t);
+    lnk[w] = k < n ? Y.meta((int)t)[k] : 0u;
+  }
 #else  // one thread per state, S words each
   for (int t = threadIdx.x; t < F; t += NT) {
     const uint32_t n = *Y.nl(t);
