@@ -1,10 +1,17 @@
-// coop_bench.hip — microbenchmark of the value pass's segmented selection
-// (coop_select.hpp, never the product): every wave runs chains of adds on
-// 2S-lane segments like phase B of estep_values — S new likelihoods (few
-// distinct values, so ties occur) behind the segment's S kept ones, then
-// std::nth_element(.., S-1, ..) — and a checksum of the kept lists.
+// coop_bench.hip — microbenchmark of k-best list selections (never the
+// product): chains of adds like phase B of estep_values — S new likelihoods
+// (few distinct values, so ties occur) behind a list's S kept ones, then
+// std::nth_element(.., S-1, ..).  Every mode processes the same lists (list
+// g's values depend only on g, the add and the position) and prints a
+// checksum of the kept lists, which must agree between modes.
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -I hmc_amd/csrc tools/diag/coop_bench.hip -o coop_bench
-//   ./coop_bench [waves_per_cu] [adds]
+//   ./coop_bench [waves_per_cu] [adds] [mode] [S]
+//   mode 0: 2S-lane segments, 64/2S lists per wave (seg_nth_slots, LDS slots)
+//   (mode 1, one list per wave in registers with wave-uniform scalar control,
+//   was measured at 6 200 cycles per add alone and 1.0 ns per add at 24 waves
+//   per CU — slower than mode 0 — and removed; profiles/r03/coop/)
+//   mode 2: one list per lane, sequential libstdc++ code on an LDS column
+//   mode 3: one list per lane, mask partition (nth_element_greater_masks)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -22,57 +29,94 @@ __device__ inline uint32_t mix(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
+__device__ inline double val(uint32_t g, int r, int k) { return (double)(mix(g * 1000003u + (uint32_t)r * 64u + (uint32_t)k) % 64u); }
 
-__global__ __launch_bounds__(64) void bench(int S, int adds, double *out) {
+__device__ inline double fold(double acc) {
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  return acc;
+}
+
+__global__ __launch_bounds__(64) void bench_seg(int S, int adds, double *out) {
   extern __shared__ unsigned char sm[];
   const int lane = threadIdx.x;
   SegScratch ss{(int *)sm, (int *)sm + 64, (int *)sm + 128, (double *)(sm + 1024), (uint32_t *)(sm + 1024 + 512)};
   const Seg sg = make_seg(2 * S);
   const int G = 64 / (2 * S);
   const bool in = sg.g < G;
-  uint32_t h = mix(blockIdx.x * 64 + lane);
+  const uint32_t g = blockIdx.x * G + sg.g;
   if (in && sg.k < S) {
-    ss.slik[lane] = (double)(mix(h) % 64);
+    ss.slik[lane] = val(g, 0, sg.k);
     ss.smeta[lane] = sg.k;
   }
   wave_lds_sync();
-  for (int r = 0; r < adds; ++r) {
-    h = mix(h + r);
+  for (int r = 1; r <= adds; ++r) {
     if (in && sg.k >= S) {
-      ss.slik[lane] = (double)(h % 64);
-      ss.smeta[lane] = 1000u * r + sg.k;
+      ss.slik[lane] = val(g, r, sg.k - S);
+      ss.smeta[lane] = 64u * r + sg.k - S;
     }
     wave_lds_sync();
     seg_nth_slots(in ? 2 * S : 0, S - 1, sg, ss);
   }
   double acc = 0.0;
   if (in && sg.k < S) acc = ss.slik[lane] * (double)(ss.smeta[lane] % 97);
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  acc = fold(acc);
+  if (lane == 0) out[blockIdx.x] = acc;
+}
+
+template <bool MASKS>
+__global__ __launch_bounds__(64) void bench_lane(int S, int adds, double *out) {
+  extern __shared__ unsigned char sm[];
+  const int lane = threadIdx.x;
+  const uint32_t g = blockIdx.x * 64 + lane;
+  // column `lane` of a [2S][64] image: element k at row k
+  double *col = (double *)sm + lane;
+  uint32_t *mcol = (uint32_t *)(sm + (size_t)2 * S * 64 * 8) + lane;
+  const LinkList L{col, mcol, 64};
+  for (int k = 0; k < S; ++k) L.set(k, val(g, 0, k), (uint32_t)k);
+  for (int r = 1; r <= adds; ++r) {
+    for (int k = 0; k < S; ++k) L.set(S + k, val(g, r, k), 64u * r + k);
+    if (MASKS) nth_element_greater_masks(L, 2 * S, S - 1, 2 * S);
+    else nth_element_greater(L, 2 * S, S - 1);
+  }
+  double acc = 0.0;
+  for (int k = 0; k < S; ++k) acc += L.l(k) * (double)(L.m(k) % 97);
+  acc = fold(acc);
   if (lane == 0) out[blockIdx.x] = acc;
 }
 
 int main(int argc, char **argv) {
-  const int wpc = argc > 1 ? atoi(argv[1]) : 16, adds = argc > 2 ? atoi(argv[2]) : 2000, S = 10;
+  const int wpc = argc > 1 ? atoi(argv[1]) : 16, adds = argc > 2 ? atoi(argv[2]) : 2000;
+  const int mode = argc > 3 ? atoi(argv[3]) : 0, S = argc > 4 ? atoi(argv[4]) : 10;
   int cu = 256;
-  hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0);
-  const int grid = cu * wpc;
+  (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0);
+  // mode 0: lists = cu * wpc * (64 / 2S);
+  // modes 2/3: wpc waves of 64 lists per CU.  Mode 0 with the same wpc and
+  // mode 2/3 with wpc / (32 / S) process the same lists.
+  const int G = 64 / (2 * S);
+  const int lists = mode >= 2 ? cu * wpc * 64 : cu * wpc * G;
+  if (mode < 0 || mode == 1 || mode > 3) return 1;
+  int grid = mode == 0 ? cu * wpc : (lists + 63) / 64;
+  size_t lds = mode >= 2 ? (size_t)2 * S * 64 * 12 : 2048;
+  void (*kern)(int, int, double *) =
+      mode == 0 ? bench_seg : (mode == 2 ? bench_lane<false> : bench_lane<true>);
+  if (lds > 65536) (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   double *out;
-  hipMalloc(&out, grid * sizeof(double));
+  (void)hipMalloc(&out, grid * sizeof(double));
   hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
-  hipLaunchKernelGGL(bench, dim3(grid), dim3(64), 2048, 0, S, 10, out);
-  hipEventRecord(e0, 0);
-  hipLaunchKernelGGL(bench, dim3(grid), dim3(64), 2048, 0, S, adds, out);
-  hipEventRecord(e1, 0);
-  hipEventSynchronize(e1);
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, 0, S, 10, out);
+  (void)hipEventRecord(e0, 0);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, 0, S, adds, out);
+  (void)hipEventRecord(e1, 0);
+  (void)hipEventSynchronize(e1);
   float ms = 0;
-  hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventElapsedTime(&ms, e0, e1);
   double *h = (double *)malloc(grid * sizeof(double)), cs = 0;
-  hipMemcpy(h, out, grid * sizeof(double), hipMemcpyDeviceToHost);
+  (void)hipMemcpy(h, out, grid * sizeof(double), hipMemcpyDeviceToHost);
   for (int i = 0; i < grid; ++i) cs += h[i];
-  const double segs = (double)grid * (64 / (2 * S));
-  printf("waves/CU %d adds %d: %.2f ms, %.1f ns per add per segment (wall), %.0f cycles per add per wave at 2.4 GHz, checksum %.17g\n",
-         wpc, adds, ms, ms * 1e6 / (segs * adds), ms * 1e-3 * 2.4e9 / adds, cs);
+  printf("mode %d S %d lists %d (%d waves, %.1f per CU) adds %d: %.2f ms, %.2f ns per add (throughput), "
+         "%.0f cycles per add per list at 2.4 GHz (latency), checksum %.17g\n",
+         mode, S, lists, grid, (double)grid / cu, adds, ms, ms * 1e6 / ((double)lists * adds), ms * 1e-3 * 2.4e9 / adds, cs);
   return 0;
 }
