@@ -37,9 +37,11 @@ __host__ __device__ inline unsigned long long trace_links(unsigned long long off
 // s's list, reversed flag, and the homozygous rule (a homozygous link entering
 // a pair with different last alleles loses the flag and, when reversed, its
 // likelihood).  Groups of GRP links: the loads of a group issue together.
+// tl != nullptr: the link words also go to tl[k0 + k] (the trace record of
+// the locus, written while the list is built).
 template <int GRP = 8>
 __device__ inline void copy_extended(const double *xl, const uint32_t *xm, double *yl, uint32_t *ym, int k0, int ns,
-                                     uint32_t s, double tpv, bool rev, bool differ) {
+                                     uint32_t s, double tpv, bool rev, bool differ, uint32_t *tl = nullptr) {
   for (int k = 0; k < ns; k += GRP) {
     double v[GRP];
     uint32_t m[GRP];
@@ -58,8 +60,10 @@ __device__ inline void copy_extended(const double *xl, const uint32_t *xm, doubl
           if (rev) lk = 0.0;
           homo = false;
         }
+        const uint32_t mw = meta_pack(s, (uint32_t)(k + u), rev, homo, false);
         yl[k0 + k + u] = lk;
-        ym[k0 + k + u] = meta_pack(s, (uint32_t)(k + u), rev, homo, false);
+        ym[k0 + k + u] = mw;
+        if (tl) tl[k0 + k + u] = mw;
       }
   }
 }

@@ -789,6 +789,30 @@ __device__ inline unsigned long long k2_trace_alloc(const ValueArgs &a, K2Shared
   return off;
 }
 
+// Trace record of locus j allocated before its lists are built: phase A
+// writes every state's header and link words as it builds the list, the end
+// of a chain of adds overwrites its state's (no second pass over the
+// frontier).  Returns false when the trace store is full.
+struct TraceRec {
+  uint32_t *hdr, *lnk;
+  unsigned long long off;
+};
+__device__ inline bool k2_trace_begin(const ValueArgs &a, K2Shared *bs, int F, unsigned long long &cur,
+                                      unsigned long long &end, TraceRec &tr) {
+  const unsigned long long words = trace_locus_words((unsigned long long)F, a.S);
+  tr.off = k2_trace_alloc(a, bs, cur, end, words);
+  if (tr.off + words > a.trace_cap) return false;
+  tr.hdr = a.trace + tr.off + 1;
+  tr.lnk = a.trace + trace_links(tr.off, (uint32_t)F);
+  return true;
+}
+__device__ inline void k2_trace_end(const ValueArgs &a, const TraceRec &tr, int F, int j, int bi) {
+  if (threadIdx.x == 0) {
+    a.trace[tr.off] = (uint32_t)F;
+    a.loc_off[(size_t)bi * (a.L + 1) + j] = tr.off;
+  }
+}
+
 // The finished k-best lists of locus j into the trace store (same layout as
 // the fused kernel: [F][headers][pad][F x S link words]).
 __device__ inline bool k2_write_trace(const ValueArgs &a, K2Shared *bs, const VFront &Y, const uint32_t *Rhd, int F,
@@ -946,6 +970,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
         bs->tie = 0;
 
       }
+      TraceRec tr;
+      if (!k2_trace_begin(a, bs, F, tcur, tend, tr)) {
+        status = EST_OVERFLOW_TRACE;
+        break;
+      }
       // A: one thread per state — extension constructor (HaploPair.cpp:35-61),
       // the appends that still fit (HaploPair::add without selection,
       // :63-84) and the whole ordered forward sum (:42, :66)
@@ -971,25 +1000,33 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
               fwd = rb + u == cb ? v : fwd + v;
             }
         }
-        // extension constructor + the appends that still fit
+        // extension constructor + the appends that still fit; the link words
+        // also go to the trace record (a state with a chain of adds gets its
+        // final words at the chain's end)
         uint32_t w = Rct[cb];
         uint32_t s = cw_state(w), ns = cw_ns(w);
         double *yl = Y.lik(t);
         uint32_t *ym = Y.meta(t);
-        copy_extended<HMC_PA_UNROLL>(X.lik((int)s), X.meta((int)s), yl, ym, 0, (int)ns, s, tpv, cw_rev(w), differ);
+        uint32_t *tl = tr.lnk + (size_t)t * S;
+        copy_extended<HMC_PA_UNROLL>(X.lik((int)s), X.meta((int)s), yl, ym, 0, (int)ns, s, tpv, cw_rev(w), differ, tl);
         int k = (int)ns, r0 = ce;
         for (int r = cb + 1; r < ce; ++r) {
           w = Rct[r];
           s = cw_state(w);
           ns = cw_ns(w);
           if (k + (int)ns <= S) {
-            copy_extended<HMC_PA_UNROLL>(X.lik((int)s), X.meta((int)s), yl, ym, k, (int)ns, s, tpv, cw_rev(w), differ);
+            copy_extended<HMC_PA_UNROLL>(X.lik((int)s), X.meta((int)s), yl, ym, k, (int)ns, s, tpv, cw_rev(w), differ,
+                                         tl);
             k += (int)ns;
           } else {
             r0 = r;
             break;
           }
         }
+        if (r0 == ce) {  // the list is final: zero the unused link words
+          for (int q = k; q < S; ++q) tl[q] = 0u;
+        }
+        tr.hdr[t] = (hd & 0xFFFFu) | (uint32_t)k << 16;
         *Y.fwd(t) = fwd;
         *Y.nl(t) = (uint32_t)k;
         *Y.r0(t) = (uint32_t)r0;
@@ -1106,16 +1143,22 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
               // FAST: a tie recorded on the way that is still at the final cut
               if (FAST && tie_v != 0.0 && tie_v == ss.slik[sg.base + S - 1]) bs->tie = 1;
               tie_v = 0.0;
+              uint32_t *tl = tr.lnk + (size_t)st * S;
               if constexpr (WIDE) {
                 for (int kk = sg.k; kk < S; kk += WAVE) {
                   Y.lik(st)[kk] = slot_l[kk - sg.k];
                   Y.meta(st)[kk] = slot_m[kk - sg.k];
+                  tl[kk] = slot_m[kk - sg.k];
                 }
               } else if (sg.k < S) {
                 Y.lik(st)[sg.k] = *slot_l;
                 Y.meta(st)[sg.k] = *slot_m;
+                tl[sg.k] = *slot_m;
               }
-              if (sg.k == 0) *Y.nl(st) = (uint32_t)S;
+              if (sg.k == 0) {
+                *Y.nl(st) = (uint32_t)S;
+                tr.hdr[st] = (Rhd[st] & 0xFFFFu) | (uint32_t)S << 16;
+              }
               ci = -1;
             }
           }
@@ -1131,7 +1174,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
         status = EST_NEEDS_ORDER;
         break;
       }
-      if (!k2_write_trace(a, bs, Y, Rhd, F, j, bi, tcur, tend)) status = EST_OVERFLOW_TRACE;
+      k2_trace_end(a, tr, F, j, bi);
       K2_ST(3);
       K2_CNT(11, 1);
       const VFront T = X;
