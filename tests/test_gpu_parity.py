@@ -94,10 +94,12 @@ def test_estep_on_reference_model(oracle_mod, name, S, mode):
 
 @pytest.mark.parametrize("name", ["n60", "a3miss5", "a8", "n300"])
 @pytest.mark.parametrize("shape", [(1, 12, 1, 20), (4, 3, 4, 4), (4, 1, 2, 8), (1, 4, 3, 8), (4, 2, 16, 1),
-                                   (1, 8, 8, 2), (4, 2, 5, 3), (16, 1, 4, 4), (16, 1, 16, 1), (8, 2, 8, 2)])
+                                   (1, 8, 8, 2), (4, 2, 5, 3), (16, 1, 4, 4), (16, 1, 16, 1), (8, 2, 8, 2),
+                                   (1, 16, 1, 20), (1, 20, 2, 8), (4, 4, 8, 2)])
 def test_estep_pass_shapes(oracle_mod, name, shape):
     """Launch shapes of the split E-step's passes (hmc_set_pass_shapes:
-    structure waves per individual 1, 4, 8 or 16, individuals per CU, value-pass
+    structure waves per individual 1, 4, 8 or 16, individuals per CU — the
+    3, 4 and 5 waves-per-SIMD builds of the structure pass —, value-pass
     shape up to 16 waves per individual) change nothing: the E-step on the M0 model equals
     HaploModel::resolveAll bit for bit."""
     p = panel(name)

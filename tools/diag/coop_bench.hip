@@ -12,6 +12,8 @@
 //   per CU — slower than mode 0 — and removed; profiles/r03/coop/)
 //   mode 2: one list per lane, sequential libstdc++ code on an LDS column
 //   mode 3: one list per lane, mask partition (nth_element_greater_masks)
+//   mode 4: as mode 0 with two sets of segments per wave, interleaved
+//   mode 5: two elements per lane, S lanes per list (seg2_nth_slots)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -63,6 +65,75 @@ __global__ __launch_bounds__(64) void bench_seg(int S, int adds, double *out) {
   if (lane == 0) out[blockIdx.x] = acc;
 }
 
+// mode 4: two sets of 64 / 2S lists per wave, selections interleaved
+// (seg_nth_slots_multi<2>)
+__global__ __launch_bounds__(64) void bench_seg2(int S, int adds, double *out) {
+  extern __shared__ unsigned char sm[];
+  const int lane = threadIdx.x;
+  SegScratch ss[2] = {
+      {(int *)sm, (int *)sm + 64, (int *)sm + 128, (double *)(sm + 1024), (uint32_t *)(sm + 1024 + 512)},
+      {(int *)(sm + 2048), (int *)(sm + 2048) + 64, (int *)(sm + 2048) + 128, (double *)(sm + 2048 + 1024),
+       (uint32_t *)(sm + 2048 + 1024 + 512)}};
+  const Seg sg = make_seg(2 * S);
+  const int G = 64 / (2 * S);
+  const bool in = sg.g < G;
+  uint32_t g[2];
+  for (int u = 0; u < 2; ++u) {
+    g[u] = (blockIdx.x * 2 + u) * G + sg.g;
+    if (in && sg.k < S) {
+      ss[u].slik[lane] = val(g[u], 0, sg.k);
+      ss[u].smeta[lane] = sg.k;
+    }
+  }
+  wave_lds_sync();
+  for (int r = 1; r <= adds; ++r) {
+    for (int u = 0; u < 2; ++u)
+      if (in && sg.k >= S) {
+        ss[u].slik[lane] = val(g[u], r, sg.k - S);
+        ss[u].smeta[lane] = 64u * r + sg.k - S;
+      }
+    wave_lds_sync();
+    const int n[2] = {in ? 2 * S : 0, in ? 2 * S : 0}, nth[2] = {S - 1, S - 1};
+    seg_nth_slots_multi<2>(n, nth, sg, ss);
+  }
+  double acc = 0.0;
+  for (int u = 0; u < 2; ++u)
+    if (in && sg.k < S) acc += ss[u].slik[lane] * (double)(ss[u].smeta[lane] % 97);
+  acc = fold(acc);
+  if (lane == 0) out[blockIdx.x] = acc;
+}
+
+// mode 5: two elements per lane, S lanes per list (seg2_nth_slots)
+__global__ __launch_bounds__(64) void bench_seg2e(int S, int adds, double *out) {
+  extern __shared__ unsigned char sm[];
+  const int lane = threadIdx.x;
+  // slots: (64 / S + 1) x 2S <= 160 per wave (lanes past the last segment
+  // address a dead segment of their own)
+  SegScratch ss{(int *)sm, (int *)(sm + 640), (int *)(sm + 1280), (double *)(sm + 2304), (uint32_t *)(sm + 3584)};
+  const Seg sg = make_seg(S);
+  const int G = 64 / S;
+  const bool in = sg.g < G;
+  const uint32_t g = blockIdx.x * G + sg.g;
+  const int sb = sg.g * 2 * S;
+  if (in) {
+    ss.slik[sb + sg.k] = val(g, 0, sg.k);
+    ss.smeta[sb + sg.k] = sg.k;
+  }
+  wave_lds_sync();
+  for (int r = 1; r <= adds; ++r) {
+    if (in) {
+      ss.slik[sb + S + sg.k] = val(g, r, sg.k);
+      ss.smeta[sb + S + sg.k] = 64u * r + sg.k;
+    }
+    wave_lds_sync();
+    seg2_nth_slots(in ? 2 * S : 0, S - 1, sg, ss);
+  }
+  double acc = 0.0;
+  if (in) acc = ss.slik[sb + sg.k] * (double)(ss.smeta[sb + sg.k] % 97);
+  acc = fold(acc);
+  if (lane == 0) out[blockIdx.x] = acc;
+}
+
 template <bool MASKS>
 __global__ __launch_bounds__(64) void bench_lane(int S, int adds, double *out) {
   extern __shared__ unsigned char sm[];
@@ -93,12 +164,14 @@ int main(int argc, char **argv) {
   // modes 2/3: wpc waves of 64 lists per CU.  Mode 0 with the same wpc and
   // mode 2/3 with wpc / (32 / S) process the same lists.
   const int G = 64 / (2 * S);
-  const int lists = mode >= 2 ? cu * wpc * 64 : cu * wpc * G;
-  if (mode < 0 || mode == 1 || mode > 3) return 1;
-  int grid = mode == 0 ? cu * wpc : (lists + 63) / 64;
-  size_t lds = mode >= 2 ? (size_t)2 * S * 64 * 12 : 2048;
+  const int lists = mode == 2 || mode == 3 ? cu * wpc * 64 : cu * wpc * G;
+  if (mode < 0 || mode == 1 || mode > 5) return 1;
+  const int G5 = 64 / S;
+  int grid = mode == 0 ? cu * wpc : (mode == 4 ? cu * wpc / 2 : (mode == 5 ? (lists + G5 - 1) / G5 : (lists + 63) / 64));
+  size_t lds = mode == 2 || mode == 3 ? (size_t)2 * S * 64 * 12 : (mode == 4 ? 4096 : (mode == 5 ? 4608 : 2048));
   void (*kern)(int, int, double *) =
-      mode == 0 ? bench_seg : (mode == 2 ? bench_lane<false> : bench_lane<true>);
+      mode == 0 ? bench_seg
+                : (mode == 2 ? bench_lane<false> : (mode == 3 ? bench_lane<true> : (mode == 4 ? bench_seg2 : bench_seg2e)));
   if (lds > 65536) (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   double *out;
   (void)hipMalloc(&out, grid * sizeof(double));

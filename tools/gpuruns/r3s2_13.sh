@@ -1,0 +1,10 @@
+set -o pipefail
+mkdir -p gpurun_out/r13
+B=tools/diag/coop_bench
+for w in 2 8 16 20 32; do
+  for mode in 0 5; do
+    timeout -k 5 60 $B $w 300 $mode 10 >> gpurun_out/r13/coop.log 2>&1 || { echo "fail w=$w mode=$mode"; cat gpurun_out/r13/coop.log; exit 1; }
+  done
+done
+for S in 3 5 8 16; do for mode in 0 5; do timeout -k 5 60 $B 16 200 $mode $S >> gpurun_out/r13/coop.log 2>&1 || exit 1; done; done
+cat gpurun_out/r13/coop.log

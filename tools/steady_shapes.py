@@ -2,7 +2,7 @@
 M1 with the automatic shapes, then per shape "vnw:vipc" the E-step on the M1
 model twice (the model does not change, so neither may LL or R_E).
 
-    python tools/steady_shapes.py CFG vnw:vipc ...   (0:0 = automatic)
+    python tools/steady_shapes.py CFG [s1nw:s1ipc:]vnw:vipc ...   (0 = automatic)
 """
 import os
 import sys
@@ -18,8 +18,9 @@ m.find_patterns()
 m.resolve_all()
 m.find_patterns()
 for sh in sys.argv[2:] or ["0:0"]:
-    vnw, vipc = (int(x) for x in sh.split(":"))
-    m.set_pass_shapes(0, 0, vnw, vipc)
+    f = [int(x) for x in sh.split(":")]
+    f = [0, 0] + f if len(f) == 2 else f
+    m.set_pass_shapes(*f)
     for r in range(2):
         ll, H, re = m.resolve_all()
         s = m.estep_split_stats()
