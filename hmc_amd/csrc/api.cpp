@@ -284,6 +284,7 @@ struct Ctx {
   // at context creation from HMC_DEBUG_MEM / HMC_DIAG_MINE
   bool debug_mem = false, diag_mine = false;
   bool value_fast = false;   // value-only k-best lists first, the exact pass for ties only (hmc_set_value_mode)
+  int value_pair = 1;        // two links per lane in phase B: 0 never, 1 heavy groups, 2 every group (hmc_set_value_layout)
   uint64_t trace_bytes = 0, rec_bytes = 0;  // E-step store budgets (0 = automatic)
 
   Panel pan;
@@ -2530,7 +2531,9 @@ struct Ctx {
         v.scratch = d_scr2.p;
         v.scratch_stride = per2;
         v.fcap = fgrp;
-        v.lds_fc = s2_tier(S, vnw, vipc);
+        // heavy groups (many chains per locus) select two links per lane
+        const bool pair = !value_fast && S <= 16 && (value_pair == 2 || (value_pair == 1 && heavy));
+        v.lds_fc = s2_tier(S, vnw, vipc, pair);
         v.trace = d_trace.p;
         v.trace_cap = d_trace.n;
         v.trace_cursor = d_trace_cursor.p;
@@ -2550,7 +2553,7 @@ struct Ctx {
         if ((e = hipMemsetAsync(d_nextq.p + 1, 0, 4, st))) return hipfail(e, "estep");
         const bool fast = value_fast && S <= 32;  // lists longer than a wavefront: exact order only
         hipEventRecord(ev[0], st);
-        if ((e = launch_estep_values(v, grid2, vnw, fast, vwpe, st))) return hipfail(e, "estep_values launch");
+        if ((e = launch_estep_values(v, grid2, vnw, fast, vwpe, st, pair))) return hipfail(e, "estep_values launch");
         hipEventRecord(ev[1], st);
         if ((rc = read_status(sset, (int)k, true))) return rc;
         hipEventElapsedTime(&ms, ev[0], ev[1]);
@@ -2704,10 +2707,10 @@ struct Ctx {
     cc = 0;
   }
   // LDS tier of pass 2: states per frontier for the block's LDS share.
-  static int s2_tier(int S, int nw, int ipc) {
+  static int s2_tier(int S, int nw, int ipc, bool pair = false) {
     const int budget = 160 * 1024 / std::max(1, ipc) - 256;
     for (int f = 4096; f >= 4; f -= 4)
-      if ((int)estep_s2_lds_bytes(S, f, nw) <= budget) return f;
+      if ((int)estep_s2_lds_bytes(S, f, nw, pair) <= budget) return f;
     return 0;
   }
 
@@ -3230,6 +3233,12 @@ int hmc_last_exact_stats(const hmc_ctx *h, int *rounds, uint64_t *candidates, do
 int hmc_set_value_mode(hmc_ctx *h, int mode) {
   if (!h || mode < 0 || mode > 1) return HMC_EARG;  // 0: value-only + re-runs, 1: libstdc++ permutations
   h->c.value_fast = mode == 0;
+  return HMC_OK;
+}
+
+int hmc_set_value_layout(hmc_ctx *h, int mode) {
+  if (!h || mode < 0 || mode > 2) return HMC_EARG;  // 0 never, 1 heavy groups, 2 every group
+  h->c.value_pair = mode;
   return HMC_OK;
 }
 

@@ -242,6 +242,137 @@ __device__ inline void seg_nth_slots(int n, int nth, const Seg &sg, const SegScr
   }
 }
 
+// The same selection with two elements per lane: segment g of W = S lanes
+// holds a list of up to 2S <= 32 links in its slots [g*2W, g*2W + 2W); lane k
+// of the segment carries positions k (element 0) and k + W (element 1), so a
+// wavefront works on 64 / W lists (S = 10: 6) instead of 64 / 2W.  The
+// per-segment work of a partition (median, stop masks, cut) is shared by the
+// two elements; only the per-element compares, ranks and moves double.  The
+// permutation is the one of seg_nth_slots (the stop masks are assembled from
+// the two elements' ballots, bit p = position p).  sg = make_seg(W); the
+// scratch arrays hold (64 / W + 1) x 2W slots: lanes past the last segment
+// address a dead segment of their own.
+__device__ inline void seg2_nth_slots(int n, int nth, const Seg &sg, const SegScratch &ss) {
+  const int lane = (int)(threadIdx.x & 63);
+  const int W = sg.sw, k = sg.k;
+  int first = 0, last = n, depth = n > 0 ? lg2_floor(n) * 2 : 0;
+  const bool act = n > 0 && nth != n && sg.mask != 0ull;
+  const int sb = sg.g * 2 * W;  // the segment's first slot
+  double *sl = ss.slik + sb;
+  uint32_t *sm = ss.smeta + sb;
+  int *lp = ss.lpos + sb, *rp = ss.rpos + sb;
+  int *jl0 = ss.junk + lane, *jl1 = ss.junk + 64 + lane, *jr0 = ss.junk + 128 + lane, *jr1 = ss.junk + 192 + lane;
+  const int kmax = 2 * W - 1;
+  const int p0 = k, p1 = k + W;  // this lane's positions
+  while (true) {
+    const bool part = act && last - first > 3 && depth > 0;
+    if (!wave_ballot(part)) break;
+    depth -= part ? 1 : 0;
+    // std::__move_median_to_first(first, first+1, mid, last-1) (stl_algo.h:79-102)
+    const int a = first + 1, b = first + ((last - first) >> 1), c = last > 0 ? last - 1 : 0;
+    const double va = sl[a], vb = sl[b], vc = sl[c], vf = sl[first];
+    const double v0 = sl[p0], v1 = sl[p1];
+    const uint32_t m0 = sm[p0], m1 = sm[p1];
+    const int idx = (va > vb ? 4 : 0) | (vb > vc ? 2 : 0) | (va > vc ? 1 : 0);
+    const int w = (22561 >> (2 * idx)) & 3;
+    const int r = w == 0 ? a : (w == 1 ? b : c);
+    const double pivot = w == 0 ? va : (w == 1 ? vb : vc);
+    // the value each position holds once the median is at first
+    const double pv0 = p0 == first ? pivot : (p0 == r ? vf : v0);
+    const double pv1 = p1 == first ? pivot : (p1 == r ? vf : v1);
+    // stop masks over positions: ballot bits of element 0 at [0, W), element 1 at [W, 2W)
+    const uint32_t le = seg_bits(wave_ballot(!(pv0 > pivot)), sg) | seg_bits(wave_ballot(!(pv1 > pivot)), sg) << W;
+    const uint32_t ge = seg_bits(wave_ballot(!(pivot > pv0)), sg) | seg_bits(wave_ballot(!(pivot > pv1)), sg) << W;
+    const uint32_t below_last = last >= 32 ? ~0u : ((1u << last) - 1u);
+    const uint32_t inR = part ? below_last & ~((1u << first) - 1u) : 0u;  // [first, last)
+    const uint32_t inL = inR & ~(1u << first);                             // (first, last)
+    const uint32_t Lw = le & inL, Rw = ge & inR;
+    const int nL = __popc(Lw), nR = __popc(Rw);
+    // each element's position once the median is at first
+    const int x0 = !part ? p0 : (p0 == first ? r : (p0 == r ? first : p0));
+    const int x1 = !part ? p1 : (p1 == first ? r : (p1 == r ? first : p1));
+    const bool isL0 = part && ((Lw >> x0) & 1u), isR0 = part && ((Rw >> x0) & 1u);
+    const bool isL1 = part && ((Lw >> x1) & 1u), isR1 = part && ((Rw >> x1) & 1u);
+    const uint32_t xb0 = (1u << x0) - 1u, xb1 = (1u << x1) - 1u;
+    const int kL0 = __popc(Lw & xb0), kL1 = __popc(Lw & xb1);
+    const int kR0 = nR - 1 - __popc(Rw & xb0), kR1 = nR - 1 - __popc(Rw & xb1);
+    *(isL0 ? lp + kL0 : jl0) = x0;
+    *(isL1 ? lp + kL1 : jl1) = x1;
+    *(isR0 ? rp + kR0 : jr0) = x0;
+    *(isR1 ? rp + kR1 : jr1) = x1;
+    wave_lds_sync();
+    const int qR0 = rp[kL0 < kmax ? kL0 : kmax], qR1 = rp[kL1 < kmax ? kL1 : kmax];
+    const int qL0 = lp[kR0 < 0 ? 0 : (kR0 < kmax ? kR0 : kmax)];
+    const int qL1 = lp[kR1 < 0 ? 0 : (kR1 < kmax ? kR1 : kmax)];
+    const bool lsw0 = isL0 && kL0 < nR && x0 < qR0, lsw1 = isL1 && kL1 < nR && x1 < qR1;
+    const bool rsw0 = isR0 && kR0 < nL && qL0 < x0, rsw1 = isR1 && kR1 < nL && qL1 < x1;
+    const int d0 = lsw0 ? qR0 : (rsw0 ? qL0 : x0), d1 = lsw1 ? qR1 : (rsw1 ? qL1 : x1);
+    sl[d0] = v0;
+    sm[d0] = m0;
+    sl[d1] = v1;
+    sm[d1] = m1;
+    // cut = min(l_K, r_{K-1}) (see seg_nth_slots); bits by pre-median position,
+    // position r reported by the element at first
+    const uint32_t bl = seg_bits(wave_ballot(isL0 && !lsw0), sg) | seg_bits(wave_ballot(isL1 && !lsw1), sg) << W;
+    const uint32_t br = seg_bits(wave_ballot(rsw0), sg) | seg_bits(wave_ballot(rsw1), sg) << W;
+    const uint32_t keep = ~((1u << first) | (1u << r));
+    const uint32_t ml = (bl & keep) | (((bl >> first) & 1u) << r);
+    const uint32_t mr = (br & keep) | (((br >> first) & 1u) << r);
+    const int lK = seg_lowest(ml), rK = seg_lowest(mr);
+    const int cut = lK < rK ? lK : rK;
+    wave_lds_sync();
+    first = part && cut <= nth ? cut : first;
+    last = part && cut > nth ? cut : last;
+  }
+  // depth limit: std::__heap_select + iter_swap on the segment's first lane
+  const bool heap = act && last - first > 3;
+  if (wave_ballot(heap)) {
+    if (heap && k == 0) {
+      const LinkList wl{sl, sm, 1};
+      heap_select(wl, first, nth + 1, last);
+      wl.swap(first, nth);
+    }
+    wave_lds_sync();
+  }
+  // std::__insertion_sort of the <= 3 remaining elements (stl_algo.h:1819-1849)
+  const bool ins = act && !heap && last - first > 1;
+  if (wave_ballot(ins)) {
+    const int len = last - first;
+    const int f0 = first < kmax ? first : kmax;
+    const int f1 = first + 1 < kmax ? first + 1 : kmax, f2 = first + 2 < kmax ? first + 2 : kmax;
+    double y0 = sl[f0], y1 = sl[f1], y2 = sl[f2];
+    uint32_t t0 = sm[f0], t1 = sm[f1], t2 = sm[f2];
+    if (y1 > y0) {
+      const double t = y1; y1 = y0; y0 = t;
+      const uint32_t u = t1; t1 = t0; t0 = u;
+    }
+    if (len > 2) {
+      if (y2 > y0) {
+        const double t = y2; const uint32_t u = t2;
+        y2 = y1; t2 = t1; y1 = y0; t1 = t0; y0 = t; t0 = u;
+      } else if (y2 > y1) {
+        const double t = y2; const uint32_t u = t2;
+        y2 = y1; t2 = t1; y1 = t; t1 = u;
+      }
+    }
+    const int j0 = p0 - first, j1 = p1 - first;
+    const bool mine0 = ins && (j0 == 0 || j0 == 1 || (j0 == 2 && len > 2));
+    const bool mine1 = ins && (j1 == 0 || j1 == 1 || (j1 == 2 && len > 2));
+    const double z0 = j0 == 0 ? y0 : (j0 == 1 ? y1 : y2), z1 = j1 == 0 ? y0 : (j1 == 1 ? y1 : y2);
+    const uint32_t u0 = j0 == 0 ? t0 : (j0 == 1 ? t1 : t2), u1 = j1 == 0 ? t0 : (j1 == 1 ? t1 : t2);
+    wave_lds_sync();
+    if (mine0) {
+      sl[p0] = z0;
+      sm[p0] = u0;
+    }
+    if (mine1) {
+      sl[p1] = z1;
+      sm[p1] = u1;
+    }
+    wave_lds_sync();
+  }
+}
+
 // Value-only top-S of every segment's list (slots [0, n), n <= SW): each
 // element's rank is the number of elements greater than it plus the equal ones
 // in lower slots, and the S best are written to slots [0, S) in rank order.

@@ -751,18 +751,22 @@ struct K2Plan {
 };
 
 // Selection slots per wave: one wavefront of lists of 2S links (S <= 32), or
-// one list of 2S links (S > 32).
-__host__ __device__ inline int k2_slots(int S) { return 2 * S > WAVE ? 2 * S : WAVE; }
+// one list of 2S links (S > 32); with two links per lane (PAIR builds,
+// S <= 16) 64 / S lists of 2S plus a dead segment for the lanes past the last.
+__host__ __device__ inline int k2_slots(int S, bool pair = false) {
+  return pair ? (WAVE / S + 1) * 2 * S : (2 * S > WAVE ? 2 * S : WAVE);
+}
 
-__host__ __device__ inline K2Plan k2_plan(int S, int fc, int nw) {
+__host__ __device__ inline K2Plan k2_plan(int S, int fc, int nw, bool pair = false) {
   K2Plan p;
   int o = 0;
   auto take = [&](int bytes) { int r = o; o += (bytes + 15) & ~15; return r; };
-  p.o_lpos = take(nw * WAVE * 4);
-  p.o_rpos = take(nw * WAVE * 4);
-  p.o_junk = take(nw * 2 * WAVE * 4);
-  p.o_slik = take(nw * k2_slots(S) * 8);
-  p.o_smeta = take(nw * k2_slots(S) * 4);
+  const int sl = k2_slots(S, pair), pos = pair ? sl : WAVE;
+  p.o_lpos = take(nw * pos * 4);
+  p.o_rpos = take(nw * pos * 4);
+  p.o_junk = take(nw * (pair ? 4 : 2) * WAVE * 4);
+  p.o_slik = take(nw * sl * 8);
+  p.o_smeta = take(nw * sl * 4);
   p.o_bs = take((int)sizeof(K2Shared));
   p.o_front[0] = take(fc * (16 + 12 * S));
   p.o_front[1] = take(fc * (16 + 12 * S));
@@ -877,7 +881,7 @@ __device__ inline bool k2_write_trace(const ValueArgs &a, K2Shared *bs, const VF
 #define HMC_PA_UNROLL 4
 #endif
 size_t estep_s2_scratch_bytes(int fcap, int S) { return 2 * k2_front_bytes(fcap, S); }
-size_t estep_s2_lds_bytes(int S, int fc, int nw) { return (size_t)k2_plan(S, fc, nw).bytes; }
+size_t estep_s2_lds_bytes(int S, int fc, int nw, bool pair) { return (size_t)k2_plan(S, fc, nw, pair).bytes; }
 
 // WPE: resident waves per SIMD the register allocation targets — 4 (127
 // VGPRs: shapes of up to 16 waves per CU) or 5 (96 VGPRs, a few spills in
@@ -891,20 +895,26 @@ size_t estep_s2_lds_bytes(int S, int fc, int nw) { return (size_t)k2_plan(S, fc,
 // WIDE: sample sizes 33..64 — lists of up to 2S = 128 links, one per wave,
 // each lane holding positions k and k + 64, selection by the sequential
 // libstdc++ code on the wave's first lane (the sw > 32 path of seg_nth_slots).
-template <bool FAST, int WPE, bool WIDE = false>
+// PAIR: two links per lane in phase B (seg2_nth_slots: S lanes and 64 / S
+// lists of up to 2S links per wavefront, S <= 16) — heavy groups, whose loci
+// have many chains of adds (cfg 3's E1: ~130), get 2x the lists per wave.
+template <bool FAST, int WPE, bool WIDE = false, bool PAIR = false>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) void estep_values(ValueArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int S = a.S, L = a.L, hl = a.head_len;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;
   const int NT = blockDim.x, NW = NT / WAVE;
-  const K2Plan plan = k2_plan(S, a.lds_fc, NW);
+  const K2Plan plan = k2_plan(S, a.lds_fc, NW, PAIR);
   K2Shared *bs = (K2Shared *)(smem + plan.o_bs);
-  const int sws = k2_slots(S);  // selection slots per wave
-  const SegScratch ss{(int *)(smem + plan.o_lpos) + wv * WAVE, (int *)(smem + plan.o_rpos) + wv * WAVE,
-                      (int *)(smem + plan.o_junk) + wv * 2 * WAVE, (double *)(smem + plan.o_slik) + wv * sws,
+  const int sws = k2_slots(S, PAIR);  // selection slots per wave
+  const int sps = PAIR ? sws : WAVE;  // stop-position slots per wave
+  const SegScratch ss{(int *)(smem + plan.o_lpos) + wv * sps, (int *)(smem + plan.o_rpos) + wv * sps,
+                      (int *)(smem + plan.o_junk) + wv * (PAIR ? 4 : 2) * WAVE, (double *)(smem + plan.o_slik) + wv * sws,
                       (uint32_t *)(smem + plan.o_smeta) + wv * sws};
-  const Seg sg = make_seg(WIDE ? WAVE : 2 * S);
-  const int G = WIDE ? 1 : WAVE / (2 * S);
+  const Seg sg = make_seg(WIDE ? WAVE : (PAIR ? S : 2 * S));
+  const int G = WIDE ? 1 : (PAIR ? WAVE / S : WAVE / (2 * S));
+  // PAIR: this lane's two positions are slots sb + k and sb + k + S
+  const int sb = sg.g * 2 * S;
   const LinkList W{(double *)(smem + plan.o_slik), (uint32_t *)(smem + plan.o_smeta), 1};  // final selection
 
   char *sp = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
@@ -1055,8 +1065,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
         double tpv = 0.0, tie_v = 0.0;
         uint32_t wc = 0, wn = 0;
         bool differ = false, done = sg.g >= G;
-        double *slot_l = ss.slik + lane;
-        uint32_t *slot_m = ss.smeta + lane;
+        // this lane's first slot (position k; PAIR: also k + S, one segment of
+        // slots further than the 2S-lane layout's)
+        double *slot_l = ss.slik + sb + sg.k;
+        uint32_t *slot_m = ss.smeta + sb + sg.k;
         while (true) {
           const bool idle = !done && ci < 0;
           if (wave_ballot(idle)) {
@@ -1114,8 +1126,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
             if constexpr (WIDE) {
               for (int kk = sg.k; kk < n; kk += WAVE)
                 if (kk >= k0) extend(kk);
-            } else if (sg.k >= k0 && sg.k < n) {
-              extend(sg.k);
+            } else {
+              if (sg.k >= k0 && sg.k < n) extend(sg.k);
+              if (PAIR && sg.k + S >= k0 && sg.k + S < n) extend(sg.k + S);
             }
             wc = wn;
             wn = r + 2 < re_ ? Rct[r + 2] : 0u;
@@ -1130,6 +1143,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           if (FAST) {
             const double tv = seg_rank_select(n, S, sg, ss);
             tie_v = tv > tie_v ? tv : tie_v;
+          } else if (PAIR) {
+            seg2_nth_slots(n, S - 1, sg, ss);
           } else {
             seg_nth_slots(n, S - 1, sg, ss);
           }
@@ -1273,16 +1288,17 @@ hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStre
   return hipGetLastError();
 }
 
-hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, int wpe, hipStream_t st) {
+hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, int wpe, hipStream_t st, bool pair) {
   if (a.S < 1 || a.S > S_MAX || a.fcap > F_MAX || a.lds_fc < 0 || nw < 1 || nw > 16 || (wpe != 4 && wpe != 5) ||
-      (a.S > 32 && fast))
+      (a.S > 32 && fast) || (pair && (fast || a.S > 16)))
     return hipErrorInvalidValue;
-  const size_t lds = estep_s2_lds_bytes(a.S, a.lds_fc, nw);
+  const size_t lds = estep_s2_lds_bytes(a.S, a.lds_fc, nw, pair);
   static size_t lds_attr = 0;
   if (lds > 65536 && lds > lds_attr) {
     for (const void *f : {(const void *)estep_values<true, 4>, (const void *)estep_values<false, 4>,
                           (const void *)estep_values<true, 5>, (const void *)estep_values<false, 5>,
-                          (const void *)estep_values<false, 4, true>}) {
+                          (const void *)estep_values<false, 4, true>, (const void *)estep_values<false, 4, false, true>,
+                          (const void *)estep_values<false, 5, false, true>}) {
       hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
     }
@@ -1291,6 +1307,9 @@ hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, 
   const dim3 g(grid), b(WAVE * nw);
   if (a.S > 32) {  // lists of more than one wavefront: exact order only
     hipLaunchKernelGGL((estep_values<false, 4, true>), g, b, lds, st, a);
+  } else if (pair) {
+    if (wpe == 5) hipLaunchKernelGGL((estep_values<false, 5, false, true>), g, b, lds, st, a);
+    else hipLaunchKernelGGL((estep_values<false, 4, false, true>), g, b, lds, st, a);
   } else if (wpe == 5) {
     if (fast) hipLaunchKernelGGL((estep_values<true, 5>), g, b, lds, st, a);
     else hipLaunchKernelGGL((estep_values<false, 5>), g, b, lds, st, a);

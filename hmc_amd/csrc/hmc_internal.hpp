@@ -221,11 +221,12 @@ hipError_t launch_estep(const EstepArgs &a, int grid, int nw, hipStream_t st);
 size_t estep_s1_scratch_bytes(int fcap, int hcap, int ccap, int nw);
 size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax, int nw);
 size_t estep_s2_scratch_bytes(int fcap, int S);
-size_t estep_s2_lds_bytes(int S, int fc, int nw);
+size_t estep_s2_lds_bytes(int S, int fc, int nw, bool pair = false);
 // nw: wavefronts per individual, 1 or 4
 hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStream_t st);
 // wpe: 4 or 5 resident waves per SIMD (register budget of the instantiation)
-hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, int wpe, hipStream_t st);
+hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, int wpe, hipStream_t st,
+                               bool pair = false);
 hipError_t launch_traceback(const TracebackArgs &a, int total_cands, hipStream_t st);
 hipError_t launch_transpose_rows_u8(const uint8_t *in, const int32_t *rowmap, uint8_t *out, int rows, int cols,
                                     hipStream_t st);

@@ -236,6 +236,12 @@ class HaploModel:
         permutations for everyone; default).  Results are identical."""
         self._check(lib().hmc_set_value_mode(self._h, {"fast": 0, "exact": 1}[mode]))
 
+    def set_value_layout(self, mode: int):
+        """Phase-B layout of the value pass (hmc_set_value_layout): two links
+        per lane for 0 never, 1 heavy groups (default), 2 every group.  Results
+        are identical."""
+        self._check(lib().hmc_set_value_layout(self._h, mode))
+
     # ----------------------------------------------------------------- panel
     def load(self, genos: GenoData):
         a = np.ascontiguousarray(genos.alleles, dtype=np.int32)

@@ -134,6 +134,27 @@ def test_value_only_mode_with_order_reruns(oracle_mod, name, S):
     assert 0 <= st["n_order_rerun"] <= p.N
 
 
+@pytest.mark.parametrize("name", ["n60", "a3miss5", "a8", "n300"])
+@pytest.mark.parametrize("S,shape", [(10, None), (1, None), (2, None), (3, None), (5, None), (16, None),
+                                     (10, (0, 0, 8, 2)), (10, (0, 0, 2, 8)), (7, (0, 0, 4, 4))])
+def test_value_pair_layout(oracle_mod, name, S, shape):
+    """hmc_set_value_layout(2): phase B of the value pass with two links per
+    lane (seg2_nth_slots: S lanes and 64 / S lists per wavefront) for every
+    group and launch shape — same E-step, bit for bit, as
+    HaploModel::resolveAll."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=S)
+    o.find_patterns()
+    m = gpu_model(p, S)
+    m.set_value_layout(2)
+    if shape:
+        m.set_pass_shapes(*shape)
+    m.find_patterns()
+    ll_g, H, re_g = m.resolve_all()
+    o.reset_counters()
+    assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
+
+
 @pytest.mark.parametrize("S", [1, 2, 5, 16, 17, 24, 32, 33, 40, 64])
 def test_estep_sample_sizes(oracle_mod, S):
     p = panel("miss2")
