@@ -284,7 +284,7 @@ struct Ctx {
   // at context creation from HMC_DEBUG_MEM / HMC_DIAG_MINE
   bool debug_mem = false, diag_mine = false;
   bool value_fast = false;   // value-only k-best lists first, the exact pass for ties only (hmc_set_value_mode)
-  int value_pair = 1;        // two links per lane in phase B: 0 never, 1 heavy groups, 2 every group (hmc_set_value_layout)
+  int value_pair = 2;        // two links per lane in phase B: 0 never, 1 heavy groups, 2 every group (hmc_set_value_layout)
   uint64_t trace_bytes = 0, rec_bytes = 0;  // E-step store budgets (0 = automatic)
 
   Panel pan;
@@ -2531,7 +2531,7 @@ struct Ctx {
         v.scratch = d_scr2.p;
         v.scratch_stride = per2;
         v.fcap = fgrp;
-        // heavy groups (many chains per locus) select two links per lane
+        // two links per lane (cfg 3: E1 values 2.68 -> 2.34 s, E2 ~3 % less)
         const bool pair = !value_fast && S <= 16 && (value_pair == 2 || (value_pair == 1 && heavy));
         v.lds_fc = s2_tier(S, vnw, vipc, pair);
         v.trace = d_trace.p;

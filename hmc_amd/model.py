@@ -238,7 +238,7 @@ class HaploModel:
 
     def set_value_layout(self, mode: int):
         """Phase-B layout of the value pass (hmc_set_value_layout): two links
-        per lane for 0 never, 1 heavy groups (default), 2 every group.  Results
+        per lane for 0 never, 1 heavy groups, 2 every group (default).  Results
         are identical."""
         self._check(lib().hmc_set_value_layout(self._h, mode))
 

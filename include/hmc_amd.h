@@ -335,8 +335,9 @@ int hmc_set_value_mode(hmc_ctx *ctx, int mode);
 /* Phase-B layout of the value pass (results identical): the overflowing adds'
  * selections with two links per lane (S lanes and 64 / S lists per
  * wavefront, sample_size <= 16) instead of one (2S lanes, 64 / 2S lists).
- * Mode 0: never; 1 (default): groups of heavy individuals (the first E-step
- * on a genotype-mined model: many chains of adds per locus); 2: every group. */
+ * Mode 0: never; 1: groups of heavy individuals (the first E-step on a
+ * genotype-mined model: many chains of adds per locus); 2 (default): every
+ * group. */
 int hmc_set_value_layout(hmc_ctx *ctx, int mode);
 /* Individuals the last E-step re-ran with the libstdc++ permutations (mode 0)
  * and the device time of those re-runs (ms, part of values_ms). */

@@ -13,6 +13,7 @@ from hmc_amd import synth  # noqa: E402
 
 cfg = int(sys.argv[1])
 m = hmc_amd.HaploModel()
+m.set_value_layout(int(os.environ.get("LAYOUT", "2")))  # phase-B layout (hmc_set_value_layout)
 m.load(hmc_amd.GenoData.from_panel(synth.config_panel(cfg)))
 m.find_patterns()
 m.resolve_all()
