@@ -14,6 +14,7 @@
 //   mode 3: one list per lane, mask partition (nth_element_greater_masks)
 //   mode 4: as mode 0 with two sets of segments per wave, interleaved
 //   mode 5: two elements per lane, S lanes per list (seg2_nth_slots)
+//   mode 6: four elements per lane, ceil(S / 2) lanes per list (segE_nth_slots<4>)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -187,6 +188,166 @@ __device__ inline double fold(double acc) {
   return acc;
 }
 
+// E links per lane (E = 2 is seg2_nth_slots): segment of W = ceil(2S / E)
+// lanes, lane k carries positions k + j W (j < E); sg = make_seg(W); slots
+// (64 / W + 1) x E W per wave.  Measured here only.
+template <int E>
+__device__ inline void segE_nth_slots(int n, int nth, const Seg &sg, const SegScratch &ss) {
+  const int lane = (int)(threadIdx.x & 63);
+  const int W = sg.sw, k = sg.k;
+  int first = 0, last = n, depth = n > 0 ? lg2_floor(n) * 2 : 0;
+  const bool act = n > 0 && nth != n && sg.mask != 0ull;
+  const int sb = sg.g * E * W;
+  double *sl = ss.slik + sb;
+  uint32_t *sm = ss.smeta + sb;
+  int *lp = ss.lpos + sb, *rp = ss.rpos + sb;
+  const int kmax = E * W - 1;
+  while (true) {
+    const bool part = act && last - first > 3 && depth > 0;
+    if (!wave_ballot(part)) break;
+    depth -= part ? 1 : 0;
+    const int a = first + 1, b = first + ((last - first) >> 1), c = last > 0 ? last - 1 : 0;
+    const double va = sl[a], vb = sl[b], vc = sl[c], vf = sl[first];
+    const int idx = (va > vb ? 4 : 0) | (vb > vc ? 2 : 0) | (va > vc ? 1 : 0);
+    const int w = (22561 >> (2 * idx)) & 3;
+    const int r = w == 0 ? a : (w == 1 ? b : c);
+    const double pivot = w == 0 ? va : (w == 1 ? vb : vc);
+    double v[E];
+    uint32_t m[E];
+    int x[E], kL[E], kR[E];
+    bool isL[E], isR[E];
+    uint32_t le = 0, ge = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const int p = k + j * W;
+      v[j] = sl[p];
+      m[j] = sm[p];
+      const double pv = p == first ? pivot : (p == r ? vf : v[j]);
+      le |= seg_bits(wave_ballot(!(pv > pivot)), sg) << (j * W);
+      ge |= seg_bits(wave_ballot(!(pivot > pv)), sg) << (j * W);
+      x[j] = !part ? p : (p == first ? r : (p == r ? first : p));
+    }
+    const uint32_t below_last = last >= 32 ? ~0u : ((1u << last) - 1u);
+    const uint32_t inR = part ? below_last & ~((1u << first) - 1u) : 0u;
+    const uint32_t inL = inR & ~(1u << first);
+    const uint32_t Lw = le & inL, Rw = ge & inR;
+    const int nL = __popc(Lw), nR = __popc(Rw);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      isL[j] = part && ((Lw >> x[j]) & 1u);
+      isR[j] = part && ((Rw >> x[j]) & 1u);
+      const uint32_t xb = (1u << x[j]) - 1u;
+      kL[j] = __popc(Lw & xb);
+      kR[j] = nR - 1 - __popc(Rw & xb);
+      *(isL[j] ? lp + kL[j] : ss.junk + j * 64 + lane) = x[j];
+      *(isR[j] ? rp + kR[j] : ss.junk + (E + j) * 64 + lane) = x[j];
+    }
+    wave_lds_sync();
+    uint32_t bl = 0, br = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const int qR = rp[kL[j] < kmax ? kL[j] : kmax];
+      const int qL = lp[kR[j] < 0 ? 0 : (kR[j] < kmax ? kR[j] : kmax)];
+      const bool lsw = isL[j] && kL[j] < nR && x[j] < qR;
+      const bool rsw = isR[j] && kR[j] < nL && qL < x[j];
+      const int d = lsw ? qR : (rsw ? qL : x[j]);
+      sl[d] = v[j];
+      sm[d] = m[j];
+      bl |= seg_bits(wave_ballot(isL[j] && !lsw), sg) << (j * W);
+      br |= seg_bits(wave_ballot(rsw), sg) << (j * W);
+    }
+    const uint32_t keep = ~((1u << first) | (1u << r));
+    const uint32_t ml = (bl & keep) | (((bl >> first) & 1u) << r);
+    const uint32_t mr = (br & keep) | (((br >> first) & 1u) << r);
+    const int lK = seg_lowest(ml), rK = seg_lowest(mr);
+    const int cut = lK < rK ? lK : rK;
+    wave_lds_sync();
+    first = part && cut <= nth ? cut : first;
+    last = part && cut > nth ? cut : last;
+  }
+  const bool heap = act && last - first > 3;
+  if (wave_ballot(heap)) {
+    if (heap && k == 0) {
+      const LinkList wl{sl, sm, 1};
+      heap_select(wl, first, nth + 1, last);
+      wl.swap(first, nth);
+    }
+    wave_lds_sync();
+  }
+  const bool ins = act && !heap && last - first > 1;
+  if (wave_ballot(ins)) {
+    const int len = last - first;
+    const int f0 = first < kmax ? first : kmax;
+    const int f1 = first + 1 < kmax ? first + 1 : kmax, f2 = first + 2 < kmax ? first + 2 : kmax;
+    double y0 = sl[f0], y1 = sl[f1], y2 = sl[f2];
+    uint32_t t0 = sm[f0], t1 = sm[f1], t2 = sm[f2];
+    if (y1 > y0) {
+      const double t = y1; y1 = y0; y0 = t;
+      const uint32_t u = t1; t1 = t0; t0 = u;
+    }
+    if (len > 2) {
+      if (y2 > y0) {
+        const double t = y2; const uint32_t u = t2;
+        y2 = y1; t2 = t1; y1 = y0; t1 = t0; y0 = t; t0 = u;
+      } else if (y2 > y1) {
+        const double t = y2; const uint32_t u = t2;
+        y2 = y1; t2 = t1; y1 = t; t1 = u;
+      }
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const int p = k + j * W, q = p - first;
+      if (ins && (q == 0 || q == 1 || (q == 2 && len > 2))) {
+        sl[p] = q == 0 ? y0 : (q == 1 ? y1 : y2);
+        sm[p] = q == 0 ? t0 : (q == 1 ? t1 : t2);
+      }
+    }
+    wave_lds_sync();
+  }
+}
+
+// mode 6: four links per lane (segE_nth_slots<4>)
+__global__ __launch_bounds__(64) void bench_seg4e(int S, int adds, double *out) {
+  extern __shared__ unsigned char sm[];
+  const int lane = threadIdx.x;
+  const int W = (2 * S + 3) / 4;
+  // slots (64 / W + 1) x 4W <= 16 x 20 = 320 per wave
+  SegScratch ss{(int *)sm, (int *)(sm + 1280), (int *)(sm + 2560), (double *)(sm + 4608), (uint32_t *)(sm + 7168)};
+  const Seg sg = make_seg(W);
+  const int G = 64 / W;
+  const bool in = sg.g < G;
+  const uint32_t g = blockIdx.x * G + sg.g;
+  const int sb = sg.g * 4 * W;
+  for (int j = 0; j < 4; ++j) {
+    const int p = sg.k + j * W;
+    if (in && p < S) {
+      ss.slik[sb + p] = val(g, 0, p);
+      ss.smeta[sb + p] = p;
+    }
+  }
+  wave_lds_sync();
+  for (int r = 1; r <= adds; ++r) {
+    for (int j = 0; j < 4; ++j) {
+      const int p = sg.k + j * W;
+      if (in && p >= S && p < 2 * S) {
+        ss.slik[sb + p] = val(g, r, p - S);
+        ss.smeta[sb + p] = 64u * r + p - S;
+      }
+    }
+    wave_lds_sync();
+    segE_nth_slots<4>(in ? 2 * S : 0, S - 1, sg, ss);
+  }
+  double acc = 0.0;
+  for (int j = 0; j < 4; ++j) {
+    const int p = sg.k + j * W;
+    if (in && p < S) acc += ss.slik[sb + p] * (double)(ss.smeta[sb + p] % 97);
+  }
+  acc = fold(acc);
+  if (lane == 0) out[blockIdx.x] = acc;
+}
+
+
 __global__ __launch_bounds__(64) void bench_seg(int S, int adds, double *out) {
   extern __shared__ unsigned char sm[];
   const int lane = threadIdx.x;
@@ -314,13 +475,16 @@ int main(int argc, char **argv) {
   // mode 2/3 with wpc / (32 / S) process the same lists.
   const int G = 64 / (2 * S);
   const int lists = mode == 2 || mode == 3 ? cu * wpc * 64 : cu * wpc * G;
-  if (mode < 0 || mode == 1 || mode > 5) return 1;
-  const int G5 = 64 / S;
-  int grid = mode == 0 ? cu * wpc : (mode == 4 ? cu * wpc / 2 : (mode == 5 ? (lists + G5 - 1) / G5 : (lists + 63) / 64));
-  size_t lds = mode == 2 || mode == 3 ? (size_t)2 * S * 64 * 12 : (mode == 4 ? 4096 : (mode == 5 ? 4608 : 2048));
+  if (mode < 0 || mode == 1 || mode > 6) return 1;
+  const int G5 = 64 / S, G6 = 64 / ((2 * S + 3) / 4);
+  int grid = mode == 0 ? cu * wpc
+                       : (mode == 4 ? cu * wpc / 2
+                                    : (mode == 5 ? (lists + G5 - 1) / G5 : (mode == 6 ? (lists + G6 - 1) / G6 : (lists + 63) / 64)));
+  size_t lds = mode == 2 || mode == 3 ? (size_t)2 * S * 64 * 12 : (mode == 4 ? 4096 : (mode == 5 ? 4608 : (mode == 6 ? 8448 : 2048)));
   void (*kern)(int, int, double *) =
       mode == 0 ? bench_seg
-                : (mode == 2 ? bench_lane<false> : (mode == 3 ? bench_lane<true> : (mode == 4 ? bench_seg2 : bench_seg2e)));
+                : (mode == 2 ? bench_lane<false>
+                             : (mode == 3 ? bench_lane<true> : (mode == 4 ? bench_seg2 : (mode == 5 ? bench_seg2e : bench_seg4e))));
   if (lds > 65536) (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   double *out;
   (void)hipMalloc(&out, grid * sizeof(double));
