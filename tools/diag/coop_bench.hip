@@ -15,6 +15,7 @@
 //   mode 4: as mode 0 with two sets of segments per wave, interleaved
 //   mode 5: two elements per lane, S lanes per list (seg2_nth_slots)
 //   mode 6: four elements per lane, ceil(S / 2) lanes per list (segE_nth_slots<4>)
+//   mode 7: as mode 5 with lane-major slots (seg2m_nth_slots)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -307,6 +308,181 @@ __device__ inline void segE_nth_slots(int n, int nth, const Seg &sg, const SegSc
   }
 }
 
+// Two links per lane with lane-major slots: position p of segment g lives
+// in slot g W + p (p < W) or 64 + g W + p - W (p >= W), so the lanes' own
+// reads and writes of both links are consecutive (bank-conflict free).
+struct PairSlots {
+  double *l;      // [128]
+  uint32_t *m;    // [128]
+  int gw, W;
+  __device__ int at(int p) const { return gw + p + (p >= W ? 64 - W : 0); }
+  __device__ double lv(int p) const { return l[at(p)]; }
+  // LinkList-like view for the sequential heap select
+  __device__ double l_(int p) const { return l[at(p)]; }
+};
+struct PairView {
+  double *lk;
+  uint32_t *mt;
+  int gw, W;
+  __device__ int at(int p) const { return gw + p + (p >= W ? 64 - W : 0); }
+  __device__ double l(int k) const { return lk[at(k)]; }
+  __device__ uint32_t m(int k) const { return mt[at(k)]; }
+  __device__ void set(int k, double x, uint32_t y) const {
+    lk[at(k)] = x;
+    mt[at(k)] = y;
+  }
+  __device__ void copy(int dst, int src) const { set(dst, l(src), m(src)); }
+  __device__ void swap(int a, int b) const {
+    const double x = l(a);
+    const uint32_t y = m(a);
+    copy(a, b);
+    set(b, x, y);
+  }
+  __device__ bool gt(int a, int b) const { return l(a) > l(b); }
+};
+
+__device__ inline void seg2m_nth_slots(int n, int nth, const Seg &sg, double *slik, uint32_t *smeta, int *lpos,
+                                       int *rpos, int *junk) {
+  const int lane = (int)(threadIdx.x & 63);
+  const int W = sg.sw, k = sg.k;
+  int first = 0, last = n, depth = n > 0 ? lg2_floor(n) * 2 : 0;
+  const bool act = n > 0 && nth != n && sg.mask != 0ull;
+  const PairView V{slik, smeta, sg.g * W, W};
+  const int sb = sg.g * 2 * W;
+  int *lp = lpos + sb, *rp = rpos + sb;
+  int *jl0 = junk + lane, *jl1 = junk + 64 + lane, *jr0 = junk + 128 + lane, *jr1 = junk + 192 + lane;
+  const int kmax = 2 * W - 1;
+  const int p0 = k, p1 = k + W;
+  double *s0 = slik + lane, *s1 = slik + 64 + lane;  // this lane's own slots
+  uint32_t *t0s = smeta + lane, *t1s = smeta + 64 + lane;
+  while (true) {
+    const bool part = act && last - first > 3 && depth > 0;
+    if (!wave_ballot(part)) break;
+    depth -= part ? 1 : 0;
+    const int a = first + 1, b = first + ((last - first) >> 1), c = last > 0 ? last - 1 : 0;
+    const double va = V.l(a), vb = V.l(b), vc = V.l(c), vf = V.l(first);
+    const double v0 = *s0, v1 = *s1;
+    const uint32_t m0 = *t0s, m1 = *t1s;
+    const int idx = (va > vb ? 4 : 0) | (vb > vc ? 2 : 0) | (va > vc ? 1 : 0);
+    const int w = (22561 >> (2 * idx)) & 3;
+    const int r = w == 0 ? a : (w == 1 ? b : c);
+    const double pivot = w == 0 ? va : (w == 1 ? vb : vc);
+    const double pv0 = p0 == first ? pivot : (p0 == r ? vf : v0);
+    const double pv1 = p1 == first ? pivot : (p1 == r ? vf : v1);
+    const uint32_t le = seg_bits(wave_ballot(!(pv0 > pivot)), sg) | seg_bits(wave_ballot(!(pv1 > pivot)), sg) << W;
+    const uint32_t ge = seg_bits(wave_ballot(!(pivot > pv0)), sg) | seg_bits(wave_ballot(!(pivot > pv1)), sg) << W;
+    const uint32_t below_last = last >= 32 ? ~0u : ((1u << last) - 1u);
+    const uint32_t inR = part ? below_last & ~((1u << first) - 1u) : 0u;
+    const uint32_t inL = inR & ~(1u << first);
+    const uint32_t Lw = le & inL, Rw = ge & inR;
+    const int nL = __popc(Lw), nR = __popc(Rw);
+    const int x0 = !part ? p0 : (p0 == first ? r : (p0 == r ? first : p0));
+    const int x1 = !part ? p1 : (p1 == first ? r : (p1 == r ? first : p1));
+    const bool isL0 = part && ((Lw >> x0) & 1u), isR0 = part && ((Rw >> x0) & 1u);
+    const bool isL1 = part && ((Lw >> x1) & 1u), isR1 = part && ((Rw >> x1) & 1u);
+    const uint32_t xb0 = (1u << x0) - 1u, xb1 = (1u << x1) - 1u;
+    const int kL0 = __popc(Lw & xb0), kL1 = __popc(Lw & xb1);
+    const int kR0 = nR - 1 - __popc(Rw & xb0), kR1 = nR - 1 - __popc(Rw & xb1);
+    *(isL0 ? lp + kL0 : jl0) = x0;
+    *(isL1 ? lp + kL1 : jl1) = x1;
+    *(isR0 ? rp + kR0 : jr0) = x0;
+    *(isR1 ? rp + kR1 : jr1) = x1;
+    wave_lds_sync();
+    const int qR0 = rp[kL0 < kmax ? kL0 : kmax], qR1 = rp[kL1 < kmax ? kL1 : kmax];
+    const int qL0 = lp[kR0 < 0 ? 0 : (kR0 < kmax ? kR0 : kmax)];
+    const int qL1 = lp[kR1 < 0 ? 0 : (kR1 < kmax ? kR1 : kmax)];
+    const bool lsw0 = isL0 && kL0 < nR && x0 < qR0, lsw1 = isL1 && kL1 < nR && x1 < qR1;
+    const bool rsw0 = isR0 && kR0 < nL && qL0 < x0, rsw1 = isR1 && kR1 < nL && qL1 < x1;
+    const int d0 = lsw0 ? qR0 : (rsw0 ? qL0 : x0), d1 = lsw1 ? qR1 : (rsw1 ? qL1 : x1);
+    V.set(d0, v0, m0);
+    V.set(d1, v1, m1);
+    const uint32_t bl = seg_bits(wave_ballot(isL0 && !lsw0), sg) | seg_bits(wave_ballot(isL1 && !lsw1), sg) << W;
+    const uint32_t br = seg_bits(wave_ballot(rsw0), sg) | seg_bits(wave_ballot(rsw1), sg) << W;
+    const uint32_t keep = ~((1u << first) | (1u << r));
+    const uint32_t ml = (bl & keep) | (((bl >> first) & 1u) << r);
+    const uint32_t mr = (br & keep) | (((br >> first) & 1u) << r);
+    const int lK = seg_lowest(ml), rK = seg_lowest(mr);
+    const int cut = lK < rK ? lK : rK;
+    wave_lds_sync();
+    first = part && cut <= nth ? cut : first;
+    last = part && cut > nth ? cut : last;
+  }
+  const bool heap = act && last - first > 3;
+  if (wave_ballot(heap)) {
+    if (heap && k == 0) {
+      heap_select(V, first, nth + 1, last);
+      V.swap(first, nth);
+    }
+    wave_lds_sync();
+  }
+  const bool ins = act && !heap && last - first > 1;
+  if (wave_ballot(ins)) {
+    const int len = last - first;
+    const int f0 = first < kmax ? first : kmax;
+    const int f1 = first + 1 < kmax ? first + 1 : kmax, f2 = first + 2 < kmax ? first + 2 : kmax;
+    double y0 = V.l(f0), y1 = V.l(f1), y2 = V.l(f2);
+    uint32_t t0 = V.m(f0), t1 = V.m(f1), t2 = V.m(f2);
+    if (y1 > y0) {
+      const double t = y1; y1 = y0; y0 = t;
+      const uint32_t u = t1; t1 = t0; t0 = u;
+    }
+    if (len > 2) {
+      if (y2 > y0) {
+        const double t = y2; const uint32_t u = t2;
+        y2 = y1; t2 = t1; y1 = y0; t1 = t0; y0 = t; t0 = u;
+      } else if (y2 > y1) {
+        const double t = y2; const uint32_t u = t2;
+        y2 = y1; t2 = t1; y1 = t; t1 = u;
+      }
+    }
+    const int j0 = p0 - first, j1 = p1 - first;
+    const bool mine0 = ins && (j0 == 0 || j0 == 1 || (j0 == 2 && len > 2));
+    const bool mine1 = ins && (j1 == 0 || j1 == 1 || (j1 == 2 && len > 2));
+    const double z0 = j0 == 0 ? y0 : (j0 == 1 ? y1 : y2), z1 = j1 == 0 ? y0 : (j1 == 1 ? y1 : y2);
+    const uint32_t u0 = j0 == 0 ? t0 : (j0 == 1 ? t1 : t2), u1 = j1 == 0 ? t0 : (j1 == 1 ? t1 : t2);
+    wave_lds_sync();
+    if (mine0) {
+      *s0 = z0;
+      *t0s = u0;
+    }
+    if (mine1) {
+      *s1 = z1;
+      *t1s = u1;
+    }
+    wave_lds_sync();
+  }
+}
+
+// mode 7: two links per lane, lane-major slots (seg2m_nth_slots)
+__global__ __launch_bounds__(64) void bench_seg2m(int S, int adds, double *out) {
+  extern __shared__ unsigned char sm[];
+  const int lane = threadIdx.x;
+  int *lpos = (int *)sm, *rpos = (int *)(sm + 640), *junk = (int *)(sm + 1280);
+  double *slik = (double *)(sm + 2304);          // 128 doubles
+  uint32_t *smeta = (uint32_t *)(sm + 2304 + 1024);  // 128
+  const Seg sg = make_seg(S);
+  const int G = 64 / S;
+  const bool in = sg.g < G;
+  const uint32_t g = blockIdx.x * G + sg.g;
+  if (in) {
+    slik[lane] = val(g, 0, sg.k);
+    smeta[lane] = sg.k;
+  }
+  wave_lds_sync();
+  for (int r = 1; r <= adds; ++r) {
+    if (in) {
+      slik[64 + lane] = val(g, r, sg.k);
+      smeta[64 + lane] = 64u * r + sg.k;
+    }
+    wave_lds_sync();
+    seg2m_nth_slots(in ? 2 * S : 0, S - 1, sg, slik, smeta, lpos, rpos, junk);
+  }
+  double acc = 0.0;
+  if (in) acc = slik[lane] * (double)(smeta[lane] % 97);
+  acc = fold(acc);
+  if (lane == 0) out[blockIdx.x] = acc;
+}
+
 // mode 6: four links per lane (segE_nth_slots<4>)
 __global__ __launch_bounds__(64) void bench_seg4e(int S, int adds, double *out) {
   extern __shared__ unsigned char sm[];
@@ -475,16 +651,19 @@ int main(int argc, char **argv) {
   // mode 2/3 with wpc / (32 / S) process the same lists.
   const int G = 64 / (2 * S);
   const int lists = mode == 2 || mode == 3 ? cu * wpc * 64 : cu * wpc * G;
-  if (mode < 0 || mode == 1 || mode > 6) return 1;
+  if (mode < 0 || mode == 1 || mode > 7) return 1;
   const int G5 = 64 / S, G6 = 64 / ((2 * S + 3) / 4);
   int grid = mode == 0 ? cu * wpc
                        : (mode == 4 ? cu * wpc / 2
-                                    : (mode == 5 ? (lists + G5 - 1) / G5 : (mode == 6 ? (lists + G6 - 1) / G6 : (lists + 63) / 64)));
-  size_t lds = mode == 2 || mode == 3 ? (size_t)2 * S * 64 * 12 : (mode == 4 ? 4096 : (mode == 5 ? 4608 : (mode == 6 ? 8448 : 2048)));
+                                    : (mode == 5 || mode == 7 ? (lists + G5 - 1) / G5
+                                                              : (mode == 6 ? (lists + G6 - 1) / G6 : (lists + 63) / 64)));
+  size_t lds = mode == 2 || mode == 3 ? (size_t)2 * S * 64 * 12 : (mode == 4 ? 4096 : (mode == 5 || mode == 7 ? 4608 : (mode == 6 ? 8448 : 2048)));
   void (*kern)(int, int, double *) =
       mode == 0 ? bench_seg
                 : (mode == 2 ? bench_lane<false>
-                             : (mode == 3 ? bench_lane<true> : (mode == 4 ? bench_seg2 : (mode == 5 ? bench_seg2e : bench_seg4e))));
+                             : (mode == 3 ? bench_lane<true>
+                                          : (mode == 4 ? bench_seg2
+                                                       : (mode == 5 ? bench_seg2e : (mode == 6 ? bench_seg4e : bench_seg2m)))));
   if (lds > 65536) (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   double *out;
   (void)hipMalloc(&out, grid * sizeof(double));
