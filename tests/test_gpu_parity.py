@@ -155,6 +155,25 @@ def test_value_pair_layout(oracle_mod, name, S, shape):
     assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
 
 
+@pytest.mark.parametrize("name", ["n60", "a3miss5", "a8", "n300"])
+@pytest.mark.parametrize("S,shape", [(10, None), (3, None), (10, (0, 0, 8, 2))])
+def test_value_one_link_layout(oracle_mod, name, S, shape):
+    """hmc_set_value_layout(0): the round-2 phase-B layout (2S lanes, one link
+    per lane; still the automatic one for S > 16) — same E-step, bit for bit,
+    as HaploModel::resolveAll."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=S)
+    o.find_patterns()
+    m = gpu_model(p, S)
+    m.set_value_layout(0)
+    if shape:
+        m.set_pass_shapes(*shape)
+    m.find_patterns()
+    ll_g, H, re_g = m.resolve_all()
+    o.reset_counters()
+    assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
+
+
 @pytest.mark.parametrize("S", [1, 2, 5, 16, 17, 24, 32, 33, 40, 64])
 def test_estep_sample_sizes(oracle_mod, S):
     p = panel("miss2")
