@@ -51,8 +51,12 @@ from hmc_amd import synth  # noqa: E402
 
 METRIC = "individuals×loci/sec per EM iter, synthetic panel, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E (spec)
-PMC_DIR = os.path.join(ROOT, "profiles", "r03")
+PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r04", "r03")]  # newest profile of the workload first
 DBL_MAX = sys.float_info.max
+# What bounds estep_values (SQ counters under profiles/): the
+# roofline above prices it against HBM, but the kernel moves ~1/30 of peak —
+# its waves are parked on dependent LDS round trips and barriers.
+LIMITER = "issue/latency: dependent selection steps and per-locus barriers (SQ counters, DESIGN.md 9), not HBM bandwidth"
 
 
 def parse():
@@ -210,6 +214,7 @@ def main():
         m.em_rewind()
 
     chain = {"it": 0, "old_ll": -DBL_MAX, "ended": False}
+    run_log = []  # (R_E, value-pass launches) of every E-step this process runs after M0, in order (PMC pairing)
 
     def em_step(force_m: bool = False):
         """One step of the converged chain (or, force_m, an iteration that
@@ -226,6 +231,7 @@ def main():
         wall = time.perf_counter() - t_s
         t = m.timings()
         sp = m.estep_split_stats()
+        run_log.append([int(log["r_e"]), int(sp["value_passes"])])
         progress(f"EM iteration {it}: LL {log['log_likelihood']:.6f}, R_E {log['r_e']}, "
                  f"E {t['estep_forward_ms'] + t['estep_traceback_ms']:.0f} ms "
                  f"(structure {sp['structure_ms']:.0f} in {sp['structure_passes']}, values {sp['values_ms']:.0f} in "
@@ -331,7 +337,9 @@ def main():
                 "bound": "hbm", "kernel": "estep_values",
                 "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                 "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                "traffic_over_alg": pmc.get("traffic_over_alg") if pmc else None,
                 "traffic_source": pmc.get("source") if pmc else None,
+                "limiter": LIMITER,
                 "alg_bytes_per_launch": 8.0 * r_e_all / world / max(1, n_launch),
                 "avg_launch_ms": val_ms / max(1, n_launch),
                 "launches": n_launch,
@@ -346,6 +354,7 @@ def main():
             "m0": {"seconds": t_m0, "patterns": P0, "r_m": rm0},
             "library": ident,
             "per_step": [{k: (round(v, 6) if isinstance(v, float) else v) for k, v in s.items()} for s in steps],
+            "run_estep_log": run_log,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -355,16 +364,19 @@ def main():
 
 def pmc_summary(tag):
     """rocprofv3 PMC summary (HBM bytes per estep_values launch) of this
-    workload, committed under profiles/r03/ by tools/profile_round.sh; None
-    when this configuration has not been profiled."""
-    p = os.path.join(PMC_DIR, f"pmc_estep_values_{tag}.json")
-    try:
-        with open(p) as f:
-            d = json.load(f)
-        d["source"] = os.path.relpath(p, ROOT)
-        return d
-    except (OSError, ValueError):
-        return None
+    workload, committed under profiles/rNN/ by tools/profile_round.sh (the
+    newest round that has one); None when this configuration has not been
+    profiled."""
+    for d in PMC_DIRS:
+        p = os.path.join(d, f"pmc_estep_values_{tag}.json")
+        try:
+            with open(p) as f:
+                out = json.load(f)
+            out["source"] = os.path.relpath(p, ROOT)
+            return out
+        except (OSError, ValueError):
+            continue
+    return None
 
 
 def cpu_baseline(m, panel, args):

@@ -45,6 +45,7 @@ _SIGS = [
     ("hmc_rccl_comm_init", _i, [_i, _i, _i, _vp, _P(_vp)]),
     ("hmc_rccl_comm_destroy", _i, [_vp]),
     ("hmc_set_reduction", _i, [_vp, _i]),
+    ("hmc_set_force_collectives", _i, [_vp, _i]),
     ("hmc_ctx_destroy", None, [_vp]),
     ("hmc_ctx_error", _cp, [_vp]),
     ("hmc_set_params", _i, [_vp, _d, _d, _i, _i, _i]),

@@ -259,7 +259,7 @@ struct Ctx {
   enum { RED_ORDERED = 0, RED_ALLREDUCE = 1 };
   int reduction = RED_ORDERED;
   // A one-rank context on a one-rank RCCL communicator runs every collective
-  // anyway (test hook, HMC_FORCE_COLLECTIVES=1 at creation): results are
+  // anyway (test hook, hmc_set_force_collectives): results are
   // unchanged, so the RCCL calls can be exercised on a one-GPU machine.
   bool force_coll = false;
   bool multi() const { return world > 1 || force_coll; }
@@ -552,6 +552,7 @@ struct Ctx {
     if ((e = hipStreamSynchronize(st))) return hipfail(e, "upload_panel");
     have_panel = true;
     have_model = have_samples = have_estep = have_best = false;
+    snap.valid = false;  // a saved table belongs to the panel it was built on
     P = 0;
     H = 0;
     return HMC_OK;
@@ -966,6 +967,9 @@ struct Ctx {
   int exact_walk_group(ExactArgs &x, int k, int dev_cu) {
     const int L = pan.L;
     hipError_t e;
+    if (exact_walk_lds_bytes(tr_maxd, x.fmax) > EXACT_WALK_LDS_MAX)
+      return fail(HMC_EUNSUPPORTED, "exact M-step: a frontier of %d states (trie depth %d) exceeds the walk's LDS bitmap",
+                  x.fmax, tr_maxd);
     x.scratch_stride = exact_walk_scratch_doubles(tr_maxd, x.fmax, x.width);
     const long long items = (long long)k * L;
     // 28 waves per CU (7 per SIMD at 64 VGPRs), fewer when the per-wave lists
@@ -1248,7 +1252,22 @@ struct Ctx {
     return w >= L ? L : std::max(w, 1);
   }
 
+  // A search that fails after its first block has started has overwritten
+  // part of the table (rows, node window): the context then holds no model
+  // and no candidate tree, so no later E-step or spelling runs on a half-built
+  // table.
+  bool mine_touched = false;
   int mine_impl(int *P_out, uint64_t *rm_out, int bynum_rounds) {
+    mine_touched = false;
+    const int rc = mine_impl_body(P_out, rm_out, bynum_rounds);
+    if (rc != HMC_OK && mine_touched) {
+      have_model = false;
+      tree_gen = ~0ull;
+      model_gen = ++next_gen;
+    }
+    return rc;
+  }
+  int mine_impl_body(int *P_out, uint64_t *rm_out, int bynum_rounds) {
     if (!have_panel) return fail(HMC_EARG, "no panel loaded");
     const int L = pan.L;
     hipError_t e;
@@ -1274,6 +1293,7 @@ struct Ctx {
     long long id_base = 0;    // patterns of the blocks above
     uint64_t rm_bynum = 0;
     int rc, nblocks = 0;
+    mine_touched = true;
     for (int hi = L; hi > 0;) {
       const int lo = std::max(0, hi - W);
       MineBlock mb;
@@ -1301,6 +1321,12 @@ struct Ctx {
                 nblocks, lo, hi, id_base, (long long)mb.first_node, (long long)mb.end_node);
       hi = lo;
     }
+    {  // before anything is committed: a failed successor walk leaves no table
+      int merr = 0;
+      if ((e = hipMemcpyAsync(&merr, d_mine_err.p, 4, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+        return hipfail(e, "mine");
+      if (merr) return fail(HMC_EUNSUPPORTED, "successor walk left the node window (blocks of %d start loci)", W);
+    }
     tree_complete = nblocks == 1;
     P = (int)id_base;
     if (!tree_complete) {  // a partial tree is of no further use (strings come from ppat): give its memory back
@@ -1312,12 +1338,6 @@ struct Ctx {
       wbase = 0;
     } else {
       last_mine_window_gb = (double)node_cap * 70.0 / 1e9;
-    }
-    {
-      int merr = 0;
-      if ((e = hipMemcpyAsync(&merr, d_mine_err.p, 4, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
-        return hipfail(e, "mine");
-      if (merr) return fail(HMC_EUNSUPPORTED, "successor walk left the node window (blocks of %d start loci)", W);
     }
     std::vector<unsigned long long> rm_slots((size_t)RM_SLOTS * 16);
     if ((e = hipMemcpyAsync(rm_slots.data(), d_rm.p, rm_slots.size() * 8, hipMemcpyDeviceToHost, st)))
@@ -1944,13 +1964,18 @@ struct Ctx {
     // stores (fewer groups) measured no faster and crowd out the next M0.  The
     // trace cap keeps cfg 3's E2.. (~90 GB of traces) in one value pass.)
     trace_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.42), 120ull << 30),
-                                      1ull << 20) / 4;
+                                      1ull << 16) / 4;
     rec_budget = std::max<uint64_t>(rec_bytes ? rec_bytes : trace_bytes ? trace_bytes
                                     : std::min<uint64_t>((uint64_t)(avail * 0.28), 80ull << 30),
-                                    1ull << 20) / 4;
+                                    1ull << 16) / 4;
     if (debug_mem)
       fprintf(stderr, "[hmc] E-step: free %.1f GB, stores %.1f + %.1f GB, budgets trace %.1f rec %.1f GB\n",
               freeb / 1e9, d_trace.n * 4 / 1e9, d_rec.n * 4 / 1e9, trace_budget * 4 / 1e9, rec_budget * 4 / 1e9);
+    // Stores sized by an earlier E-step when more HBM was free (E1, before an
+    // exact M-step's tables) shrink to this E-step's budgets: the pass
+    // scratch is allocated from what they leave free.
+    if (d_trace.n > trace_budget) d_trace.release();
+    if (d_rec.n > rec_budget) d_rec.release();
     h_total.assign(n, 0.0);
     h_ncand.assign(n, 0);
     h_status.assign(n, 0);
@@ -2049,6 +2074,22 @@ struct Ctx {
   uint64_t trace_budget = 0, rec_budget = 0;  // words
   int n_struct_passes = 0, n_value_passes = 0;
 
+  // Pass scratch, allocated while the stores hold most of HBM: on a failure
+  // the trace store (dead before a value pass is launched) and, when
+  // `rec_dead`, the record store give their memory back; the caller
+  // re-ensures them afterwards.
+  uint64_t rec_words = 0;
+  hipError_t scratch_ensure(DevBuf<char> &b, size_t bytes, bool rec_dead) {
+    hipError_t e = b.ensure(bytes);
+    if (e != hipErrorOutOfMemory) return e;
+    (void)hipGetLastError();
+    d_trace.release();
+    if ((e = b.ensure(bytes)) != hipErrorOutOfMemory || !rec_dead) return e;
+    (void)hipGetLastError();
+    d_rec.release();
+    return b.ensure(bytes);
+  }
+
   // Grow a store (contents dropped) to hold `words`, within `budget`.
   int ensure_store(DevBuf<uint32_t> &b, uint64_t words, uint64_t budget, const char *what) {
     if (b.n >= words && b.p) return HMC_OK;
@@ -2097,10 +2138,7 @@ struct Ctx {
     a.n_order = 0;
     a.cost = d_cost.p;
     a.stamps = d_stamps.p;
-    a.diag_indiv = -1;
-#ifdef HMC_STAMPS  // diagnostic build only: stamp one batch index
-    if (const char *di = getenv("HMC_DIAG_INDIV")) a.diag_indiv = atoi(di);
-#endif
+    a.diag_indiv = -1;  // diagnostic build: stamps of every individual
     return a;
   }
 
@@ -2303,7 +2341,7 @@ struct Ctx {
           }
         }
         np = k;
-        if ((rc = ensure_store(d_rec, r, rec_budget, "record store"))) return rc;
+        rec_words = r;
         std::vector<unsigned long long> rb(n, 0), rs(n, 0);
         for (int q = 0; q < np; ++q) {
           rb[pending[q]] = base[pending[q]];
@@ -2314,7 +2352,8 @@ struct Ctx {
           return hipfail(e, "estep");
       }
       const int hcap1 = next_pow2(2 * fcap);
-      const int ccap1 = (int)std::min<int64_t>(INT32_MAX / 2, (int64_t)ccap_mult * fcap);
+      // (exact records pack a locus's contribution count in 22 bits, R[3] = C << 10 | npairs)
+      const int ccap1 = (int)std::min<int64_t>(exact ? EXACT_C_MAX : INT32_MAX / 2, (int64_t)ccap_mult * fcap);
       // structure pass: one wave per individual; 12 per CU (3 per SIMD at 145
       // VGPRs) above 8 per CU, so cfg 3's E1 groups of 2 200-2 700 run in one
       // round (profiles/r02/e1_groups/: 603-658 -> 484-586 ms per group).  On a
@@ -2333,9 +2372,12 @@ struct Ctx {
       const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1, nw1);
       // (huge frontiers: fewer resident individuals rather than scratch past SCRATCH_MAX)
       const int grid1 = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::min(np, dev_cu * bpc1), SCRATCH_MAX / per1));
-      if ((e = d_scr1.ensure(per1 * grid1)) || (e = d_rec_off.ensure((size_t)n * (L + 1))) ||
+      // the scratch first: both stores are dead here (the groups before have
+      // been traced back), so they give way to it when HBM is short
+      if ((e = scratch_ensure(d_scr1, per1 * grid1, true)) || (e = d_rec_off.ensure((size_t)n * (L + 1))) ||
           (e = d_rec_cursor.ensure(1)) || (e = hipMemsetAsync(d_rec_cursor.p, 0, 8, st)))
         return hipfail(e, "estep pass-1 alloc");
+      if ((rc = ensure_store(d_rec, rec_words, rec_budget, "record store"))) return rc;
       if ((rc = upload_order(d_order, pending.data(), np))) return rc;
       StructArgs s1;
       s1.pan = dev_panel();
@@ -2399,6 +2441,8 @@ struct Ctx {
         if (s == EST_NO_HEAD_PATTERN) return fail(HMC_ENOPATTERN, "Can not find matching pattern!");
         if (s == EST_OVERFLOW_CONTRIB) {  // missing genotypes: up to amax^2 contributions per state
           if ((int64_t)ccap_mult * fcap >= INT32_MAX / 2) return fail(HMC_EUNSUPPORTED, "too many contributions at a locus");
+          if (exact && ccap1 >= EXACT_C_MAX)
+            return fail(HMC_EUNSUPPORTED, "exact M-step: more than %d contributions at a locus", EXACT_C_MAX);
           ccap_mult *= 2;
           return ESTEP_RESTART;
         }
@@ -2519,7 +2563,8 @@ struct Ctx {
         fgrp = std::min(fcap, (fgrp + 63) & ~63);
         const size_t per2 = estep_s2_scratch_bytes(fgrp, S);
         const int grid2 = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::min<int>(G2, (int)k), SCRATCH_MAX / per2));
-        if ((e = d_scr2.ensure(per2 * grid2))) return hipfail(e, "estep pass-2 scratch");
+        if ((e = scratch_ensure(d_scr2, per2 * grid2, false))) return hipfail(e, "estep pass-2 scratch");
+        if ((rc = ensure_store(d_trace, std::max<uint64_t>(t, 1), trace_budget, "trace store"))) return rc;
         ValueArgs v;
         v.S = S;
         v.L = L;
@@ -2912,6 +2957,7 @@ struct Ctx {
   struct Snap {
     bool valid = false, table_on_host = false;
     int P = 0, head_len = 1, n_head = 0;
+    int L = 0, amax = 0;  // the panel's shape when saved (successor rows are amax wide)
     uint64_t gen = 0;
     DevBuf<int32_t> start, len, node, ppat;
     DevBuf<double> freq, prefix, tp;
@@ -2955,6 +3001,8 @@ struct Ctx {
         (head_len > 1 && (e = dcopy(snap.head_al, d_head_al, p * head_len))) || (e = hipStreamSynchronize(st)))
       return hipfail(e, "model_save");
     snap.P = P;
+    snap.L = pan.L;
+    snap.amax = pan.amax;
     snap.head_len = head_len;
     snap.n_head = n_head;
     snap.gen = model_gen;
@@ -2970,6 +3018,8 @@ struct Ctx {
   }
   int em_rewind() {
     if (!snap.valid) return fail(HMC_EARG, "no saved model (hmc_model_save)");
+    if (!have_panel || snap.L != pan.L || snap.amax != pan.amax)
+      return fail(HMC_EARG, "the saved model belongs to another panel");
     const size_t p = (size_t)std::max(snap.P, 1), A = (size_t)pan.amax;
     hipError_t e;
     if ((e = dcopy(t_start, snap.start, p)) || (e = dcopy(t_len, snap.len, p)) || (e = dcopy(t_node, snap.node, p)) ||
@@ -3079,8 +3129,7 @@ int hmc_ctx_create_dist(int device, int rank, int world, const void *unique_id, 
   if (rc) return rc;
   h->c.rank = rank;
   h->c.world = world;
-  if (world == 1 && getenv("HMC_FORCE_COLLECTIVES")) h->c.force_coll = true;
-  if (world > 1 || h->c.force_coll) {
+  {  // a unique id means an RCCL communicator, also at world 1 (hmc_set_force_collectives)
     ncclUniqueId id;
     memcpy(&id, unique_id, sizeof id);
     ncclResult_t r = ncclCommInitRank(&h->c.comm, world, id, rank);
@@ -3103,7 +3152,15 @@ int hmc_ctx_create_comm(int device, void *rccl_comm, hmc_ctx **out) {
   h->c.own_comm = false;
   h->c.rank = r;
   h->c.world = w;
-  if (w == 1 && getenv("HMC_FORCE_COLLECTIVES")) h->c.force_coll = true;
+  return HMC_OK;
+}
+
+int hmc_set_force_collectives(hmc_ctx *h, int on) {
+  if (!h) return HMC_EARG;
+  hmc::Ctx &c = h->c;
+  if (on && c.world == 1 && !c.comm && !c.host_fn)
+    return c.fail(HMC_EARG, "force_collectives: the context has no communicator (create it with a unique id or a comm)");
+  c.force_coll = on != 0 && c.world == 1;
   return HMC_OK;
 }
 
@@ -3463,7 +3520,7 @@ int hmc_write_file(hmc_ctx *h, const char *format, const char *path, const char 
 }
 
 int hmc_write_patterns(hmc_ctx *h, const char *path) {
-  if (!h || !path || !h->c.have_model || (!h->c.tree_ok() && !h->c.table_on_host)) return HMC_EARG;
+  if (!h || !path || !h->c.have_model) return HMC_EARG;
   hmc::Ctx &c = h->c;
   const int P = c.P, L = c.pan.L;
   std::vector<int32_t> st(P), ln(P);
@@ -3473,7 +3530,18 @@ int hmc_write_patterns(hmc_ctx *h, const char *path) {
   int maxlen = 1;
   for (int i = 0; i < P; ++i) maxlen = std::max(maxlen, ln[i]);
   std::vector<int32_t> al((size_t)P * maxlen);
-  if ((rc = hmc_get_patterns(h, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, al.data(), maxlen))) return rc;
+  if (c.table_on_host) {
+    if ((rc = hmc_get_patterns(h, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, al.data(), maxlen))) return rc;
+  } else {
+    // spelled from the prefix ids (no candidate tree needed: blocked searches
+    // and rewound tables qualify); a table whose strings are unknown fails
+    // here instead of being written with its last alleles only
+    std::vector<int64_t> off;
+    std::vector<uint8_t> a8;
+    if ((rc = c.spell_table(ln, off, a8))) return rc;
+    for (int i = 0; i < P; ++i)
+      for (int k = 0; k < ln[i]; ++k) al[(size_t)i * maxlen + k] = c.pan.symbol(st[i] + k, a8[off[i] + k]);
+  }
   FILE *fp = fopen(path, "w");
   if (!fp) return c.fail(HMC_EIO, "Can not open file %s!", path);
   fprintf(fp, "Frequency\tLength\t");

@@ -653,7 +653,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         R[0] = (uint32_t)Fn;
         R[1] = (uint32_t)Cv;
         R[2] = (uint32_t)nch;
-        R[3] = a.exact ? (uint32_t)C << 10 | (uint32_t)npairs : 0u;  // C < 2^22, npairs < 2^10 (amax <= 44 in exact mode)
+        // C <= EXACT_C_MAX (the host caps ccap in exact mode), npairs < 2^10 (amax <= 44 in exact mode)
+        R[3] = a.exact ? (uint32_t)C << 10 | (uint32_t)npairs : 0u;
         roff[i + 1] = o;
       }
       S1_ST(3);
@@ -1267,6 +1268,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
 hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStream_t st) {
   if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > F_MAX || (a.hcap & (a.hcap - 1)) || a.lds_hc < 1 ||
       (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || a.lds_cc < 0 || a.ccap < 1 || a.mod.head_len < 1 ||
+      (a.exact && a.ccap > EXACT_C_MAX) ||
       (a.mod.head_len > 1 && (!a.mod.hf_off || !a.mod.hf_pairs || !a.mod.hf_status)) ||
       (nw != 1 && nw != 4 && nw != 8 && nw != 16))
     return hipErrorInvalidValue;

@@ -482,7 +482,13 @@ hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st) {
   if (a.n_order <= 0) return hipSuccess;
   if (a.width < 1 || a.width > 64) return hipErrorInvalidValue;
   const size_t lds = exact_walk_lds_bytes(a.max_depth, a.fmax);
-  if (lds > 65536) return hipErrorInvalidValue;
+  if (lds > EXACT_WALK_LDS_MAX) return hipErrorInvalidValue;  // the host reports it (exact_walk_group)
+  static size_t lds_attr = 0;
+  if (lds > 65536 && lds > lds_attr) {  // wide frontiers: a larger reached-state bitmap, fewer waves per CU
+    hipError_t e = hipFuncSetAttribute((const void *)exact_walk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    lds_attr = lds;
+  }
   hipLaunchKernelGGL(exact_walk, dim3(grid), dim3(WAVE), lds, st, a);
   return hipGetLastError();
 }

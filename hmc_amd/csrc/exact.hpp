@@ -40,5 +40,6 @@ hipError_t launch_exact_fb(const ExactArgs &a, int grid, hipStream_t st);
 hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st);
 size_t exact_walk_scratch_doubles(int max_depth, int fmax, int width);
 size_t exact_walk_lds_bytes(int max_depth, int fmax);
+constexpr size_t EXACT_WALK_LDS_MAX = 160 * 1024;  // gfx950 LDS per workgroup
 
 }  // namespace hmc

@@ -12,6 +12,7 @@ constexpr int S_MAX = 64;    // sample_size limit (lists of 2S links: segments o
                              // S = 32, one list per wave over two lanes' slots above; fused kernel: 32)
 constexpr int A_MAX = 64;    // alleles per locus limit (allele indices are u8; exact M-step: 44)
 constexpr int WAVE = 64;
+constexpr int EXACT_C_MAX = (1 << 22) - 1;  // contributions per locus in an exact-M-step record (22-bit field)
 
 // Link metadata word (one k-best entry, HaploPairLink HaploPair.h:14-28):
 //   bits 0-15 predecessor state, 16-23 index in the predecessor's list,

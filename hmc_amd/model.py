@@ -205,6 +205,10 @@ class HaploModel:
         "allreduce" (one collective per mining level, last-bit drift)."""
         self._check(lib().hmc_set_reduction(self._h, {"ordered": 0, "allreduce": 1}[mode]))
 
+    def set_force_collectives(self, on: bool = True):
+        """Test hook: a one-rank context with a communicator runs every collective."""
+        self._check(lib().hmc_set_force_collectives(self._h, int(bool(on))))
+
     def set_estep_mode(self, mode: int):
         """0 = split E-step (structure pass + value pass, default), 1 = fused kernel."""
         self._check(lib().hmc_set_estep_mode(self._h, int(mode)))

@@ -59,6 +59,11 @@ int hmc_rccl_comm_destroy(void *comm);
  * several ranks share one GPU (tests) or run over any host transport. */
 typedef int (*hmc_allreduce_fn)(double *buf, size_t n, void *user);
 int hmc_ctx_create_hostcoll(int device, int rank, int world, hmc_allreduce_fn fn, void *user, hmc_ctx **out);
+/* Test hook: a one-rank context made with a unique id or a communicator runs
+ * every collective of the sharded path anyway (results unchanged), so the
+ * RCCL calls are exercised on a one-GPU machine.  HMC_EARG on a context
+ * without a communicator. */
+int hmc_set_force_collectives(hmc_ctx *ctx, int on);
 void hmc_ctx_destroy(hmc_ctx *ctx);
 const char *hmc_ctx_error(const hmc_ctx *ctx);
 

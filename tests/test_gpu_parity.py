@@ -92,10 +92,16 @@ def test_estep_on_reference_model(oracle_mod, name, S, mode):
     assert_estep_equal(m, o, ll_g, ll_o, H, re_g)
 
 
-@pytest.mark.parametrize("name", ["n60", "a3miss5", "a8", "n300"])
-@pytest.mark.parametrize("shape", [(1, 12, 1, 20), (4, 3, 4, 4), (4, 1, 2, 8), (1, 4, 3, 8), (4, 2, 16, 1),
-                                   (1, 8, 8, 2), (4, 2, 5, 3), (16, 1, 4, 4), (16, 1, 16, 1), (8, 2, 8, 2),
-                                   (1, 16, 1, 20), (1, 20, 2, 8), (4, 4, 8, 2)])
+# the shapes the automatic rule selects (structure 1 x 4/8/12, 4 x 2, 16 x 1;
+# values 1 x 20, 2 x 8, 3 x 8, 8 x 2, 16 / c x c) on two panels, and stress
+# shapes the rule never picks on the stress panel (3 alleles, 5 % missing)
+_AUTO_SHAPES = [(1, 12, 1, 20), (4, 2, 8, 2), (1, 8, 2, 8), (1, 4, 3, 8), (16, 1, 16, 1), (16, 1, 8, 2)]
+_STRESS_SHAPES = [(4, 3, 4, 4), (4, 1, 2, 8), (4, 2, 16, 1), (1, 8, 8, 2), (4, 2, 5, 3), (8, 2, 8, 2),
+                  (1, 16, 1, 20), (1, 20, 2, 8)]
+
+
+@pytest.mark.parametrize("name,shape", [(n, s) for n in ("a3miss5", "n300") for s in _AUTO_SHAPES]
+                         + [("a3miss5", s) for s in _STRESS_SHAPES])
 def test_estep_pass_shapes(oracle_mod, name, shape):
     """Launch shapes of the split E-step's passes (hmc_set_pass_shapes:
     structure waves per individual 1, 4, 8 or 16, individuals per CU — the
@@ -113,8 +119,7 @@ def test_estep_pass_shapes(oracle_mod, name, shape):
     assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
 
 
-@pytest.mark.parametrize("name", ["cfg1", "a3miss5", "a8", "n300"])
-@pytest.mark.parametrize("S", [10, 3])
+@pytest.mark.parametrize("name,S", [("cfg1", 10), ("a3miss5", 3), ("a8", 10), ("n300", 3)])
 def test_value_only_mode_with_order_reruns(oracle_mod, name, S):
     """hmc_set_value_mode(0): value-only k-best lists (seg_rank_select), the
     libstdc++ permutations only for individuals with ties — same E-step, bit
@@ -134,9 +139,10 @@ def test_value_only_mode_with_order_reruns(oracle_mod, name, S):
     assert 0 <= st["n_order_rerun"] <= p.N
 
 
-@pytest.mark.parametrize("name", ["n60", "a3miss5", "a8", "n300"])
-@pytest.mark.parametrize("S,shape", [(10, None), (1, None), (2, None), (3, None), (5, None), (16, None),
-                                     (10, (0, 0, 8, 2)), (10, (0, 0, 2, 8)), (7, (0, 0, 4, 4))])
+@pytest.mark.parametrize("name,S,shape", [("a3miss5", S, sh) for S, sh in
+                                          [(10, None), (1, None), (2, None), (3, None), (5, None), (16, None),
+                                           (10, (0, 0, 8, 2)), (10, (0, 0, 2, 8)), (7, (0, 0, 4, 4))]]
+                         + [(n, 10, None) for n in ("n60", "a8", "n300")])
 def test_value_pair_layout(oracle_mod, name, S, shape):
     """hmc_set_value_layout(2): phase B of the value pass with two links per
     lane (seg2_nth_slots: S lanes and 64 / S lists per wavefront) for every
@@ -155,8 +161,8 @@ def test_value_pair_layout(oracle_mod, name, S, shape):
     assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
 
 
-@pytest.mark.parametrize("name", ["n60", "a3miss5", "a8", "n300"])
-@pytest.mark.parametrize("S,shape", [(10, None), (3, None), (10, (0, 0, 8, 2))])
+@pytest.mark.parametrize("name,S,shape", [("a3miss5", 10, None), ("a3miss5", 3, None), ("a3miss5", 10, (0, 0, 8, 2)),
+                                          ("n300", 10, None), ("a8", 3, None)])
 def test_value_one_link_layout(oracle_mod, name, S, shape):
     """hmc_set_value_layout(0): the round-2 phase-B layout (2S lanes, one link
     per lane; still the automatic one for S > 16) — same E-step, bit for bit,
@@ -879,13 +885,12 @@ def _rccl_comm_one_rank():
 
 @pytest.mark.parametrize("how", ["unique_id", "caller_comm"])
 @pytest.mark.parametrize("reduction", ["ordered", "allreduce"])
-def test_rccl_collectives_one_rank(oracle_mod, monkeypatch, how, reduction):
+def test_rccl_collectives_one_rank(oracle_mod, how, reduction):
     """The RCCL branch (ncclCommInitRank, ncclBroadcast of the ordered
     reduction, ncclAllReduce) run on a one-rank communicator: with
-    HMC_FORCE_COLLECTIVES=1 a one-rank context executes every collective, so
+    hmc_set_force_collectives a one-rank context executes every collective, so
     the whole EM goes through RCCL on a one-GPU machine — LL, resolutions and
     the HaploComp log equal the restatement's."""
-    monkeypatch.setenv("HMC_FORCE_COLLECTIVES", "1")
     p = panel("a3miss5")
     if how == "unique_id":
         m = hmc_amd.HaploModel(device=0, rank=0, world=1, unique_id=hmc_amd.HaploModel.unique_id())
@@ -893,6 +898,7 @@ def test_rccl_collectives_one_rank(oracle_mod, monkeypatch, how, reduction):
     else:
         rccl, comm = _rccl_comm_one_rank()
         m = hmc_amd.HaploModel(device=0, rccl_comm=comm.value)
+    m.set_force_collectives(True)
     m.set_reduction(reduction)
     m.max_iteration = 10
     res = m.run(hmc_amd.GenoData.from_panel(p))
@@ -1091,6 +1097,32 @@ def test_exact_em_against_oracle(oracle_mod, name):
     assert m.iterations == r["iterations"]
     assert np.allclose([x["ll"] for x in m.log], r["ll"], rtol=1e-9, atol=0)
     assert np.mean(np.all(res == r["resolutions"], axis=(1, 2))) >= 0.99
+
+
+def test_exact_em_estep_after_store_shrink(oracle_mod):
+    """The E-step after an exact M-step (HaploModel.cpp:139-145) when HBM is
+    shorter than the stores the first E-step grew (cfg 3's OOM in round 3):
+    budgets cut to about an eighth of E1's trace make the stores give way to
+    the pass scratch and the E-step run in groups; E2 equals the run with
+    automatic budgets bit for bit (LL, R_E, totals, resolutions)."""
+    p = panel("n60")
+    runs = []
+    for shrink in (False, True):
+        m = gpu_model(p)
+        m.exact_estimate = True
+        m.find_patterns()
+        ll1, H1, re1 = m.resolve_all()
+        m.find_patterns()  # estimatePatterns
+        if shrink:
+            m.set_store_budgets(trace_bytes=max(1 << 16, re1 // 2), record_bytes=max(1 << 16, re1 // 2))
+        ll, H, re = m.resolve_all()
+        st = m.estep_split_stats()
+        runs.append((float(ll).hex(), H, re, m.estep_results()["total"].copy(), m.resolutions().copy(), st))
+        m.close()
+    (a, b) = runs
+    assert b[5]["structure_passes"] + b[5]["value_passes"] > a[5]["structure_passes"] + a[5]["value_passes"], (a[5], b[5])
+    assert a[:3] == b[:3]
+    assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
 
 
 # ------------------------------------------------ full-size chain digests

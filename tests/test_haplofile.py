@@ -157,20 +157,27 @@ def test_write_read_round_trip(tmp_path, fmt):
 
 
 @pytest.mark.gpu
-def test_write_patterns(tmp_path):
+@pytest.mark.parametrize("block", [0, 3])
+def test_write_patterns(tmp_path, block):
     """writePattern (.patterns): one line per pattern in id order with freq/N,
-    the length and the long-format alleles; checked against the table."""
+    the length and the long-format alleles; checked against the table.
+    block = 3: the search runs in blocks of 3 start loci, which leaves no
+    complete candidate tree — the strings come from the prefix ids."""
     p = synth.founder_mosaic(30, 20, A=2, seed=3)
     m = hmc_amd.HaploModel()
     m.load(hmc_amd.GenoData.from_panel(p))
+    if block:
+        m.set_mine_block(block)
     m.find_patterns()
+    if block:
+        assert m.mine_stats()["blocks"] > 1
     out = str(tmp_path / "x.patterns")
     assert hmc_amd.lib().hmc_write_patterns(m._h, out.encode()) == 0
     pt = m.patterns()
     lines = open(out).read().splitlines()
     assert lines[0].split("\t")[:2] == ["Frequency", "Length"]
     assert len(lines) == 1 + len(pt["start"])
-    for i in (0, len(lines) // 2, len(lines) - 2):
+    for i in list(range(0, len(lines) - 1, max(1, len(lines) // 40))) + [len(lines) - 2]:
         f, ln, al = lines[i + 1].split("\t")
         assert float(f) == pytest.approx(pt["freq"][i] / p.N, abs=5e-7) and int(ln) == pt["len"][i]
         v = [int(x) for x in al.split()]
