@@ -2553,15 +2553,26 @@ struct Ctx {
         int vipc = vp_ipc > 0 ? vp_ipc
                               : (small_heavy ? per_cu
                                              : (vnw == 1 ? 20 : (vnw >= 8 ? 2 : (vnw >= 4 ? 4 : 8))));  // a half-given shape completes by the same rule
-        const int G2 = std::max(1, std::min(waves > 0 ? waves : dev_cu * vipc, n));
-        // register budget: 5 waves per SIMD once the shape asks for more than 16 per CU
-        const int vwpe = vnw * vipc > 16 && vnw * vipc <= 20 ? 5 : 4;
         // the HBM tier of the value frontiers holds the group's largest
         // frontier (pass 1 measured it), not the structure pass's capacity
         int fgrp = 1;
         for (size_t q = 0; q < k; ++q) fgrp = std::max(fgrp, (int)fbig[sset[pos + q]]);
         fgrp = std::min(fcap, (fgrp + 63) & ~63);
-        const size_t per2 = estep_s2_scratch_bytes(fgrp, S);
+        // two links per lane (cfg 3: E1 values 2.68 -> 2.34 s, E2 ~3 % less)
+        const bool pair = !value_fast && S <= 16 && (value_pair == 2 || (value_pair == 1 && heavy));
+        // Dataflow value pass (estep_df.hip): one wave walks the loci and
+        // builds the lists, the others run the chains of adds of any open locus.
+        DfShape df;
+        const bool use_df = !value_fast && S <= 32 && (value_pass == VP_DATAFLOW || (value_pass == VP_AUTO && df_auto(heavy))) &&
+                            df_shape(S, pair, heavy, small_heavy, per_cu, fgrp, df);
+        if (use_df) {
+          vnw = df.nw;
+          vipc = df.ipc;
+        }
+        const int G2 = std::max(1, std::min(waves > 0 ? waves : dev_cu * vipc, n));
+        // register budget: 5 waves per SIMD once the shape asks for more than 16 per CU
+        const int vwpe = vnw * vipc > 16 && vnw * vipc <= 20 ? 5 : 4;
+        const size_t per2 = use_df ? estep_df_scratch_bytes(fgrp, S, df.R) : estep_s2_scratch_bytes(fgrp, S);
         const int grid2 = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::min<int>(G2, (int)k), SCRATCH_MAX / per2));
         if ((e = scratch_ensure(d_scr2, per2 * grid2, false))) return hipfail(e, "estep pass-2 scratch");
         if ((rc = ensure_store(d_trace, std::max<uint64_t>(t, 1), trace_budget, "trace store"))) return rc;
@@ -2576,9 +2587,7 @@ struct Ctx {
         v.scratch = d_scr2.p;
         v.scratch_stride = per2;
         v.fcap = fgrp;
-        // two links per lane (cfg 3: E1 values 2.68 -> 2.34 s, E2 ~3 % less)
-        const bool pair = !value_fast && S <= 16 && (value_pair == 2 || (value_pair == 1 && heavy));
-        v.lds_fc = s2_tier(S, vnw, vipc, pair);
+        v.lds_fc = use_df ? df.fc : s2_tier(S, vnw, vipc, pair);
         v.trace = d_trace.p;
         v.trace_cap = d_trace.n;
         v.trace_cursor = d_trace_cursor.p;
@@ -2598,7 +2607,13 @@ struct Ctx {
         if ((e = hipMemsetAsync(d_nextq.p + 1, 0, 4, st))) return hipfail(e, "estep");
         const bool fast = value_fast && S <= 32;  // lists longer than a wavefront: exact order only
         hipEventRecord(ev[0], st);
-        if ((e = launch_estep_values(v, grid2, vnw, fast, vwpe, st, pair))) return hipfail(e, "estep_values launch");
+        if (use_df) {
+          if ((e = launch_estep_values_df(v, grid2, vnw, vwpe, pair, df.R, df.qcap, st)))
+            return hipfail(e, "estep_values_df launch");
+        } else if ((e = launch_estep_values(v, grid2, vnw, fast, vwpe, st, pair))) {
+          return hipfail(e, "estep_values launch");
+        }
+        last_value_df = use_df;
         hipEventRecord(ev[1], st);
         if ((rc = read_status(sset, (int)k, true))) return rc;
         hipEventElapsedTime(&ms, ev[0], ev[1]);
@@ -2634,6 +2649,7 @@ struct Ctx {
           const int bi = sset[pos + q];
           if (h_status[bi] == EST_OVERFLOW_TRACE) return fail(HMC_EHIP, "trace store overflow with exact sizes");
           if (h_status[bi] == EST_NEEDS_ORDER) return fail(HMC_EHIP, "exact value pass reported a tie");
+          if (h_status[bi] == EST_DF_STALL) return fail(HMC_EHIP, "dataflow value pass stalled (individual %d)", i0 + bi);
           if (h_status[bi] == EST_NEEDS_EXACT) h_redo.push_back(bi);
         }
         // ---- exact fallback: individuals whose forward likelihood underflowed.
@@ -2751,6 +2767,38 @@ struct Ctx {
     hc = 16;
     cc = 0;
   }
+  // Shape of the dataflow value pass: waves per individual (one A wave, the
+  // rest B), individuals per CU, ring slots, queue slots, LDS states per slot.
+  // False when it cannot run (LDS for the flags and one slot's tier).
+  enum { VP_AUTO = 0, VP_CLASSIC = 1, VP_DATAFLOW = 2 };
+  int value_pass = VP_AUTO;  // hmc_set_value_pass
+  int df_ring = 3;
+  bool last_value_df = false;
+  struct DfShape {
+    int nw = 0, ipc = 0, R = 3, qcap = 64, fc = 0;
+  };
+  bool df_auto(bool heavy) const { (void)heavy; return false; }
+  bool df_shape(int S, bool pair, bool heavy, bool small_heavy, int per_cu, int fgrp, DfShape &d) const {
+    d.nw = vp_nw > 0 ? std::max(2, vp_nw) : (small_heavy ? std::max(2, 16 / per_cu) : (heavy ? 8 : 2));
+    d.ipc = vp_ipc > 0 ? vp_ipc : (small_heavy ? per_cu : (heavy ? 2 : 8));
+    if (d.nw * d.ipc > 20) d.ipc = std::max(1, 20 / d.nw);
+    d.R = df_ring;
+    const int G = pair ? WAVE / S : WAVE / (2 * S);
+    const int nseg = (d.nw - 1) * G;
+    d.qcap = 64;
+    while (d.qcap < std::max(4 * nseg, heavy ? 512 : 64)) d.qcap *= 2;
+    const int budget = 160 * 1024 / std::max(1, d.ipc) - 256;
+    if ((int)estep_df_lds_bytes(S, 0, d.nw, pair, d.R, d.qcap, fgrp) > budget) return false;
+    int lo = 0, hi = fgrp;  // largest LDS tier that fits
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) / 2;
+      if ((int)estep_df_lds_bytes(S, mid, d.nw, pair, d.R, d.qcap, fgrp) <= budget) lo = mid;
+      else hi = mid - 1;
+    }
+    d.fc = lo;
+    return true;
+  }
+
   // LDS tier of pass 2: states per frontier for the block's LDS share.
   static int s2_tier(int S, int nw, int ipc, bool pair = false) {
     const int budget = 160 * 1024 / std::max(1, ipc) - 256;
@@ -3290,6 +3338,19 @@ int hmc_last_exact_stats(const hmc_ctx *h, int *rounds, uint64_t *candidates, do
 int hmc_set_value_mode(hmc_ctx *h, int mode) {
   if (!h || mode < 0 || mode > 1) return HMC_EARG;  // 0: value-only + re-runs, 1: libstdc++ permutations
   h->c.value_fast = mode == 0;
+  return HMC_OK;
+}
+
+int hmc_set_value_pass(hmc_ctx *h, int mode, int ring) {
+  if (!h || mode < 0 || mode > 2 || ring < 0 || ring == 1 || ring == 2 || ring > 4) return HMC_EARG;
+  h->c.value_pass = mode;  // 0 automatic, 1 locus-synchronous (estep_values), 2 dataflow (estep_values_df)
+  h->c.df_ring = ring ? ring : 3;
+  return HMC_OK;
+}
+
+int hmc_last_value_pass(const hmc_ctx *h, int *dataflow) {
+  if (!h) return HMC_EARG;
+  if (dataflow) *dataflow = h->c.last_value_df ? 1 : 0;
   return HMC_OK;
 }
 

@@ -1,0 +1,667 @@
+// estep_df.hip — the value pass of the split E-step as a dataflow over loci.
+//
+// estep_values (estep_split.hip) replays each locus's structure record in two
+// phases with a block barrier after each: every state's constructor and the
+// appends that still fit (phase A, a thread per state), then the adds that
+// overflow S as chains of selections on lane segments (phase B).  A locus
+// therefore ends on its longest chain while the other segments idle (cfg 3's
+// E1: 6.8 selection steps per locus on the critical path against 4.7 of work
+// per segment; its E2: 11 steps, most segments idle).  A state's list only
+// depends on its predecessors' final lists (HaploPair.cpp:35-89), so here the
+// block's waves run different loci at once:
+//
+//   A (wave 0) walks the loci in order.  A lane takes a state of the current
+//     locus — the chains first, longest first (the record's chain list), then
+//     the other states — and, once every predecessor it reads is final (one
+//     bit per state of the previous locus), builds the state's list exactly as
+//     phase A does: the ordered forward sum, the extension constructor and the
+//     appends that fit.  A list that is complete is final at once; a chain's
+//     state goes to the chain queue.
+//   B (waves 1..NW-1) cut into segments of S lanes (two links per lane) or 2S
+//     lanes; a segment takes the next chain from the queue, whatever its locus,
+//     and runs its adds with the libstdc++-exact segmented selection
+//     (coop_select.hpp), then marks the state final.
+//
+// Locus j's frontier lives in ring slot j % R (R >= 3).  A opens locus j only
+// when locus j-R+1 — the last reader of the slot's previous occupant, locus
+// j-R — is complete, so A runs up to R-2 loci ahead of the oldest open chain.
+// Every list is built by the same operations in the same order as in
+// estep_values, so the frontiers, the trace store and the results are
+// identical; only the interleaving across states changes.
+//
+// Queue: a ring of `qcap` words in LDS.  B segments take tickets (an LDS
+// counter); A writes the entry of ticket t into slot t % qcap once the slot is
+// empty, tagged with the lap t / qcap so a segment never takes an entry of
+// another lap.  After the last locus (or an abort) A queues one END entry per
+// segment, so every ticket taken is served and the queue is empty again.
+#include "hmc_internal.hpp"
+#include "select.hpp"
+#include "coop_select.hpp"
+#include "estep_common.hpp"
+#include "value_front.hpp"
+
+namespace hmc {
+
+namespace {
+
+constexpr int DF_RMAX = 4;
+constexpr uint32_t QE_VALID = 1u << 31, QE_END = 1u << 30;
+constexpr int QE_LAP = 24;   // bits 24..29: ticket lap
+constexpr int QE_SLOT = 21;  // bits 21..23: ring slot; 0..20 state
+// Watchdog: a wait that polls this often without progress (~10^8 cycles, far
+// beyond any chain) means a broken invariant; the block then stops the
+// individual with EST_DF_STALL instead of spinning forever.
+constexpr int DF_SPIN_MAX = 1 << 22;
+constexpr int DF_STALL = 2;  // DfShared::abort value
+
+struct DfRing {
+  unsigned long long rec;  // word offset of the locus's structure record
+  unsigned long long tr;   // word offset of its trace record
+  int F;
+  int done;  // states whose lists are final
+};
+
+struct DfShared {
+  DfRing ring[DF_RMAX];
+  int q_head;  // tickets taken by the B segments
+  int abort;   // A stopped the individual (underflow, trace store full)
+  int status;  // the individual's status for the final selection
+  int q;       // next individual (block broadcast)
+};
+
+struct DfPlan {
+  int o_lpos, o_rpos, o_junk, o_slik, o_smeta, o_sh, o_queue, o_ascr, o_flags, o_front;
+  int front_stride, flag_words, bytes;
+  int R, qcap, qlog, G, sws;  // ring slots, queue slots (2^qlog), segments per B wave, selection slots per B wave
+};
+
+__host__ __device__ inline int df_slots(int S, bool pair) {
+  return pair ? (WAVE / S + 1) * 2 * S : (2 * S > WAVE ? 2 * S : WAVE);
+}
+
+// nb: B waves; fc: LDS states per ring slot; fcap: states per slot (HBM tier
+// size, and the flag bits)
+__host__ __device__ inline DfPlan df_plan(int S, int fc, int nb, bool pair, int R, int qcap, int fcap) {
+  DfPlan p;
+  int o = 0;
+  auto take = [&](int bytes) { int r = o; o += (bytes + 15) & ~15; return r; };
+  const int sl = df_slots(S, pair), pos = pair ? sl : WAVE;
+  p.o_lpos = take(nb * pos * 4);
+  p.o_rpos = take(nb * pos * 4);
+  p.o_junk = take(nb * (pair ? 4 : 2) * WAVE * 4);
+  p.o_slik = take(nb * sl * 8);
+  p.o_smeta = take(nb * sl * 4);
+  p.o_sh = take((int)sizeof(DfShared));
+  p.o_queue = take(qcap * 4);
+  p.o_ascr = take(WAVE * 4);
+  p.flag_words = (fcap + 31) / 32;
+  p.o_flags = take(R * p.flag_words * 4);
+  p.front_stride = (fc * (16 + 12 * S) + 15) & ~15;
+  p.o_front = take(R * p.front_stride);
+  p.bytes = o;
+  p.R = R;
+  p.qcap = qcap;
+  p.qlog = 0;
+  while ((1 << p.qlog) < qcap) ++p.qlog;
+  p.G = pair ? WAVE / S : WAVE / (2 * S);
+  p.sws = sl;
+  return p;
+}
+
+__device__ inline int ld_vol(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ inline uint32_t ld_vol(const uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ inline void st_vol(uint32_t *p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ inline void rel_wg() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
+__device__ inline void acq_wg() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); }
+
+}  // namespace
+
+size_t estep_df_lds_bytes(int S, int fc, int nw, bool pair, int R, int qcap, int fcap) {
+  return (size_t)df_plan(S, fc, nw - 1, pair, R, qcap, fcap).bytes;
+}
+size_t estep_df_scratch_bytes(int fcap, int S, int R) { return (size_t)R * k2_front_bytes(fcap, S); }
+
+// WPE: resident waves per SIMD of the register allocation (4 or 5).  PAIR:
+// segments of S lanes with two links per lane (S <= 16), else 2S lanes (S <= 32).
+template <int WPE, bool PAIR>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) void estep_values_df(ValueArgs a,
+                                                                                                DfPlan plan) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int S = a.S, L = a.L, hl = a.head_len;
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;
+  const int NW = blockDim.x / WAVE, NB = NW - 1;
+  const int R = plan.R, qcap = plan.qcap;
+  DfShared *sh = (DfShared *)(smem + plan.o_sh);
+  uint32_t *queue = (uint32_t *)(smem + plan.o_queue);
+  int *ascr = (int *)(smem + plan.o_ascr);
+  const int qmask = qcap - 1, qlog = plan.qlog;
+  char *sp = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
+  const size_t hbm_slot = k2_front_bytes(a.fcap, S);
+  auto front = [&](int slot) {
+    return VFront{smem + plan.o_front + (size_t)slot * plan.front_stride, (unsigned char *)sp + (size_t)slot * hbm_slot,
+                  a.lds_fc, a.fcap, S};
+  };
+  auto flags = [&](int slot) { return (uint32_t *)(smem + plan.o_flags) + (size_t)slot * plan.flag_words; };
+  // B waves: the selection layout of estep_values
+  const int bw = wv - 1;
+  const int sws = plan.sws;
+  const int sps = PAIR ? sws : WAVE;
+  const int bo = bw < 0 ? 0 : bw;
+  const SegScratch ss{(int *)(smem + plan.o_lpos) + bo * sps, (int *)(smem + plan.o_rpos) + bo * sps,
+                      (int *)(smem + plan.o_junk) + bo * (PAIR ? 4 : 2) * WAVE, (double *)(smem + plan.o_slik) + bo * sws,
+                      (uint32_t *)(smem + plan.o_smeta) + bo * sws};
+  const Seg sg = make_seg(PAIR ? S : 2 * S);
+  const int G = plan.G;
+  const int nseg = NB * G;
+  const int sb = sg.g * 2 * S;
+  const LinkList W{(double *)(smem + plan.o_slik), (uint32_t *)(smem + plan.o_smeta), 1};  // final selection
+
+  for (int i = tid; i < qcap; i += blockDim.x) queue[i] = 0u;
+  __syncthreads();
+  auto next_q = [&]() -> int {
+    __syncthreads();
+    if (tid == 0) sh->q = atomicAdd(a.next_q, 1) + (int)gridDim.x;
+    __syncthreads();
+    return sh->q;
+  };
+  for (int q = blockIdx.x; q < a.n_order; q = next_q()) {
+    const int bi = a.order[q];
+    const unsigned long long t_indiv = __builtin_amdgcn_s_memtime();
+    int status0 = a.status[bi];
+    if (status0 == EST_NEEDS_ORDER) status0 = EST_OK;  // the re-run of a value-only pass
+    if (status0 != EST_OK) {
+      if (tid == 0) {
+        a.total[bi] = 0.0;
+        a.ncand[bi] = 0;
+        a.cost[bi] = 0;
+      }
+      continue;
+    }
+    const unsigned long long *roff = a.rec_off + (size_t)bi * (L + 1);
+    if (tid == 0) {
+      sh->q_head = 0;
+      sh->abort = 0;
+      sh->status = EST_OK;
+    }
+    __syncthreads();
+
+    if (wv == 0) {
+      // ================================================================ A ====
+      unsigned long long tcur = a.trace_base[bi];
+      int status = EST_OK;
+      uint32_t qtail = 0;  // tickets queued (wave-uniform)
+      // queue `npush` entries from the lanes where `push` holds, in lane order
+      auto enqueue = [&](bool push, uint32_t entry) {
+        const uint64_t m = wave_ballot(push);
+        if (!m) return;
+        if (push) {
+          const uint32_t t = qtail + (uint32_t)__popcll(m & lanemask_lt());
+          uint32_t *slot = queue + (t & (uint32_t)qmask);
+          int guard = 0;
+          while (ld_vol(slot) != 0u) {  // ticket t - qcap not taken yet
+            if (++guard > DF_SPIN_MAX || ld_vol(&sh->abort) == DF_STALL) {
+              atomicExch(&sh->abort, DF_STALL);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (ld_vol(&sh->abort) != DF_STALL) st_vol(slot, entry | QE_VALID | ((t >> qlog) & 63u) << QE_LAP);
+        }
+        qtail += (uint32_t)__popcll(m);
+      };
+      // locus j into ring slot j % R: ring info, trace record, flags cleared
+      auto open_locus = [&](int j) -> bool {
+        const int b = j % R;
+        const uint32_t *Rj = a.rec + roff[j];
+        const int F = (int)Rj[0];
+        const unsigned long long words = trace_locus_words((unsigned long long)F, S);
+        const unsigned long long off = tcur;
+        tcur += words;
+        if (off + words > a.trace_cap) return false;
+        uint32_t *fl = flags(b);
+        for (int w = lane; w < (F + 31) / 32; w += WAVE) fl[w] = 0u;
+        if (lane == 0) {
+          DfRing &g = sh->ring[b];
+          g.rec = roff[j];
+          g.tr = off;
+          g.F = F;
+          g.done = 0;
+          a.trace[off] = (uint32_t)F;
+          a.loc_off[(size_t)bi * (L + 1) + j] = off;
+        }
+        wave_lds_sync();
+        return true;
+      };
+      // ---- head list (HaploPair.cpp:14-33) ---------------------------------
+      if (!open_locus(hl)) {
+        status = EST_OVERFLOW_TRACE;
+      } else {
+        const int b = hl % R;
+        const uint32_t *Rh = a.rec + roff[hl];
+        const int F = (int)Rh[0];
+        const double *Rtp = (const double *)(Rh + 4);
+        const uint32_t *Rhd = Rh + 4 + 2 * F;
+        const VFront Y = front(b);
+        const unsigned long long off = sh->ring[b].tr;
+        uint32_t *thd = a.trace + off + 1, *tln = a.trace + trace_links(off, (uint32_t)F);
+        for (int t = lane; t < F; t += WAVE) {
+          const bool homo = (Rhd[t] >> 24) & 1u;
+          const double tpv = Rtp[t];
+          const uint32_t mw = meta_pack(0, 0, false, homo, true);
+          *Y.fwd(t) = homo ? tpv : tpv * 2.0;
+          Y.lik(t)[0] = tpv;
+          Y.meta(t)[0] = mw;
+          *Y.nl(t) = 1;
+          thd[t] = (Rhd[t] & 0xFFFFu) | 1u << 16;
+          uint32_t *tl = tln + (size_t)t * S;
+          tl[0] = mw;
+          for (int k = 1; k < S; ++k) tl[k] = 0u;
+        }
+        rel_wg();
+        uint32_t *fl = flags(b);
+        for (int w = lane; w < (F + 31) / 32; w += WAVE) {
+          const int nb = F - 32 * w;
+          st_vol(fl + w, nb >= 32 ? ~0u : ((1u << nb) - 1u));
+        }
+        if (lane == 0) atomicAdd(&sh->ring[b].done, F);
+      }
+      // ---- forward over loci ------------------------------------------------
+      for (int j = hl + 1; j <= L && status == EST_OK; ++j) {
+        // the slot's previous occupant, locus j - R, must be complete (its last
+        // chains write into the slot) and so must its readers, locus j - R + 1
+        for (int jg = j - R; jg <= j - R + 1; ++jg) {
+          if (jg < hl) continue;
+          const DfRing *g = &sh->ring[jg % R];
+          int guard = 0;
+          while (ld_vol(&g->done) != ld_vol(&g->F)) {
+            if (++guard > DF_SPIN_MAX || ld_vol(&sh->abort) == DF_STALL) {
+              if (lane == 0) atomicExch(&sh->abort, DF_STALL);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+        }
+        if (ld_vol(&sh->abort) == DF_STALL) {
+          status = EST_DF_STALL;
+          break;
+        }
+        if (!open_locus(j)) {
+          status = EST_OVERFLOW_TRACE;
+          break;
+        }
+        const int b = j % R, bx = (j - 1) % R;
+        const VFront X = front(bx), Y = front(b);
+        const uint32_t *xfl = flags(bx);
+        uint32_t *yfl = flags(b);
+        const uint32_t *Rj = a.rec + roff[j];
+        const int F = (int)Rj[0], C = (int)Rj[1], NCH = (int)Rj[2];
+        const double *Rtp = (const double *)(Rj + 4);
+        const uint32_t *Rhd = Rj + 4 + 2 * F, *Rcb = Rhd + F, *Rct = Rcb + F + 1, *Rch = Rct + C;
+        const unsigned long long toff = sh->ring[b].tr;
+        uint32_t *thd = a.trace + toff + 1, *tln = a.trace + trace_links(toff, (uint32_t)F);
+        int st = -1, rchk = 0;   // this lane's state, its first contribution not known to be final
+        int nextc = 0, scan = 0;  // next chain position, next candidate of the sweep over the others
+        bool underflow = false;
+        int idle = 0;  // iterations in a row without a ready state (watchdog)
+        while (true) {
+          // ---- free lanes take states: chains first (longest first), then the rest
+          uint64_t fm = wave_ballot(st < 0);
+          if (fm && nextc < NCH) {
+            const int rk = __popcll(fm & lanemask_lt());
+            const int nt = min(__popcll(fm), NCH - nextc);
+            if (st < 0 && rk < nt) {
+              st = (int)Rch[nextc + rk];
+              rchk = (int)Rcb[st];
+            }
+            nextc += nt;
+            fm = wave_ballot(st < 0);
+          }
+          if (fm && nextc >= NCH && scan < F) {
+            const int t = scan + lane;
+            const bool cand = t < F && !(Rhd[t < F ? t : 0] & HDR_CHAIN);
+            const uint64_t cm = wave_ballot(cand);
+            const int nc = __popcll(cm), nt = min(__popcll(fm), nc);
+            if (cand) ascr[__popcll(cm & lanemask_lt())] = t;
+            wave_lds_sync();
+            const int rk = __popcll(fm & lanemask_lt());
+            if (st < 0 && rk < nt) {
+              st = ascr[rk];
+              rchk = (int)Rcb[st];
+            }
+            scan = nt < nc ? ascr[nt] : scan + WAVE;
+            wave_lds_sync();
+          }
+          const uint64_t held = wave_ballot(st >= 0);
+          if (!held) {
+            if (nextc >= NCH && scan >= F) break;
+            if (++idle > DF_SPIN_MAX) {
+              status = EST_DF_STALL;
+              break;
+            }
+            continue;
+          }
+          // ---- readiness: every predecessor this state reads is final
+          bool ready = false;
+          if (st >= 0) {
+            const int ce = (int)Rcb[st + 1];
+            int r = rchk;
+            while (r < ce) {
+              const uint32_t p = cw_state(Rct[r]);
+              if (!((ld_vol(xfl + (p >> 5)) >> (p & 31u)) & 1u)) break;
+              ++r;
+            }
+            rchk = r;
+            ready = r == ce;
+          }
+          if (!wave_ballot(ready)) {
+            if (++idle > DF_SPIN_MAX || ld_vol(&sh->abort) == DF_STALL) {
+              status = EST_DF_STALL;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+          }
+          idle = 0;
+          acq_wg();
+          // ---- phase A of estep_values for the ready states: the extension
+          // constructor (HaploPair.cpp:35-61), the appends that fit (:63-84)
+          // and the ordered forward sum (:42, :66)
+          bool chain = false, fin = false;
+          if (ready) {
+            const int t = st;
+            const double tpv = Rtp[t];
+            const uint32_t hd = Rhd[t];
+            const bool differ = (hd & 0xFFu) != ((hd >> 8) & 0xFFu);
+            const int cb = (int)Rcb[t], ce = (int)Rcb[t + 1];
+            double fwd = 0.0;
+            for (int rb = cb; rb < ce; rb += 4) {
+              uint32_t ws[4];
+              double fs[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) ws[u] = rb + u < ce ? Rct[rb + u] : Rct[cb];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) fs[u] = *X.fwd((int)cw_state(ws[u]));
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                if (rb + u < ce) {
+                  const double v = fs[u] * tpv;
+                  fwd = rb + u == cb ? v : fwd + v;
+                }
+            }
+            uint32_t w = Rct[cb];
+            uint32_t s = cw_state(w), ns = cw_ns(w);
+            double *yl = Y.lik(t);
+            uint32_t *ym = Y.meta(t);
+            uint32_t *tl = tln + (size_t)t * S;
+            copy_extended<4>(X.lik((int)s), X.meta((int)s), yl, ym, 0, (int)ns, s, tpv, cw_rev(w), differ, tl);
+            int k = (int)ns, r0 = ce;
+            for (int r = cb + 1; r < ce; ++r) {
+              w = Rct[r];
+              s = cw_state(w);
+              ns = cw_ns(w);
+              if (k + (int)ns <= S) {
+                copy_extended<4>(X.lik((int)s), X.meta((int)s), yl, ym, k, (int)ns, s, tpv, cw_rev(w), differ, tl);
+                k += (int)ns;
+              } else {
+                r0 = r;
+                break;
+              }
+            }
+            if (r0 == ce)
+              for (int qq = k; qq < S; ++qq) tl[qq] = 0u;
+            thd[t] = (hd & 0xFFFFu) | (uint32_t)k << 16;
+            *Y.fwd(t) = fwd;
+            *Y.nl(t) = (uint32_t)k;
+            *Y.r0(t) = (uint32_t)r0;
+            if (!(fwd > 0.0) && j < L) underflow = true;
+            chain = r0 < ce;
+            fin = !chain;
+          }
+          rel_wg();
+          if (fin) atomicOr(yfl + (st >> 5), 1u << (st & 31));
+          const int nfin = __popcll(wave_ballot(fin));
+          if (lane == 0 && nfin) atomicAdd(&sh->ring[b].done, nfin);
+          enqueue(chain, (uint32_t)b << QE_SLOT | (uint32_t)(chain ? st : 0));
+          if (ready) st = -1;
+          if (wave_ballot(underflow)) {
+            status = EST_NEEDS_EXACT;
+            break;
+          }
+          if (ld_vol(&sh->abort) == DF_STALL) {
+            status = EST_DF_STALL;
+            break;
+          }
+        }
+      }
+      // END for every B segment: each has taken, or will take, one more ticket
+      if (status == EST_DF_STALL && lane == 0) atomicExch(&sh->abort, DF_STALL);
+      if (lane == 0) {
+        sh->status = status;
+        if (status != EST_OK) atomicCAS(&sh->abort, 0, 1);
+      }
+      if (status != EST_DF_STALL)
+        for (int e = 0; e < nseg; e += WAVE) enqueue(e + lane < nseg, QE_END);
+      if (ld_vol(&sh->abort) == DF_STALL && lane == 0) sh->status = EST_DF_STALL;
+    } else {
+      // ================================================================ B ====
+      // a segment's chain: ring slot, state, next add r of [r, re_), list
+      // length k0 before the add, link words of adds r and r + 1
+      int ticket = -1, cs = 0, st = 0, r = 0, re_ = 0, k0 = 0;
+      bool have = false, done = sg.g >= G;
+      double tpv = 0.0;
+      bool differ = false;
+      uint32_t wc = 0, wn = 0;
+      double *slot_l = ss.slik + sb + sg.k;
+      uint32_t *slot_m = ss.smeta + sb + sg.k;
+      int idle = 0;  // iterations in a row with no segment at work (watchdog)
+      while (true) {
+        if (ld_vol(&sh->abort) == DF_STALL) break;
+        const bool want = !done && !have;
+        if (wave_ballot(want)) {
+          int tk = ticket;
+          if (want && sg.k == 0 && tk < 0) tk = atomicAdd(&sh->q_head, 1);
+          tk = __shfl(tk, sg.base);
+          uint32_t e = 0u;
+          if (want && sg.k == 0) e = ld_vol(queue + (tk & qmask));
+          e = __shfl(e, sg.base);
+          ticket = want ? tk : ticket;
+          const bool got = want && (e & QE_VALID) && ((e >> QE_LAP) & 63u) == (((uint32_t)tk >> qlog) & 63u);
+          if (got) {
+            if (sg.k == 0) st_vol(queue + (tk & qmask), 0u);  // only the segment's first lane read it
+            acq_wg();
+            ticket = -1;
+            if (e & QE_END) {
+              done = true;
+            } else {
+              cs = (int)((e >> QE_SLOT) & 7u);
+              st = (int)(e & F_MASK);
+              const DfRing &g = sh->ring[cs];
+              const uint32_t *Rj = a.rec + g.rec;
+              const int F = g.F;
+              const double *Rtp = (const double *)(Rj + 4);
+              const uint32_t *Rhd = Rj + 4 + 2 * F, *Rcb = Rhd + F, *Rct = Rcb + F + 1;
+              const VFront Y = front(cs);
+              r = (int)*Y.r0(st);
+              re_ = (int)Rcb[st + 1];
+              tpv = Rtp[st];
+              const uint32_t hd = Rhd[st];
+              differ = (hd & 0xFFu) != ((hd >> 8) & 0xFFu);
+              k0 = (int)*Y.nl(st);
+              wc = Rct[r];
+              wn = r + 1 < re_ ? Rct[r + 1] : 0u;
+              if (sg.k < k0) {
+                *slot_l = Y.lik(st)[sg.k];
+                *slot_m = Y.meta(st)[sg.k];
+              }
+              have = true;
+            }
+          }
+        }
+        if (!wave_ballot(have)) {
+          if (!wave_ballot(!done)) break;
+          if (++idle > DF_SPIN_MAX) {
+            if (lane == 0) {
+              atomicExch(&sh->abort, DF_STALL);
+              sh->status = EST_DF_STALL;
+            }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+          continue;
+        }
+        idle = 0;
+        int n = 0;
+        if (have) {
+          const VFront X = front((cs + R - 1) % R);
+          const uint32_t s = cw_state(wc), ns = cw_ns(wc);
+          const bool rev = cw_rev(wc);
+          n = k0 + (int)ns;
+          // HaploPair::add transformation (HaploPair.cpp:63-80)
+          auto extend = [&](int kk) {
+            const int qk = kk - k0;
+            double lk;
+            uint32_t pm;
+            X.ld_link((int)s, qk, lk, pm);
+            lk *= tpv;
+            bool homo = meta_homo(pm);
+            if (differ && homo) {
+              if (rev) lk = 0.0;
+              homo = false;
+            }
+            slot_l[kk - sg.k] = lk;
+            slot_m[kk - sg.k] = meta_pack(s, (uint32_t)qk, rev, homo, false);
+          };
+          if (sg.k >= k0 && sg.k < n) extend(sg.k);
+          if (PAIR && sg.k + S >= k0 && sg.k + S < n) extend(sg.k + S);
+          wc = wn;
+          if (r + 2 < re_) {
+            const DfRing &g = sh->ring[cs];
+            const uint32_t *Rj = a.rec + g.rec;
+            const int F = g.F;
+            wn = (Rj + 4 + 2 * F + F + F + 1)[r + 2];
+          } else {
+            wn = 0u;
+          }
+        }
+        wave_lds_sync();
+        if (PAIR) seg2_nth_slots(n, S - 1, sg, ss);
+        else seg_nth_slots(n, S - 1, sg, ss);
+        if (have) {
+          k0 = S;
+          if (++r == re_) {  // the chain's list is final
+            const DfRing &g = sh->ring[cs];
+            const VFront Y = front(cs);
+            const uint32_t *Rj = a.rec + g.rec;
+            const int F = g.F;
+            const uint32_t *Rhd = Rj + 4 + 2 * F;
+            uint32_t *tl = a.trace + trace_links(g.tr, (uint32_t)F) + (size_t)st * S;
+            if (sg.k < S) {
+              Y.lik(st)[sg.k] = *slot_l;
+              Y.meta(st)[sg.k] = *slot_m;
+              tl[sg.k] = *slot_m;
+            }
+            if (sg.k == 0) {
+              *Y.nl(st) = (uint32_t)S;
+              a.trace[g.tr + 1 + st] = (Rhd[st] & 0xFFFFu) | (uint32_t)S << 16;
+            }
+            rel_wg();
+            wave_lds_sync();  // the segment's stores are all issued before its flag
+            if (sg.k == 0) {
+              atomicOr(flags(cs) + (st >> 5), 1u << (st & 31));
+              atomicAdd(&sh->ring[cs].done, 1);
+            }
+            have = false;
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- final selection (HaploBuilder.cpp:87-116) ------------------------
+    if (tid == 0) {
+      a.cost[bi] = (int32_t)((__builtin_amdgcn_s_memtime() - t_indiv) >> 10);
+      int status = sh->status;
+      int cnt = 0;
+      double total = 0.0;
+      const VFront X = front(L % R);
+      const int Fp = sh->ring[L % R].F;
+      if (status == EST_OK) {
+        for (int t = 0; t < Fp; ++t) {
+          total += *X.fwd(t);
+          const uint32_t n = *X.nl(t);
+          for (uint32_t k = 0; k < n; ++k) {
+            double lk = X.lik(t)[k];
+            const bool homo = meta_homo(X.meta(t)[k]);
+            if (!homo) lk *= 2.0;
+            W.set(cnt++, lk, meta_pack((uint32_t)t, k, false, homo, false));
+          }
+          if (cnt > S) {
+            if (cnt <= 32) nth_element_greater_masks(W, cnt, S - 1, cnt);
+            else nth_element_greater(W, cnt, S - 1);
+            cnt = S;
+          }
+        }
+        sort_greater(W, cnt, (int *)(smem + plan.o_lpos));
+      }
+      a.status[bi] = status;
+      if (status == EST_OK) {
+        double coverage = 0.0;
+        for (int c = 0; c < cnt; ++c) {
+          const uint32_t mm = W.m(c);
+          const uint32_t t = meta_pred(mm), k = meta_idx(mm);
+          const double own = X.lik((int)t)[k];
+          const double prior = meta_homo(mm) ? own : own * 2.0;  // HaploPair.cpp:97-102
+          const double post = prior / total;
+          coverage += post;
+          a.cand_state[(size_t)bi * S_MAX + c] = t;
+          a.cand_idx[(size_t)bi * S_MAX + c] = k;
+          a.prior[(size_t)bi * S_MAX + c] = prior;
+          a.posterior[(size_t)bi * S_MAX + c] = post;
+        }
+        for (int c = 0; c < cnt; ++c)  // HaploModel.cpp:97-98
+          a.weight[(size_t)bi * S_MAX + c] = a.posterior[(size_t)bi * S_MAX + c] / coverage;
+      } else {
+        cnt = 0;
+      }
+      a.total[bi] = total;
+      a.ncand[bi] = cnt;
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_estep_values_df(const ValueArgs &a, int grid, int nw, int wpe, bool pair, int R, int qcap,
+                                  hipStream_t st) {
+  const int G = pair ? WAVE / a.S : WAVE / (2 * a.S);
+  if (a.S < 1 || a.S > 32 || (pair && a.S > 16) || nw < 2 || nw > 16 || (wpe != 4 && wpe != 5) || R < 3 ||
+      R > DF_RMAX || qcap < 64 || (qcap & (qcap - 1)) || qcap > 4096 || qcap < (nw - 1) * G || !a.trace_base ||
+      a.fcap > F_MAX || a.lds_fc < 0 || a.lds_fc > a.fcap)
+    return hipErrorInvalidValue;
+  const DfPlan plan = df_plan(a.S, a.lds_fc, nw - 1, pair, R, qcap, a.fcap);
+  const size_t lds = (size_t)plan.bytes;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  static size_t lds_attr = 0;
+  if (lds > 65536 && lds > lds_attr) {
+    for (const void *f : {(const void *)estep_values_df<4, true>, (const void *)estep_values_df<4, false>,
+                          (const void *)estep_values_df<5, true>, (const void *)estep_values_df<5, false>}) {
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    lds_attr = lds;
+  }
+  const dim3 g(grid), b(WAVE * nw);
+  if (pair) {
+    if (wpe == 5) hipLaunchKernelGGL((estep_values_df<5, true>), g, b, lds, st, a, plan);
+    else hipLaunchKernelGGL((estep_values_df<4, true>), g, b, lds, st, a, plan);
+  } else {
+    if (wpe == 5) hipLaunchKernelGGL((estep_values_df<5, false>), g, b, lds, st, a, plan);
+    else hipLaunchKernelGGL((estep_values_df<4, false>), g, b, lds, st, a, plan);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace hmc

@@ -46,6 +46,10 @@ __host__ __device__ inline uint32_t hdr_pack(uint32_t al_a, uint32_t al_b, uint3
   return (al_a & 0xFFu) | ((al_b & 0xFFu) << 8) | ((n & 0xFFu) << 16);
 }
 
+// Structure-record header word of a state (estep_split.hip): bit 27 marks a
+// state whose adds overflow S (a chain of selections in the value pass).
+constexpr uint32_t HDR_CHAIN = 1u << 27;
+
 // E-step status codes written per individual.
 enum EStatus : int32_t {
   EST_OK = 0,
@@ -55,6 +59,7 @@ enum EStatus : int32_t {
   EST_NO_HEAD_PATTERN = -3,    // "Can not find matching pattern!" (HaploBuilder.cpp:215-217)
   EST_OVERFLOW_REC = -4,       // structure-record store exhausted (split E-step)
   EST_OVERFLOW_CONTRIB = -5,   // more contributions at a locus than the structure pass's capacity
+  EST_DF_STALL = -6,           // dataflow value pass: a wait made no progress (watchdog; a bug, reported)
   EST_NEEDS_EXACT = 2,         // split E-step: a forward likelihood underflowed to 0 before
                                // the last locus, so extend() would skip that pair
                                // (HaploBuilder.cpp:237) — re-run on the fused kernel
@@ -228,6 +233,13 @@ hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStre
 // wpe: 4 or 5 resident waves per SIMD (register budget of the instantiation)
 hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, int wpe, hipStream_t st,
                                bool pair = false);
+// Dataflow value pass (estep_df.hip): one A wave + nw-1 B waves per
+// individual, a ring of R >= 3 frontiers, a chain queue of qcap (power of two)
+// slots.  S <= 32 (pair: S <= 16), exact order only, trace_base required.
+size_t estep_df_lds_bytes(int S, int fc, int nw, bool pair, int R, int qcap, int fcap);
+size_t estep_df_scratch_bytes(int fcap, int S, int R);
+hipError_t launch_estep_values_df(const ValueArgs &a, int grid, int nw, int wpe, bool pair, int R, int qcap,
+                                  hipStream_t st);
 hipError_t launch_traceback(const TracebackArgs &a, int total_cands, hipStream_t st);
 hipError_t launch_transpose_rows_u8(const uint8_t *in, const int32_t *rowmap, uint8_t *out, int rows, int cols,
                                     hipStream_t st);

@@ -246,6 +246,17 @@ class HaploModel:
         are identical."""
         self._check(lib().hmc_set_value_layout(self._h, mode))
 
+    def set_value_pass(self, mode: str, ring: int = 0):
+        """Value-pass schedule (hmc_set_value_pass): "auto", "classic" (locus
+        by locus) or "dataflow"; ring = frontiers kept by the dataflow pass
+        (3 or 4, 0 = 3).  Results are identical."""
+        self._check(lib().hmc_set_value_pass(self._h, {"auto": 0, "classic": 1, "dataflow": 2}[mode], int(ring)))
+
+    def last_value_pass_dataflow(self) -> bool:
+        d = C.c_int()
+        self._check(lib().hmc_last_value_pass(self._h, C.byref(d)))
+        return bool(d.value)
+
     # ----------------------------------------------------------------- panel
     def load(self, genos: GenoData):
         a = np.ascontiguousarray(genos.alleles, dtype=np.int32)

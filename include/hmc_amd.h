@@ -344,6 +344,16 @@ int hmc_set_value_mode(hmc_ctx *ctx, int mode);
  * genotype-mined model: many chains of adds per locus); 2 (default): every
  * group. */
 int hmc_set_value_layout(hmc_ctx *ctx, int mode);
+/* Schedule of the value pass (results identical): 1 = locus by locus (every
+ * state's constructor and appends, a block barrier, the chains of adds, a
+ * barrier); 2 = dataflow (one wavefront builds the lists in locus order as
+ * soon as a state's predecessors are final, the others run the chains of
+ * adds of any open locus; `ring` = frontiers kept, 3 or 4, 0 = 3); 0
+ * (default) = automatic.  The same HaploPair::add sequence per state
+ * (HaploPair.cpp:35-89) either way. */
+int hmc_set_value_pass(hmc_ctx *ctx, int mode, int ring);
+/* 1 when the last value-pass launch ran the dataflow schedule. */
+int hmc_last_value_pass(const hmc_ctx *ctx, int *dataflow);
 /* Individuals the last E-step re-ran with the libstdc++ permutations (mode 0)
  * and the device time of those re-runs (ms, part of values_ms). */
 int hmc_last_estep_order(const hmc_ctx *ctx, int *n_rerun, double *rerun_ms);

@@ -180,6 +180,47 @@ def test_value_one_link_layout(oracle_mod, name, S, shape):
     assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
 
 
+@pytest.mark.parametrize("name,S,shape,ring", [
+    ("a3miss5", 10, None, 3), ("a3miss5", 10, None, 4), ("n300", 10, None, 3), ("a8", 10, None, 3),
+    ("n60", 10, None, 3), ("a3miss5", 3, None, 3), ("a3miss5", 1, None, 3), ("a3miss5", 16, None, 4),
+    ("a3miss5", 17, None, 3), ("a8", 24, None, 3), ("a3miss5", 32, None, 4),
+    ("a3miss5", 10, (0, 0, 8, 2), 3), ("n300", 10, (0, 0, 3, 4), 3), ("a3miss5", 5, (0, 0, 16, 1), 4),
+    ("a8", 10, (0, 0, 2, 10), 3)])
+def test_dataflow_value_pass(oracle_mod, name, S, shape, ring):
+    """hmc_set_value_pass(dataflow): one wavefront builds the lists locus by
+    locus as soon as a state's predecessors are final, the others run the
+    chains of adds of any open locus (estep_df.hip) — the E-step on the M0
+    model equals HaploModel::resolveAll bit for bit, for sample sizes with two
+    links per lane (S <= 16) and one (17..32), ring of 3 or 4 frontiers, 2 to
+    16 waves per individual."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=S)
+    o.find_patterns()
+    m = gpu_model(p, S)
+    m.set_value_pass("dataflow", ring)
+    if shape:
+        m.set_pass_shapes(*shape)
+    m.find_patterns()
+    ll_g, H, re_g = m.resolve_all()
+    assert m.last_value_pass_dataflow()
+    o.reset_counters()
+    assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
+
+
+@pytest.mark.parametrize("name", ["n60", "miss2"])
+def test_dataflow_full_em(oracle_mod, name):
+    """The whole EM with the dataflow value pass: iteration count, LL, R_E and
+    accepted pairs equal the restatement's."""
+    p = panel(name)
+    m = gpu_model(p, max_iteration=10)
+    m.set_value_pass("dataflow")
+    res = m.run()
+    r = oracle_mod.Oracle(p.alleles, p.types, sample_size=10, max_iter=10).run()
+    assert m.iterations == r["iterations"]
+    assert [x["ll"] for x in m.log] == r["ll"].tolist()
+    assert np.array_equal(res, r["resolutions"])
+
+
 @pytest.mark.parametrize("S", [1, 2, 5, 16, 17, 24, 32, 33, 40, 64])
 def test_estep_sample_sizes(oracle_mod, S):
     p = panel("miss2")
@@ -674,7 +715,8 @@ def test_edge_cases(oracle_mod):
         assert np.array_equal(res, r["resolutions"])
 
 
-def test_underflow_unresolved(oracle_mod):
+@pytest.mark.parametrize("vpass", ["classic", "dataflow"])
+def test_underflow_unresolved(oracle_mod, vpass):
     """Raw double products underflow on long i.i.d. panels; those individuals
     are unresolved (HaploBuilder.cpp:117-124), LL = -inf and the EM stops —
     both implementations must agree on all of it."""
@@ -683,6 +725,7 @@ def test_underflow_unresolved(oracle_mod):
     o = oracle_mod.Oracle(a, "S" * 2500, sample_size=4, max_iter=3)
     r = o.run()
     m = hmc_amd.HaploModel()
+    m.set_value_pass(vpass)
     m.sample_size = 4
     m.max_iteration = 3
     res = m.run(hmc_amd.GenoData(a, "S" * 2500))
