@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <functional>
 #include <cfloat>
 #include <chrono>
 #include <cmath>
@@ -696,6 +697,7 @@ struct Ctx {
   static constexpr int MINE_RETRY = 1000;
   static constexpr int MINE_SPLIT = 1001;  // a block ran out of device memory: re-run it narrower
   int bynum_need = 0;  // round the replay needed beyond the mined tree
+  double bynum_theta_last = -1.0;  // the last findPatternByNum threshold (m_min_freq)
   // ------------------------------------------------------- exact M-step --
   // PatternManager::estimatePatterns (PatternManager.cpp:364-410) and
   // extendPatterns (:412-438) on the host, HaploBuilder::estimateFrequency
@@ -915,7 +917,7 @@ struct Ctx {
   size_t xacc_nc = 0;
 
   // exact_fb + exact_walk over the group d_order2[0, k) (structure records in place)
-  int exact_group(const int32_t *ids, int k) {
+  int exact_group(const int32_t *ids, int k, const std::function<int(std::vector<int32_t> &)> &rerun = nullptr) {
     const int L = pan.L;
     int dev_cu = 256;
     hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, device);
@@ -951,12 +953,29 @@ struct Ctx {
         (e = hipMemcpyAsync(fm.data(), d_xfmax.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
         (e = hipStreamSynchronize(st)))
       return hipfail(e, "exact_fb");
-    int fmax = 1;
-    for (int q = 0; q < k; ++q) {
-      if (xs[ids[q]] == EST_NEEDS_EXACT)
-        return fail(HMC_EUNSUPPORTED, "exact M-step: a forward likelihood underflows (individual %d)", i0 + ids[q]);
-      fmax = std::max(fmax, fm[ids[q]]);
+    std::vector<int32_t> redo;
+    for (int q = 0; q < k; ++q)
+      if (xs[ids[q]] == EST_NEEDS_EXACT) redo.push_back(ids[q]);
+    if (!redo.empty()) {  // their records again, pruned, then their fwd/bwd sums
+      if (!rerun) return fail(HMC_EHIP, "exact M-step: a forward likelihood underflows (individual %d)", i0 + redo[0]);
+      int rc;
+      if ((rc = rerun(redo))) return rc;
+      const int nr = (int)redo.size();
+      if ((e = d_redo.ensure(nr))) return hipfail(e, "exact underflow re-run");
+      if ((rc = upload_order(d_redo, redo.data(), nr))) return rc;
+      ExactArgs x2 = x;
+      x2.order = d_redo.p;
+      x2.n_order = nr;
+      if ((e = launch_exact_fb(x2, std::max(1, std::min(nr, dev_cu * 8)), st))) return hipfail(e, "exact_fb");
+      if ((e = hipMemcpyAsync(xs.data(), d_xstatus.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
+          (e = hipMemcpyAsync(fm.data(), d_xfmax.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
+          (e = hipStreamSynchronize(st)))
+        return hipfail(e, "exact_fb");
+      for (int r : redo)
+        if (xs[r] == EST_NEEDS_EXACT) return fail(HMC_EHIP, "exact M-step: pruned records still underflow (individual %d)", i0 + r);
     }
+    int fmax = 1;
+    for (int q = 0; q < k; ++q) fmax = std::max(fmax, fm[ids[q]]);
     x.fmax = fmax;
     xc_fmax = fmax;
     xc_k = k;
@@ -1109,8 +1128,11 @@ struct Ctx {
   // PatternManager::estimatePatterns (PatternManager.cpp:364-410).
   int estimate_patterns(int *P_out, uint64_t *rm_out) {
     if (!have_estep) return fail(HMC_EARG, "exact M-step needs an E-step first");
-    if (num_patterns > 0 && model != 1)
-      return fail(HMC_EUNSUPPORTED, "exact M-step after findPatternByNum (num_patterns > 0)");
+    // after findPatternByNum the reference estimates at that search's last
+    // threshold (m_min_freq, PatternManager.cpp:53-60, 364-408)
+    const bool bynum = num_patterns > 0 && model != 1;
+    if (bynum && !(bynum_theta_last > 0))
+      return fail(HMC_EARG, "exact M-step after findPatternByNum needs the search's threshold (mine first)");
     if (pan.amax > 44)  // the records pack a locus's allele pairs (amax (amax + 1) / 2) in 10 bits
       return fail(HMC_EUNSUPPORTED, "exact M-step with more than 44 alleles per locus");
     hipEventRecord(ev[4], st);
@@ -1118,7 +1140,7 @@ struct Ctx {
     int mxl = max_len <= 0 ? L : max_len;  // m_max_len / m_min_len of the last findPatternByFreq
     int mnl = std::max(min_len, 1);
     mxl = std::max(mxl, mnl);
-    double mf = current_min_freq();
+    double mf = bynum ? bynum_theta_last : current_min_freq();
     if (model == 1) {  // findPatternBlock: m_min_freq = -1 (PatternManager.cpp:75-88)
       mnl = mxl = std::max(1, mc_order + 1);
       mf = -1.0;
@@ -1757,6 +1779,7 @@ struct Ctx {
       return hipfail(e, "bynum");
     P = (int)out.size();
     rm_out = rm;
+    bynum_theta_last = theta;  // m_min_freq after the search (estimatePatterns filters by it)
     return HMC_OK;
   }
 
@@ -2079,9 +2102,9 @@ struct Ctx {
   // `rec_dead`, the record store give their memory back; the caller
   // re-ensures them afterwards.
   uint64_t rec_words = 0;
-  hipError_t scratch_ensure(DevBuf<char> &b, size_t bytes, bool rec_dead) {
+  hipError_t scratch_ensure(DevBuf<char> &b, size_t bytes, bool rec_dead, bool trace_dead) {
     hipError_t e = b.ensure(bytes);
-    if (e != hipErrorOutOfMemory) return e;
+    if (e != hipErrorOutOfMemory || !trace_dead) return e;
     (void)hipGetLastError();
     d_trace.release();
     if ((e = b.ensure(bytes)) != hipErrorOutOfMemory || !rec_dead) return e;
@@ -2354,71 +2377,87 @@ struct Ctx {
       const int hcap1 = next_pow2(2 * fcap);
       // (exact records pack a locus's contribution count in 22 bits, R[3] = C << 10 | npairs)
       const int ccap1 = (int)std::min<int64_t>(exact ? EXACT_C_MAX : INT32_MAX / 2, (int64_t)ccap_mult * fcap);
-      // structure pass: one wave per individual; 12 per CU (3 per SIMD at 145
-      // VGPRs) above 8 per CU, so cfg 3's E1 groups of 2 200-2 700 run in one
-      // round (profiles/r02/e1_groups/: 603-658 -> 484-586 ms per group).  On a
-      // model larger than the panel (the genotype-mined M0: 2.5 patterns per
-      // individual-locus at cfg 3, 0.3 later) frontiers are large (cfg 3 E1:
-      // 470 states per locus, 80 % of them past a one-wave block's LDS tier):
-      // four waves per individual, two per CU (each block's LDS tier holds
-      // more of the frontier: cfg 3 E1 structure 1.65 -> 1.32 s against three
-      // per CU, profiles/r03/e1/e1_s1shapes.log)
-      const bool heavy_model = (double)P > (double)pan.N * (double)pan.L;
-      // (a heavy group of at most one individual per CU — cfg 4's per-rank E1,
-      // records of ~250 MB per individual — takes the whole CU: 16 waves)
-      const int nw1 = s1_nw > 0 ? s1_nw : (heavy_model ? (np <= dev_cu ? 16 : 4) : 1);
-      const int bpc1 = s1_ipc > 0 ? s1_ipc
-                                  : (nw1 == 16 ? 1 : (nw1 == 4 ? 2 : (np > 8 * dev_cu ? 12 : (np > 4 * dev_cu ? 8 : 4))));
-      const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1, nw1);
-      // (huge frontiers: fewer resident individuals rather than scratch past SCRATCH_MAX)
-      const int grid1 = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::min(np, dev_cu * bpc1), SCRATCH_MAX / per1));
-      // the scratch first: both stores are dead here (the groups before have
-      // been traced back), so they give way to it when HBM is short
-      if ((e = scratch_ensure(d_scr1, per1 * grid1, true)) || (e = d_rec_off.ensure((size_t)n * (L + 1))) ||
-          (e = d_rec_cursor.ensure(1)) || (e = hipMemsetAsync(d_rec_cursor.p, 0, 8, st)))
-        return hipfail(e, "estep pass-1 alloc");
-      if ((rc = ensure_store(d_rec, rec_words, rec_budget, "record store"))) return rc;
-      if ((rc = upload_order(d_order, pending.data(), np))) return rc;
-      StructArgs s1;
-      s1.pan = dev_panel();
-      s1.mod = dev_model();
-      s1.S = S;
-      s1.indiv_begin = i0;
-      s1.order = d_order.p;
-      s1.n_order = np;
-      s1.scratch = d_scr1.p;
-      s1.scratch_stride = per1;
-      s1.fcap = fcap;
-      s1.hcap = hcap1;
-      s1.ccap = ccap1;
-      s1_tier(160 * 1024 / bpc1 - 256, pan.amax, nw1, s1.lds_fc, s1.lds_hc, s1.lds_cc);
-      s1.rec = d_rec.p;
-      s1.rec_cap = d_rec.n;
-      s1.rec_cursor = d_rec_cursor.p;
-      s1.rec_base = d_rbase.p;
-      s1.rec_size = d_recsz.p;
-      s1.rec_off = d_rec_off.p;
-      s1.rec_need = d_rneed.p;
-      s1.trace_need = d_tneed.p;
-      s1.status = dstatus;
-      s1.re_count = exact ? d_xre.p : d_re.p;
-      s1.fmax = exact ? d_xfmax.p : d_fmax.p;
-      s1.max_states = d_maxst.p;
-      s1.stamps = d_stamps.p + 20;
-      s1.exact = exact;
-      if ((e = d_nextq.ensure(2)) || (e = hipMemsetAsync(d_nextq.p, 0, 8, st))) return hipfail(e, "estep");
-      s1.next_q = d_nextq.p;
-      hipEventRecord(ev[0], st);
-      if ((e = launch_estep_structure(s1, grid1, nw1, st))) return hipfail(e, "estep_structure launch");
-      hipEventRecord(ev[1], st);
-      if ((e = hipMemcpyAsync(rneed.data(), d_rneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
-          (e = hipMemcpyAsync(tneed.data(), d_tneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
-          (e = hipMemcpyAsync(fbig.data(), s1.fmax, (size_t)n * 4, hipMemcpyDeviceToHost, st)))
-        return hipfail(e, "estep_structure");
-      if ((rc = read_status(pending, np, false, dstatus))) return rc;
-      hipEventElapsedTime(&ms, ev[0], ev[1]);
-      ms_s1 += ms;
-      ++n_struct_passes;
+      // Structure pass over ids[0, np_) in the record regions set above (d_rbase /
+      // d_recsz).  prune_: with extend()'s forward test (HaploBuilder.cpp:237),
+      // for the individuals the value pass found underflowing.
+      auto structure_pass = [&](const int32_t *ids, int np_, bool prune_) -> int {
+        int rc;
+        hipError_t e;
+        float ms = 0;
+        // structure pass: one wave per individual; 12 per CU (3 per SIMD at 145
+        // VGPRs) above 8 per CU, so cfg 3's E1 groups of 2 200-2 700 run in one
+        // round (profiles/r02/e1_groups/: 603-658 -> 484-586 ms per group).  On a
+        // model larger than the panel (the genotype-mined M0: 2.5 patterns per
+        // individual-locus at cfg 3, 0.3 later) frontiers are large (cfg 3 E1:
+        // 470 states per locus, 80 % of them past a one-wave block's LDS tier):
+        // four waves per individual, two per CU (each block's LDS tier holds
+        // more of the frontier: cfg 3 E1 structure 1.65 -> 1.32 s against three
+        // per CU, profiles/r03/e1/e1_s1shapes.log)
+        const bool heavy_model = (double)P > (double)pan.N * (double)pan.L;
+        // (a heavy group of at most one individual per CU — cfg 4's per-rank E1,
+        // records of ~250 MB per individual — takes the whole CU: 16 waves)
+        const int nw1 = s1_nw > 0 ? s1_nw : (heavy_model ? (np_ <= dev_cu ? 16 : 4) : 1);
+        const int bpc1 = s1_ipc > 0 ? s1_ipc
+                                    : (nw1 == 16 ? 1 : (nw1 == 4 ? 2 : (np_ > 8 * dev_cu ? 12 : (np_ > 4 * dev_cu ? 8 : 4))));
+        const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1, nw1, prune_);
+        // (huge frontiers: fewer resident individuals rather than scratch past SCRATCH_MAX)
+        const int grid1 = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::min(np_, dev_cu * bpc1), SCRATCH_MAX / per1));
+        // the scratch first: both stores are dead here (the groups before have
+        // been traced back), so they give way to it when HBM is short
+        // (a prune re-run runs between a value pass and its traceback: both stores are live)
+        if ((e = scratch_ensure(d_scr1, per1 * grid1, !prune_, !prune_)) || (e = d_rec_off.ensure((size_t)n * (L + 1))) ||
+            (e = d_rec_cursor.ensure(1)) || (e = hipMemsetAsync(d_rec_cursor.p, 0, 8, st)))
+          return hipfail(e, "estep pass-1 alloc");
+        if ((rc = ensure_store(d_rec, rec_words, rec_budget, "record store"))) return rc;
+        if ((rc = upload_order(d_order, ids, np_))) return rc;
+        StructArgs s1;
+        s1.pan = dev_panel();
+        s1.mod = dev_model();
+        s1.S = S;
+        s1.indiv_begin = i0;
+        s1.order = d_order.p;
+        s1.n_order = np_;
+        s1.scratch = d_scr1.p;
+        s1.scratch_stride = per1;
+        s1.fcap = fcap;
+        s1.hcap = hcap1;
+        s1.ccap = ccap1;
+        s1_tier(160 * 1024 / bpc1 - 256, pan.amax, nw1, s1.lds_fc, s1.lds_hc, s1.lds_cc);
+        s1.rec = d_rec.p;
+        s1.rec_cap = d_rec.n;
+        s1.rec_cursor = d_rec_cursor.p;
+        s1.rec_base = d_rbase.p;
+        s1.rec_size = d_recsz.p;
+        s1.rec_off = d_rec_off.p;
+        s1.rec_need = d_rneed.p;
+        s1.trace_need = d_tneed.p;
+        s1.status = dstatus;
+        s1.re_count = exact ? d_xre.p : d_re.p;
+        s1.fmax = exact ? d_xfmax.p : d_fmax.p;
+        s1.max_states = d_maxst.p;
+        s1.stamps = d_stamps.p + 20;
+        s1.exact = exact;
+        s1.prune = prune_;
+        if ((e = d_nextq.ensure(2)) || (e = hipMemsetAsync(d_nextq.p, 0, 8, st))) return hipfail(e, "estep");
+        s1.next_q = d_nextq.p;
+        hipEventRecord(ev[0], st);
+        if ((e = launch_estep_structure(s1, grid1, nw1, st))) return hipfail(e, "estep_structure launch");
+        hipEventRecord(ev[1], st);
+        if ((e = hipMemcpyAsync(rneed.data(), d_rneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
+            (e = hipMemcpyAsync(tneed.data(), d_tneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
+            (e = hipMemcpyAsync(fbig.data(), s1.fmax, (size_t)n * 4, hipMemcpyDeviceToHost, st)))
+          return hipfail(e, "estep_structure");
+        if ((rc = read_status(pending, np_, false, dstatus))) return rc;
+        hipEventElapsedTime(&ms, ev[0], ev[1]);
+        if (prune_) {
+          ms_fb += ms;
+        } else {
+          ms_s1 += ms;
+          ++n_struct_passes;
+        }
+        return HMC_OK;
+      };
+      if ((rc = structure_pass(pending.data(), np, false))) return rc;
       if (debug_mem) {
         int ndef = 0;
         uint64_t rsum = 0, rmax = 0, tsum = 0, rres = 0;
@@ -2521,7 +2560,10 @@ struct Ctx {
           return hipfail(e, "estep");
         if ((rc = upload_order(d_order2, sset.data() + pos, (int)k))) return rc;
         if (exact) {
-          if ((rc = exact_group(sset.data() + pos, (int)k))) return rc;
+          // individuals whose forward likelihood underflows: records rebuilt with
+          // extend()'s forward test (HaploBuilder.cpp:237, 291-314) before the walk
+          auto rerun = [&](std::vector<int32_t> &ids) { return structure_pass(ids.data(), (int)ids.size(), true); };
+          if ((rc = exact_group(sset.data() + pos, (int)k, rerun))) return rc;
           pos += k;
           continue;
         }
@@ -2574,7 +2616,7 @@ struct Ctx {
         const int vwpe = vnw * vipc > 16 && vnw * vipc <= 20 ? 5 : 4;
         const size_t per2 = use_df ? estep_df_scratch_bytes(fgrp, S, df.R) : estep_s2_scratch_bytes(fgrp, S);
         const int grid2 = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::min<int>(G2, (int)k), SCRATCH_MAX / per2));
-        if ((e = scratch_ensure(d_scr2, per2 * grid2, false))) return hipfail(e, "estep pass-2 scratch");
+        if ((e = scratch_ensure(d_scr2, per2 * grid2, false, true))) return hipfail(e, "estep pass-2 scratch");
         if ((rc = ensure_store(d_trace, std::max<uint64_t>(t, 1), trace_budget, "trace store"))) return rc;
         ValueArgs v;
         v.S = S;
@@ -2652,38 +2694,40 @@ struct Ctx {
           if (h_status[bi] == EST_DF_STALL) return fail(HMC_EHIP, "dataflow value pass stalled (individual %d)", i0 + bi);
           if (h_status[bi] == EST_NEEDS_EXACT) h_redo.push_back(bi);
         }
-        // ---- exact fallback: individuals whose forward likelihood underflowed.
-        // The fused kernel's frontiers are subsets of pass 1's (it skips pairs
-        // with fwd <= 0, HaploBuilder.cpp:237), so it fits the same region.
+        // ---- individuals whose forward likelihood underflowed: the reference
+        // skips a pair with fwd <= 0 (extend(), HaploBuilder.cpp:237), which
+        // changes their structure.  Their records are rebuilt with that test
+        // (structure pass, prune) in their own regions — a subset of the
+        // frontiers just walked, so they fit — and their lists re-built.
         n_fallback += (int)h_redo.size();
-        if (!h_redo.empty() && S > 32)
-          return fail(HMC_EUNSUPPORTED, "forward likelihood underflow with sample_size > 32 (%d individuals)",
-                      (int)h_redo.size());
         if (!h_redo.empty()) {
           const int nr = (int)h_redo.size();
-          EstepArgs f = estep_args(S);
-          const int grid = std::min(G, nr);
-          if ((e = d_scratch.ensure(f.scratch_stride * grid)) || (e = d_redo.ensure(nr))) return hipfail(e, "estep fallback");
+          if ((rc = structure_pass(h_redo.data(), nr, true))) return rc;
+          for (int r : h_redo) {
+            const int s = h_status[r];
+            if (s != EST_OK_PRUNED && s != EST_UNRESOLVED)
+              return fail(HMC_EHIP, "underflow re-run: structure status %d (individual %d)", s, i0 + r);
+          }
+          if ((e = d_redo.ensure(nr))) return hipfail(e, "estep underflow re-run");
           if ((rc = upload_order(d_redo, h_redo.data(), nr))) return rc;
-          f.scratch = d_scratch.p;
-          f.order = d_redo.p;
-          f.n_order = nr;
-          f.trace_base = d_tbase.p;
+          ValueArgs v2 = v;
+          v2.order = d_redo.p;
+          v2.n_order = nr;
+          if ((e = hipMemsetAsync(d_nextq.p + 1, 0, 4, st))) return hipfail(e, "estep");
           hipEventRecord(ev[0], st);
-          if ((e = launch_estep(f, grid, estep_nw, st))) return hipfail(e, "estep_forward launch");
+          if (use_df) {
+            if ((e = launch_estep_values_df(v2, std::max(1, std::min(G2, nr)), vnw, vwpe, pair, df.R, df.qcap, st)))
+              return hipfail(e, "estep_values_df launch");
+          } else if ((e = launch_estep_values(v2, std::max(1, std::min(G2, nr)), vnw, false, vwpe, st, pair))) {
+            return hipfail(e, "estep_values launch");
+          }
           hipEventRecord(ev[1], st);
           if ((rc = read_status(sset, (int)k, true))) return rc;
           hipEventElapsedTime(&ms, ev[0], ev[1]);
           ms_fb += ms;
-          for (int r : h_redo) {
-            const int s = h_status[r];
-            if (s == EST_OVERFLOW_FRONTIER) {
-              if (fcap >= F_MAX) return fail(HMC_EUNSUPPORTED, "frontier exceeds %d states", F_MAX);
-              fcap = (int)std::min<int64_t>(F_MAX, (int64_t)fcap * 4);  // x4: each overflow costs a whole pass
-              return ESTEP_RESTART;
-            }
-            if (s == EST_OVERFLOW_TRACE) return fail(HMC_EHIP, "fallback trace exceeds its region");
-          }
+          for (int r : h_redo)
+            if (h_status[r] != EST_OK && h_status[r] != EST_UNRESOLVED)
+              return fail(HMC_EHIP, "underflow re-run: value status %d (individual %d)", h_status[r], i0 + r);
         }
         if ((rc = traceback_group((int)k))) return rc;
         pos += k;

@@ -173,6 +173,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
     const unsigned long long t_indiv = __builtin_amdgcn_s_memtime();
     int status0 = a.status[bi];
     if (status0 == EST_NEEDS_ORDER) status0 = EST_OK;  // the re-run of a value-only pass
+    const bool pruned = status0 == EST_OK_PRUNED;      // records built with extend()'s forward test
+    if (pruned) status0 = EST_OK;
     if (status0 != EST_OK) {
       if (tid == 0) {
         a.total[bi] = 0.0;
@@ -417,7 +419,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
             *Y.fwd(t) = fwd;
             *Y.nl(t) = (uint32_t)k;
             *Y.r0(t) = (uint32_t)r0;
-            if (!(fwd > 0.0) && j < L) underflow = true;
+            if (!(fwd > 0.0) && j < L && !pruned) underflow = true;
             chain = r0 < ce;
             fin = !chain;
           }

@@ -244,9 +244,9 @@ __device__ inline unsigned long long rec_alloc(const StructArgs &a, const Blk<NW
 
 __host__ __device__ inline size_t k1_front_words(int fcap) { return al256((size_t)fcap * 4) / 4; }
 
-size_t estep_s1_scratch_bytes(int fcap, int hcap, int ccap, int nw) {
+size_t estep_s1_scratch_bytes(int fcap, int hcap, int ccap, int nw, bool prune) {
   return 2 * al256(F_NARR * k1_front_words(fcap) * 4) + al256((size_t)hcap * k1_slot_bytes(nw)) +
-         al256((size_t)ccap * 12);
+         al256((size_t)ccap * 12) + (prune ? 2 * al256((size_t)fcap * 8) : 0);
 }
 size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax, int nw) {
   return (size_t)k1_plan(fc, hc, cc, amax * (amax + 1) / 2, nw).bytes;
@@ -304,6 +304,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
   const K1Keys K{smem + plan.o_keys, (unsigned char *)sp, a.lds_hc, a.hcap, NW};
   sp += al256((size_t)a.hcap * k1_slot_bytes(NW));
   const CTier CT{(uint32_t *)(smem + plan.o_contrib), (uint32_t *)sp, a.lds_cc, a.ccap};
+  sp += al256((size_t)a.ccap * 12);
+  // prune: forward likelihoods of the previous and the current frontier (HBM)
+  double *fwx = a.prune ? (double *)sp : nullptr, *fwy = a.prune ? (double *)sp + al256((size_t)a.fcap * 8) / 8 : nullptr;
   // the key table's plainly stored fields; with several waves the HBM tier is
   // read past the vector L1 (another wave of the block may have written it)
   auto kcnt = [&](uint32_t sl) -> uint32_t {
@@ -431,6 +434,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
       }
     }
 
+    if (a.prune && status == EST_OK) {  // head pairs' forward likelihoods (HaploPair.cpp:27-32)
+      for (int t = tid; t < Fp; t += NT) {
+        const uint32_t lo = *X.at(F_LO, t), hi = *X.at(F_HI, t);
+        const double tpv = a.mod.freq[lo] * a.mod.freq[hi];
+        fwx[t] = lo == hi ? tpv : tpv * 2.0;
+      }
+      B.sync();
+    }
     // ---- structure of the forward over loci (HaploBuilder.cpp:47-82) -------
     S1_ST(5);
     for (int i = hl; i < L && status == EST_OK; ++i) {
@@ -507,7 +518,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         uint32_t lo = 0, hi = 0, slot = 0;
         bool rev = false;
         if (valid) {
-          valid = sa != NONE && sb != NONE;
+          // extend(): a pair whose forward likelihood is 0 is not extended
+          // (HaploBuilder.cpp:237), then both successors must exist (:239-243)
+          valid = sa != NONE && sb != NONE && (!a.prune || fwx[s] > 0.0);
           rev = sa > sb;  // addHaploPair: id_a > id_b -> swap, reversed
           lo = rev ? sb : sa;
           hi = rev ? sa : sb;
@@ -661,6 +674,20 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         roff[i + 1] = o;
       }
       S1_ST(3);
+      if (a.prune) {  // the new states' forward likelihoods, in add order (HaploPair.cpp:42, :66)
+        B.sync();
+        for (int t = tid; t < Fn; t += NT) {
+          double f = 1.0;  // counting (no records): sizes only, nothing pruned
+          if (!counting) {
+            const double tpv = Rtp[t];
+            for (uint32_t r = Rcb[t]; r < Rcb[t + 1]; ++r) {
+              const double v = fwx[cw_state(Rct[r])] * tpv;
+              f = r == Rcb[t] ? v : f + v;
+            }
+          }
+          fwy[t] = f;
+        }
+      }
       // m_best_pair.clear() for the next locus
       for (int t0 = 0; t0 < Fn; t0 += NT) {
         const int t = t0 + tid;
@@ -674,6 +701,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
       const IdFront T = X;
       X = Y;
       Y = T;
+      double *const ft = fwx;
+      fwx = fwy;
+      fwy = ft;
       Fp = Fn;
       S1_ST(4);
     }
@@ -682,6 +712,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
       status = EST_OVERFLOW_REC;
     fbig = Fp > fbig ? Fp : fbig;
     if (status < 0) reset_tables();  // aborted mid-locus: keys may be left
+    if (status == EST_OK && a.prune) status = EST_OK_PRUNED;
     re = B.reduce_u64(re);
     if (tid == 0) {
       a.rec_need[bi] = rneed;
@@ -897,6 +928,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
     const unsigned long long t_indiv = __builtin_amdgcn_s_memtime();
     int status = a.status[bi];
     if (status == EST_NEEDS_ORDER) status = EST_OK;  // the re-run of a value-only pass
+    const bool pruned = status == EST_OK_PRUNED;     // records built with extend()'s forward test
+    if (pruned) status = EST_OK;
     if (status != EST_OK) {  // pass 1 found no resolution (dead frontier)
       if (tid == 0) {
         a.total[bi] = 0.0;
@@ -1002,7 +1035,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
         *Y.fwd(t) = fwd;
         *Y.nl(t) = (uint32_t)k;
         *Y.r0(t) = (uint32_t)r0;
-        if (!(fwd > 0.0) && j < L) bs->flag = 1;
+        if (!(fwd > 0.0) && j < L && !pruned) bs->flag = 1;
 
       }
       __syncthreads();

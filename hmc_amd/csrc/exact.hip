@@ -71,7 +71,9 @@ __global__ __launch_bounds__(256) void exact_fb(ExactArgs a) {
   __shared__ int flag;
   for (int q = blockIdx.x; q < a.n_order; q += gridDim.x) {
     const int bi = a.order[q];
-    if (a.status[bi] != EST_OK) continue;
+    const int st0 = a.status[bi];
+    if (st0 != EST_OK && st0 != EST_OK_PRUNED) continue;
+    const bool pruned = st0 == EST_OK_PRUNED;  // zero forward likelihoods are expected (not extended)
     const unsigned long long *roff = a.rec_off + (size_t)bi * (L + 1);
     unsigned long long *xo = a.x_off + (size_t)bi * (L + 1);
     // x-store layout per locus: fwd[F] then bwd[F] (doubles), even word offsets
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(256) void exact_fb(ExactArgs a) {
           f = r == R.cb[t] ? v : f + v;
         }
         fw[t] = f;
-        if (!(f > 0.0) && j < L) flag = 1;  // extend() would skip this pair (HaploBuilder.cpp:237)
+        if (!(f > 0.0) && j < L && !pruned) flag = 1;  // extend() would skip this pair (HaploBuilder.cpp:237)
       }
       __syncthreads();
     }
@@ -203,7 +205,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
     const int q = (int)(it / L), start = (int)(it % L);
     const int bi = a.order[q];
     const int root = a.tr_root[start];
-    if (root < 0 || a.status[bi] != EST_OK) continue;
+    if (root < 0 || (a.status[bi] != EST_OK && a.status[bi] != EST_OK_PRUNED)) continue;
     const double pg = a.gprob[bi];  // P(genotype) of the last E-step (HaploModel.cpp:109, HaploBuilder.cpp:294)
     if (!(pg > 0.0)) continue;
     const unsigned long long *roff = a.rec_off + (size_t)bi * (L + 1);

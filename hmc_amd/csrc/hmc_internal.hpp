@@ -65,6 +65,9 @@ enum EStatus : int32_t {
                                // (HaploBuilder.cpp:237) — re-run on the fused kernel
   EST_NEEDS_ORDER = 3,         // value-only value pass: a tie makes the result depend on
                                // the libstdc++ list order — re-run on the exact value pass
+  EST_OK_PRUNED = 4,           // structure records built with extend()'s forward test
+                               // (HaploBuilder.cpp:237): pairs whose forward likelihood is 0
+                               // are not extended; the value pass then expects zeros
 };
 
 // Panel resident in HBM.
@@ -167,6 +170,11 @@ struct StructArgs {
   // orientation counts — the forward links of HaploPair (HaploPair.cpp:44,67)
   // in push order; trace_need then counts the fwd/bwd store (4 words/state).
   bool exact;
+  // extend()'s test (HaploBuilder.cpp:237): forward likelihoods are summed per
+  // state as the records are built and a pair whose sum is 0 is not extended.
+  // For individuals whose likelihoods underflow (the value pass reports
+  // EST_NEEDS_EXACT); status EST_OK_PRUNED.  Scratch: estep_s1_scratch_bytes(.., prune)
+  bool prune = false;
   int32_t *next_q;                // dynamic schedule: order entries taken after the first gridDim.x (zeroed)
   int32_t *status;                // [batch]
   unsigned long long *re_count;   // [batch]
@@ -224,7 +232,7 @@ size_t estep_scratch_bytes(int fcap, int hcap, int S, int nw);
 size_t estep_lds_bytes(int S, int fc, int hc, int nw, int amax);
 hipError_t launch_test_coop_nth(double *lik, uint32_t *tag, const int *off, const int *n, const int *nth, int count, int sw, hipStream_t st);
 hipError_t launch_estep(const EstepArgs &a, int grid, int nw, hipStream_t st);
-size_t estep_s1_scratch_bytes(int fcap, int hcap, int ccap, int nw);
+size_t estep_s1_scratch_bytes(int fcap, int hcap, int ccap, int nw, bool prune = false);
 size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax, int nw);
 size_t estep_s2_scratch_bytes(int fcap, int S);
 size_t estep_s2_lds_bytes(int S, int fc, int nw, bool pair = false);

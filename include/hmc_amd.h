@@ -80,9 +80,8 @@ int hmc_set_reduction(hmc_ctx *ctx, int mode);
 /* HaploModel public parameters (HaploModel.h:15-26; CLI defaults HMC.cpp:35-47).
  * min_freq_abs > 0 overrides min_freq exactly as HaploModel::findPatterns does
  * (HaploModel.cpp:54-56).  sample_size 1..64 (HaploPair's k-best lists,
- * HaploBuilder.cpp:44, HaploPair.cpp:85-88; above 32 the split E-step only,
- * and an individual whose forward likelihood underflows returns
- * HMC_EUNSUPPORTED); larger values fail the E-step with HMC_EUNSUPPORTED. */
+ * HaploBuilder.cpp:44, HaploPair.cpp:85-88; above 32 the split E-step only);
+ * larger values fail the E-step with HMC_EUNSUPPORTED. */
 int hmc_set_params(hmc_ctx *ctx, double min_freq_abs, double min_freq, int min_pattern_len, int max_pattern_len,
                    int sample_size);
 
@@ -315,13 +314,14 @@ int hmc_set_pass_shapes(hmc_ctx *ctx, int structure_waves, int structure_ipc, in
 int hmc_set_store_budgets(hmc_ctx *ctx, uint64_t trace_bytes, uint64_t record_bytes);
 /* E-step implementation: 0 (default) = two passes, a structure pass that
  * replays extendAll/addHaploPair (HaploBuilder.cpp:226-261) on pattern ids
- * and a value pass with the k-best lists, falling back to 1 for individuals
- * whose forward likelihood underflows; 1 = the fused single-pass kernel.
- * Both produce identical results. */
+ * and a value pass with the k-best lists; individuals whose forward
+ * likelihood underflows are re-run through a structure pass that applies
+ * extend()'s forward test (HaploBuilder.cpp:237); 1 = the fused single-pass
+ * kernel (sample_size <= 32).  Both produce identical results. */
 int hmc_set_estep_mode(hmc_ctx *ctx, int mode);
 /* Split E-step of the last hmc_resolve_all: device ms of the structure pass,
- * the value pass and the fused fallback, and the number of individuals that
- * took the fallback. */
+ * the value pass and the underflow re-runs, and the number of individuals
+ * re-run. */
 int hmc_last_estep_split(const hmc_ctx *ctx, double *structure_ms, double *values_ms, double *fallback_ms,
                          int *n_fallback);
 /* Launches of the last hmc_resolve_all: structure passes and value passes

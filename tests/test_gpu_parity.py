@@ -715,18 +715,20 @@ def test_edge_cases(oracle_mod):
         assert np.array_equal(res, r["resolutions"])
 
 
-@pytest.mark.parametrize("vpass", ["classic", "dataflow"])
-def test_underflow_unresolved(oracle_mod, vpass):
+@pytest.mark.parametrize("vpass,S", [("classic", 4), ("dataflow", 4), ("classic", 40)])
+def test_underflow_unresolved(oracle_mod, vpass, S):
     """Raw double products underflow on long i.i.d. panels; those individuals
     are unresolved (HaploBuilder.cpp:117-124), LL = -inf and the EM stops —
-    both implementations must agree on all of it."""
+    both implementations must agree on all of it.  The individuals whose
+    forward likelihoods reach 0 are re-built with extend()'s forward test
+    (HaploBuilder.cpp:237): any sample size, either value-pass schedule."""
     rng = np.random.default_rng(5)
     a = (rng.integers(0, 2, (6, 2, 2500)) + ord("1")).astype(np.int32)
-    o = oracle_mod.Oracle(a, "S" * 2500, sample_size=4, max_iter=3)
+    o = oracle_mod.Oracle(a, "S" * 2500, sample_size=S, max_iter=3)
     r = o.run()
     m = hmc_amd.HaploModel()
     m.set_value_pass(vpass)
-    m.sample_size = 4
+    m.sample_size = S
     m.max_iteration = 3
     res = m.run(hmc_amd.GenoData(a, "S" * 2500))
     assert [x["ll"] for x in m.log] == r["ll"].tolist()
@@ -1124,6 +1126,42 @@ def test_exact_single_allele_frequencies(oracle_mod):
         j = list(sym[k]).index(pt["alleles"][i, 0])
         assert abs(pt["freq"][i] - fr[k, j]) <= 1e-12
         assert pt["prefix"][i] == 1.0
+
+
+@pytest.mark.parametrize("K,N,L,num", [(2, 40, 30, 150), (3, 50, 40, 400)])
+def test_exact_mstep_after_find_pattern_by_num(oracle_mod, K, N, L, num):
+    """--exact-estimate with num_patterns > 0: M0 by findPatternByNum, E1,
+    then estimatePatterns at the search's last threshold (m_min_freq,
+    PatternManager.cpp:53-60, 364-408) — the restatement's table (ids,
+    strings, successors exact; frequencies 1e-6 relative) — and the whole EM."""
+    p = synth.founder_mosaic(N, L, A=2, K=K, seed=5)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
+    o.set_num_patterns(num)
+    o.find_patterns()
+    o.resolve_all()
+    P_o, _ = o.estimate_patterns()
+    po = o.patterns()
+    m = gpu_model(p, num_patterns=num)
+    m.exact_estimate = True
+    m.find_patterns()
+    m.resolve_all()
+    P_g, _ = m.find_patterns()
+    pg = m.patterns()
+    assert P_g == P_o
+    for k in ("start", "len", "alleles", "succ"):
+        assert np.array_equal(pg[k], po[k]), k
+    for k in ("freq", "prefix", "tp"):
+        assert _rel_close(pg[k], po[k]), k
+    m2 = gpu_model(p, max_iteration=6, num_patterns=num)
+    m2.exact_estimate = True
+    res = m2.run()
+    o2 = oracle_mod.Oracle(p.alleles, p.types, sample_size=10, max_iter=6)
+    o2.set_num_patterns(num)
+    o2.set_exact(True)
+    r = o2.run()
+    assert m2.iterations == r["iterations"]
+    assert np.allclose([x["ll"] for x in m2.log], r["ll"], rtol=1e-9, atol=0)
+    assert np.mean(np.all(res == r["resolutions"], axis=(1, 2))) >= 0.99
 
 
 @pytest.mark.parametrize("name", ["cfg1", "n60", "miss2"])
