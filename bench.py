@@ -56,6 +56,9 @@ DBL_MAX = sys.float_info.max
 # What bounds estep_values (SQ counters under profiles/): the
 # roofline above prices it against HBM, but the kernel moves ~1/30 of peak —
 # its waves are parked on dependent LDS round trips and barriers.
+# The sampled CPU estimate checked against the whole single-thread chain at
+# cfg 2 (bench.py --config 2 --cpu-validate on a GPU box, same run).
+VALIDATION_NOTE = "profiles/r04/cpu_validate_cfg2.json"
 LIMITER = "issue/latency: dependent selection steps and per-locus barriers (SQ counters, DESIGN.md 9), not HBM bandwidth"
 
 
@@ -77,7 +80,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-indiv", type=int, default=20, help="individuals per CPU E-step sample (E_k, k >= 2)")
     ap.add_argument("--cpu-indiv-e1", type=int, default=6, help="individuals of the CPU E_1 sample (M0 model)")
-    ap.add_argument("--cpu-roots", type=int, default=10, help="start loci per CPU M-step sample")
+    ap.add_argument("--cpu-roots", type=int, default=30, help="start loci per CPU M-step sample")
+    ap.add_argument("--cpu-validate", action="store_true",
+                    help="also time the whole chain on the CPU restatement (1 thread) next to the sampled "
+                         "estimate: minutes at cfg 2, hours at cfg 3")
     ap.add_argument("--trace-bytes", type=int, default=0, help="E-step store budget per store (0: automatic)")
     ap.add_argument("--reduction", default="ordered", choices=["ordered", "allreduce"],
                     help="cross-rank M-step sums: rank-ordered (bit-identical to one GPU) or one all-reduce")
@@ -424,6 +430,17 @@ def cpu_baseline(m, panel, args):
         old_ll, it = ll, it + 1
     t_chain = sum(p["seconds"] * p["scale"] for p in parts)
     t_iter = t_chain / it
+    validation = None
+    if args.cpu_validate:  # the same chain in full, M0 to the stop, one thread (HaploModel::run)
+        oracle.set_threads(1)
+        full = oracle.Oracle(panel.alleles, panel.types, sample_size=args.sample_size, max_iter=100).run()
+        n_e, n_m = len(full["t_e"]), max(0, full["iterations"] - 1)
+        t_full = float(sum(full["t_e"][:n_e]) + sum(full["t_m"][:n_m]))
+        validation = {"full_chain_iterations": int(full["iterations"]), "full_chain_seconds": t_full,
+                      "full_t_iter_s": t_full / full["iterations"], "sampled_t_iter_s": t_iter,
+                      "sampled_over_full": t_iter / (t_full / full["iterations"]),
+                      "full_parts_s": {"E": [float(x) for x in full["t_e"][:n_e]],
+                                       "M": [float(x) for x in full["t_m"][:n_m]]}}
     return {
         "value": N * L / t_iter, "unit": "individual·loci/s", "cores": 1, "kind": "port",
         "sample": f"converged chain of {it} EM iterations ({', '.join(p['step'] for p in parts)}): E_1 over "
@@ -431,6 +448,7 @@ def cpu_baseline(m, panel, args):
                   f"cost order, M_k over {kr} start loci spread over [0, {L}), each scaled to the panel; "
                   f"oracle/hmc_oracle.cpp g++ -O2, 1 thread",
         "parts": parts, "t_iter_s": t_iter, "sample_seconds": sum(p["seconds"] for p in parts),
+        "validation": validation if validation else VALIDATION_NOTE,
     }
 
 

@@ -1,0 +1,883 @@
+// ctx_estep.cpp — Ctx members: the E-step: HaploModel::resolveAll through the structure and value passes.
+#include "ctx.hpp"
+
+namespace hmc {
+
+int Ctx::build_head_frontier() {
+  const int n = nloc(), hl = head_len;
+  const int nh = (int)h_head_ids.size();
+  if (nh == 0 && !h_head_al.empty()) return fail(HMC_EARG, "head alleles without heads");
+  // the start-0 length-hl pattern matching `as` (MISSING = wildcard): the
+  // trie walk of PatternTree.cpp:98-134 goes from locus hl-1 down and keeps
+  // the first full-length hit, i.e. the smallest allele index at the
+  // highest missing locus first
+  auto lookup = [&](const std::vector<uint8_t> &as) -> uint32_t {
+    int best = -1;
+    for (int h = 0; h < nh; ++h) {
+      const uint8_t *al = h_head_al.data() + (size_t)h * hl;
+      bool ok = true;
+      for (int k = 0; k < hl && ok; ++k) ok = as[k] == MISSING || as[k] == al[k];
+      if (!ok) continue;
+      if (best < 0) { best = h; continue; }
+      const uint8_t *bl = h_head_al.data() + (size_t)best * hl;
+      for (int k = hl - 1; k >= 0; --k)
+        if (al[k] != bl[k]) {
+          if (al[k] < bl[k]) best = h;
+          break;
+        }
+    }
+    return best < 0 ? NONE : h_head_ids[best];
+  };
+  std::vector<uint32_t> off(n + 1, 0), pairs;
+  std::vector<int32_t> status(n, EST_OK);
+  for (int i = 0; i < n; ++i) {
+    off[i] = (uint32_t)(pairs.size() / 2);
+    const uint8_t *g0 = pan.idx.data() + ((size_t)(i0 + i) * 2) * pan.L, *g1 = g0 + pan.L;
+    for (int h = 0; h < nh && status[i] == EST_OK; ++h) {
+      const uint8_t *H = h_head_al.data() + (size_t)h * hl;
+      bool match = true;  // HaploPattern::isMatch(genotype): every locus matches one allele
+      for (int j = 0; j < hl && match; ++j)
+        match = g0[j] == MISSING || g1[j] == MISSING || g0[j] == H[j] || g1[j] == H[j];
+      if (!match) continue;
+      std::vector<std::vector<uint8_t>> last(1), next;
+      for (int j = 0; j < hl; ++j) {
+        next.clear();
+        const bool miss0 = g0[j] == MISSING, miss1 = g1[j] == MISSING;
+        const bool isMissing = miss0 && miss1, hasMissing = miss0 || miss1;
+        const bool hasAllele = g0[j] == H[j] || g1[j] == H[j];  // Allele == (missing == missing)
+        const bool het = !(hasMissing || g0[j] == g1[j]);
+        if (isMissing || (hasMissing && hasAllele)) {
+          for (auto &as : last)
+            for (int k = 0; k < (int)pan.sym[j].size(); ++k)
+              if (pan.sym[j][k].second > 0) {
+                next.push_back(as);
+                next.back().push_back((uint8_t)k);
+              }
+        } else if (het) {
+          for (auto &as : last) {
+            next.push_back(as);
+            next.back().push_back(H[j] == g0[j] ? g1[j] : g0[j]);
+          }
+        } else {
+          for (auto &as : last) {
+            next.push_back(as);
+            next.back().push_back(g0[j]);
+          }
+        }
+        last.swap(next);
+      }
+      for (auto &as : last) {
+        const uint32_t q = lookup(as);
+        if (q == NONE) { status[i] = EST_NO_HEAD_PATTERN; break; }
+        if (q >= h_head_ids[h]) {
+          pairs.push_back(h_head_ids[h]);
+          pairs.push_back(q);
+        }
+      }
+    }
+  }
+  off[n] = (uint32_t)(pairs.size() / 2);
+  hipError_t e;
+  if ((e = d_hf_off.ensure(n + 1)) || (e = d_hf_pairs.ensure(std::max<size_t>(pairs.size(), 2))) ||
+      (e = d_hf_status.ensure(std::max(n, 1))) ||
+      (e = hipMemcpyAsync(d_hf_off.p, off.data(), (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st)) ||
+      (!pairs.empty() && (e = hipMemcpyAsync(d_hf_pairs.p, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, st))) ||
+      (n && (e = hipMemcpyAsync(d_hf_status.p, status.data(), (size_t)n * 4, hipMemcpyHostToDevice, st))) ||
+      (e = hipStreamSynchronize(st)))
+    return hipfail(e, "head frontier");
+  hf_valid = true;
+  return HMC_OK;
+}
+
+int Ctx::estep(double *ll_out, int *H_out, uint64_t *re_out) {
+  if (!have_model) return fail(HMC_EARG, "no pattern model");
+  if (head_len > 1) {
+    if (h_head_al.size() != h_head_ids.size() * (size_t)head_len || (h_head_ids.empty() && n_head > 0))
+      return fail(HMC_EUNSUPPORTED, "head_len > 1 needs the head patterns' alleles (mined tables only)");
+    int rc = build_head_frontier();
+    if (rc) return rc;
+  }
+  const int L = pan.L, S = this->S(), n = nloc();
+  if (S > S_MAX) return fail(HMC_EUNSUPPORTED, "sample_size > %d", S_MAX);
+  if (S > 32 && estep_mode != ESTEP_SPLIT)
+    return fail(HMC_EUNSUPPORTED, "sample_size > 32 needs the split E-step (hmc_set_estep_mode 0)");
+  hipError_t e;
+  if ((e = d_total.ensure(n)) || (e = d_ncand.ensure(n)) || (e = d_status.ensure(n)) || (e = d_re.ensure(n)) ||
+      (e = d_sbase.ensure(n)) || (e = d_prior.ensure((size_t)n * S_MAX)) || (e = d_post.ensure((size_t)n * S_MAX)) ||
+      (e = d_weight.ensure((size_t)n * S_MAX)) || (e = d_cstate.ensure((size_t)n * S_MAX)) ||
+      (e = d_cidx.ensure((size_t)n * S_MAX)) || (e = d_rows.ensure((size_t)2 * S * n * L)) ||
+      (e = d_wslot.ensure((size_t)2 * S * n)) || (e = d_trace_cursor.ensure(1)) || (e = d_maxst.ensure(1)) ||
+      (e = d_fmax.ensure(n)) || (e = d_loc_off.ensure((size_t)n * (L + 1))) || (e = d_order.ensure(n)) ||
+      (e = d_order2.ensure(n)) || (e = d_cost.ensure(n)) || (e = d_tbase.ensure(n)) || (e = d_rbase.ensure(n)) ||
+      (e = d_rneed.ensure(n)) || (e = d_tneed.ensure(n)) || (e = d_recsz.ensure(n)))
+    return hipfail(e, "estep alloc");
+  // store budgets: trace store and record store grow (never shrink) up to these
+  size_t freeb = 0, totb = 0;
+  hipMemGetInfo(&freeb, &totb);
+  const double avail = (double)freeb + (double)d_trace.n * 4 + (double)d_rec.n * 4;
+  // Frontier capacity of the structure pass: a frontier past it restarts the
+  // E-step with twice the capacity (cfg 3's E1 on the M0 model needs 2^14:
+  // three restarts from 2^11, ~0.6 s).  With HBM to spare, start there: the
+  // pass's per-block scratch is ~190 B per state (3 GB per 1 000 blocks).
+  if (!fcap_user_set && fcap < FCAP_BIG && avail > 96e9) fcap = FCAP_BIG;
+  // (cfg 3's E1 with the M0 model needs ~2x HBM in records + traces; larger
+  // stores (fewer groups) measured no faster and crowd out the next M0.  The
+  // trace cap keeps cfg 3's E2.. (~90 GB of traces) in one value pass.)
+  trace_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.42), 120ull << 30),
+                                    1ull << 16) / 4;
+  rec_budget = std::max<uint64_t>(rec_bytes ? rec_bytes : trace_bytes ? trace_bytes
+                                  : std::min<uint64_t>((uint64_t)(avail * 0.28), 80ull << 30),
+                                  1ull << 16) / 4;
+  if (debug_mem)
+    fprintf(stderr, "[hmc] E-step: free %.1f GB, stores %.1f + %.1f GB, budgets trace %.1f rec %.1f GB\n",
+            freeb / 1e9, d_trace.n * 4 / 1e9, d_rec.n * 4 / 1e9, trace_budget * 4 / 1e9, rec_budget * 4 / 1e9);
+  // Stores sized by an earlier E-step when more HBM was free (E1, before an
+  // exact M-step's tables) shrink to this E-step's budgets: the pass
+  // scratch is allocated from what they leave free.
+  if (d_trace.n > trace_budget) d_trace.release();
+  if (d_rec.n > rec_budget) d_rec.release();
+  h_total.assign(n, 0.0);
+  h_ncand.assign(n, 0);
+  h_status.assign(n, 0);
+  h_re.assign(n, 0);
+  h_sbase.assign(n, 0);
+  for (int i = 0; i < n; ++i) h_sbase[i] = 2 * S * i;  // sample slots of individual i
+  if ((e = hipMemcpyAsync(d_sbase.p, h_sbase.data(), (size_t)n * 4, hipMemcpyHostToDevice, st)) ||
+      (e = hipMemsetAsync(d_maxst.p, 0, 4, st)) || (e = hipMemsetAsync(d_ncand.p, 0, (size_t)n * 4, st)))
+    return hipfail(e, "estep");
+  if ((e = d_stamps.ensure(40)) || (e = hipMemsetAsync(d_stamps.p, 0, 40 * 8, st))) return hipfail(e, "stamps");
+  // heaviest individuals first (cost of the previous E-step; before the
+  // first one, the number of heterozygous or missing loci)
+  if ((int)h_cost.size() != n) {
+    h_cost.assign(n, 0);
+    for (int i = 0; i < n; ++i)
+      for (int k = 0; k < L; ++k) {
+        const uint8_t x = pan.idx[((size_t)(i0 + i) * 2) * L + k], y = pan.idx[((size_t)(i0 + i) * 2 + 1) * L + k];
+        h_cost[i] += (x != y || x == MISSING) ? 1 : 0;
+      }
+  }
+  std::vector<int32_t> order(n);
+  for (int q = 0; q < n; ++q) order[q] = q;
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return h_cost[x] > h_cost[y]; });
+  if ((e = hipMemcpyAsync(d_cost.p, h_cost.data(), (size_t)n * 4, hipMemcpyHostToDevice, st)))
+    return hipfail(e, "estep");
+  ms_fwd = ms_tb = 0;
+  ms_s1 = ms_s2 = ms_fb = ms_order = 0;
+  n_fallback = n_order_redo = 0;
+  n_struct_passes = n_value_passes = 0;
+  int rc = 0;
+  while (true) {  // a frontier overflow (fcap grows) restarts the E-step
+    rc = estep_mode == ESTEP_SPLIT ? estep_split(order) : estep_fused(order);
+    if (rc != ESTEP_RESTART) break;
+  }
+  if (rc) return rc;
+  if (estep_mode == ESTEP_SPLIT) ms_fwd = ms_s1 + ms_s2 + ms_fb;
+  // samples in the reference's order: individuals in order, candidates in
+  // order, h0 then h1 (HaploModel.cpp:105-106)
+  std::vector<int32_t> rowmap;
+  rowmap.reserve((size_t)2 * S * n);
+  for (int i = 0; i < n; ++i)
+    for (int c = 0; c < 2 * h_ncand[i]; ++c) rowmap.push_back(h_sbase[i] + c);
+  H = (int)rowmap.size();
+  std::vector<double> wslot((size_t)2 * S * n), w(H);
+  if ((e = d_samp_lm.ensure((size_t)std::max(H, 1) * L)) || (e = d_rowmap.ensure(std::max(H, 1))) ||
+      (e = d_w.ensure(std::max(H, 1))))
+    return hipfail(e, "samples");
+  if ((H && (e = hipMemcpyAsync(d_rowmap.p, rowmap.data(), (size_t)H * 4, hipMemcpyHostToDevice, st))) ||
+      (e = launch_transpose_rows_u8(d_rows.p, d_rowmap.p, d_samp_lm.p, H, L, st)) ||
+      (e = hipMemcpyAsync(wslot.data(), d_wslot.p, wslot.size() * 8, hipMemcpyDeviceToHost, st)) ||
+      (e = hipMemcpyAsync(h_total.data(), d_total.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
+      (e = hipMemcpyAsync(h_re.data(), d_re.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
+      (e = hipMemcpyAsync(h_cost.data(), d_cost.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
+      (e = hipStreamSynchronize(st)))
+    return hipfail(e, "estep");
+  for (int h = 0; h < H; ++h) w[h] = wslot[rowmap[h]];
+  if (H && ((e = hipMemcpyAsync(d_w.p, w.data(), (size_t)H * 8, hipMemcpyHostToDevice, st)) ||
+            (e = hipStreamSynchronize(st))))
+    return hipfail(e, "estep");
+  h_rowmap.swap(rowmap);
+  // ll += log(genotype probability) in individual order (HaploModel.cpp:110);
+  // HaploData::checkTotalWeight (HaploData.cpp:120-126) in sample order
+  double red[2] = {0.0, 0.0};
+  auto local_sums = [&](double *acc) {
+    double ll = acc[0], tw = acc[1];
+    for (int i = 0; i < n; ++i) ll += log(h_total[i]);
+    for (int h = 0; h < H; ++h) tw += w[h];
+    acc[0] = ll;
+    acc[1] = tw;
+  };
+  if (multi() && reduction == RED_ORDERED) {
+    for (int r = 0; r < world; ++r) {  // the chain continues rank by rank
+      if (r == rank) local_sums(red);
+      if ((rc = bcast_host(red, 2, r))) return rc;
+    }
+  } else {
+    local_sums(red);
+    if ((rc = allreduce_host(red, 2))) return rc;
+  }
+  const double ll = red[0];
+  total_weight = red[1];
+  uint64_t re = 0;
+  for (int i = 0; i < n; ++i) re += h_re[i];
+  have_samples = true;
+  have_estep = true;
+  if (ll_out) *ll_out = ll;
+  if (H_out) *H_out = H;
+  if (re_out) *re_out = re;
+  return HMC_OK;
+}
+
+int Ctx::ensure_store(DevBuf<uint32_t> &b, uint64_t words, uint64_t budget, const char *what) {
+  if (b.n >= words && b.p) return HMC_OK;
+  if (words > budget) return fail(HMC_ENOMEM, "%s: one individual needs %llu words (budget %llu)", what,
+                                  (unsigned long long)words, (unsigned long long)budget);
+  b.release();  // 1.25x headroom: a store of tens of GB is mapped eagerly, re-allocations are slow
+  const uint64_t want = std::min<uint64_t>(budget, words + words / 4);
+  hipError_t e = b.ensure(want);
+  if (e == hipErrorOutOfMemory && want > words) {  // the device is shared: no headroom
+    (void)hipGetLastError();
+    e = b.ensure(words);
+  }
+  if (e) return hipfail(e, what);
+  return HMC_OK;
+}
+
+EstepArgs Ctx::estep_args(int S) {
+  EstepArgs a;
+  a.pan = dev_panel();
+  a.mod = dev_model();
+  a.S = S;
+  a.indiv_begin = i0;
+  a.indiv_end = i1;
+  a.scratch = d_scratch.p;
+  a.fcap = fcap;
+  a.hcap = next_pow2(2 * fcap);
+  a.scratch_stride = estep_scratch_bytes(fcap, a.hcap, S, estep_nw);
+  lds_tier(S, a.lds_fc, a.lds_hc);
+  a.trace = d_trace.p;
+  a.trace_cap = d_trace.n;
+  a.trace_cursor = d_trace_cursor.p;
+  a.trace_base = nullptr;
+  a.loc_off = d_loc_off.p;
+  a.total = d_total.p;
+  a.ncand = d_ncand.p;
+  a.status = d_status.p;
+  a.cand_state = d_cstate.p;
+  a.cand_idx = d_cidx.p;
+  a.prior = d_prior.p;
+  a.posterior = d_post.p;
+  a.weight = d_weight.p;
+  a.re_count = d_re.p;
+  a.max_states = d_maxst.p;
+  a.fmax = d_fmax.p;
+  a.order = nullptr;
+  a.n_order = 0;
+  a.cost = d_cost.p;
+  a.stamps = d_stamps.p;
+  a.diag_indiv = -1;  // diagnostic build: stamps of every individual
+  return a;
+}
+
+int Ctx::traceback_group(int k) {
+  TracebackArgs t;
+  t.L = pan.L;
+  t.S = S();
+  t.head_len = head_len;
+  t.nbatch = k;
+  t.order = d_order2.p;
+  t.indiv_begin = i0;
+  t.mod = dev_model();
+  t.trace = d_trace.p;
+  t.loc_off = d_loc_off.p;
+  t.ncand = d_ncand.p;
+  t.cand_state = d_cstate.p;
+  t.cand_idx = d_cidx.p;
+  t.weight = d_weight.p;
+  t.sample_base = d_sbase.p;
+  t.rows = d_rows.p;
+  t.w_out = d_wslot.p;
+  hipError_t e;
+  hipEventRecord(ev[2], st);
+  if ((e = launch_traceback(t, 0, st))) return hipfail(e, "traceback");
+  hipEventRecord(ev[3], st);
+  if ((e = hipStreamSynchronize(st))) return hipfail(e, "traceback");
+  float ms = 0;
+  hipEventElapsedTime(&ms, ev[2], ev[3]);
+  ms_tb += ms;
+  return HMC_OK;
+}
+
+int Ctx::estep_fused(const std::vector<int32_t> &order) {
+  const int S = this->S(), n = nloc();
+  int dev_cu = 256;
+  hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, device);
+  const int G = std::max(1, std::min(waves > 0 ? waves : dev_cu * std::max(8, lds_waves_per_cu), n));
+  hipError_t e;
+  size_t pos = 0;
+  int batch = n;
+  if (d_trace.n == 0) {
+    int rc = ensure_store(d_trace, std::min<uint64_t>(trace_budget, std::max<uint64_t>((uint64_t)n * pan.L * (1 + S) * 96, 16ull << 20)),
+                          trace_budget, "trace store");
+    if (rc) return rc;
+  }
+  while (pos < order.size()) {
+    const int k = (int)std::min<size_t>(batch, order.size() - pos);
+    EstepArgs a = estep_args(S);
+    const int grid = std::min(G, k);
+    if ((e = d_scratch.ensure(a.scratch_stride * grid))) return hipfail(e, "estep scratch");
+    a.scratch = d_scratch.p;
+    int rc = upload_order(d_order2, order.data() + pos, k);
+    if (rc) return rc;
+    a.order = d_order2.p;
+    a.n_order = k;
+    if ((e = hipMemsetAsync(d_trace_cursor.p, 0, 8, st))) return hipfail(e, "estep");
+    hipEventRecord(ev[0], st);
+    if ((e = launch_estep(a, grid, estep_nw, st))) return hipfail(e, "estep_forward launch");
+    hipEventRecord(ev[1], st);
+    if ((rc = read_status(order, k, true))) return rc;
+    float ms = 0;
+    hipEventElapsedTime(&ms, ev[0], ev[1]);
+    ms_fwd += ms;
+    bool ovf_trace = false;
+    for (int q = 0; q < k; ++q) {
+      const int s = h_status[order[pos + q]];
+      if (s == EST_NO_HEAD_PATTERN) return fail(HMC_ENOPATTERN, "Can not find matching pattern!");
+      if (s == EST_OVERFLOW_FRONTIER) {
+        if (fcap >= F_MAX) return fail(HMC_EUNSUPPORTED, "frontier exceeds %d states", F_MAX);
+        fcap = (int)std::min<int64_t>(F_MAX, (int64_t)fcap * 4);  // x4: each overflow costs a whole pass
+        return ESTEP_RESTART;
+      }
+      if (s == EST_OVERFLOW_TRACE) ovf_trace = true;
+    }
+    if (ovf_trace) {
+      if (d_trace.n < trace_budget) {  // grow the store before splitting the group
+        if ((rc = ensure_store(d_trace, std::min<uint64_t>(trace_budget, d_trace.n * 4), trace_budget, "trace store")))
+          return rc;
+        continue;
+      }
+      if (k == 1) return fail(HMC_ENOMEM, "trace store too small for one individual");
+      batch = std::max(1, k / 2);
+      continue;
+    }
+    if ((rc = traceback_group(k))) return rc;
+    pos += k;
+  }
+  return HMC_OK;
+}
+
+int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
+  const int S = this->S(), n = nloc(), L = pan.L;
+  int32_t *dstatus = exact ? d_xstatus.p : d_status.p;
+  int dev_cu = 256;
+  hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, device);
+  const int G = std::max(1, std::min(waves > 0 ? waves : dev_cu * std::max(8, lds_waves_per_cu), n));
+  hipError_t e;
+  float ms = 0;
+  std::vector<int32_t> pending(order), sset, rest;
+  std::vector<unsigned long long> rneed(n, 0), tneed(n, 0), base(n, 0), rsz(n, 0);
+  std::vector<int32_t> fbig(n, 0);  // largest frontier of each individual (structure pass)
+  // Every individual gets its own record region: its exact size once a pass
+  // has measured it (`exact_need`), else an estimate — the previous E-step's
+  // size when the model is of the same scale, or the records-per-cost ratio
+  // of the individuals measured so far.  A region that turns out too small
+  // only defers that individual (it keeps walking without writing and
+  // reports its exact size), so no pass is ever repeated in full.
+  std::vector<char> exact_need(n, 0);
+  std::vector<unsigned long long> est(n, 0);
+  const bool prev_ok = !exact && (int)prev_rneed.size() == n && prev_P > 0 && P < 2 * (int64_t)prev_P &&
+                       2 * (int64_t)P > prev_P;
+  if (prev_ok)
+    for (int i = 0; i < n; ++i) est[i] = prev_rneed[i] + prev_rneed[i] / 10 + 64;
+  bool have_est = prev_ok;
+  int rc;
+  while (!pending.empty()) {
+    // ---- pass 1: structure records --------------------------------------
+    int np = (int)pending.size();
+    {
+      uint64_t r = 0, t = 0;
+      int k = 0;
+      // the first pass spans the whole cost range and later estimates use the
+      // measured individuals nearest in cost (cfg 3 E1 after E5: 7.1 -> 5.9 s,
+      // deferred 1 713 -> 12 per group, profiles/r02/e1_groups/)
+      if (!have_est) {  // nothing measured yet: 4 per CU share the store evenly
+        k = std::min(np, 4 * dev_cu);
+        if (np > k) {  // every np/k-th of the heaviest-first list
+          std::vector<int32_t> pick, other;
+          pick.reserve(k);
+          other.reserve(np - k);
+          for (int q = 0; q < np; ++q)
+            ((int64_t)q * k / np != (int64_t)(q - 1) * k / np || q == 0 ? pick : other).push_back(pending[q]);
+          pending = pick;
+          pending.insert(pending.end(), other.begin(), other.end());
+          k = (int)pick.size();
+        }
+        const uint64_t share = rec_budget / (uint64_t)k;
+        for (int q = 0; q < k; ++q) {
+          base[pending[q]] = (uint64_t)q * share;
+          rsz[pending[q]] = share;
+        }
+        r = share * (uint64_t)k;
+      } else {  // the prefix whose regions (and measured traces) fit the budgets
+        uint64_t r_est = 0;
+        while (k < np) {
+          const int bi = pending[k];
+          const uint64_t need = exact_need[bi] ? rneed[bi] : std::min<uint64_t>(est[bi], rec_budget);
+          // (estimated traces are not counted: groups cut by records and then
+          // split by exact traces measured faster at cfg 3's E1)
+          const uint64_t tn = exact_need[bi] ? tneed[bi] : 0;
+          if (k > 0 && (r + need > rec_budget || t + tn > trace_budget)) break;
+          rsz[bi] = need;
+          r += need;
+          t += tn;
+          r_est += exact_need[bi] ? 0 : need;
+          ++k;
+        }
+        // the store left over goes to the estimated regions (up to 3x), so
+        // fewer individuals are deferred to a pass of their own (A/B on one
+        // box, cfg 3: E1 value passes 3.88 -> 3.60 s, E2 structure 218 -> 177 ms)
+        const double grow = r_est > 0 && r < rec_budget
+                                ? std::min(3.0, 1.0 + (double)(rec_budget - r) / (double)r_est)
+                                : 1.0;
+        r = 0;
+        for (int q = 0; q < k; ++q) {
+          const int bi = pending[q];
+          if (!exact_need[bi]) rsz[bi] = std::min<uint64_t>((uint64_t)((double)rsz[bi] * grow), rec_budget);
+          if (r + rsz[bi] > rec_budget) rsz[bi] = rec_budget - r;
+          base[bi] = r;
+          r += rsz[bi];
+        }
+      }
+      np = k;
+      rec_words = r;
+      std::vector<unsigned long long> rb(n, 0), rs(n, 0);
+      for (int q = 0; q < np; ++q) {
+        rb[pending[q]] = base[pending[q]];
+        rs[pending[q]] = rsz[pending[q]];
+      }
+      if ((e = hipMemcpyAsync(d_rbase.p, rb.data(), (size_t)n * 8, hipMemcpyHostToDevice, st)) ||
+          (e = hipMemcpyAsync(d_recsz.p, rs.data(), (size_t)n * 8, hipMemcpyHostToDevice, st)))
+        return hipfail(e, "estep");
+    }
+    const int hcap1 = next_pow2(2 * fcap);
+    // (exact records pack a locus's contribution count in 22 bits, R[3] = C << 10 | npairs)
+    const int ccap1 = (int)std::min<int64_t>(exact ? EXACT_C_MAX : INT32_MAX / 2, (int64_t)ccap_mult * fcap);
+    // Structure pass over ids[0, np_) in the record regions set above (d_rbase /
+    // d_recsz).  prune_: with extend()'s forward test (HaploBuilder.cpp:237),
+    // for the individuals the value pass found underflowing.
+    auto structure_pass = [&](const int32_t *ids, int np_, bool prune_) -> int {
+      int rc;
+      hipError_t e;
+      float ms = 0;
+      // structure pass: one wave per individual; 12 per CU (3 per SIMD at 145
+      // VGPRs) above 8 per CU, so cfg 3's E1 groups of 2 200-2 700 run in one
+      // round (profiles/r02/e1_groups/: 603-658 -> 484-586 ms per group).  On a
+      // model larger than the panel (the genotype-mined M0: 2.5 patterns per
+      // individual-locus at cfg 3, 0.3 later) frontiers are large (cfg 3 E1:
+      // 470 states per locus, 80 % of them past a one-wave block's LDS tier):
+      // four waves per individual, two per CU (each block's LDS tier holds
+      // more of the frontier: cfg 3 E1 structure 1.65 -> 1.32 s against three
+      // per CU, profiles/r03/e1/e1_s1shapes.log)
+      const bool heavy_model = (double)P > (double)pan.N * (double)pan.L;
+      // (a heavy group of at most one individual per CU — cfg 4's per-rank E1,
+      // records of ~250 MB per individual — takes the whole CU: 16 waves)
+      const int nw1 = s1_nw > 0 ? s1_nw : (heavy_model ? (np_ <= dev_cu ? 16 : 4) : 1);
+      const int bpc1 = s1_ipc > 0 ? s1_ipc
+                                  : (nw1 == 16 ? 1 : (nw1 == 4 ? 2 : (np_ > 8 * dev_cu ? 12 : (np_ > 4 * dev_cu ? 8 : 4))));
+      const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1, nw1, prune_);
+      // (huge frontiers: fewer resident individuals rather than scratch past SCRATCH_MAX)
+      const int grid1 = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::min(np_, dev_cu * bpc1), SCRATCH_MAX / per1));
+      // the scratch first: both stores are dead here (the groups before have
+      // been traced back), so they give way to it when HBM is short
+      // (a prune re-run runs between a value pass and its traceback: both stores are live)
+      if ((e = scratch_ensure(d_scr1, per1 * grid1, !prune_, !prune_)) || (e = d_rec_off.ensure((size_t)n * (L + 1))) ||
+          (e = d_rec_cursor.ensure(1)) || (e = hipMemsetAsync(d_rec_cursor.p, 0, 8, st)))
+        return hipfail(e, "estep pass-1 alloc");
+      if ((rc = ensure_store(d_rec, rec_words, rec_budget, "record store"))) return rc;
+      if ((rc = upload_order(d_order, ids, np_))) return rc;
+      StructArgs s1;
+      s1.pan = dev_panel();
+      s1.mod = dev_model();
+      s1.S = S;
+      s1.indiv_begin = i0;
+      s1.order = d_order.p;
+      s1.n_order = np_;
+      s1.scratch = d_scr1.p;
+      s1.scratch_stride = per1;
+      s1.fcap = fcap;
+      s1.hcap = hcap1;
+      s1.ccap = ccap1;
+      s1_tier(160 * 1024 / bpc1 - 256, pan.amax, nw1, s1.lds_fc, s1.lds_hc, s1.lds_cc);
+      s1.rec = d_rec.p;
+      s1.rec_cap = d_rec.n;
+      s1.rec_cursor = d_rec_cursor.p;
+      s1.rec_base = d_rbase.p;
+      s1.rec_size = d_recsz.p;
+      s1.rec_off = d_rec_off.p;
+      s1.rec_need = d_rneed.p;
+      s1.trace_need = d_tneed.p;
+      s1.status = dstatus;
+      s1.re_count = exact ? d_xre.p : d_re.p;
+      s1.fmax = exact ? d_xfmax.p : d_fmax.p;
+      s1.max_states = d_maxst.p;
+      s1.stamps = d_stamps.p + 20;
+      s1.exact = exact;
+      s1.prune = prune_;
+      if ((e = d_nextq.ensure(2)) || (e = hipMemsetAsync(d_nextq.p, 0, 8, st))) return hipfail(e, "estep");
+      s1.next_q = d_nextq.p;
+      hipEventRecord(ev[0], st);
+      if ((e = launch_estep_structure(s1, grid1, nw1, st))) return hipfail(e, "estep_structure launch");
+      hipEventRecord(ev[1], st);
+      if ((e = hipMemcpyAsync(rneed.data(), d_rneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
+          (e = hipMemcpyAsync(tneed.data(), d_tneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
+          (e = hipMemcpyAsync(fbig.data(), s1.fmax, (size_t)n * 4, hipMemcpyDeviceToHost, st)))
+        return hipfail(e, "estep_structure");
+      if ((rc = read_status(pending, np_, false, dstatus))) return rc;
+      hipEventElapsedTime(&ms, ev[0], ev[1]);
+      if (prune_) {
+        ms_fb += ms;
+      } else {
+        ms_s1 += ms;
+        ++n_struct_passes;
+      }
+      return HMC_OK;
+    };
+    if ((rc = structure_pass(pending.data(), np, false))) return rc;
+    if (debug_mem) {
+      int ndef = 0;
+      uint64_t rsum = 0, rmax = 0, tsum = 0, rres = 0;
+      for (int q = 0; q < np; ++q) {
+        const int bi = pending[q];
+        ndef += h_status[bi] == EST_OVERFLOW_REC ? 1 : 0;
+        rsum += rneed[bi];
+        rmax = std::max<uint64_t>(rmax, rneed[bi]);
+        tsum += tneed[bi];
+        rres += rsz[bi];
+      }
+      fprintf(stderr, "[hmc] structure pass %d: %d individuals, %.1f ms; deferred %d, records need %.2f GB (max %.1f MB, "
+              "reserved %.2f GB), traces %.2f GB\n", n_struct_passes, np, ms, ndef, rsum * 4e-9, rmax * 4e-6, rres * 4e-9,
+              tsum * 4e-9);
+    }
+    sset.clear();
+    rest.clear();
+    for (int q = 0; q < np; ++q) {
+      const int bi = pending[q], s = h_status[bi];
+      if (s == EST_NO_HEAD_PATTERN) return fail(HMC_ENOPATTERN, "Can not find matching pattern!");
+      if (s == EST_OVERFLOW_CONTRIB) {  // missing genotypes: up to amax^2 contributions per state
+        if ((int64_t)ccap_mult * fcap >= INT32_MAX / 2) return fail(HMC_EUNSUPPORTED, "too many contributions at a locus");
+        if (exact && ccap1 >= EXACT_C_MAX)
+          return fail(HMC_EUNSUPPORTED, "exact M-step: more than %d contributions at a locus", EXACT_C_MAX);
+        ccap_mult *= 2;
+        return ESTEP_RESTART;
+      }
+      if (s == EST_OVERFLOW_FRONTIER) {  // (deferring only these individuals measured slower)
+        if (fcap >= F_MAX) return fail(HMC_EUNSUPPORTED, "frontier exceeds %d states", F_MAX);
+        if (debug_mem) fprintf(stderr, "[hmc] frontier over %d states: capacity x4, E-step restarts\n", fcap);
+        fcap = (int)std::min<int64_t>(F_MAX, (int64_t)fcap * 4);  // x4: each overflow costs a whole pass
+        return ESTEP_RESTART;
+      }
+      if (s == EST_OVERFLOW_REC) {
+        if (exact_need[bi]) return fail(HMC_EHIP, "record store overflow with exact sizes");
+        rest.push_back(bi);
+      } else {
+        sset.push_back(bi);
+      }
+      exact_need[bi] = 1;
+    }
+    for (int q = np; q < (int)pending.size(); ++q) rest.push_back(pending[q]);
+    // estimates for the individuals not measured yet: records per unit of
+    // cost of those measured (after a pass where estimates fell short, or
+    // when there were none)
+    {
+      int deferred = 0;
+      double rs_ = 0, cs = 0;
+      for (int i = 0; i < n; ++i)
+        if (exact_need[i]) {
+          rs_ += (double)rneed[i];
+          cs += (double)std::max(1, h_cost[i]);
+        }
+      for (int q = 0; q < np; ++q) deferred += h_status[pending[q]] == EST_OVERFLOW_REC ? 1 : 0;
+      if (!have_est || deferred * 10 > np) {
+        const double ratio = cs > 0 ? rs_ / cs : 0.0;
+        std::vector<std::pair<int, double>> cr;  // (cost, records per cost) of the measured
+        for (int i = 0; i < n; ++i)
+          if (exact_need[i]) cr.emplace_back(std::max(1, h_cost[i]), (double)rneed[i] / std::max(1, h_cost[i]));
+        std::sort(cr.begin(), cr.end());
+        for (int bi : rest) {
+          if (exact_need[bi]) continue;
+          const int c = std::max(1, h_cost[bi]);
+          if (cr.empty()) {
+            est[bi] = (uint64_t)(1.25 * ratio * c) + 64;
+            continue;
+          }
+          // the largest ratio among the 4 measured nearest in cost on each side
+          const int at = (int)(std::lower_bound(cr.begin(), cr.end(), std::make_pair(c, -1.0)) - cr.begin());
+          double q = 0.0;
+          for (int u = std::max(0, at - 4); u < std::min((int)cr.size(), at + 4); ++u) q = std::max(q, cr[u].second);
+          est[bi] = (uint64_t)(1.1 * q * c) + 64;
+        }
+        have_est = true;
+      }
+    }
+    // ---- pass 2: values, in groups whose traces fit the store -------------
+    size_t pos = 0;
+    while (pos < sset.size()) {
+      uint64_t t = 0;
+      size_t k = 0;
+      while (pos + k < sset.size() && (k == 0 || t + tneed[sset[pos + k]] <= trace_budget)) {
+        base[sset[pos + k]] = t;
+        t += tneed[sset[pos + k]];
+        ++k;
+      }
+      // traces over the budget by a few individuals while structure groups
+      // still follow: those join the next group (re-walked there, exact sizes
+      // known) instead of a value pass of their own, which would cost one
+      // heavy individual's whole latency (cfg 3 E1: 61-78 individuals,
+      // 230-270 ms each, profiles/r02/e1_groups/)
+      if (pos == 0 && !exact && !rest.empty() && k < sset.size() && 4 * (sset.size() - k) <= sset.size()) {
+        rest.insert(rest.begin(), sset.begin() + (std::ptrdiff_t)k, sset.end());
+        sset.resize(k);
+      }
+      if ((rc = ensure_store(d_trace, std::max<uint64_t>(t, 1), trace_budget, "trace store"))) return rc;
+      std::vector<unsigned long long> tb(n, 0);
+      for (size_t q = 0; q < k; ++q) tb[sset[pos + q]] = base[sset[pos + q]];
+      if ((e = hipMemcpyAsync(d_tbase.p, tb.data(), (size_t)n * 8, hipMemcpyHostToDevice, st)))
+        return hipfail(e, "estep");
+      if ((rc = upload_order(d_order2, sset.data() + pos, (int)k))) return rc;
+      if (exact) {
+        // individuals whose forward likelihood underflows: records rebuilt with
+        // extend()'s forward test (HaploBuilder.cpp:237, 291-314) before the walk
+        auto rerun = [&](std::vector<int32_t> &ids) { return structure_pass(ids.data(), (int)ids.size(), true); };
+        if ((rc = exact_group(sset.data() + pos, (int)k, rerun))) return rc;
+        pos += k;
+        continue;
+      }
+      // by individuals per CU (cfg 3 and its rank shards, tools/shard_shapes.py,
+      // profiles/r02/shard_shapes/): 1:16 from 32 per CU (10 000: 557 vs 615 ms
+      // at 2:8), 2:8 from 8 (4 994: 290 vs 333 ms at 1:16), else 3:8 (1 239:
+      // 101 vs 112 ms at 2:8)
+      // (1:20 runs the 5-waves-per-SIMD build: 505-514 vs 535-558 ms at
+      // 1:16 for cfg 3's E3, profiles/r02/values_ab/)
+      // Heavy individuals (the first E-step on the genotype-mined model: cfg 3's
+      // E1 averages ~3 000 record words per locus against ~650 later) take 4
+      // waves each, 4 per CU: more selection segments per individual and a
+      // 4x larger LDS frontier tier (cfg 3 E1 value passes 3.84 -> 2.99 s,
+      // profiles/r03/e1_shapes/).
+      double rw = 0;
+      for (size_t q = 0; q < k; ++q) rw += (double)rneed[sset[pos + q]];
+      const bool heavy = rw / ((double)k * L) > 1500.0;
+      // Heavy groups too small to give every CU four individuals (records and
+      // traces of hundreds of MB each: cfg 4's per-rank E1 on the 720 M-pattern
+      // M0 runs in groups of ~200) spread the CU's 16 waves over fewer
+      // individuals: more selection segments and LDS per individual.
+      const int per_cu = (int)((k + dev_cu - 1) / dev_cu);
+      const bool small_heavy = heavy && per_cu < 4;
+      // (heavy groups filling the GPU: 8 waves x 2 per CU, cfg 3 E1 values
+      // 2.95 -> 2.68 s against 4 x 4, profiles/r03/e1/e1_wide.log)
+      int vnw = vp_nw > 0 ? vp_nw
+                          : (small_heavy ? 16 / per_cu
+                                         : (heavy ? 8 : ((int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3))));
+      int vipc = vp_ipc > 0 ? vp_ipc
+                            : (small_heavy ? per_cu
+                                           : (vnw == 1 ? 20 : (vnw >= 8 ? 2 : (vnw >= 4 ? 4 : 8))));  // a half-given shape completes by the same rule
+      // the HBM tier of the value frontiers holds the group's largest
+      // frontier (pass 1 measured it), not the structure pass's capacity
+      int fgrp = 1;
+      for (size_t q = 0; q < k; ++q) fgrp = std::max(fgrp, (int)fbig[sset[pos + q]]);
+      fgrp = std::min(fcap, (fgrp + 63) & ~63);
+      // two links per lane (cfg 3: E1 values 2.68 -> 2.34 s, E2 ~3 % less)
+      const bool pair = !value_fast && S <= 16 && (value_pair == 2 || (value_pair == 1 && heavy));
+      // Dataflow value pass (estep_df.hip): one wave walks the loci and
+      // builds the lists, the others run the chains of adds of any open locus.
+      DfShape df;
+      const bool use_df = !value_fast && S <= 32 && (value_pass == VP_DATAFLOW || (value_pass == VP_AUTO && df_auto(heavy))) &&
+                          df_shape(S, pair, heavy, small_heavy, per_cu, fgrp, df);
+      if (use_df) {
+        vnw = df.nw;
+        vipc = df.ipc;
+      }
+      const int G2 = std::max(1, std::min(waves > 0 ? waves : dev_cu * vipc, n));
+      // register budget: 5 waves per SIMD once the shape asks for more than 16 per CU
+      const int vwpe = vnw * vipc > 16 && vnw * vipc <= 20 ? 5 : 4;
+      const size_t per2 = use_df ? estep_df_scratch_bytes(fgrp, S, df.R) : estep_s2_scratch_bytes(fgrp, S);
+      const int grid2 = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::min<int>(G2, (int)k), SCRATCH_MAX / per2));
+      if ((e = scratch_ensure(d_scr2, per2 * grid2, false, true))) return hipfail(e, "estep pass-2 scratch");
+      if ((rc = ensure_store(d_trace, std::max<uint64_t>(t, 1), trace_budget, "trace store"))) return rc;
+      ValueArgs v;
+      v.S = S;
+      v.L = L;
+      v.head_len = head_len;
+      v.order = d_order2.p;
+      v.n_order = (int)k;
+      v.rec = d_rec.p;
+      v.rec_off = d_rec_off.p;
+      v.scratch = d_scr2.p;
+      v.scratch_stride = per2;
+      v.fcap = fgrp;
+      v.lds_fc = use_df ? df.fc : s2_tier(S, vnw, vipc, pair);
+      v.trace = d_trace.p;
+      v.trace_cap = d_trace.n;
+      v.trace_cursor = d_trace_cursor.p;
+      v.trace_base = d_tbase.p;
+      v.loc_off = d_loc_off.p;
+      v.status = d_status.p;
+      v.total = d_total.p;
+      v.ncand = d_ncand.p;
+      v.cand_state = d_cstate.p;
+      v.cand_idx = d_cidx.p;
+      v.prior = d_prior.p;
+      v.posterior = d_post.p;
+      v.weight = d_weight.p;
+      v.cost = d_cost.p;
+      v.stamps = d_stamps.p;
+      v.next_q = d_nextq.p + 1;
+      if ((e = hipMemsetAsync(d_nextq.p + 1, 0, 4, st))) return hipfail(e, "estep");
+      const bool fast = value_fast && S <= 32;  // lists longer than a wavefront: exact order only
+      hipEventRecord(ev[0], st);
+      if (use_df) {
+        if ((e = launch_estep_values_df(v, grid2, vnw, vwpe, pair, df.R, df.qcap, st)))
+          return hipfail(e, "estep_values_df launch");
+      } else if ((e = launch_estep_values(v, grid2, vnw, fast, vwpe, st, pair))) {
+        return hipfail(e, "estep_values launch");
+      }
+      last_value_df = use_df;
+      hipEventRecord(ev[1], st);
+      if ((rc = read_status(sset, (int)k, true))) return rc;
+      hipEventElapsedTime(&ms, ev[0], ev[1]);
+      ms_s2 += ms;
+      ++n_value_passes;
+      if (debug_mem)
+        fprintf(stderr, "[hmc] value pass %d: %zu individuals, %.1f ms\n", n_value_passes, k, ms);
+      // ---- ties: individuals whose result would depend on the libstdc++ list
+      // order re-run on the exact value pass, in their own trace regions
+      std::vector<int> h_order;
+      for (size_t q = 0; q < k; ++q)
+        if (h_status[sset[pos + q]] == EST_NEEDS_ORDER) h_order.push_back(sset[pos + q]);
+      n_order_redo += (int)h_order.size();
+      if (!h_order.empty()) {
+        const int nr = (int)h_order.size();
+        if ((e = d_redo.ensure(nr))) return hipfail(e, "estep order re-run");
+        if ((rc = upload_order(d_redo, h_order.data(), nr))) return rc;
+        ValueArgs v2 = v;
+        v2.order = d_redo.p;
+        v2.n_order = nr;
+        if ((e = hipMemsetAsync(d_nextq.p + 1, 0, 4, st))) return hipfail(e, "estep");
+        hipEventRecord(ev[0], st);
+        if ((e = launch_estep_values(v2, std::max(1, std::min(G2, nr)), vnw, false, vwpe, st)))
+          return hipfail(e, "estep_values launch");
+        hipEventRecord(ev[1], st);
+        if ((rc = read_status(sset, (int)k, true))) return rc;
+        hipEventElapsedTime(&ms, ev[0], ev[1]);
+        ms_s2 += ms;
+        ms_order += ms;
+      }
+      h_redo.clear();
+      for (size_t q = 0; q < k; ++q) {
+        const int bi = sset[pos + q];
+        if (h_status[bi] == EST_OVERFLOW_TRACE) return fail(HMC_EHIP, "trace store overflow with exact sizes");
+        if (h_status[bi] == EST_NEEDS_ORDER) return fail(HMC_EHIP, "exact value pass reported a tie");
+        if (h_status[bi] == EST_DF_STALL) return fail(HMC_EHIP, "dataflow value pass stalled (individual %d)", i0 + bi);
+        if (h_status[bi] == EST_NEEDS_EXACT) h_redo.push_back(bi);
+      }
+      // ---- individuals whose forward likelihood underflowed: the reference
+      // skips a pair with fwd <= 0 (extend(), HaploBuilder.cpp:237), which
+      // changes their structure.  Their records are rebuilt with that test
+      // (structure pass, prune) in their own regions — a subset of the
+      // frontiers just walked, so they fit — and their lists re-built.
+      n_fallback += (int)h_redo.size();
+      if (!h_redo.empty()) {
+        const int nr = (int)h_redo.size();
+        if ((rc = structure_pass(h_redo.data(), nr, true))) return rc;
+        for (int r : h_redo) {
+          const int s = h_status[r];
+          if (s != EST_OK_PRUNED && s != EST_UNRESOLVED)
+            return fail(HMC_EHIP, "underflow re-run: structure status %d (individual %d)", s, i0 + r);
+        }
+        if ((e = d_redo.ensure(nr))) return hipfail(e, "estep underflow re-run");
+        if ((rc = upload_order(d_redo, h_redo.data(), nr))) return rc;
+        ValueArgs v2 = v;
+        v2.order = d_redo.p;
+        v2.n_order = nr;
+        if ((e = hipMemsetAsync(d_nextq.p + 1, 0, 4, st))) return hipfail(e, "estep");
+        hipEventRecord(ev[0], st);
+        if (use_df) {
+          if ((e = launch_estep_values_df(v2, std::max(1, std::min(G2, nr)), vnw, vwpe, pair, df.R, df.qcap, st)))
+            return hipfail(e, "estep_values_df launch");
+        } else if ((e = launch_estep_values(v2, std::max(1, std::min(G2, nr)), vnw, false, vwpe, st, pair))) {
+          return hipfail(e, "estep_values launch");
+        }
+        hipEventRecord(ev[1], st);
+        if ((rc = read_status(sset, (int)k, true))) return rc;
+        hipEventElapsedTime(&ms, ev[0], ev[1]);
+        ms_fb += ms;
+        for (int r : h_redo)
+          if (h_status[r] != EST_OK && h_status[r] != EST_UNRESOLVED)
+            return fail(HMC_EHIP, "underflow re-run: value status %d (individual %d)", h_status[r], i0 + r);
+      }
+      if ((rc = traceback_group((int)k))) return rc;
+      pos += k;
+    }
+    pending.swap(rest);
+  }
+  if (!exact) {
+    prev_rneed = rneed;
+    prev_P = P;
+  }
+  return HMC_OK;
+}
+
+bool Ctx::df_shape(int S, bool pair, bool heavy, bool small_heavy, int per_cu, int fgrp, DfShape &d) const {
+  d.nw = vp_nw > 0 ? std::max(2, vp_nw) : (small_heavy ? std::max(2, 16 / per_cu) : (heavy ? 8 : 2));
+  d.ipc = vp_ipc > 0 ? vp_ipc : (small_heavy ? per_cu : (heavy ? 2 : 8));
+  if (d.nw * d.ipc > 20) d.ipc = std::max(1, 20 / d.nw);
+  d.R = df_ring;
+  const int G = pair ? WAVE / S : WAVE / (2 * S);
+  const int nseg = (d.nw - 1) * G;
+  d.qcap = 64;
+  while (d.qcap < std::max(4 * nseg, heavy ? 512 : 64)) d.qcap *= 2;
+  const int budget = 160 * 1024 / std::max(1, d.ipc) - 256;
+  if ((int)estep_df_lds_bytes(S, 0, d.nw, pair, d.R, d.qcap, fgrp) > budget) return false;
+  int lo = 0, hi = fgrp;  // largest LDS tier that fits
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) / 2;
+    if ((int)estep_df_lds_bytes(S, mid, d.nw, pair, d.R, d.qcap, fgrp) <= budget) lo = mid;
+    else hi = mid - 1;
+  }
+  d.fc = lo;
+  return true;
+}
+
+DevModel Ctx::dev_model() const {
+  DevModel m;
+  m.P = P;
+  m.succ = t_succ.p;
+  m.tp = t_tp.p;
+  m.freq = t_freq.p;
+  m.last = t_last.p;
+  m.n_head = n_head;
+  m.head_len = head_len;
+  m.head_ids = d_head_ids.p;
+  m.head_pat0 = d_head_pat0.p;
+  if (head_len > 1) {
+    m.hf_base = i0;
+    m.hf_off = d_hf_off.p;
+    m.hf_pairs = d_hf_pairs.p;
+    m.hf_status = d_hf_status.p;
+    m.head_al = d_head_al.p;
+  }
+  return m;
+}
+
+int Ctx::resolutions_idx(std::vector<uint8_t> &out) {
+  if (!have_estep) return fail(HMC_EARG, "no E-step has run");
+  const int n = nloc(), L = pan.L;
+  hipError_t e;
+  if ((e = d_res.ensure((size_t)n * 2 * L))) return hipfail(e, "resolutions");
+  if ((e = launch_gather_resolutions(d_rows.p, L, d_sbase.p, d_ncand.p, d_geno_im.p, i0, n, d_res.p, st)))
+    return hipfail(e, "resolutions");
+  out.resize((size_t)n * 2 * L);
+  if ((e = hipMemcpyAsync(out.data(), d_res.p, out.size(), hipMemcpyDeviceToHost, st)) ||
+      (e = hipStreamSynchronize(st)))
+    return hipfail(e, "resolutions");
+  return HMC_OK;
+}
+}  // namespace hmc
