@@ -228,6 +228,12 @@ int hmc_set_value_pass(hmc_ctx *h, int mode, int ring) {
   return HMC_OK;
 }
 
+int hmc_set_structure_pass(hmc_ctx *h, int version) {
+  if (!h || version < 0 || version > 2) return HMC_EARG;  // 0 = automatic
+  h->c.structure_pass_version = version == 0 ? 1 : version;
+  return HMC_OK;
+}
+
 int hmc_last_value_pass(const hmc_ctx *h, int *dataflow) {
   if (!h) return HMC_EARG;
   if (dataflow) *dataflow = h->c.last_value_df ? 1 : 0;

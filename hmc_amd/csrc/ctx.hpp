@@ -822,10 +822,13 @@ struct Ctx {
 
   // LDS tiers of pass 1 (one wave per individual, `budget` bytes): states per
   // frontier, key slots (2x, power of two), contributions per locus (2x).
-  static void s1_tier(int budget, int amax, int nw, int &fc, int &hc, int &cc) {
+  // structure pass: 2 = estep_structure2 (fewer block hand-offs per locus), 1 = estep_structure
+  int structure_pass_version = 1;  // hmc_set_structure_pass
+  static void s1_tier(int budget, int amax, int nw, int &fc, int &hc, int &cc, bool v2 = false) {
     for (int f = 2048; f >= 16; f -= 16) {
       const int h = next_pow2(2 * f), c = 2 * f;
-      if ((int)estep_s1_lds_bytes(f, h, c, amax, nw) <= budget) { fc = f; hc = h; cc = c; return; }
+      const size_t b = v2 ? estep_s1v2_lds_bytes(f, h, c, amax, nw) : estep_s1_lds_bytes(f, h, c, amax, nw);
+      if ((int)b <= budget) { fc = f; hc = h; cc = c; return; }
     }
     fc = 0;
     hc = 16;

@@ -483,7 +483,8 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
       const int nw1 = s1_nw > 0 ? s1_nw : (heavy_model ? (np_ <= dev_cu ? 16 : 4) : 1);
       const int bpc1 = s1_ipc > 0 ? s1_ipc
                                   : (nw1 == 16 ? 1 : (nw1 == 4 ? 2 : (np_ > 8 * dev_cu ? 12 : (np_ > 4 * dev_cu ? 8 : 4))));
-      const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1, nw1, prune_);
+      const bool v2 = structure_pass_version == 2;
+      const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1, v2 ? 2 : nw1, prune_);
       // (huge frontiers: fewer resident individuals rather than scratch past SCRATCH_MAX)
       const int grid1 = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::min(np_, dev_cu * bpc1), SCRATCH_MAX / per1));
       // the scratch first: both stores are dead here (the groups before have
@@ -506,7 +507,7 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
       s1.fcap = fcap;
       s1.hcap = hcap1;
       s1.ccap = ccap1;
-      s1_tier(160 * 1024 / bpc1 - 256, pan.amax, nw1, s1.lds_fc, s1.lds_hc, s1.lds_cc);
+      s1_tier(160 * 1024 / bpc1 - 256, pan.amax, nw1, s1.lds_fc, s1.lds_hc, s1.lds_cc, v2);
       s1.rec = d_rec.p;
       s1.rec_cap = d_rec.n;
       s1.rec_cursor = d_rec_cursor.p;
@@ -525,7 +526,8 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
       if ((e = d_nextq.ensure(2)) || (e = hipMemsetAsync(d_nextq.p, 0, 8, st))) return hipfail(e, "estep");
       s1.next_q = d_nextq.p;
       hipEventRecord(ev[0], st);
-      if ((e = launch_estep_structure(s1, grid1, nw1, st))) return hipfail(e, "estep_structure launch");
+      if ((e = v2 ? launch_estep_structure2(s1, grid1, nw1, st) : launch_estep_structure(s1, grid1, nw1, st)))
+        return hipfail(e, "estep_structure launch");
       hipEventRecord(ev[1], st);
       if ((e = hipMemcpyAsync(rneed.data(), d_rneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
           (e = hipMemcpyAsync(tneed.data(), d_tneed.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||

@@ -727,6 +727,463 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
   S1_FLUSH
 }
 
+// ======================================================= pass 1, v2 ======
+//
+// The same structure records with fewer block-wide hand-offs per locus
+// (estep_structure: ~26 barriers per locus, five per chunk of NT
+// contributions, which the cfg 3 E1 stamps show as the pass's cost).  Each
+// thread owns a contiguous run of the locus's contributions in extendAll
+// order and a contiguous run of the new states, so creation order and each
+// state's contribution order come from three block scans instead of a
+// per-chunk ranking:
+//   1. every contribution: successor key, insert-or-find its slot, and per
+//      slot atomically: the first contribution (min), the count, the sum of
+//      predecessor list lengths;
+//   2. a contribution that is its slot's first creates a state: numbered by
+//      an exclusive scan of those flags in contribution order (= the order in
+//      which addHaploPair creates pairs, HaploBuilder.cpp:246-261);
+//   3. states: first positions by an exclusive scan of their counts; a slot
+//      with one contribution places it directly, the others append to their
+//      state's segment and take as rank the number of members before them.
+// Slot fields (K1Keys with nw = 2: the lane-mask words hold firstc, ns, fill).
+__host__ __device__ inline K1Plan k2s_plan(int fc, int hc, int cc, int npm, int nw) {
+  K1Plan p;
+  int o = 0;
+  auto take = [&](int bytes) { int r = o; o += (bytes + 15) & ~15; return r; };
+  p.o_pairs = take((npm + 2) * 4 + 3 * npm);
+  p.o_bucket = take(NBUCKET * 4);
+  p.o_red = take((2 * nw + 8) * 4 + nw * 8 + 16);
+  p.o_front[0] = take(F_NARR * fc * 4);
+  p.o_front[1] = take(F_NARR * fc * 4);
+  p.o_keys = take(hc * k1_slot_bytes(2));
+  p.o_contrib = take(3 * cc * 4);
+  p.bytes = o;
+  return p;
+}
+size_t estep_s1v2_lds_bytes(int fc, int hc, int cc, int amax, int nw) {
+  return (size_t)k2s_plan(fc, hc, cc, amax * (amax + 1) / 2, nw).bytes;
+}
+
+enum { C2_SR, C2_SL, C2_AUX };  // contribution: (pred | reversed), slot (NONE: no pair), segment scratch
+constexpr uint32_t FIRST_NONE = 0xFFFFFFFFu;
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) void estep_structure2(StructArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  constexpr int NT = 64 * NW;
+  const int npm = a.pan.amax * (a.pan.amax + 1) / 2;
+  const K1Plan plan = k2s_plan(a.lds_fc, a.lds_hc, a.lds_cc, npm, NW);
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;
+  const Blk<NW> B{(int *)(smem + plan.o_red), tid, lane, wv};
+  const int S = a.S, L = a.pan.L, amax = a.pan.amax, hl = a.mod.head_len;
+  int *pr_off = (int *)(smem + plan.o_pairs);  // [npm+2]; [npm+1] = npairs
+  uint8_t *pr_x = (uint8_t *)(pr_off + npm + 2);
+  uint8_t *pr_y = pr_x + npm;
+  uint8_t *pr_o = pr_y + npm;
+  int *bucket = (int *)(smem + plan.o_bucket);
+
+  char *sp = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
+  const int gs = (int)k1_front_words(a.fcap);
+  const IdFront FA{(uint32_t *)(smem + plan.o_front[0]), (uint32_t *)sp, a.lds_fc, gs};
+  sp += al256(F_NARR * (size_t)gs * 4);
+  const IdFront FB{(uint32_t *)(smem + plan.o_front[1]), (uint32_t *)sp, a.lds_fc, gs};
+  sp += al256(F_NARR * (size_t)gs * 4);
+  const K1Keys K{smem + plan.o_keys, (unsigned char *)sp, a.lds_hc, a.hcap, 2};
+  sp += al256((size_t)a.hcap * k1_slot_bytes(2));
+  const CTier CT{(uint32_t *)(smem + plan.o_contrib), (uint32_t *)sp, a.lds_cc, a.ccap};
+  sp += al256((size_t)a.ccap * 12);
+  double *fwx = a.prune ? (double *)sp : nullptr, *fwy = a.prune ? (double *)sp + al256((size_t)a.fcap * 8) / 8 : nullptr;
+  // slot fields: atomically updated ones are read past the vector L1 in the HBM tier
+  auto f_first = [&](uint32_t sl) { return (uint32_t *)K.lanes(sl); };
+  auto f_ns = [&](uint32_t sl) { return (uint32_t *)K.lanes(sl) + 1; };
+  auto f_fill = [&](uint32_t sl) { return (uint32_t *)K.lanes(sl) + 2; };
+  auto rd = [&](uint32_t *p, uint32_t sl) -> uint32_t { return sl < (uint32_t)K.hc ? *p : ld_acq(p); };
+
+  auto reset_tables = [&]() {
+    for (int h = tid; h < K.hc + a.hcap; h += NT) {
+      *K.key(h) = KEY_EMPTY;
+      *f_first(h) = FIRST_NONE;
+      *f_ns(h) = 0;
+      *f_fill(h) = 0;
+      *K.cnt(h) = 0;
+    }
+    __threadfence();
+    B.sync();
+  };
+  reset_tables();
+
+  auto next_q = [&]() -> int {
+    int t = 0;
+    if (tid == 0) t = atomicAdd(a.next_q, 1);
+    return B.bcast(t) + (int)gridDim.x;
+  };
+  for (int q = blockIdx.x; q < a.n_order; q = next_q()) {
+    const int bi = a.order[q];
+    const int gi = a.indiv_begin + bi;
+    const uchar2 *g = a.pan.geno_im + (size_t)gi * L;
+    unsigned long long *roff = a.rec_off + (size_t)bi * (L + 1);
+    int status = EST_OK;
+    unsigned long long re = 0;
+    unsigned long long rcur = a.rec_base ? a.rec_base[bi] : 0;
+    unsigned long long rend = a.rec_base ? (a.rec_size ? rcur + a.rec_size[bi] : ~0ull) : 0;
+    bool counting = false;
+    unsigned long long rneed = 0, tneed = 0;
+    IdFront X = FA, Y = FB;
+
+    // ---- initHeadList (HaploBuilder.cpp:153-224), as in estep_structure ----
+    int Fp0 = 0, st0 = EST_OK;
+    if (tid == 0 && hl > 1) {
+      const int li = gi - a.mod.hf_base;
+      st0 = a.mod.hf_status[li];
+      for (uint32_t t = a.mod.hf_off[li]; t < a.mod.hf_off[li + 1] && st0 == EST_OK; ++t) {
+        if (Fp0 >= a.fcap) { st0 = EST_OVERFLOW_FRONTIER; break; }
+        *X.at(F_LO, Fp0) = a.mod.hf_pairs[2 * t];
+        *X.at(F_HI, Fp0) = a.mod.hf_pairs[2 * t + 1];
+        *X.at(F_NL, Fp0) = 1;
+        ++Fp0;
+      }
+    }
+    if (tid == 0 && hl == 1) {
+      const uchar2 g0 = g[0];
+      const bool m0 = g0.x == MISSING, m1 = g0.y == MISSING;
+      for (int hix = 0; hix < a.mod.n_head; ++hix) {
+        const uint32_t head = a.mod.head_ids[hix];
+        const uint8_t ah = a.mod.last[head];
+        if (!(m0 || m1 || g0.x == ah || g0.y == ah)) continue;
+        const bool hasAllele = g0.x == ah || g0.y == ah;
+        const bool expand = (m0 && m1) || ((m0 || m1) && hasAllele);
+        const int nx = expand ? (int)a.pan.anum[0] : 1;
+        for (int k = 0; k < nx; ++k) {
+          uint32_t xk;
+          if (expand) {
+            if (!(a.pan.afreq[k] > 0)) continue;
+            xk = (uint32_t)k;
+          } else {
+            xk = (!m0 && !m1 && g0.x != g0.y) ? ((ah == g0.x) ? g0.y : g0.x) : g0.x;
+          }
+          const uint32_t hq = xk == MISSING ? a.mod.head_pat0[amax] : a.mod.head_pat0[xk];
+          if (hq == NONE) { st0 = EST_NO_HEAD_PATTERN; break; }
+          if (hq < head) continue;
+          if (Fp0 >= a.fcap) { st0 = EST_OVERFLOW_FRONTIER; break; }
+          *X.at(F_LO, Fp0) = head;
+          *X.at(F_HI, Fp0) = hq;
+          *X.at(F_NL, Fp0) = 1;
+          ++Fp0;
+        }
+        if (st0 != EST_OK) break;
+      }
+    }
+    int Fp = B.bcast(Fp0);
+    status = B.bcast(st0);
+    int fbig = Fp;
+    B.sync();
+    if (status == EST_OK) {
+      const unsigned long long words = 4 + 4ull * Fp + 1 + (a.exact ? 2ull * Fp : 0ull);
+      rneed += (words + 1) & ~1ull;
+      tneed += a.exact ? 4ull * Fp + 2 : trace_locus_words((unsigned long long)Fp, S);
+      const unsigned long long o = rec_alloc<NW>(a, B, rcur, rend, words);
+      if (o == REC_NONE) {
+        counting = true;
+        if (tid == 0) re += (unsigned long long)Fp;
+      } else {
+        uint32_t *R = a.rec + o;
+        double *Rtp = (double *)(R + 4);
+        uint32_t *Rhd = R + 4 + 2 * Fp, *Rcb = Rhd + Fp;
+        for (int t = tid; t < Fp; t += NT) {
+          const uint32_t lo = *X.at(F_LO, t), hi = *X.at(F_HI, t);
+          Rtp[t] = a.mod.freq[lo] * a.mod.freq[hi];
+          Rhd[t] = (uint32_t)a.mod.last[lo] | (uint32_t)a.mod.last[hi] << 8 | 1u << 16 | (lo == hi ? 1u << 24 : 0u);
+          Rcb[t] = 0;
+          if (a.exact) {
+            Rcb[Fp + 1 + t] = lo;
+            Rcb[2 * Fp + 1 + t] = hi;
+          }
+        }
+        if (tid == 0) {
+          Rcb[Fp] = 0;
+          R[0] = (uint32_t)Fp;
+          R[1] = 0;
+          R[2] = 0;
+          R[3] = 0;
+          roff[hl] = o;
+          re += (unsigned long long)Fp;
+        }
+      }
+    }
+    if (a.prune && status == EST_OK) {
+      for (int t = tid; t < Fp; t += NT) {
+        const uint32_t lo = *X.at(F_LO, t), hi = *X.at(F_HI, t);
+        const double tpv = a.mod.freq[lo] * a.mod.freq[hi];
+        fwx[t] = lo == hi ? tpv : tpv * 2.0;
+      }
+      B.sync();
+    }
+
+    // ---- structure of the forward over loci (HaploBuilder.cpp:47-82) -------
+    for (int i = hl; i < L && status == EST_OK; ++i) {
+      if (Fp == 0) { status = EST_UNRESOLVED; break; }
+      const uchar2 gg = g[i];
+      // allele pairs in extendAll call order; a locus without missing alleles
+      // has one pair, which every thread derives itself (no hand-off)
+      const bool simple = gg.x != MISSING && gg.y != MISSING;
+      if (!simple) {
+        if (tid == 0) {
+          const double *af = a.pan.afreq + (size_t)i * amax;
+          const int an = a.pan.anum[i];
+          int np = 0;
+          auto push = [&](int x, int y) { pr_x[np] = (uint8_t)x; pr_y[np] = (uint8_t)y; pr_o[np] = x == y ? 1 : 2; ++np; };
+          if (gg.x == MISSING && gg.y == MISSING) {
+            for (int j = 0; j < an; ++j)
+              if (af[j] > 0)
+                for (int k = j; k < an; ++k)
+                  if (af[k] > 0) push(j, k);
+          } else if (gg.x == MISSING) {
+            for (int j = 0; j < an; ++j)
+              if (af[j] > 0) push(j, gg.y);
+          } else {
+            for (int j = 0; j < an; ++j)
+              if (af[j] > 0) push(j, gg.x);
+          }
+          int off = 0;
+          for (int p = 0; p < np; ++p) { pr_off[p] = off; off += Fp * pr_o[p]; }
+          pr_off[np] = off;
+          pr_off[npm + 1] = np;
+        }
+        B.sync();
+      }
+      const int npairs = simple ? 1 : pr_off[npm + 1];
+      const int o1 = simple ? (gg.x == gg.y ? 1 : 2) : 0;
+      const int C = simple ? Fp * o1 : pr_off[npairs];
+      if (C > a.ccap) { status = EST_OVERFLOW_CONTRIB; break; }
+      // contribution c -> (predecessor state, orientation, alleles)
+      auto decode = [&](int c, uint32_t &s, uint32_t &x, uint32_t &y) {
+        int oo, local;
+        uint32_t px, py;
+        if (simple) {
+          oo = o1;
+          local = c;
+          px = gg.x;
+          py = gg.y;
+        } else {
+          int p = 0;
+          while (p + 1 < npairs && c >= pr_off[p + 1]) ++p;
+          oo = pr_o[p];
+          local = c - pr_off[p];
+          px = pr_x[p];
+          py = pr_y[p];
+        }
+        const int o = oo == 2 ? (local & 1) : 0;
+        s = oo == 2 ? (uint32_t)(local >> 1) : (uint32_t)local;
+        x = o ? py : px;
+        y = o ? px : py;
+      };
+      const int Q = (C + NT - 1) / NT;  // this thread's contributions: [c0, c1)
+      const int c0 = min(C, tid * Q), c1 = min(C, c0 + Q);
+      // ---- 1. keys, slots; per slot: first contribution, count, predecessor lengths
+      for (int cb = c0; cb < c1; cb += 4) {
+        uint32_t sa[4], sb[4], ss[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          sa[u] = sb[u] = NONE;
+          ss[u] = 0;
+          if (cb + u < c1) {
+            uint32_t x, y;
+            decode(cb + u, ss[u], x, y);
+            const bool live = !a.prune || fwx[ss[u]] > 0.0;  // extend(): fwd <= 0 is not extended (HaploBuilder.cpp:237)
+            if (live) {
+              sa[u] = a.mod.succ[(size_t)*X.at(F_LO, (int)ss[u]) * amax + x];
+              sb[u] = a.mod.succ[(size_t)*X.at(F_HI, (int)ss[u]) * amax + y];
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (cb + u >= c1) continue;
+          const int c = cb + u;
+          const bool valid = sa[u] != NONE && sb[u] != NONE;
+          const bool rev = sa[u] > sb[u];  // addHaploPair: id_a > id_b -> swap, reversed
+          uint32_t slot = NONE;
+          if (valid) {
+            const uint32_t lo = rev ? sb[u] : sa[u], hi = rev ? sa[u] : sb[u];
+            slot = k1_key_slot(K, ((unsigned long long)lo << 32) | hi, key_hash(lo, hi));
+            atomicMin(f_first(slot), (uint32_t)c);
+            atomicAdd(K.cnt(slot), 1u);
+            atomicAdd(f_ns(slot), *X.at(F_NL, (int)ss[u]));
+          }
+          *CT.at(C2_SR, c) = cw_pack(ss[u], rev);
+          *CT.at(C2_SL, c) = slot;
+        }
+      }
+      __threadfence_block();
+      B.sync();
+      // ---- 2. new states in creation order
+      int mynew = 0;
+      for (int c = c0; c < c1; ++c) {
+        const uint32_t sl = *CT.at(C2_SL, c);
+        if (sl != NONE && rd(f_first(sl), sl) == (uint32_t)c) ++mynew;
+      }
+      int Fn = 0;
+      int st = B.scan(mynew, &Fn);
+      if (Fn > a.fcap) { status = EST_OVERFLOW_FRONTIER; break; }
+      if (Fn == 0) { status = EST_UNRESOLVED; break; }
+      for (int c = c0; c < c1; ++c) {
+        const uint32_t sl = *CT.at(C2_SL, c);
+        if (sl != NONE && rd(f_first(sl), sl) == (uint32_t)c) {
+          const unsigned long long key = sl < (uint32_t)K.hc ? *K.key(sl) : ld_acq(K.key(sl));
+          *K.state(sl) = (uint32_t)st;
+          *Y.at(F_LO, st) = (uint32_t)(key >> 32);
+          *Y.at(F_HI, st) = (uint32_t)key;
+          *Y.at(F_SLOT, st) = sl;
+          ++st;
+        }
+      }
+      fbig = Fn > fbig ? Fn : fbig;
+      if (tid < NBUCKET) bucket[tid] = 0;
+      __threadfence_block();
+      B.sync();
+      // ---- 3. states: first positions (scan of counts), list lengths, chains
+      const int QS = (Fn + NT - 1) / NT;
+      const int t0 = min(Fn, tid * QS), t1 = min(Fn, t0 + QS);
+      int mycnt = 0;
+      for (int t = t0; t < t1; ++t) mycnt += (int)rd(K.cnt(*Y.at(F_SLOT, t)), *Y.at(F_SLOT, t));
+      int Cv = 0;
+      int cpos = B.scan(mycnt, &Cv);
+      for (int t = t0; t < t1; ++t) {
+        const uint32_t sl = *Y.at(F_SLOT, t);
+        const int m = (int)rd(K.cnt(sl), sl);
+        *Y.at(F_CB, t) = (uint32_t)cpos;
+        cpos += m;
+        const uint32_t nsum = rd(f_ns(sl), sl);
+        const uint32_t nl = nsum < (uint32_t)S ? nsum : (uint32_t)S;
+        *Y.at(F_NL, t) = nl;
+        re += nl;
+        if (nsum > (uint32_t)S)  // bucket 0 = most contributions
+          atomicAdd(&bucket[NBUCKET - 1 - (m - 1 < NBUCKET - 1 ? m - 1 : NBUCKET - 1)], 1);
+      }
+      const unsigned long long words =
+          4 + 4ull * Fn + 1 + (unsigned long long)Cv + Fn + (a.exact ? (unsigned long long)C + npairs : 0ull);
+      rneed += (words + 1) & ~1ull;
+      tneed += a.exact ? 4ull * Fn + 2 : trace_locus_words((unsigned long long)Fn, S);
+      __threadfence_block();
+      B.sync();
+      const unsigned long long o = counting ? 0 : rec_alloc<NW>(a, B, rcur, rend, words);
+      if (o == REC_NONE) counting = true;
+      uint32_t *R = a.rec + (counting ? 0 : o);  // not dereferenced while counting
+      double *Rtp = (double *)(R + 4);
+      uint32_t *Rhd = R + 4 + 2 * Fn, *Rcb = Rhd + Fn, *Rct = Rcb + Fn + 1, *Rch = Rct + Cv;
+      int nch = 0;
+      {  // every wave scans the 32 bucket counts; wave 0 writes the offsets
+        const int b = lane < NBUCKET ? bucket[lane] : 0;
+        const int incl = wave_incl_scan(b);
+        nch = __shfl(incl, 63);
+        B.sync();
+        if (wv == 0 && lane < NBUCKET) bucket[lane] = incl - b;
+      }
+      // contributions of slots with more than one: into their state's segment
+      for (int c = c0; c < c1; ++c) {
+        const uint32_t sl = *CT.at(C2_SL, c);
+        if (sl != NONE && rd(K.cnt(sl), sl) > 1u) {
+          const uint32_t stt = rd(K.state(sl), sl);
+          const uint32_t pos = atomicAdd(f_fill(sl), 1u);
+          *CT.at(C2_AUX, (int)(*Y.at(F_CB, (int)stt) + pos)) = (uint32_t)c;
+        }
+      }
+      __threadfence_block();
+      B.sync();
+      // the records: per state (creation order) and per contribution (add order)
+      if (!counting) {
+        for (int t = t0; t < t1; ++t) {
+          const uint32_t lo = *Y.at(F_LO, t), hi = *Y.at(F_HI, t), sl = *Y.at(F_SLOT, t);
+          const uint32_t nl = *Y.at(F_NL, t);
+          const uint32_t nsum = rd(f_ns(sl), sl);
+          Rtp[t] = a.mod.tp[lo] * a.mod.tp[hi];  // m_transition_prob, HaploPair.cpp:42
+          Rhd[t] = (uint32_t)a.mod.last[lo] | (uint32_t)a.mod.last[hi] << 8 | nl << 16 | (nsum > (uint32_t)S ? HDR_CHAIN : 0u);
+          Rcb[t] = *Y.at(F_CB, t);
+          if (nsum > (uint32_t)S) {
+            const int m = (int)rd(K.cnt(sl), sl);
+            const int pos = atomicAdd(&bucket[NBUCKET - 1 - (m - 1 < NBUCKET - 1 ? m - 1 : NBUCKET - 1)], 1);
+            Rch[pos] = (uint32_t)t;
+          }
+        }
+        uint32_t *Rout = Rct + Cv + nch;  // exact: contributions in extendAll order, then pair orientations
+        for (int c = c0; c < c1; ++c) {
+          const uint32_t sl = *CT.at(C2_SL, c);
+          const uint32_t w = *CT.at(C2_SR, c);
+          uint32_t stt = NONE;
+          if (sl != NONE) {
+            stt = rd(K.state(sl), sl);
+            const uint32_t m = rd(K.cnt(sl), sl), cb = *Y.at(F_CB, (int)stt);
+            uint32_t rank = 0;
+            if (m > 1u)  // members of the state before this one, in contribution order
+              for (uint32_t k = 0; k < m; ++k) rank += *CT.at(C2_AUX, (int)(cb + k)) < (uint32_t)c ? 1u : 0u;
+            const uint32_t ns = *X.at(F_NL, (int)cw_state(w));
+            Rct[cb + rank] = w | ns << 24;
+          }
+          if (a.exact) Rout[c] = stt == NONE ? NONE : (stt | (w & CW_REV));
+        }
+        if (a.exact)
+          for (int p = tid; p < npairs; p += NT) Rout[C + p] = simple ? (uint32_t)o1 : pr_o[p];
+        if (tid == 0) {
+          Rcb[Fn] = (uint32_t)Cv;
+          R[0] = (uint32_t)Fn;
+          R[1] = (uint32_t)Cv;
+          R[2] = (uint32_t)nch;
+          // C <= EXACT_C_MAX (the host caps ccap in exact mode), npairs < 2^10 (amax <= 44 in exact mode)
+          R[3] = a.exact ? (uint32_t)C << 10 | (uint32_t)npairs : 0u;
+          roff[i + 1] = o;
+        }
+      }
+      if (a.prune) {  // the new states' forward likelihoods, in add order (HaploPair.cpp:42, :66)
+        B.sync();
+        for (int t = t0; t < t1; ++t) {
+          double f = 1.0;  // counting (no records): sizes only, nothing pruned
+          if (!counting) {
+            const double tpv = Rtp[t];
+            for (uint32_t r = Rcb[t]; r < Rcb[t + 1]; ++r) {
+              const double v = fwx[cw_state(Rct[r])] * tpv;
+              f = r == Rcb[t] ? v : f + v;
+            }
+          }
+          fwy[t] = f;
+        }
+      }
+      // m_best_pair.clear() for the next locus
+      for (int t = t0; t < t1; ++t) {
+        const uint32_t sl = *Y.at(F_SLOT, t);
+        *K.key(sl) = KEY_EMPTY;
+        *f_first(sl) = FIRST_NONE;
+        *f_ns(sl) = 0;
+        *f_fill(sl) = 0;
+        *K.cnt(sl) = 0;
+      }
+      __threadfence_block();
+      B.sync();
+      const IdFront T = X;
+      X = Y;
+      Y = T;
+      double *const ft = fwx;
+      fwx = fwy;
+      fwy = ft;
+      Fp = Fn;
+    }
+    if (status == EST_OK && Fp == 0) status = EST_UNRESOLVED;
+    if (counting && status != EST_OVERFLOW_FRONTIER && status != EST_OVERFLOW_CONTRIB && status != EST_NO_HEAD_PATTERN)
+      status = EST_OVERFLOW_REC;
+    fbig = Fp > fbig ? Fp : fbig;
+    if (status < 0) reset_tables();  // aborted mid-locus: keys may be left
+    if (status == EST_OK && a.prune) status = EST_OK_PRUNED;
+    re = B.reduce_u64(re);
+    if (tid == 0) {
+      a.rec_need[bi] = rneed;
+      a.trace_need[bi] = tneed;
+      a.status[bi] = status;
+      a.re_count[bi] = re;
+      a.fmax[bi] = fbig;
+      atomicMax(a.max_states, (unsigned)fbig);
+    }
+  }
+}
+
 // ============================================================ pass 2 ======
 
 namespace {
@@ -1257,6 +1714,31 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
     K2_ST(5);
   }
   K2_FLUSH
+}
+
+hipError_t launch_estep_structure2(const StructArgs &a, int grid, int nw, hipStream_t st) {
+  if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > F_MAX || (a.hcap & (a.hcap - 1)) || a.lds_hc < 1 ||
+      (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || a.lds_cc < 0 || a.ccap < 1 || a.mod.head_len < 1 ||
+      (a.exact && a.ccap > EXACT_C_MAX) ||
+      (a.mod.head_len > 1 && (!a.mod.hf_off || !a.mod.hf_pairs || !a.mod.hf_status)) ||
+      (nw != 1 && nw != 4 && nw != 8 && nw != 16))
+    return hipErrorInvalidValue;
+  const size_t lds = estep_s1v2_lds_bytes(a.lds_fc, a.lds_hc, a.lds_cc, a.pan.amax, nw);
+  static size_t lds_attr[4] = {0, 0, 0, 0};
+  const int ix = nw == 16 ? 3 : (nw == 8 ? 2 : (nw == 4 ? 1 : 0));
+  const void *f = nw == 16 ? (const void *)estep_structure2<16>
+                           : (nw == 8 ? (const void *)estep_structure2<8>
+                                      : (nw == 4 ? (const void *)estep_structure2<4> : (const void *)estep_structure2<1>));
+  if (lds > 65536 && lds > lds_attr[ix]) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    lds_attr[ix] = lds;
+  }
+  if (nw == 16) hipLaunchKernelGGL(estep_structure2<16>, dim3(grid), dim3(16 * WAVE), lds, st, a);
+  else if (nw == 8) hipLaunchKernelGGL(estep_structure2<8>, dim3(grid), dim3(8 * WAVE), lds, st, a);
+  else if (nw == 4) hipLaunchKernelGGL(estep_structure2<4>, dim3(grid), dim3(4 * WAVE), lds, st, a);
+  else hipLaunchKernelGGL(estep_structure2<1>, dim3(grid), dim3(WAVE), lds, st, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStream_t st) {

@@ -238,6 +238,10 @@ size_t estep_s2_scratch_bytes(int fcap, int S);
 size_t estep_s2_lds_bytes(int S, int fc, int nw, bool pair = false);
 // nw: wavefronts per individual, 1 or 4
 hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStream_t st);
+// The same records with fewer block hand-offs per locus (estep_split.hip,
+// "pass 1, v2"); sized with estep_s1v2_lds_bytes and estep_s1_scratch_bytes(.., nw = 2, ..).
+size_t estep_s1v2_lds_bytes(int fc, int hc, int cc, int amax, int nw);
+hipError_t launch_estep_structure2(const StructArgs &a, int grid, int nw, hipStream_t st);
 // wpe: 4 or 5 resident waves per SIMD (register budget of the instantiation)
 hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, int wpe, hipStream_t st,
                                bool pair = false);

@@ -252,6 +252,11 @@ class HaploModel:
         (3 or 4, 0 = 3).  Results are identical."""
         self._check(lib().hmc_set_value_pass(self._h, {"auto": 0, "classic": 1, "dataflow": 2}[mode], int(ring)))
 
+    def set_structure_pass(self, version: int):
+        """Structure pass (hmc_set_structure_pass): 1 per-chunk ranking, 2 three
+        block scans per locus, 0 automatic.  Results are identical."""
+        self._check(lib().hmc_set_structure_pass(self._h, int(version)))
+
     def last_value_pass_dataflow(self) -> bool:
         d = C.c_int()
         self._check(lib().hmc_last_value_pass(self._h, C.byref(d)))

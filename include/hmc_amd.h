@@ -352,6 +352,12 @@ int hmc_set_value_layout(hmc_ctx *ctx, int mode);
  * (default) = automatic.  The same HaploPair::add sequence per state
  * (HaploPair.cpp:35-89) either way. */
 int hmc_set_value_pass(hmc_ctx *ctx, int mode, int ring);
+/* Structure pass of the split E-step (results identical): 1 = per chunk of
+ * contributions a ranking hand-off (lane masks, four block barriers per
+ * chunk); 2 = three block scans per locus (creation order from each key's
+ * first contribution, add order from each state's member segment); 0 =
+ * automatic. */
+int hmc_set_structure_pass(hmc_ctx *ctx, int version);
 /* 1 when the last value-pass launch ran the dataflow schedule. */
 int hmc_last_value_pass(const hmc_ctx *ctx, int *dataflow);
 /* Individuals the last E-step re-ran with the libstdc++ permutations (mode 0)

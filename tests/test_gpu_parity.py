@@ -207,6 +207,50 @@ def test_dataflow_value_pass(oracle_mod, name, S, shape, ring):
     assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
 
 
+@pytest.mark.parametrize("name,shape,S", [
+    ("a3miss5", None, 10), ("n300", None, 10), ("a8", None, 10), ("miss2", None, 3), ("cfg1", None, 10),
+    ("a3miss5", (4, 2, 0, 0), 10), ("a3miss5", (16, 1, 0, 0), 5), ("n300", (4, 2, 0, 0), 10),
+    ("a8", (1, 12, 0, 0), 40), ("a4", (8, 2, 0, 0), 10)])
+def test_structure_pass_v2(oracle_mod, name, shape, S):
+    """hmc_set_structure_pass(2): creation order from each key's first
+    contribution and add order from each state's member segment (three block
+    scans per locus) — the E-step on the M0 model equals
+    HaploModel::resolveAll bit for bit, with both value-pass schedules."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=S)
+    o.find_patterns()
+    o.reset_counters()
+    ll_o = o.resolve_all()
+    for vpass in ("classic", "dataflow"):
+        m = gpu_model(p, S)
+        m.set_structure_pass(2)
+        m.set_value_pass(vpass)
+        if shape:
+            m.set_pass_shapes(*shape)
+        m.find_patterns()
+        ll_g, H, re_g = m.resolve_all()
+        assert_estep_equal(m, o, ll_g, ll_o, H, re_g)
+        m.close()
+
+
+@pytest.mark.parametrize("name", ["n60", "miss2"])
+def test_structure_pass_v2_exact_em(oracle_mod, name):
+    """The exact M-step's records (forward links in extendAll order, pair
+    orientations) from the v2 structure pass: the whole exact EM as with v1."""
+    p = panel(name)
+    r = None
+    logs = []
+    for v in (1, 2):
+        m = gpu_model(p, max_iteration=6)
+        m.exact_estimate = True
+        m.set_structure_pass(v)
+        res = m.run()
+        logs.append(([x["ll"] for x in m.log], res))
+        m.close()
+    assert logs[0][0] == logs[1][0]
+    assert np.array_equal(logs[0][1], logs[1][1])
+
+
 @pytest.mark.parametrize("name", ["n60", "miss2"])
 def test_dataflow_full_em(oracle_mod, name):
     """The whole EM with the dataflow value pass: iteration count, LL, R_E and
@@ -715,8 +759,8 @@ def test_edge_cases(oracle_mod):
         assert np.array_equal(res, r["resolutions"])
 
 
-@pytest.mark.parametrize("vpass,S", [("classic", 4), ("dataflow", 4), ("classic", 40)])
-def test_underflow_unresolved(oracle_mod, vpass, S):
+@pytest.mark.parametrize("vpass,S,sv", [("classic", 4, 1), ("dataflow", 4, 1), ("classic", 40, 1), ("dataflow", 4, 2)])
+def test_underflow_unresolved(oracle_mod, vpass, S, sv):
     """Raw double products underflow on long i.i.d. panels; those individuals
     are unresolved (HaploBuilder.cpp:117-124), LL = -inf and the EM stops —
     both implementations must agree on all of it.  The individuals whose
@@ -728,6 +772,7 @@ def test_underflow_unresolved(oracle_mod, vpass, S):
     r = o.run()
     m = hmc_amd.HaploModel()
     m.set_value_pass(vpass)
+    m.set_structure_pass(sv)
     m.sample_size = S
     m.max_iteration = 3
     res = m.run(hmc_amd.GenoData(a, "S" * 2500))

@@ -1,6 +1,6 @@
 """A/B of the value-pass schedules along the converged chain (E1, M1, E2, M2,
-E3 from M0): per configuration "mode:ring:vnw:vipc" (mode classic | dataflow,
-0 = automatic) the chain restarts from M0 (hmc_em_rewind) and each E-step's
+E3 from M0): per configuration "mode:ring:vnw:vipc[:sv]" (mode classic | dataflow,
+0 = automatic; sv = structure pass version 1 or 2) the chain restarts from M0 (hmc_em_rewind) and each E-step's
 device ms of the passes is printed.  LL and R_E must not depend on the
 schedule.
 
@@ -25,7 +25,9 @@ P, _ = m.find_patterns()
 print(f"cfg {cfg}: M0 {P} patterns {time.perf_counter() - t0:.1f} s", flush=True)
 m.model_save()
 for c in confs:
-    mode, ring, vnw, vipc = c.split(":")
+    f = c.split(":")
+    mode, ring, vnw, vipc = f[:4]
+    m.set_structure_pass(int(f[4]) if len(f) > 4 else 1)
     m.set_value_pass(mode, int(ring))
     m.set_pass_shapes(0, 0, int(vnw), int(vipc))
     m.em_rewind()
