@@ -96,7 +96,7 @@ __host__ __device__ inline DfPlan df_plan(int S, int fc, int nb, bool pair, int 
   p.o_ascr = take(WAVE * 4);
   p.flag_words = (fcap + 31) / 32;
   p.o_flags = take(R * p.flag_words * 4);
-  p.front_stride = (fc * (16 + 12 * S) + 15) & ~15;
+  p.front_stride = (fc * (24 + 8 * S) + 15) & ~15;
   p.o_front = take(R * p.front_stride);
   p.bytes = o;
   p.R = R;
@@ -106,6 +106,59 @@ __host__ __device__ inline DfPlan df_plan(int S, int fc, int nb, bool pair, int 
   p.G = pair ? WAVE / S : WAVE / (2 * S);
   p.sws = sl;
   return p;
+}
+
+// A ring slot's frontier: forward likelihood, list length, first add that
+// overflows, the homozygous flags of the list's links (bit k), and the S
+// likelihoods of every state; [0, fc) in LDS, the rest in HBM.  The link
+// words themselves live only in the trace record (the traceback reads them
+// there; a chain's partial list is read back from it): per state 24 + 8 S
+// bytes instead of the locus-synchronous pass's 16 + 12 S.
+struct DfFront {
+  unsigned char *l, *g;
+  int fc, fcap, S;
+  __device__ double *fwd(int t) const { return t < fc ? (double *)l + t : (double *)g + (t - fc); }
+  __device__ uint32_t *nl(int t) const {
+    return t < fc ? (uint32_t *)(l + (size_t)fc * 8) + t : (uint32_t *)(g + (size_t)fcap * 8) + (t - fc);
+  }
+  __device__ uint32_t *r0(int t) const {
+    return t < fc ? (uint32_t *)(l + (size_t)fc * 12) + t : (uint32_t *)(g + (size_t)fcap * 12) + (t - fc);
+  }
+  __device__ unsigned long long *hm(int t) const {
+    return t < fc ? (unsigned long long *)(l + (size_t)fc * 16) + t
+                  : (unsigned long long *)(g + (size_t)fcap * 16) + (t - fc);
+  }
+  __device__ double *lik(int t) const {
+    return t < fc ? (double *)(l + (size_t)fc * 24) + t * S : (double *)(g + (size_t)fcap * 24) + (size_t)(t - fc) * S;
+  }
+};
+__host__ __device__ inline size_t df_front_bytes(int fcap, int S) { return al256((size_t)fcap * (24 + 8 * S)); }
+
+// Copy the first ns links of predecessor s (likelihoods xl, homozygous flags
+// xhm) into a list at position k0, transformed as by the extension
+// constructor / add (HaploPair.cpp:35-80, as copy_extended); the link words
+// go to the trace record tl, the new flags into *yhm.
+__device__ inline void df_copy_extended(const double *xl, unsigned long long xhm, double *yl, unsigned long long &yhm,
+                                        int k0, int ns, uint32_t s, double tpv, bool rev, bool differ, uint32_t *tl) {
+  for (int k = 0; k < ns; k += 4) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (k + u < ns) v[u] = xl[k + u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (k + u < ns) {
+        double lk = v[u] * tpv;
+        bool homo = (xhm >> (k + u)) & 1ull;
+        if (differ && homo) {
+          if (rev) lk = 0.0;
+          homo = false;
+        }
+        yl[k0 + k + u] = lk;
+        yhm |= (unsigned long long)homo << (k0 + k + u);
+        tl[k0 + k + u] = meta_pack(s, (uint32_t)(k + u), rev, homo, false);
+      }
+  }
 }
 
 __device__ inline int ld_vol(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
@@ -123,7 +176,7 @@ __device__ inline void acq_wg() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "work
 size_t estep_df_lds_bytes(int S, int fc, int nw, bool pair, int R, int qcap, int fcap) {
   return (size_t)df_plan(S, fc, nw - 1, pair, R, qcap, fcap).bytes;
 }
-size_t estep_df_scratch_bytes(int fcap, int S, int R) { return (size_t)R * k2_front_bytes(fcap, S); }
+size_t estep_df_scratch_bytes(int fcap, int S, int R) { return (size_t)R * df_front_bytes(fcap, S); }
 
 // WPE: resident waves per SIMD of the register allocation (4 or 5).  PAIR:
 // segments of S lanes with two links per lane (S <= 16), else 2S lanes (S <= 32).
@@ -140,9 +193,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
   int *ascr = (int *)(smem + plan.o_ascr);
   const int qmask = qcap - 1, qlog = plan.qlog;
   char *sp = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
-  const size_t hbm_slot = k2_front_bytes(a.fcap, S);
+  const size_t hbm_slot = df_front_bytes(a.fcap, S);
   auto front = [&](int slot) {
-    return VFront{smem + plan.o_front + (size_t)slot * plan.front_stride, (unsigned char *)sp + (size_t)slot * hbm_slot,
+    return DfFront{smem + plan.o_front + (size_t)slot * plan.front_stride, (unsigned char *)sp + (size_t)slot * hbm_slot,
                   a.lds_fc, a.fcap, S};
   };
   auto flags = [&](int slot) { return (uint32_t *)(smem + plan.o_flags) + (size_t)slot * plan.flag_words; };
@@ -247,7 +300,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
         const int F = (int)Rh[0];
         const double *Rtp = (const double *)(Rh + 4);
         const uint32_t *Rhd = Rh + 4 + 2 * F;
-        const VFront Y = front(b);
+        const DfFront Y = front(b);
         const unsigned long long off = sh->ring[b].tr;
         uint32_t *thd = a.trace + off + 1, *tln = a.trace + trace_links(off, (uint32_t)F);
         for (int t = lane; t < F; t += WAVE) {
@@ -256,7 +309,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           const uint32_t mw = meta_pack(0, 0, false, homo, true);
           *Y.fwd(t) = homo ? tpv : tpv * 2.0;
           Y.lik(t)[0] = tpv;
-          Y.meta(t)[0] = mw;
+          *Y.hm(t) = homo ? 1ull : 0ull;
           *Y.nl(t) = 1;
           thd[t] = (Rhd[t] & 0xFFFFu) | 1u << 16;
           uint32_t *tl = tln + (size_t)t * S;
@@ -296,7 +349,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           break;
         }
         const int b = j % R, bx = (j - 1) % R;
-        const VFront X = front(bx), Y = front(b);
+        const DfFront X = front(bx), Y = front(b);
         const uint32_t *xfl = flags(bx);
         uint32_t *yfl = flags(b);
         const uint32_t *Rj = a.rec + roff[j];
@@ -397,16 +450,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
             uint32_t w = Rct[cb];
             uint32_t s = cw_state(w), ns = cw_ns(w);
             double *yl = Y.lik(t);
-            uint32_t *ym = Y.meta(t);
+            unsigned long long yhm = 0ull;
             uint32_t *tl = tln + (size_t)t * S;
-            copy_extended<4>(X.lik((int)s), X.meta((int)s), yl, ym, 0, (int)ns, s, tpv, cw_rev(w), differ, tl);
+            df_copy_extended(X.lik((int)s), *X.hm((int)s), yl, yhm, 0, (int)ns, s, tpv, cw_rev(w), differ, tl);
             int k = (int)ns, r0 = ce;
             for (int r = cb + 1; r < ce; ++r) {
               w = Rct[r];
               s = cw_state(w);
               ns = cw_ns(w);
               if (k + (int)ns <= S) {
-                copy_extended<4>(X.lik((int)s), X.meta((int)s), yl, ym, k, (int)ns, s, tpv, cw_rev(w), differ, tl);
+                df_copy_extended(X.lik((int)s), *X.hm((int)s), yl, yhm, k, (int)ns, s, tpv, cw_rev(w), differ, tl);
                 k += (int)ns;
               } else {
                 r0 = r;
@@ -417,6 +470,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
               for (int qq = k; qq < S; ++qq) tl[qq] = 0u;
             thd[t] = (hd & 0xFFFFu) | (uint32_t)k << 16;
             *Y.fwd(t) = fwd;
+            *Y.hm(t) = yhm;
             *Y.nl(t) = (uint32_t)k;
             *Y.r0(t) = (uint32_t)r0;
             if (!(fwd > 0.0) && j < L && !pruned) underflow = true;
@@ -486,7 +540,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
               const int F = g.F;
               const double *Rtp = (const double *)(Rj + 4);
               const uint32_t *Rhd = Rj + 4 + 2 * F, *Rcb = Rhd + F, *Rct = Rcb + F + 1;
-              const VFront Y = front(cs);
+              const DfFront Y = front(cs);
               r = (int)*Y.r0(st);
               re_ = (int)Rcb[st + 1];
               tpv = Rtp[st];
@@ -495,9 +549,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
               k0 = (int)*Y.nl(st);
               wc = Rct[r];
               wn = r + 1 < re_ ? Rct[r + 1] : 0u;
-              if (sg.k < k0) {
+              if (sg.k < k0) {  // the partial list: likelihoods here, link words in the trace record
                 *slot_l = Y.lik(st)[sg.k];
-                *slot_m = Y.meta(st)[sg.k];
+                *slot_m = a.trace[trace_links(g.tr, (uint32_t)F) + (size_t)st * S + sg.k];
               }
               have = true;
             }
@@ -518,18 +572,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
         idle = 0;
         int n = 0;
         if (have) {
-          const VFront X = front((cs + R - 1) % R);
+          const DfFront X = front((cs + R - 1) % R);
+          const unsigned long long xhm = *X.hm((int)cw_state(wc));
           const uint32_t s = cw_state(wc), ns = cw_ns(wc);
           const bool rev = cw_rev(wc);
           n = k0 + (int)ns;
           // HaploPair::add transformation (HaploPair.cpp:63-80)
           auto extend = [&](int kk) {
             const int qk = kk - k0;
-            double lk;
-            uint32_t pm;
-            X.ld_link((int)s, qk, lk, pm);
-            lk *= tpv;
-            bool homo = meta_homo(pm);
+            double lk = X.lik((int)s)[qk] * tpv;
+            bool homo = (xhm >> qk) & 1ull;
             if (differ && homo) {
               if (rev) lk = 0.0;
               homo = false;
@@ -556,17 +608,21 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           k0 = S;
           if (++r == re_) {  // the chain's list is final
             const DfRing &g = sh->ring[cs];
-            const VFront Y = front(cs);
+            const DfFront Y = front(cs);
             const uint32_t *Rj = a.rec + g.rec;
             const int F = g.F;
             const uint32_t *Rhd = Rj + 4 + 2 * F;
             uint32_t *tl = a.trace + trace_links(g.tr, (uint32_t)F) + (size_t)st * S;
+            const uint32_t fm = sg.k < S ? *slot_m : 0u;
             if (sg.k < S) {
               Y.lik(st)[sg.k] = *slot_l;
-              Y.meta(st)[sg.k] = *slot_m;
-              tl[sg.k] = *slot_m;
+              tl[sg.k] = fm;
             }
+            // the final list's homozygous flags, bit k = position k (lanes k < S of the segment)
+            const unsigned long long hb = (wave_ballot(have && sg.k < S && meta_homo(fm)) >> sg.base) &
+                                          (S >= 64 ? ~0ull : ((1ull << S) - 1ull));
             if (sg.k == 0) {
+              *Y.hm(st) = hb;
               *Y.nl(st) = (uint32_t)S;
               a.trace[g.tr + 1 + st] = (Rhd[st] & 0xFFFFu) | (uint32_t)S << 16;
             }
@@ -589,7 +645,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
       int status = sh->status;
       int cnt = 0;
       double total = 0.0;
-      const VFront X = front(L % R);
+      const DfFront X = front(L % R);
       const int Fp = sh->ring[L % R].F;
       if (status == EST_OK) {
         for (int t = 0; t < Fp; ++t) {
@@ -597,7 +653,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           const uint32_t n = *X.nl(t);
           for (uint32_t k = 0; k < n; ++k) {
             double lk = X.lik(t)[k];
-            const bool homo = meta_homo(X.meta(t)[k]);
+            const bool homo = (*X.hm(t) >> k) & 1ull;
             if (!homo) lk *= 2.0;
             W.set(cnt++, lk, meta_pack((uint32_t)t, k, false, homo, false));
           }
