@@ -228,6 +228,12 @@ int hmc_set_value_pass(hmc_ctx *h, int mode, int ring) {
   return HMC_OK;
 }
 
+int hmc_set_exact_walk(hmc_ctx *h, int items_per_wave) {
+  if (!h || (items_per_wave != 0 && items_per_wave != 1 && items_per_wave != 4)) return HMC_EARG;
+  h->c.exact_ipw = items_per_wave == 0 ? 1 : items_per_wave;
+  return HMC_OK;
+}
+
 int hmc_set_structure_pass(hmc_ctx *h, int version) {
   if (!h || version < 0 || version > 2) return HMC_EARG;  // 0 = automatic
   h->c.structure_pass_version = version == 0 ? 1 : version;

@@ -824,6 +824,7 @@ struct Ctx {
   // frontier, key slots (2x, power of two), contributions per locus (2x).
   // structure pass: 2 = estep_structure2 (fewer block hand-offs per locus), 1 = estep_structure
   int structure_pass_version = 1;  // hmc_set_structure_pass
+  int exact_ipw = 1;               // exact_walk items per wavefront, 1 or 4 (hmc_set_exact_walk)
   static void s1_tier(int budget, int amax, int nw, int &fc, int &hc, int &cc, bool v2 = false) {
     for (int f = 2048; f >= 16; f -= 16) {
       const int h = next_pow2(2 * f), c = 2 * f;

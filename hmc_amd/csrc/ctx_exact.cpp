@@ -247,16 +247,17 @@ int Ctx::exact_walk_group(ExactArgs &x, int k, int dev_cu) {
   if (exact_walk_lds_bytes(tr_maxd, x.fmax) > EXACT_WALK_LDS_MAX)
     return fail(HMC_EUNSUPPORTED, "exact M-step: a frontier of %d states (trie depth %d) exceeds the walk's LDS bitmap",
                 x.fmax, tr_maxd);
+  // items per wavefront: 4 (16 lanes each) when their LDS fits, else 1
+  const int ipw = exact_ipw == 4 && exact_walk_lds_bytes(tr_maxd, x.fmax) * 4 <= EXACT_WALK_LDS_MAX ? 4 : 1;
   x.scratch_stride = exact_walk_scratch_doubles(tr_maxd, x.fmax, x.width);
   const long long items = (long long)k * L;
-  // 28 waves per CU (7 per SIMD at 64 VGPRs), fewer when the per-wave lists
-  // would pass SCRATCH_MAX
-  const long long by_mem = std::max<long long>(1, (long long)(SCRATCH_MAX / (x.scratch_stride * 8)));
+  // 28 waves per CU, fewer when the per-item lists would pass SCRATCH_MAX
+  const long long by_mem = std::max<long long>(1, (long long)(SCRATCH_MAX / (x.scratch_stride * 8 * ipw)));
   const int grid = (int)std::max<long long>(1, std::min<long long>(std::min<long long>(items, (long long)dev_cu * 28), by_mem));
   // the walk's zero invariant (its lists; the child frequencies and touched
   // lists are left behind by each item and would land inside the lists of
   // a group whose depth or frontier differs): zeroed for every group
-  const size_t need = x.scratch_stride * grid;
+  const size_t need = x.scratch_stride * grid * ipw;
   if ((e = d_xscr.ensure(need)) || (e = hipMemsetAsync(d_xscr.p, 0, need * 8, st)))
     return hipfail(e, "exact scratch");
   x.scratch = d_xscr.p;
@@ -267,7 +268,7 @@ int Ctx::exact_walk_group(ExactArgs &x, int k, int dev_cu) {
     x.item0 = i0;
     x.item1 = std::min(items, i0 + slice);
     hipEventRecord(ev[0], st);
-    if ((e = launch_exact_walk(x, grid, st))) return hipfail(e, "exact_walk");
+    if ((e = launch_exact_walk(x, grid, st, ipw))) return hipfail(e, "exact_walk");
     hipEventRecord(ev[1], st);
     if ((e = hipStreamSynchronize(st))) return hipfail(e, "exact_walk");
     float ms = 0;

@@ -37,9 +37,11 @@ namespace hmc {
 
 namespace {
 
-__device__ inline double wave_sum_fixed(double x) {  // fixed butterfly: same result on every run
+// fixed butterfly over a group of GL lanes: the same result on every run
+template <int GL>
+__device__ inline double group_sum_fixed(double x) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  for (int o = GL / 2; o > 0; o >>= 1) x += __shfl_xor(x, o);
   return x;
 }
 
@@ -179,29 +181,37 @@ __device__ inline void walk_terms(bool ma, bool mb, bool rev, double w0, double 
 // union of reached states in state order (zero entries add +0.0).  Scratch
 // invariant: every dense entry not in a touched list is 0.0 (the host zeroes
 // the scratch before the launch and every item clears what it wrote).
+template <int GL>
 __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
-  extern __shared__ unsigned long long stk64[];  // per depth: descend mask, written-slot mask; then ints; marks
-  const int lane = threadIdx.x;
+  extern __shared__ unsigned long long lds64[];  // per group: per depth descend mask, written-slot mask; ints; marks
+  constexpr int NG = WAVE / GL;  // items walked at once by the wavefront, GL lanes each
+  const int lane = threadIdx.x, g = lane / GL, gl = lane % GL;
+  // this group's lanes of a wave ballot
+  auto gballot = [&](bool p) -> unsigned long long {
+    const unsigned long long b = __ballot(p);
+    return GL == WAVE ? b : (b >> (g * GL)) & ((1ull << GL) - 1ull);
+  };
   const int L = a.L, hl = a.head_len, W = a.width, maxd = a.max_depth;
   const int D = maxd + 2;
+  unsigned long long *stk64 = lds64 + (size_t)g * (exact_walk_lds_bytes(maxd, a.fmax) / 8);
   unsigned long long *sdesc = stk64, *smask = stk64 + D;
   int *snode = (int *)(stk64 + 2 * D), *snext = snode + D, *sslot = snext + D, *tcnt = sslot + D;
   uint32_t *marks = (uint32_t *)(tcnt + D);  // [fmax/32 + 1] reached-state bitmap
   const int nwords = (a.fmax + 31) >> 5;
   const size_t slot_doubles = (size_t)3 * a.fmax;
-  double *lists = a.scratch + (size_t)blockIdx.x * a.scratch_stride;      // [maxd+1][W][3][fmax]
+  double *lists = a.scratch + ((size_t)blockIdx.x * NG + g) * a.scratch_stride;  // [maxd+1][W][3][fmax]
   double *cfreq = lists + (size_t)(maxd + 1) * W * slot_doubles;          // [maxd+2][W]
   uint32_t *touched = (uint32_t *)(cfreq + (size_t)(maxd + 2) * W);       // [maxd+1][fmax]
   auto slot = [&](int d, int i) { return lists + ((size_t)d * W + i) * slot_doubles; };
-  for (int d = lane; d < D; d += WAVE) {
+  for (int d = gl; d < D; d += GL) {
     tcnt[d] = 0;
     smask[d] = 0ull;
   }
-  for (int w = lane; w < nwords; w += WAVE) marks[w] = 0u;
+  for (int w = gl; w < nwords; w += GL) marks[w] = 0u;
   __builtin_amdgcn_wave_barrier();
   __threadfence_block();
   const long long n_items = a.item1 < 0 ? (long long)a.n_order * L : a.item1;
-  for (long long it = a.item0 + blockIdx.x; it < n_items; it += gridDim.x) {
+  for (long long it = a.item0 + (long long)blockIdx.x * NG + g; it < n_items; it += (long long)gridDim.x * NG) {
     const int q = (int)(it / L), start = (int)(it % L);
     const int bi = a.order[q];
     const int root = a.tr_root[start];
@@ -218,11 +228,11 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
       const int F0 = (int)a.rec[roff[e0]];
       const double *fw = (const double *)(a.x + xo[e0]);
       double *S0 = slot(0, 0);
-      for (int t = lane; t < F0; t += WAVE) {
+      for (int t = gl; t < F0; t += GL) {
         S0[t] = fw[t];
         touched[t] = (uint32_t)t;
       }
-      if (lane == 0) {
+      if (gl == 0) {
         tcnt[0] = F0;
         smask[0] = 1ull;
         snode[0] = root;
@@ -240,9 +250,9 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
       if (snext[d] < 0) {  // ---- all children of this node, into depth d+1 ----
         unsigned long long cm = 0ull;  // alleles with a child
         if (d < maxd)
-          for (int i0 = 0; i0 < W; i0 += WAVE) {
-            const int i = i0 + lane;
-            cm |= __ballot(i < W && a.tr_child[(size_t)node * W + i] >= 0) << i0;
+          for (int i0 = 0; i0 < W; i0 += GL) {
+            const int i = i0 + gl;
+            cm |= gballot(i < W && a.tr_child[(size_t)node * W + i] >= 0) << i0;
           }
         if (cm == 0ull) {  // node done
           --d;
@@ -256,7 +266,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
         {  // the previous sibling's children at depth d+1 back to zero
           const int nc = tcnt[d + 1];
           const unsigned long long wm = smask[d + 1];
-          for (int j = lane; j < nc; j += WAVE) {
+          for (int j = gl; j < nc; j += GL) {
             const uint32_t t = Tc[j];
             for (unsigned long long m = wm; m; m &= m - 1) {
               double *C0 = slot(d + 1, __builtin_ctzll(m));
@@ -272,7 +282,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
           const RecView R(Rh, true);
           const uint32_t *plo = R.cb + Fh + 1, *phi = plo + Fh;
           bw = (const double *)(a.x + xo[hl]) + Fh;
-          for (int t = lane; t < Fh; t += WAVE) {
+          for (int t = gl; t < Fh; t += GL) {
             uint32_t xa, xb;
             if (hl == 1) {
               xa = R.hdr[t] & 0xFFu;
@@ -309,7 +319,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
           //     pair carries the allele of some child on either side
           const int np = tcnt[d];
           const int Fp = (int)a.rec[roff[locus]];  // states the links leave from
-          for (int j = lane; j < np; j += WAVE) {
+          for (int j = gl; j < np; j += GL) {
             const uint32_t s = Tp[j];
             if (P0[s] == 0.0 && P1[s] == 0.0 && P2[s] == 0.0) continue;
             uint32_t off = 0;
@@ -331,15 +341,15 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
           __threadfence_block();
           // (2) the marked states in ascending order; the bitmap back to zero
           const int nw = (R.F + 31) >> 5;
-          for (int w0 = 0; w0 < nw; w0 += WAVE) {
-            const int w = w0 + lane;
+          for (int w0 = 0; w0 < nw; w0 += GL) {
+            const int w = w0 + gl;
             uint32_t bits = w < nw ? marks[w] : 0u;
             const int c = __popc(bits);
             int incl = c;
 #pragma unroll
-            for (int dd = 1; dd < 64; dd <<= 1) {
+            for (int dd = 1; dd < GL; dd <<= 1) {
               const int y = __shfl_up(incl, dd);
-              if (lane >= dd) incl += y;
+              if (gl >= dd) incl += y;
             }
             int at = ntc + incl - c;
             while (bits) {
@@ -348,13 +358,13 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
               Tc[at++] = (uint32_t)(w * 32 + b);
             }
             if (w < nw) marks[w] = 0u;
-            ntc += __shfl(incl, 63);
+            ntc += __shfl(incl, g * GL + GL - 1);
           }
           __builtin_amdgcn_wave_barrier();
           __threadfence_block();
           // (3) each reached state gathers over its incoming contributions, for
           //     the children of its a allele and of its b allele in one pass
-          for (int j = lane; j < ntc; j += WAVE) {
+          for (int j = gl; j < ntc; j += GL) {
             const uint32_t t = Tc[j];
             const uint32_t hd = R.hdr[t];
             const uint32_t xa = hd & 0xFFu, xb = (hd >> 8) & 0xFFu;
@@ -392,25 +402,25 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
           const double *C0 = slot(d + 1, i);
           double part = 0.0;
           bool any = false;
-          for (int j = lane; j < ntc; j += WAVE) {
+          for (int j = gl; j < ntc; j += GL) {
             const uint32_t t = Tc[j];
             const double n0 = C0[t], n1 = C0[a.fmax + t], n2 = C0[2 * a.fmax + t];
             part += ((n0 + n1) + n2) * bw[t];
             any |= (n0 != 0.0) | (n1 != 0.0) | (n2 != 0.0);
           }
-          const double freq = wave_sum_fixed(part) / pg;
+          const double freq = group_sum_fixed<GL>(part) / pg;
           const int child = a.tr_child[(size_t)node * W + i];
           const int pat = a.tr_data[child];
-          if (lane == 0) {
+          if (gl == 0) {
             cfreq[(size_t)(d + 1) * W + i] = freq;
             if (pat >= 0) {
               atomicAdd(&a.acc_freq[pat], (unsigned long long)__double2ll_rn(freq * EXACT_FIXED_SCALE));
               atomicAdd(&a.acc_prefix[pat], (unsigned long long)__double2ll_rn(last_freq * EXACT_FIXED_SCALE));
             }
           }
-          if (__ballot(any) != 0ull && d + 1 <= maxd) desc |= 1ull << i;
+          if (gballot(any) != 0ull && d + 1 <= maxd) desc |= 1ull << i;
         }
-        if (lane == 0) {
+        if (gl == 0) {
           tcnt[d + 1] = ntc;
           smask[d + 1] = cm;
           sdesc[d] = desc;
@@ -428,7 +438,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
       const int i = __builtin_ctzll(left);
       const int child = a.tr_child[(size_t)node * W + i];
       __builtin_amdgcn_wave_barrier();
-      if (lane == 0) {
+      if (gl == 0) {
         snext[d] = i + 1;
         snode[d + 1] = child;
         snext[d + 1] = -1;
@@ -443,7 +453,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
       const int nc = tcnt[dd];
       const unsigned long long wm = smask[dd];
       const uint32_t *T = touched + (size_t)dd * a.fmax;
-      for (int j = lane; j < nc; j += WAVE) {
+      for (int j = gl; j < nc; j += GL) {
         const uint32_t t = T[j];
         for (unsigned long long m = wm; m; m &= m - 1) {
           double *D0 = slot(dd, __builtin_ctzll(m));
@@ -455,7 +465,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
     }
     __builtin_amdgcn_wave_barrier();
     __threadfence_block();
-    for (int dd = lane; dd < D; dd += WAVE) {
+    for (int dd = gl; dd < D; dd += GL) {
       tcnt[dd] = 0;
       smask[dd] = 0ull;
     }
@@ -469,10 +479,6 @@ size_t exact_walk_scratch_doubles(int max_depth, int fmax, int width) {
          ((size_t)(max_depth + 1) * fmax + 1) / 2;
 }
 
-size_t exact_walk_lds_bytes(int max_depth, int fmax) {
-  const size_t D = (size_t)max_depth + 2;
-  return D * 16 + D * 16 + (size_t)((fmax + 31) / 32 + 1) * 4;
-}
 
 hipError_t launch_exact_fb(const ExactArgs &a, int grid, hipStream_t st) {
   if (a.n_order <= 0) return hipSuccess;
@@ -480,18 +486,21 @@ hipError_t launch_exact_fb(const ExactArgs &a, int grid, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st) {
+hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st, int items_per_wave) {
   if (a.n_order <= 0) return hipSuccess;
-  if (a.width < 1 || a.width > 64) return hipErrorInvalidValue;
-  const size_t lds = exact_walk_lds_bytes(a.max_depth, a.fmax);
+  if (a.width < 1 || a.width > 64 || (items_per_wave != 1 && items_per_wave != 4)) return hipErrorInvalidValue;
+  const size_t lds = exact_walk_lds_bytes(a.max_depth, a.fmax) * (size_t)items_per_wave;
   if (lds > EXACT_WALK_LDS_MAX) return hipErrorInvalidValue;  // the host reports it (exact_walk_group)
-  static size_t lds_attr = 0;
-  if (lds > 65536 && lds > lds_attr) {  // wide frontiers: a larger reached-state bitmap, fewer waves per CU
-    hipError_t e = hipFuncSetAttribute((const void *)exact_walk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const void *f = items_per_wave == 4 ? (const void *)exact_walk<16> : (const void *)exact_walk<WAVE>;
+  static size_t lds_attr[2] = {0, 0};
+  const int ix = items_per_wave == 4 ? 1 : 0;
+  if (lds > 65536 && lds > lds_attr[ix]) {  // wide frontiers: a larger reached-state bitmap, fewer waves per CU
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    lds_attr = lds;
+    lds_attr[ix] = lds;
   }
-  hipLaunchKernelGGL(exact_walk, dim3(grid), dim3(WAVE), lds, st, a);
+  if (items_per_wave == 4) hipLaunchKernelGGL(exact_walk<16>, dim3(grid), dim3(WAVE), lds, st, a);
+  else hipLaunchKernelGGL(exact_walk<WAVE>, dim3(grid), dim3(WAVE), lds, st, a);
   return hipGetLastError();
 }
 

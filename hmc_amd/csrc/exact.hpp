@@ -37,9 +37,14 @@ struct ExactArgs {
 };
 
 hipError_t launch_exact_fb(const ExactArgs &a, int grid, hipStream_t st);
-hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st);
+// items_per_wave 1 (64 lanes per item) or 4 (16 lanes each); scratch: grid x items x stride
+hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st, int items_per_wave = 1);
 size_t exact_walk_scratch_doubles(int max_depth, int fmax, int width);
-size_t exact_walk_lds_bytes(int max_depth, int fmax);
+// LDS of one walked item: per depth two masks and four ints, the reached-state bitmap (8-byte multiple)
+__host__ __device__ inline size_t exact_walk_lds_bytes(int max_depth, int fmax) {
+  const size_t D = (size_t)max_depth + 2;
+  return (D * 16 + D * 16 + (size_t)((fmax + 31) / 32 + 1) * 4 + 7) & ~(size_t)7;
+}
 constexpr size_t EXACT_WALK_LDS_MAX = 160 * 1024;  // gfx950 LDS per workgroup
 
 }  // namespace hmc

@@ -257,6 +257,10 @@ class HaploModel:
         block scans per locus, 0 automatic.  Results are identical."""
         self._check(lib().hmc_set_structure_pass(self._h, int(version)))
 
+    def set_exact_walk(self, items_per_wave: int):
+        """Exact M-step walk items per wavefront (hmc_set_exact_walk): 1 or 4."""
+        self._check(lib().hmc_set_exact_walk(self._h, int(items_per_wave)))
+
     def last_value_pass_dataflow(self) -> bool:
         d = C.c_int()
         self._check(lib().hmc_last_value_pass(self._h, C.byref(d)))

@@ -358,6 +358,10 @@ int hmc_set_value_pass(hmc_ctx *ctx, int mode, int ring);
  * first contribution, add order from each state's member segment); 0 =
  * automatic. */
 int hmc_set_structure_pass(hmc_ctx *ctx, int version);
+/* Exact M-step trie walk: pattern-tree items (individual, start locus) per
+ * wavefront, 1 (64 lanes each) or 4 (16 lanes each); 0 = automatic.  The
+ * frequency sums are fixed-point integer adds, identical for any order. */
+int hmc_set_exact_walk(hmc_ctx *ctx, int items_per_wave);
 /* 1 when the last value-pass launch ran the dataflow schedule. */
 int hmc_last_value_pass(const hmc_ctx *ctx, int *dataflow);
 /* Individuals the last E-step re-ran with the libstdc++ permutations (mode 0)

@@ -1152,6 +1152,26 @@ def test_exact_mstep_against_oracle(oracle_mod, name):
         assert _rel_close(pg[k], po[k]), (k, np.max(np.abs(pg[k] - po[k]) / np.maximum(np.abs(po[k]), 1e-300)))
 
 
+@pytest.mark.parametrize("name", ["n60", "a3miss5", "a8"])
+def test_exact_walk_four_items_per_wave(oracle_mod, name):
+    """hmc_set_exact_walk(4): four (individual, start locus) items per
+    wavefront, 16 lanes each — the fixed-point frequency sums are the same
+    integers, so the table equals the one-item walk's bit for bit."""
+    p = panel(name)
+    tabs = []
+    for ipw in (1, 4):
+        m = gpu_model(p)
+        m.exact_estimate = True
+        m.set_exact_walk(ipw)
+        m.find_patterns()
+        m.resolve_all()
+        m.find_patterns()
+        tabs.append(m.patterns())
+        m.close()
+    for k in ("start", "len", "alleles", "succ", "freq", "prefix", "tp"):
+        assert np.array_equal(tabs[0][k], tabs[1][k]), k
+
+
 def test_exact_single_allele_frequencies(oracle_mod):
     """Known answer: with nothing missing, every phasing carries the same
     alleles, so the exact frequency of a length-1 pattern is the allele
