@@ -248,7 +248,8 @@ def main():
                     estep_ms=t["estep_forward_ms"] + t["estep_traceback_ms"], struct_ms=sp["structure_ms"],
                     values_ms=sp["values_ms"], fallback_ms=sp["fallback_ms"], n_fallback=sp["n_fallback"],
                     struct_passes=sp["structure_passes"], value_passes=sp["value_passes"],
-                    tb_ms=t["estep_traceback_ms"], mstep_ms=t["mstep_ms"] if go or force_m else 0.0)
+                    tb_ms=t["estep_traceback_ms"], mstep_ms=t["mstep_ms"] if go or force_m else 0.0,
+                    value_dataflow=m.last_value_pass_dataflow())
 
     for _ in range(args.warmup):
         em_step()

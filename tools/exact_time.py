@@ -1,6 +1,7 @@
 """Exact M-step (--exact-estimate) timing on a BASELINE config (env CFG,
 default 2): M0, E1, then the exact M-step (rounds, candidates, trie-walk ms,
-total ms) next to the sampling M-step on the same E1 samples, and E2 after it."""
+total ms) next to the sampling M-step on the same E1 samples, and E2 after it.
+Env IPW: exact-walk items per wavefront (1 or 4)."""
 import os
 import sys
 import time
@@ -11,6 +12,7 @@ from hmc_amd import synth  # noqa: E402
 
 p = synth.config_panel(int(os.environ.get("CFG", "2")))
 m = hmc_amd.HaploModel()
+m.set_exact_walk(int(os.environ.get("IPW", "1")))
 m.load(hmc_amd.GenoData.from_panel(p))
 P0, _ = m.find_patterns()
 ll1, H, re = m.resolve_all()
