@@ -69,8 +69,19 @@ struct DfShared {
   int q;       // next individual (block broadcast)
 };
 
+// What a B segment needs to start a chain, written by the A lane that queued
+// it (it has all of it in registers): one LDS read instead of a round of
+// record loads.  Indexed like the queue.
+struct DfChain {
+  double tpv;       // m_transition_prob of the state
+  uint32_t r, re;   // next add and the end of the state's contributions
+  uint32_t k0;      // list length after the appends | differ << 31
+  uint32_t wc, wn;  // contribution words of adds r and r + 1
+  uint32_t pad;
+};
+
 struct DfPlan {
-  int o_lpos, o_rpos, o_junk, o_slik, o_smeta, o_sh, o_queue, o_ascr, o_flags, o_front;
+  int o_lpos, o_rpos, o_junk, o_slik, o_smeta, o_sh, o_queue, o_desc, o_ascr, o_flags, o_front;
   int front_stride, flag_words, bytes;
   int R, qcap, qlog, G, sws;  // ring slots, queue slots (2^qlog), segments per B wave, selection slots per B wave
 };
@@ -93,6 +104,7 @@ __host__ __device__ inline DfPlan df_plan(int S, int fc, int nb, bool pair, int 
   p.o_smeta = take(nb * sl * 4);
   p.o_sh = take((int)sizeof(DfShared));
   p.o_queue = take(qcap * 4);
+  p.o_desc = take(qcap * (int)sizeof(DfChain));
   p.o_ascr = take(WAVE * 4);
   p.flag_words = (fcap + 31) / 32;
   p.o_flags = take(R * p.flag_words * 4);
@@ -190,6 +202,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
   const int R = plan.R, qcap = plan.qcap;
   DfShared *sh = (DfShared *)(smem + plan.o_sh);
   uint32_t *queue = (uint32_t *)(smem + plan.o_queue);
+  DfChain *desc = (DfChain *)(smem + plan.o_desc);
   int *ascr = (int *)(smem + plan.o_ascr);
   const int qmask = qcap - 1, qlog = plan.qlog;
   char *sp = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
@@ -250,7 +263,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
       int status = EST_OK;
       uint32_t qtail = 0;  // tickets queued (wave-uniform)
       // queue `npush` entries from the lanes where `push` holds, in lane order
-      auto enqueue = [&](bool push, uint32_t entry) {
+      auto enqueue = [&](bool push, uint32_t entry, const DfChain &dc) {
         const uint64_t m = wave_ballot(push);
         if (!m) return;
         if (push) {
@@ -264,7 +277,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
             }
             __builtin_amdgcn_s_sleep(1);
           }
-          if (ld_vol(&sh->abort) != DF_STALL) st_vol(slot, entry | QE_VALID | ((t >> qlog) & 63u) << QE_LAP);
+          if (ld_vol(&sh->abort) != DF_STALL) {
+            if (!(entry & QE_END)) desc[t & (uint32_t)qmask] = dc;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            st_vol(slot, entry | QE_VALID | ((t >> qlog) & 63u) << QE_LAP);
+          }
         }
         qtail += (uint32_t)__popcll(m);
       };
@@ -426,6 +443,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           // constructor (HaploPair.cpp:35-61), the appends that fit (:63-84)
           // and the ordered forward sum (:42, :66)
           bool chain = false, fin = false;
+          DfChain dc;
           if (ready) {
             const int t = st;
             const double tpv = Rtp[t];
@@ -476,12 +494,20 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
             if (!(fwd > 0.0) && j < L && !pruned) underflow = true;
             chain = r0 < ce;
             fin = !chain;
+            if (chain) {  // w = the contribution word of add r0
+              dc.tpv = tpv;
+              dc.r = (uint32_t)r0;
+              dc.re = (uint32_t)ce;
+              dc.k0 = (uint32_t)k | (differ ? 1u << 31 : 0u);
+              dc.wc = w;
+              dc.wn = r0 + 1 < ce ? Rct[r0 + 1] : 0u;
+            }
           }
           rel_wg();
           if (fin) atomicOr(yfl + (st >> 5), 1u << (st & 31));
           const int nfin = __popcll(wave_ballot(fin));
           if (lane == 0 && nfin) atomicAdd(&sh->ring[b].done, nfin);
-          enqueue(chain, (uint32_t)b << QE_SLOT | (uint32_t)(chain ? st : 0));
+          enqueue(chain, (uint32_t)b << QE_SLOT | (uint32_t)(chain ? st : 0), dc);
           if (ready) st = -1;
           if (wave_ballot(underflow)) {
             status = EST_NEEDS_EXACT;
@@ -500,7 +526,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
         if (status != EST_OK) atomicCAS(&sh->abort, 0, 1);
       }
       if (status != EST_DF_STALL)
-        for (int e = 0; e < nseg; e += WAVE) enqueue(e + lane < nseg, QE_END);
+        for (int e = 0; e < nseg; e += WAVE) enqueue(e + lane < nseg, QE_END, DfChain{});
       if (ld_vol(&sh->abort) == DF_STALL && lane == 0) sh->status = EST_DF_STALL;
     } else {
       // ================================================================ B ====
@@ -527,7 +553,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           ticket = want ? tk : ticket;
           const bool got = want && (e & QE_VALID) && ((e >> QE_LAP) & 63u) == (((uint32_t)tk >> qlog) & 63u);
           if (got) {
-            if (sg.k == 0) st_vol(queue + (tk & qmask), 0u);  // only the segment's first lane read it
             acq_wg();
             ticket = -1;
             if (e & QE_END) {
@@ -535,20 +560,23 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
             } else {
               cs = (int)((e >> QE_SLOT) & 7u);
               st = (int)(e & F_MASK);
+              const DfChain dc = desc[tk & qmask];
+              r = (int)dc.r;
+              re_ = (int)dc.re;
+              tpv = dc.tpv;
+              differ = dc.k0 >> 31;
+              k0 = (int)(dc.k0 & 0x7FFFFFFFu);
+              wc = dc.wc;
+              wn = dc.wn;
+            }
+          }
+          wave_lds_sync();  // the descriptor is read before its slot can be reused
+          if (got) {
+            if (sg.k == 0) st_vol(queue + (tk & qmask), 0u);  // only the segment's first lane read the entry
+            if (!done) {
               const DfRing &g = sh->ring[cs];
-              const uint32_t *Rj = a.rec + g.rec;
               const int F = g.F;
-              const double *Rtp = (const double *)(Rj + 4);
-              const uint32_t *Rhd = Rj + 4 + 2 * F, *Rcb = Rhd + F, *Rct = Rcb + F + 1;
               const DfFront Y = front(cs);
-              r = (int)*Y.r0(st);
-              re_ = (int)Rcb[st + 1];
-              tpv = Rtp[st];
-              const uint32_t hd = Rhd[st];
-              differ = (hd & 0xFFu) != ((hd >> 8) & 0xFFu);
-              k0 = (int)*Y.nl(st);
-              wc = Rct[r];
-              wn = r + 1 < re_ ? Rct[r + 1] : 0u;
               if (sg.k < k0) {  // the partial list: likelihoods here, link words in the trace record
                 *slot_l = Y.lik(st)[sg.k];
                 *slot_m = a.trace[trace_links(g.tr, (uint32_t)F) + (size_t)st * S + sg.k];
