@@ -835,7 +835,9 @@ bool Ctx::df_shape(int S, bool pair, bool heavy, bool small_heavy, int per_cu, i
   const int G = pair ? WAVE / S : WAVE / (2 * S);
   const int nseg = (d.nw - 1) * G;
   d.qcap = 64;
-  while (d.qcap < std::max(4 * nseg, heavy ? 512 : 64)) d.qcap *= 2;
+  // (queue slots carry a 32-byte chain descriptor: cfg 3's E1 has ~130 chains
+  // per locus, about two loci in flight)
+  while (d.qcap < std::max(4 * nseg, heavy ? 256 : 64)) d.qcap *= 2;
   const int budget = 160 * 1024 / std::max(1, d.ipc) - 256;
   if ((int)estep_df_lds_bytes(S, 0, d.nw, pair, d.R, d.qcap, fgrp) > budget) return false;
   int lo = 0, hi = fgrp;  // largest LDS tier that fits
