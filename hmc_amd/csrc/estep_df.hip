@@ -421,10 +421,18 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           if (st >= 0) {
             const int ce = (int)Rcb[st + 1];
             int r = rchk;
-            while (r < ce) {
-              const uint32_t p = cw_state(Rct[r]);
-              if (!((ld_vol(xfl + (p >> 5)) >> (p & 31u)) & 1u)) break;
-              ++r;
+            bool blocked = false;
+            while (r < ce && !blocked) {  // four contribution words per round of loads
+              uint32_t ws[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) ws[u] = r + u < ce ? Rct[r + u] : 0u;
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                if (blocked || r >= ce) break;
+                const uint32_t p = cw_state(ws[u]);
+                if (!((ld_vol(xfl + (p >> 5)) >> (p & 31u)) & 1u)) blocked = true;
+                else ++r;
+              }
             }
             rchk = r;
             ready = r == ce;
