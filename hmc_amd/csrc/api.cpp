@@ -28,6 +28,7 @@ static int ctx_init(hmc_ctx *h, int device) {
   h->c.device = device;
   h->c.debug_mem = getenv("HMC_DEBUG_MEM") != nullptr;
   h->c.diag_mine = getenv("HMC_DIAG_MINE") != nullptr;
+  h->c.check_records = getenv("HMC_CHECK_RECORDS") != nullptr;
   if ((e = hipStreamCreateWithFlags(&h->c.st, hipStreamNonBlocking))) return h->c.hipfail(e, "hipStreamCreate");
   for (auto &ev : h->c.ev)
     if ((e = hipEventCreate(&ev))) return h->c.hipfail(e, "hipEventCreate");

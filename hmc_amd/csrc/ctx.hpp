@@ -281,6 +281,8 @@ struct Ctx {
   // diagnostics only (stderr logging, never a change of what runs): read once
   // at context creation from HMC_DEBUG_MEM / HMC_DIAG_MINE
   bool debug_mem = false, diag_mine = false;
+  bool check_records = false;  // HMC_CHECK_RECORDS: validate each structure pass's records on the host
+  int validate_records(const int32_t *ids, int np_, int i0);
   bool value_fast = false;   // value-only k-best lists first, the exact pass for ties only (hmc_set_value_mode)
   int value_pair = 2;        // two links per lane in phase B: 0 never, 1 heavy groups, 2 every group (hmc_set_value_layout)
   uint64_t trace_bytes = 0, rec_bytes = 0;  // E-step store budgets (0 = automatic)

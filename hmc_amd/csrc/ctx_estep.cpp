@@ -534,6 +534,7 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
           (e = hipMemcpyAsync(fbig.data(), s1.fmax, (size_t)n * 4, hipMemcpyDeviceToHost, st)))
         return hipfail(e, "estep_structure");
       if ((rc = read_status(pending, np_, false, dstatus))) return rc;
+      if (check_records && (rc = validate_records(ids, np_, i0))) return rc;
       hipEventElapsedTime(&ms, ev[0], ev[1]);
       if (prune_) {
         ms_fb += ms;
@@ -884,4 +885,83 @@ int Ctx::resolutions_idx(std::vector<uint8_t> &out) {
     return hipfail(e, "resolutions");
   return HMC_OK;
 }
+// Diagnostic (HMC_CHECK_RECORDS): the structure records of individuals
+// ids[0, np_) against the invariants the value passes rely on — per locus,
+// contribution offsets ascending to Cv; every contribution's predecessor below
+// the previous frontier with that state's list length; a state's list length
+// min(S, sum of its contributions'); the chain flag and list exactly the states
+// whose sum exceeds S.  The first violation fails the E-step (HMC_EHIP) with
+// its individual and locus instead of letting a value pass walk bad records.
+int Ctx::validate_records(const int32_t *ids, int np_, int i0) {
+  hipError_t e;
+  if ((e = hipStreamSynchronize(st))) return hipfail(e, "validate_records");
+  const int L = pan.L, hl = head_len;
+  std::vector<unsigned long long> off(d_rec_off.n);
+  std::vector<uint32_t> rec(d_rec.n);
+  if ((e = hipMemcpy(off.data(), d_rec_off.p, off.size() * 8, hipMemcpyDeviceToHost)) ||
+      (e = hipMemcpy(rec.data(), d_rec.p, rec.size() * 4, hipMemcpyDeviceToHost)))
+    return hipfail(e, "validate_records");
+  int bad = 0;
+  for (int q = 0; q < np_ && !bad; ++q) {
+    const int bi = ids[q];
+    const int stt = h_status[bi];
+    if (stt != EST_OK && stt != EST_OK_PRUNED) continue;
+    const unsigned long long *ro = off.data() + (size_t)bi * (L + 1);
+    std::vector<uint32_t> nl_prev;
+    for (int i = hl - 1; i < L && !bad; ++i) {
+      const unsigned long long o = ro[i + 1];
+      if (o + 4 > rec.size()) { fprintf(stderr, "[hmc] records: indiv %d locus %d offset %llu past the store\n", i0 + bi, i, o); bad = 1; break; }
+      const uint32_t *R = rec.data() + o;
+      const uint32_t Fn = R[0], Cv = R[1], nch = R[2];
+      const uint32_t *Rhd = R + 4 + 2 * Fn, *Rcb = Rhd + Fn, *Rct = Rcb + Fn + 1, *Rch = Rct + Cv;
+      if (o + 4 + 4ull * Fn + 1 + Cv + nch > rec.size()) { fprintf(stderr, "[hmc] records: indiv %d locus %d past the store\n", i0 + bi, i); bad = 1; break; }
+      std::vector<uint32_t> nl(Fn);
+      uint32_t flagged = 0;
+      for (uint32_t t = 0; t < Fn && !bad; ++t) {
+        nl[t] = (Rhd[t] >> 16) & 0x7FFu;
+        if (i == hl - 1) continue;  // head locus: lists of one, no contributions
+        if (Rcb[t] > Rcb[t + 1] || Rcb[t + 1] > Cv) {
+          fprintf(stderr, "[hmc] records: indiv %d locus %d state %u: offsets %u %u (Cv %u)\n", i0 + bi, i, t, Rcb[t], Rcb[t + 1], Cv);
+          bad = 1;
+          break;
+        }
+        uint32_t sum = 0;
+        for (uint32_t r = Rcb[t]; r < Rcb[t + 1]; ++r) {
+          const uint32_t ps = cw_state(Rct[r]), ns = cw_ns(Rct[r]);
+          if (ps >= nl_prev.size() || ns != nl_prev[ps]) {
+            fprintf(stderr, "[hmc] records: indiv %d locus %d state %u add %u: predecessor %u (of %zu) ns %u\n", i0 + bi, i, t,
+                    r - Rcb[t], ps, nl_prev.size(), ns);
+            bad = 1;
+            break;
+          }
+          sum += ns;
+        }
+        const bool chain = (Rhd[t] & HDR_CHAIN) != 0;
+        if (!bad && (nl[t] != std::min<uint32_t>(sum, (uint32_t)S()) || chain != (sum > (uint32_t)S()) || Rcb[t] == Rcb[t + 1])) {
+          fprintf(stderr, "[hmc] records: indiv %d locus %d state %u: list %u, sum %u, chain %d, adds %u\n", i0 + bi, i, t, nl[t], sum,
+                  (int)chain, Rcb[t + 1] - Rcb[t]);
+          bad = 1;
+        }
+        flagged += chain ? 1u : 0u;
+      }
+      if (!bad && i >= hl) {
+        if (Rcb[Fn] != Cv || flagged != nch) {
+          fprintf(stderr, "[hmc] records: indiv %d locus %d: Rcb[F] %u Cv %u, chains %u listed %u\n", i0 + bi, i, Rcb[Fn], Cv, flagged, nch);
+          bad = 1;
+        }
+        std::vector<char> seen(Fn, 0);
+        for (uint32_t k = 0; k < nch && !bad; ++k)
+          if (Rch[k] >= Fn || seen[Rch[k]] || !(Rhd[Rch[k]] & HDR_CHAIN)) {
+            fprintf(stderr, "[hmc] records: indiv %d locus %d: chain entry %u = %u\n", i0 + bi, i, k, Rch[k]);
+            bad = 1;
+          } else {
+            seen[Rch[k]] = 1;
+          }
+      }
+      nl_prev.swap(nl);
+    }
+  }
+  return bad ? fail(HMC_EHIP, "structure records failed validation (HMC_CHECK_RECORDS)") : HMC_OK;
+}
+
 }  // namespace hmc

@@ -151,6 +151,27 @@ __device__ inline uint32_t k1_key_slot(const K1Keys &K, unsigned long long key, 
   }
 }
 
+// As k1_key_slot, but NONE when the HBM table is full (estep_structure2
+// inserts a whole locus's keys before it counts the new states, so a locus
+// with more distinct successor pairs than hcap slots must not probe forever).
+__device__ inline uint32_t k2_key_slot(const K1Keys &K, unsigned long long key, uint32_t h0) {
+  unsigned long long *lk = (unsigned long long *)K.l, *gk = (unsigned long long *)K.g;
+  uint32_t h = h0 & (uint32_t)(K.hc - 1);
+  for (int p = 0; p < PROBE_LDS; ++p) {
+    const unsigned long long prev = atomicCAS(&lk[h], KEY_EMPTY, key);
+    if (prev == KEY_EMPTY || prev == key) return h;
+    h = (h + 1) & (uint32_t)(K.hc - 1);
+  }
+  const uint32_t gmask = (uint32_t)K.hcap - 1u;
+  uint32_t g = (h0 * 0x9E3779B1u) & gmask;
+  for (int p = 0; p < K.hcap; ++p) {
+    const unsigned long long prev = atomicCAS(&gk[g], KEY_EMPTY, key);
+    if (prev == KEY_EMPTY || prev == key) return (uint32_t)K.hc + g;
+    g = (g + 1) & gmask;
+  }
+  return 0xFFFFFFFFu;
+}
+
 __device__ inline unsigned long long ld_acq(unsigned long long *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -980,6 +1001,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
       const int Q = (C + NT - 1) / NT;  // this thread's contributions: [c0, c1)
       const int c0 = min(C, tid * Q), c1 = min(C, c0 + Q);
       // ---- 1. keys, slots; per slot: first contribution, count, predecessor lengths
+      bool full = false;  // the key table is full: more new states than fcap
       for (int cb = c0; cb < c1; cb += 4) {
         uint32_t sa[4], sb[4], ss[4];
 #pragma unroll
@@ -1005,10 +1027,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
           uint32_t slot = NONE;
           if (valid) {
             const uint32_t lo = rev ? sb[u] : sa[u], hi = rev ? sa[u] : sb[u];
-            slot = k1_key_slot(K, ((unsigned long long)lo << 32) | hi, key_hash(lo, hi));
-            atomicMin(f_first(slot), (uint32_t)c);
-            atomicAdd(K.cnt(slot), 1u);
-            atomicAdd(f_ns(slot), *X.at(F_NL, (int)ss[u]));
+            slot = k2_key_slot(K, ((unsigned long long)lo << 32) | hi, key_hash(lo, hi));
+            if (slot == NONE) {
+              full = true;
+            } else {
+              atomicMin(f_first(slot), (uint32_t)c);
+              atomicAdd(K.cnt(slot), 1u);
+              atomicAdd(f_ns(slot), *X.at(F_NL, (int)ss[u]));
+            }
           }
           *CT.at(C2_SR, c) = cw_pack(ss[u], rev);
           *CT.at(C2_SL, c) = slot;
@@ -1022,9 +1048,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         const uint32_t sl = *CT.at(C2_SL, c);
         if (sl != NONE && rd(f_first(sl), sl) == (uint32_t)c) ++mynew;
       }
-      int Fn = 0;
-      int st = B.scan(mynew, &Fn);
-      if (Fn > a.fcap) { status = EST_OVERFLOW_FRONTIER; break; }
+      int Fn = 0;  // (a full table: past fcap without a hand-off of its own; < 0 on wrap-around)
+      int st = B.scan(full ? a.fcap + 1 : mynew, &Fn);
+      if (Fn > a.fcap || Fn < 0) { status = EST_OVERFLOW_FRONTIER; break; }
       if (Fn == 0) { status = EST_UNRESOLVED; break; }
       for (int c = c0; c < c1; ++c) {
         const uint32_t sl = *CT.at(C2_SL, c);
