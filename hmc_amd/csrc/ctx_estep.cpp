@@ -918,7 +918,7 @@ int Ctx::validate_records(const int32_t *ids, int np_, int i0) {
       std::vector<uint32_t> nl(Fn);
       uint32_t flagged = 0;
       for (uint32_t t = 0; t < Fn && !bad; ++t) {
-        nl[t] = (Rhd[t] >> 16) & 0x7FFu;
+        nl[t] = (Rhd[t] >> 16) & 0xFFu;  // (bit 24: the head's homozygous flag, bit 27: chain)
         if (i == hl - 1) continue;  // head locus: lists of one, no contributions
         if (Rcb[t] > Rcb[t + 1] || Rcb[t + 1] > Cv) {
           fprintf(stderr, "[hmc] records: indiv %d locus %d state %u: offsets %u %u (Cv %u)\n", i0 + bi, i, t, Rcb[t], Rcb[t + 1], Cv);

@@ -1172,6 +1172,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
           }
           fwy[t] = f;
         }
+      } else {
+        B.sync();  // every contribution's slot fields read (state, count) before they are cleared
       }
       // m_best_pair.clear() for the next locus
       for (int t = t0; t < t1; ++t) {

@@ -37,9 +37,23 @@ namespace hmc {
 
 namespace {
 
-// fixed butterfly over a group of GL lanes: the same result on every run
+// The sum of a wavefront's 64 virtual lanes in one fixed butterfly order
+// (xor 32, 16, ..., 1), for groups of GL lanes that each carry WAVE / GL
+// virtual lanes (virtual lane gl + GL k in p[k]): the in-lane steps first,
+// then the shuffles within the group.  Every GL gives the same double, so a
+// walk of four items per wavefront sums exactly as the one-item walk.
 template <int GL>
-__device__ inline double group_sum_fixed(double x) {
+__device__ inline double group_sum_fixed(double (&p)[WAVE / GL]) {
+  constexpr int NV = WAVE / GL;
+#pragma unroll
+  for (int s = NV / 2; s > 0; s >>= 1) {
+    double q[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) q[k] = p[k] + p[k ^ s];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) p[k] = q[k];
+  }
+  double x = p[0];
 #pragma unroll
   for (int o = GL / 2; o > 0; o >>= 1) x += __shfl_xor(x, o);
   return x;
@@ -400,12 +414,22 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
         for (unsigned long long m = cm; m; m &= m - 1) {
           const int i = __builtin_ctzll(m);
           const double *C0 = slot(d + 1, i);
-          double part = 0.0;
+          double part[NG];  // virtual lane gl + GL k of a 64-lane sum (group_sum_fixed)
+#pragma unroll
+          for (int k = 0; k < NG; ++k) part[k] = 0.0;
           bool any = false;
           for (int j = gl; j < ntc; j += GL) {
             const uint32_t t = Tc[j];
             const double n0 = C0[t], n1 = C0[a.fmax + t], n2 = C0[2 * a.fmax + t];
-            part += ((n0 + n1) + n2) * bw[t];
+            const double v = ((n0 + n1) + n2) * bw[t];
+            if constexpr (NG == 1) {
+              part[0] += v;
+            } else {
+              const int k = (j / GL) & (NG - 1);
+#pragma unroll
+              for (int u = 0; u < NG; ++u)
+                if (u == k) part[u] += v;
+            }
             any |= (n0 != 0.0) | (n1 != 0.0) | (n2 != 0.0);
           }
           const double freq = group_sum_fixed<GL>(part) / pg;
