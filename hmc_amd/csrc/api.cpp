@@ -229,6 +229,12 @@ int hmc_set_value_pass(hmc_ctx *h, int mode, int ring) {
   return HMC_OK;
 }
 
+int hmc_set_dataflow_waves(hmc_ctx *h, int a_waves) {
+  if (!h || a_waves < 0 || a_waves > 8) return HMC_EARG;
+  h->c.df_na = a_waves;  // 0: by the launch shape
+  return HMC_OK;
+}
+
 int hmc_set_exact_walk(hmc_ctx *h, int items_per_wave) {
   if (!h || (items_per_wave != 0 && items_per_wave != 1 && items_per_wave != 4)) return HMC_EARG;
   h->c.exact_ipw = items_per_wave == 0 ? 1 : items_per_wave;

@@ -843,9 +843,10 @@ struct Ctx {
   enum { VP_AUTO = 0, VP_CLASSIC = 1, VP_DATAFLOW = 2 };
   int value_pass = VP_AUTO;  // hmc_set_value_pass
   int df_ring = 3;
+  int df_na = 0;  // A waves of the dataflow pass (hmc_set_dataflow_waves), 0 = by the shape
   bool last_value_df = false;
   struct DfShape {
-    int nw = 0, ipc = 0, R = 3, qcap = 64, fc = 0;
+    int nw = 0, na = 1, ipc = 0, R = 3, qcap = 64, fc = 0;
   };
   bool df_auto(bool heavy) const { (void)heavy; return false; }
   bool df_shape(int S, bool pair, bool heavy, bool small_heavy, int per_cu, int fgrp, DfShape &d) const;

@@ -737,7 +737,7 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
       const bool fast = value_fast && S <= 32;  // lists longer than a wavefront: exact order only
       hipEventRecord(ev[0], st);
       if (use_df) {
-        if ((e = launch_estep_values_df(v, grid2, vnw, vwpe, pair, df.R, df.qcap, st)))
+        if ((e = launch_estep_values_df(v, grid2, vnw, df.na, vwpe, pair, df.R, df.qcap, st)))
           return hipfail(e, "estep_values_df launch");
       } else if ((e = launch_estep_values(v, grid2, vnw, fast, vwpe, st, pair))) {
         return hipfail(e, "estep_values launch");
@@ -803,7 +803,7 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
         if ((e = hipMemsetAsync(d_nextq.p + 1, 0, 4, st))) return hipfail(e, "estep");
         hipEventRecord(ev[0], st);
         if (use_df) {
-          if ((e = launch_estep_values_df(v2, std::max(1, std::min(G2, nr)), vnw, vwpe, pair, df.R, df.qcap, st)))
+          if ((e = launch_estep_values_df(v2, std::max(1, std::min(G2, nr)), vnw, df.na, vwpe, pair, df.R, df.qcap, st)))
             return hipfail(e, "estep_values_df launch");
         } else if ((e = launch_estep_values(v2, std::max(1, std::min(G2, nr)), vnw, false, vwpe, st, pair))) {
           return hipfail(e, "estep_values launch");
@@ -832,19 +832,22 @@ bool Ctx::df_shape(int S, bool pair, bool heavy, bool small_heavy, int per_cu, i
   d.nw = vp_nw > 0 ? std::max(2, vp_nw) : (small_heavy ? std::max(2, 16 / per_cu) : (heavy ? 8 : 2));
   d.ipc = vp_ipc > 0 ? vp_ipc : (small_heavy ? per_cu : (heavy ? 2 : 8));
   if (d.nw * d.ipc > 20) d.ipc = std::max(1, 20 / d.nw);
+  // A waves: a fixed share of every locus's states each (cfg 3's E1: 468
+  // states per locus, ~8 rounds of 64 for a lone A wave)
+  d.na = df_na > 0 ? std::min(df_na, d.nw - 1) : std::max(1, d.nw / 4);
   d.R = df_ring;
   const int G = pair ? WAVE / S : WAVE / (2 * S);
-  const int nseg = (d.nw - 1) * G;
+  const int nseg = (d.nw - d.na) * G;
   d.qcap = 64;
   // (queue slots carry a 32-byte chain descriptor: cfg 3's E1 has ~130 chains
   // per locus, about two loci in flight)
   while (d.qcap < std::max(4 * nseg, heavy ? 256 : 64)) d.qcap *= 2;
   const int budget = 160 * 1024 / std::max(1, d.ipc) - 256;
-  if ((int)estep_df_lds_bytes(S, 0, d.nw, pair, d.R, d.qcap, fgrp) > budget) return false;
+  if ((int)estep_df_lds_bytes(S, 0, d.nw, d.na, pair, d.R, d.qcap, fgrp) > budget) return false;
   int lo = 0, hi = fgrp;  // largest LDS tier that fits
   while (lo < hi) {
     const int mid = (lo + hi + 1) / 2;
-    if ((int)estep_df_lds_bytes(S, mid, d.nw, pair, d.R, d.qcap, fgrp) <= budget) lo = mid;
+    if ((int)estep_df_lds_bytes(S, mid, d.nw, d.na, pair, d.R, d.qcap, fgrp) <= budget) lo = mid;
     else hi = mid - 1;
   }
   d.fc = lo;

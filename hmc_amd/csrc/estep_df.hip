@@ -58,15 +58,21 @@ struct DfRing {
   unsigned long long rec;  // word offset of the locus's structure record
   unsigned long long tr;   // word offset of its trace record
   int F;
-  int done;  // states whose lists are final
+  int done;   // states whose lists are final
+  int locus;  // the locus in the slot, published once the slot is open
+  int pad;
 };
 
 struct DfShared {
   DfRing ring[DF_RMAX];
-  int q_head;  // tickets taken by the B segments
-  int abort;   // A stopped the individual (underflow, trace store full)
-  int status;  // the individual's status for the final selection
-  int q;       // next individual (block broadcast)
+  unsigned long long tcur;  // next trace word of the individual (the opener of each locus)
+  int q_head;   // tickets taken by the B segments
+  int q_tail;   // tickets queued by the A waves
+  int opening;  // the last locus an A wave has claimed to open
+  int a_fin;    // A waves done with the individual
+  int abort;    // A stopped the individual (underflow, trace store full)
+  int status;   // the individual's status for the final selection
+  int q;        // next individual (block broadcast)
 };
 
 // What a B segment needs to start a chain, written by the A lane that queued
@@ -84,15 +90,16 @@ struct DfPlan {
   int o_lpos, o_rpos, o_junk, o_slik, o_smeta, o_sh, o_queue, o_desc, o_ascr, o_flags, o_front;
   int front_stride, flag_words, bytes;
   int R, qcap, qlog, G, sws;  // ring slots, queue slots (2^qlog), segments per B wave, selection slots per B wave
+  int na;                     // A waves
 };
 
 __host__ __device__ inline int df_slots(int S, bool pair) {
   return pair ? (WAVE / S + 1) * 2 * S : (2 * S > WAVE ? 2 * S : WAVE);
 }
 
-// nb: B waves; fc: LDS states per ring slot; fcap: states per slot (HBM tier
-// size, and the flag bits)
-__host__ __device__ inline DfPlan df_plan(int S, int fc, int nb, bool pair, int R, int qcap, int fcap) {
+// na / nb: A / B waves; fc: LDS states per ring slot; fcap: states per slot
+// (HBM tier size, and the flag bits)
+__host__ __device__ inline DfPlan df_plan(int S, int fc, int na, int nb, bool pair, int R, int qcap, int fcap) {
   DfPlan p;
   int o = 0;
   auto take = [&](int bytes) { int r = o; o += (bytes + 15) & ~15; return r; };
@@ -105,7 +112,7 @@ __host__ __device__ inline DfPlan df_plan(int S, int fc, int nb, bool pair, int 
   p.o_sh = take((int)sizeof(DfShared));
   p.o_queue = take(qcap * 4);
   p.o_desc = take(qcap * (int)sizeof(DfChain));
-  p.o_ascr = take(WAVE * 4);
+  p.o_ascr = take(na * WAVE * 4);
   p.flag_words = (fcap + 31) / 32;
   p.o_flags = take(R * p.flag_words * 4);
   p.front_stride = (fc * (24 + 8 * S) + 15) & ~15;
@@ -117,6 +124,7 @@ __host__ __device__ inline DfPlan df_plan(int S, int fc, int nb, bool pair, int 
   while ((1 << p.qlog) < qcap) ++p.qlog;
   p.G = pair ? WAVE / S : WAVE / (2 * S);
   p.sws = sl;
+  p.na = na;
   return p;
 }
 
@@ -180,13 +188,14 @@ __device__ inline uint32_t ld_vol(const uint32_t *p) {
 __device__ inline void st_vol(uint32_t *p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+__device__ inline void st_vol(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ inline void rel_wg() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
 __device__ inline void acq_wg() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); }
 
 }  // namespace
 
-size_t estep_df_lds_bytes(int S, int fc, int nw, bool pair, int R, int qcap, int fcap) {
-  return (size_t)df_plan(S, fc, nw - 1, pair, R, qcap, fcap).bytes;
+size_t estep_df_lds_bytes(int S, int fc, int nw, int na, bool pair, int R, int qcap, int fcap) {
+  return (size_t)df_plan(S, fc, na, nw - na, pair, R, qcap, fcap).bytes;
 }
 size_t estep_df_scratch_bytes(int fcap, int S, int R) { return (size_t)R * df_front_bytes(fcap, S); }
 
@@ -198,7 +207,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
   extern __shared__ __align__(16) unsigned char smem[];
   const int S = a.S, L = a.L, hl = a.head_len;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;
-  const int NW = blockDim.x / WAVE, NB = NW - 1;
+  const int NW = blockDim.x / WAVE, NA = plan.na, NB = NW - NA;
   const int R = plan.R, qcap = plan.qcap;
   DfShared *sh = (DfShared *)(smem + plan.o_sh);
   uint32_t *queue = (uint32_t *)(smem + plan.o_queue);
@@ -213,7 +222,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
   };
   auto flags = [&](int slot) { return (uint32_t *)(smem + plan.o_flags) + (size_t)slot * plan.flag_words; };
   // B waves: the selection layout of estep_values
-  const int bw = wv - 1;
+  const int bw = wv - NA;
   const int sws = plan.sws;
   const int sps = PAIR ? sws : WAVE;
   const int bo = bw < 0 ? 0 : bw;
@@ -252,22 +261,32 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
     const unsigned long long *roff = a.rec_off + (size_t)bi * (L + 1);
     if (tid == 0) {
       sh->q_head = 0;
+      sh->q_tail = 0;
       sh->abort = 0;
       sh->status = EST_OK;
+      sh->opening = hl;
+      sh->a_fin = 0;
+      sh->tcur = a.trace_base[bi];
+      for (int r = 0; r < DF_RMAX; ++r) sh->ring[r].locus = -1;
     }
     __syncthreads();
 
-    if (wv == 0) {
+    if (wv < NA) {
       // ================================================================ A ====
-      unsigned long long tcur = a.trace_base[bi];
+      const int aw = wv;  // this A wave's chains and states: blocks of 64 aw, aw + NA, aw + 2 NA, ...
+      int *myascr = ascr + aw * WAVE;
       int status = EST_OK;
-      uint32_t qtail = 0;  // tickets queued (wave-uniform)
-      // queue `npush` entries from the lanes where `push` holds, in lane order
+      bool stop = false;  // another wave stopped the individual
+      // queue the entries of the lanes where `push` holds, in lane order, on
+      // consecutive tickets of the block's queue
       auto enqueue = [&](bool push, uint32_t entry, const DfChain &dc) {
         const uint64_t m = wave_ballot(push);
         if (!m) return;
+        int t0 = 0;
+        if (lane == 0) t0 = atomicAdd(&sh->q_tail, (int)__popcll(m));
+        t0 = __shfl(t0, 0);
         if (push) {
-          const uint32_t t = qtail + (uint32_t)__popcll(m & lanemask_lt());
+          const uint32_t t = (uint32_t)t0 + (uint32_t)__popcll(m & lanemask_lt());
           uint32_t *slot = queue + (t & (uint32_t)qmask);
           int guard = 0;
           while (ld_vol(slot) != 0u) {  // ticket t - qcap not taken yet
@@ -283,35 +302,56 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
             st_vol(slot, entry | QE_VALID | ((t >> qlog) & 63u) << QE_LAP);
           }
         }
-        qtail += (uint32_t)__popcll(m);
       };
-      // locus j into ring slot j % R: ring info, trace record, flags cleared
+      // wait until cond() holds; false when the individual was stopped (by
+      // another wave, or by this wave's watchdog)
+      auto wait_for = [&](auto cond) -> bool {
+        int guard = 0;
+        while (!cond()) {
+          const int ab = ld_vol(&sh->abort);
+          if (ab != 0) {
+            stop = true;
+            return false;
+          }
+          if (++guard > DF_SPIN_MAX) {
+            if (lane == 0) atomicExch(&sh->abort, DF_STALL);
+            status = EST_DF_STALL;
+            return false;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        return true;
+      };
+      // locus j into ring slot j % R: ring info, trace record, flags cleared,
+      // then the slot published (by the A wave that claimed the opening)
       auto open_locus = [&](int j) -> bool {
         const int b = j % R;
         const uint32_t *Rj = a.rec + roff[j];
         const int F = (int)Rj[0];
         const unsigned long long words = trace_locus_words((unsigned long long)F, S);
-        const unsigned long long off = tcur;
-        tcur += words;
+        const unsigned long long off = sh->tcur;
         if (off + words > a.trace_cap) return false;
         uint32_t *fl = flags(b);
         for (int w = lane; w < (F + 31) / 32; w += WAVE) fl[w] = 0u;
+        DfRing &g = sh->ring[b];
         if (lane == 0) {
-          DfRing &g = sh->ring[b];
           g.rec = roff[j];
           g.tr = off;
           g.F = F;
           g.done = 0;
+          sh->tcur = off + words;
           a.trace[off] = (uint32_t)F;
           a.loc_off[(size_t)bi * (L + 1) + j] = off;
         }
         wave_lds_sync();
+        rel_wg();
+        if (lane == 0) st_vol(&g.locus, j);
         return true;
       };
-      // ---- head list (HaploPair.cpp:14-33) ---------------------------------
-      if (!open_locus(hl)) {
+      // ---- head list (HaploPair.cpp:14-33), by A wave 0 ---------------------
+      if (aw == 0 && !open_locus(hl)) {
         status = EST_OVERFLOW_TRACE;
-      } else {
+      } else if (aw == 0) {
         const int b = hl % R;
         const uint32_t *Rh = a.rec + roff[hl];
         const int F = (int)Rh[0];
@@ -342,30 +382,32 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
         if (lane == 0) atomicAdd(&sh->ring[b].done, F);
       }
       // ---- forward over loci ------------------------------------------------
-      for (int j = hl + 1; j <= L && status == EST_OK; ++j) {
-        // the slot's previous occupant, locus j - R, must be complete (its last
-        // chains write into the slot) and so must its readers, locus j - R + 1
-        for (int jg = j - R; jg <= j - R + 1; ++jg) {
-          if (jg < hl) continue;
-          const DfRing *g = &sh->ring[jg % R];
-          int guard = 0;
-          while (ld_vol(&g->done) != ld_vol(&g->F)) {
-            if (++guard > DF_SPIN_MAX || ld_vol(&sh->abort) == DF_STALL) {
-              if (lane == 0) atomicExch(&sh->abort, DF_STALL);
-              break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-          }
-        }
-        if (ld_vol(&sh->abort) == DF_STALL) {
-          status = EST_DF_STALL;
-          break;
-        }
-        if (!open_locus(j)) {
-          status = EST_OVERFLOW_TRACE;
-          break;
-        }
+      for (int j = hl + 1; j <= L && status == EST_OK && !stop; ++j) {
         const int b = j % R, bx = (j - 1) % R;
+        // locus j-1 open (for the waves other than 0: the head); the first A
+        // wave here opens locus j, once the slot's previous occupant, locus
+        // j - R, is complete (its last chains write into the slot) and so are
+        // its readers, locus j - R + 1; the others wait for the slot
+        if (!wait_for([&] { return ld_vol(&sh->ring[bx].locus) == j - 1; })) break;
+        int won = 0;
+        if (lane == 0) won = atomicCAS(&sh->opening, j - 1, j) == j - 1;
+        won = __shfl(won, 0);
+        if (won) {
+          bool ok = true;
+          for (int jg = j - R; jg <= j - R + 1 && ok; ++jg) {
+            if (jg < hl) continue;
+            const DfRing *g = &sh->ring[jg % R];
+            ok = wait_for([&] { return ld_vol(&g->done) == ld_vol(&g->F); });
+          }
+          if (!ok) break;
+          if (!open_locus(j)) {
+            status = EST_OVERFLOW_TRACE;
+            break;
+          }
+        } else if (!wait_for([&] { return ld_vol(&sh->ring[b].locus) == j; })) {
+          break;
+        }
+        acq_wg();
         const DfFront X = front(bx), Y = front(b);
         const uint32_t *xfl = flags(bx);
         uint32_t *yfl = flags(b);
@@ -375,8 +417,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
         const uint32_t *Rhd = Rj + 4 + 2 * F, *Rcb = Rhd + F, *Rct = Rcb + F + 1, *Rch = Rct + C;
         const unsigned long long toff = sh->ring[b].tr;
         uint32_t *thd = a.trace + toff + 1, *tln = a.trace + trace_links(toff, (uint32_t)F);
-        int st = -1, rchk = 0;   // this lane's state, its first contribution not known to be final
-        int nextc = 0, scan = 0;  // next chain position, next candidate of the sweep over the others
+        int st = -1, rchk = 0;  // this lane's state, its first contribution not known to be final
+        // next chain position, next candidate of the sweep over the others: in
+        // this wave's blocks of 64 (block k of the locus when k % NA == aw)
+        int nextc = aw * WAVE, scan = aw * WAVE;
         bool underflow = false;
         int idle = 0;  // iterations in a row without a ready state (watchdog)
         while (true) {
@@ -384,27 +428,30 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           uint64_t fm = wave_ballot(st < 0);
           if (fm && nextc < NCH) {
             const int rk = __popcll(fm & lanemask_lt());
-            const int nt = min(__popcll(fm), NCH - nextc);
+            const int be = min((nextc / WAVE + 1) * WAVE, NCH);  // this block's end
+            const int nt = min(__popcll(fm), be - nextc);
             if (st < 0 && rk < nt) {
               st = (int)Rch[nextc + rk];
               rchk = (int)Rcb[st];
             }
             nextc += nt;
+            if (nextc % WAVE == 0) nextc += (NA - 1) * WAVE;  // block done: this wave's next one
             fm = wave_ballot(st < 0);
           }
           if (fm && nextc >= NCH && scan < F) {
+            const int bend = (scan / WAVE + 1) * WAVE;
             const int t = scan + lane;
-            const bool cand = t < F && !(Rhd[t < F ? t : 0] & HDR_CHAIN);
+            const bool cand = t < bend && t < F && !(Rhd[t < F ? t : 0] & HDR_CHAIN);
             const uint64_t cm = wave_ballot(cand);
             const int nc = __popcll(cm), nt = min(__popcll(fm), nc);
-            if (cand) ascr[__popcll(cm & lanemask_lt())] = t;
+            if (cand) myascr[__popcll(cm & lanemask_lt())] = t;
             wave_lds_sync();
             const int rk = __popcll(fm & lanemask_lt());
             if (st < 0 && rk < nt) {
-              st = ascr[rk];
+              st = myascr[rk];
               rchk = (int)Rcb[st];
             }
-            scan = nt < nc ? ascr[nt] : scan + WAVE;
+            scan = nt < nc ? myascr[nt] : bend + (NA - 1) * WAVE;
             wave_lds_sync();
           }
           const uint64_t held = wave_ballot(st >= 0);
@@ -438,7 +485,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
             ready = r == ce;
           }
           if (!wave_ballot(ready)) {
-            if (++idle > DF_SPIN_MAX || ld_vol(&sh->abort) == DF_STALL) {
+            if (ld_vol(&sh->abort) != 0) {
+              stop = true;
+              break;
+            }
+            if (++idle > DF_SPIN_MAX) {
               status = EST_DF_STALL;
               break;
             }
@@ -521,19 +572,24 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
             status = EST_NEEDS_EXACT;
             break;
           }
-          if (ld_vol(&sh->abort) == DF_STALL) {
-            status = EST_DF_STALL;
+          if (ld_vol(&sh->abort) != 0) {
+            stop = true;
             break;
           }
         }
       }
-      // END for every B segment: each has taken, or will take, one more ticket
       if (status == EST_DF_STALL && lane == 0) atomicExch(&sh->abort, DF_STALL);
-      if (lane == 0) {
-        sh->status = status;
-        if (status != EST_OK) atomicCAS(&sh->abort, 0, 1);
+      if (status != EST_OK && lane == 0) {
+        atomicCAS(&sh->status, EST_OK, status);
+        atomicCAS(&sh->abort, 0, 1);
       }
-      if (status != EST_DF_STALL)
+      rel_wg();
+      // the last A wave done queues END for every B segment (after every chain:
+      // each segment has taken, or will take, one more ticket)
+      int last = 0;
+      if (lane == 0) last = atomicAdd(&sh->a_fin, 1) == NA - 1;
+      last = __shfl(last, 0);
+      if (last && ld_vol(&sh->abort) != DF_STALL)
         for (int e = 0; e < nseg; e += WAVE) enqueue(e + lane < nseg, QE_END, DfChain{});
       if (ld_vol(&sh->abort) == DF_STALL && lane == 0) sh->status = EST_DF_STALL;
     } else {
@@ -728,14 +784,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
   }
 }
 
-hipError_t launch_estep_values_df(const ValueArgs &a, int grid, int nw, int wpe, bool pair, int R, int qcap,
+hipError_t launch_estep_values_df(const ValueArgs &a, int grid, int nw, int na, int wpe, bool pair, int R, int qcap,
                                   hipStream_t st) {
   const int G = pair ? WAVE / a.S : WAVE / (2 * a.S);
-  if (a.S < 1 || a.S > 32 || (pair && a.S > 16) || nw < 2 || nw > 16 || (wpe != 4 && wpe != 5) || R < 3 ||
-      R > DF_RMAX || qcap < 64 || (qcap & (qcap - 1)) || qcap > 4096 || qcap < (nw - 1) * G || !a.trace_base ||
-      a.fcap > F_MAX || a.lds_fc < 0 || a.lds_fc > a.fcap)
+  if (a.S < 1 || a.S > 32 || (pair && a.S > 16) || nw < 2 || nw > 16 || na < 1 || na >= nw || (wpe != 4 && wpe != 5) ||
+      R < 3 || R > DF_RMAX || qcap < 64 || (qcap & (qcap - 1)) || qcap > 4096 || qcap < (nw - na) * G ||
+      !a.trace_base || a.fcap > F_MAX || a.lds_fc < 0 || a.lds_fc > a.fcap)
     return hipErrorInvalidValue;
-  const DfPlan plan = df_plan(a.S, a.lds_fc, nw - 1, pair, R, qcap, a.fcap);
+  const DfPlan plan = df_plan(a.S, a.lds_fc, na, nw - na, pair, R, qcap, a.fcap);
   const size_t lds = (size_t)plan.bytes;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static size_t lds_attr = 0;

@@ -248,9 +248,9 @@ hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, 
 // Dataflow value pass (estep_df.hip): one A wave + nw-1 B waves per
 // individual, a ring of R >= 3 frontiers, a chain queue of qcap (power of two)
 // slots.  S <= 32 (pair: S <= 16), exact order only, trace_base required.
-size_t estep_df_lds_bytes(int S, int fc, int nw, bool pair, int R, int qcap, int fcap);
+size_t estep_df_lds_bytes(int S, int fc, int nw, int na, bool pair, int R, int qcap, int fcap);
 size_t estep_df_scratch_bytes(int fcap, int S, int R);
-hipError_t launch_estep_values_df(const ValueArgs &a, int grid, int nw, int wpe, bool pair, int R, int qcap,
+hipError_t launch_estep_values_df(const ValueArgs &a, int grid, int nw, int na, int wpe, bool pair, int R, int qcap,
                                   hipStream_t st);
 hipError_t launch_traceback(const TracebackArgs &a, int total_cands, hipStream_t st);
 hipError_t launch_transpose_rows_u8(const uint8_t *in, const int32_t *rowmap, uint8_t *out, int rows, int cols,

@@ -252,6 +252,11 @@ class HaploModel:
         (3 or 4, 0 = 3).  Results are identical."""
         self._check(lib().hmc_set_value_pass(self._h, {"auto": 0, "classic": 1, "dataflow": 2}[mode], int(ring)))
 
+    def set_dataflow_waves(self, a_waves: int):
+        """A waves of the dataflow value pass (hmc_set_dataflow_waves): 1..8,
+        0 = by the launch shape.  Results are identical."""
+        self._check(lib().hmc_set_dataflow_waves(self._h, int(a_waves)))
+
     def set_structure_pass(self, version: int):
         """Structure pass (hmc_set_structure_pass): 1 per-chunk ranking, 2 three
         block scans per locus, 0 automatic.  Results are identical."""

@@ -358,6 +358,11 @@ int hmc_set_value_pass(hmc_ctx *ctx, int mode, int ring);
  * first contribution, add order from each state's member segment); 0 =
  * automatic. */
 int hmc_set_structure_pass(hmc_ctx *ctx, int version);
+/* Dataflow value pass: wavefronts per individual that build the lists which
+ * need no selection (the "A" waves, each a fixed share of every locus's
+ * states), 1..8 and fewer than the waves per individual; 0 = by the launch
+ * shape.  Results are identical. */
+int hmc_set_dataflow_waves(hmc_ctx *ctx, int a_waves);
 /* Exact M-step trie walk: pattern-tree items (individual, start locus) per
  * wavefront, 1 (64 lanes each) or 4 (16 lanes each); 0 = automatic.  The
  * frequency sums are fixed-point integer adds, identical for any order. */

@@ -180,24 +180,26 @@ def test_value_one_link_layout(oracle_mod, name, S, shape):
     assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
 
 
-@pytest.mark.parametrize("name,S,shape,ring", [
-    ("a3miss5", 10, None, 3), ("a3miss5", 10, None, 4), ("n300", 10, None, 3), ("a8", 10, None, 3),
-    ("n60", 10, None, 3), ("a3miss5", 3, None, 3), ("a3miss5", 1, None, 3), ("a3miss5", 16, None, 4),
-    ("a3miss5", 17, None, 3), ("a8", 24, None, 3), ("a3miss5", 32, None, 4),
-    ("a3miss5", 10, (0, 0, 8, 2), 3), ("n300", 10, (0, 0, 3, 4), 3), ("a3miss5", 5, (0, 0, 16, 1), 4),
-    ("a8", 10, (0, 0, 2, 10), 3)])
-def test_dataflow_value_pass(oracle_mod, name, S, shape, ring):
-    """hmc_set_value_pass(dataflow): one wavefront builds the lists locus by
+@pytest.mark.parametrize("name,S,shape,ring,na", [
+    ("a3miss5", 10, None, 3, 0), ("a3miss5", 10, None, 4, 0), ("n300", 10, None, 3, 0), ("a8", 10, None, 3, 0),
+    ("n60", 10, None, 3, 0), ("a3miss5", 3, None, 3, 0), ("a3miss5", 1, None, 3, 0), ("a3miss5", 16, None, 4, 0),
+    ("a3miss5", 17, None, 3, 0), ("a8", 24, None, 3, 0), ("a3miss5", 32, None, 4, 0),
+    ("a3miss5", 10, (0, 0, 8, 2), 3, 0), ("n300", 10, (0, 0, 3, 4), 3, 0), ("a3miss5", 5, (0, 0, 16, 1), 4, 0),
+    ("a8", 10, (0, 0, 2, 10), 3, 0), ("a3miss5", 10, (0, 0, 8, 2), 3, 3), ("n300", 10, (0, 0, 4, 4), 3, 2),
+    ("a8", 10, (0, 0, 16, 1), 4, 7), ("a3miss5", 24, (0, 0, 6, 2), 3, 5)])
+def test_dataflow_value_pass(oracle_mod, name, S, shape, ring, na):
+    """hmc_set_value_pass(dataflow): A wavefronts build the lists locus by
     locus as soon as a state's predecessors are final, the others run the
     chains of adds of any open locus (estep_df.hip) — the E-step on the M0
     model equals HaploModel::resolveAll bit for bit, for sample sizes with two
     links per lane (S <= 16) and one (17..32), ring of 3 or 4 frontiers, 2 to
-    16 waves per individual."""
+    16 waves per individual, 1 to 7 A waves (na; 0 = by the shape)."""
     p = panel(name)
     o = oracle_mod.Oracle(p.alleles, p.types, sample_size=S)
     o.find_patterns()
     m = gpu_model(p, S)
     m.set_value_pass("dataflow", ring)
+    m.set_dataflow_waves(na)
     if shape:
         m.set_pass_shapes(*shape)
     m.find_patterns()
