@@ -411,7 +411,11 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
           pending.insert(pending.end(), other.begin(), other.end());
           k = (int)pick.size();
         }
-        const uint64_t share = rec_budget / (uint64_t)k;
+        // (at most 8 192 words per locus, or the store already allocated:
+        // mapping the whole budget, tens of GB, costs seconds per E-step on a
+        // fresh context; a region too small only defers its individual)
+        const uint64_t cap = std::max<uint64_t>(d_rec.n / (uint64_t)k, std::max<uint64_t>(1ull << 22, 8192ull * (uint64_t)L));
+        const uint64_t share = std::min<uint64_t>(rec_budget / (uint64_t)k, cap);
         for (int q = 0; q < k; ++q) {
           base[pending[q]] = (uint64_t)q * share;
           rsz[pending[q]] = share;
@@ -435,9 +439,10 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
         // the store left over goes to the estimated regions (up to 3x), so
         // fewer individuals are deferred to a pass of their own (A/B on one
         // box, cfg 3: E1 value passes 3.88 -> 3.60 s, E2 structure 218 -> 177 ms)
-        const double grow = r_est > 0 && r < rec_budget
-                                ? std::min(3.0, 1.0 + (double)(rec_budget - r) / (double)r_est)
-                                : 1.0;
+        // (within the store as allocated, or 1.25x the estimates: growing the
+        // allocation to the budget only for headroom costs its mapping time)
+        const uint64_t room = std::min<uint64_t>(rec_budget, std::max<uint64_t>(d_rec.n, r + r / 4));
+        const double grow = r_est > 0 && r < room ? std::min(3.0, 1.0 + (double)(room - r) / (double)r_est) : 1.0;
         r = 0;
         for (int q = 0; q < k; ++q) {
           const int bi = pending[q];
@@ -525,6 +530,9 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
       s1.prune = prune_;
       if ((e = d_nextq.ensure(2)) || (e = hipMemsetAsync(d_nextq.p, 0, 8, st))) return hipfail(e, "estep");
       s1.next_q = d_nextq.p;
+      if (debug_mem)
+        fprintf(stderr, "[hmc] structure pass v%d: %d individuals, %d waves x %d per CU, grid %d, LDS tier %d states%s\n",
+                v2 ? 2 : 1, np_, nw1, bpc1, grid1, s1.lds_fc, prune_ ? " (prune)" : "");
       hipEventRecord(ev[0], st);
       if ((e = v2 ? launch_estep_structure2(s1, grid1, nw1, st) : launch_estep_structure(s1, grid1, nw1, st)))
         return hipfail(e, "estep_structure launch");
@@ -778,7 +786,14 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
         const int bi = sset[pos + q];
         if (h_status[bi] == EST_OVERFLOW_TRACE) return fail(HMC_EHIP, "trace store overflow with exact sizes");
         if (h_status[bi] == EST_NEEDS_ORDER) return fail(HMC_EHIP, "exact value pass reported a tie");
-        if (h_status[bi] == EST_DF_STALL) return fail(HMC_EHIP, "dataflow value pass stalled (individual %d)", i0 + bi);
+        if (h_status[bi] == EST_DF_STALL) {  // the kernel leaves the watchdog's site in cost / total
+          int32_t at = 0;
+          double val = 0;
+          (void)hipMemcpy(&at, d_cost.p + bi, 4, hipMemcpyDeviceToHost);
+          (void)hipMemcpy(&val, d_total.p + bi, 8, hipMemcpyDeviceToHost);
+          return fail(HMC_EHIP, "dataflow value pass stalled (individual %d; site %d, wave %d, locus %d, value %.0f)", i0 + bi,
+                      at >> 24, (at >> 16) & 0xFF, at & 0xFFFF, val);
+        }
         if (h_status[bi] == EST_NEEDS_EXACT) h_redo.push_back(bi);
       }
       // ---- individuals whose forward likelihood underflowed: the reference

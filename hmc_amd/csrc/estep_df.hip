@@ -73,6 +73,7 @@ struct DfShared {
   int abort;    // A stopped the individual (underflow, trace store full)
   int status;   // the individual's status for the final selection
   int q;        // next individual (block broadcast)
+  int stall_at, stall_val;  // watchdog diagnostics: site << 24 | wave << 16 | locus, and a value of the site
 };
 
 // What a B segment needs to start a chain, written by the A lane that queued
@@ -243,6 +244,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
     __syncthreads();
     return sh->q;
   };
+  // the first watchdog to fire records where (reported through cost / total)
+  auto stall_note = [&](int site, int j, int val) {
+    if (atomicCAS(&sh->stall_at, 0, site << 24 | wv << 16 | (j & 0xFFFF)) == 0) sh->stall_val = val;
+  };
   for (int q = blockIdx.x; q < a.n_order; q = next_q()) {
     const int bi = a.order[q];
     const unsigned long long t_indiv = __builtin_amdgcn_s_memtime();
@@ -267,6 +272,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
       sh->opening = hl;
       sh->a_fin = 0;
       sh->tcur = a.trace_base[bi];
+      sh->stall_at = 0;
+      sh->stall_val = 0;
       for (int r = 0; r < DF_RMAX; ++r) sh->ring[r].locus = -1;
     }
     __syncthreads();
@@ -291,6 +298,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           int guard = 0;
           while (ld_vol(slot) != 0u) {  // ticket t - qcap not taken yet
             if (++guard > DF_SPIN_MAX || ld_vol(&sh->abort) == DF_STALL) {
+              if (guard > DF_SPIN_MAX) stall_note(3, 0, (int)t);
               atomicExch(&sh->abort, DF_STALL);
               break;
             }
@@ -305,7 +313,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
       };
       // wait until cond() holds; false when the individual was stopped (by
       // another wave, or by this wave's watchdog)
-      auto wait_for = [&](auto cond) -> bool {
+      auto wait_for = [&](auto cond, int site, int j, int val) -> bool {
         int guard = 0;
         while (!cond()) {
           const int ab = ld_vol(&sh->abort);
@@ -314,7 +322,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
             return false;
           }
           if (++guard > DF_SPIN_MAX) {
-            if (lane == 0) atomicExch(&sh->abort, DF_STALL);
+            if (lane == 0) {
+              stall_note(site, j, val);
+              atomicExch(&sh->abort, DF_STALL);
+            }
             status = EST_DF_STALL;
             return false;
           }
@@ -388,7 +399,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
         // wave here opens locus j, once the slot's previous occupant, locus
         // j - R, is complete (its last chains write into the slot) and so are
         // its readers, locus j - R + 1; the others wait for the slot
-        if (!wait_for([&] { return ld_vol(&sh->ring[bx].locus) == j - 1; })) break;
+        if (!wait_for([&] { return ld_vol(&sh->ring[bx].locus) == j - 1; }, 10, j, 0)) break;
         int won = 0;
         if (lane == 0) won = atomicCAS(&sh->opening, j - 1, j) == j - 1;
         won = __shfl(won, 0);
@@ -397,14 +408,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           for (int jg = j - R; jg <= j - R + 1 && ok; ++jg) {
             if (jg < hl) continue;
             const DfRing *g = &sh->ring[jg % R];
-            ok = wait_for([&] { return ld_vol(&g->done) == ld_vol(&g->F); });
+            ok = wait_for([&] { return ld_vol(&g->done) == ld_vol(&g->F); }, 11, j, jg);
           }
           if (!ok) break;
           if (!open_locus(j)) {
             status = EST_OVERFLOW_TRACE;
             break;
           }
-        } else if (!wait_for([&] { return ld_vol(&sh->ring[b].locus) == j; })) {
+        } else if (!wait_for([&] { return ld_vol(&sh->ring[b].locus) == j; }, 12, j, 0)) {
           break;
         }
         acq_wg();
@@ -458,6 +469,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           if (!held) {
             if (nextc >= NCH && scan >= F) break;
             if (++idle > DF_SPIN_MAX) {
+              if (lane == 0) stall_note(1, j, scan);
               status = EST_DF_STALL;
               break;
             }
@@ -490,6 +502,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
               break;
             }
             if (++idle > DF_SPIN_MAX) {
+              if (lane == 0) stall_note(2, j, st);  // (lane 0's state)
               status = EST_DF_STALL;
               break;
             }
@@ -653,6 +666,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           if (!wave_ballot(!done)) break;
           if (++idle > DF_SPIN_MAX) {
             if (lane == 0) {
+              stall_note(4, 0, ld_vol(&sh->q_tail) << 16 | (ld_vol(&sh->q_head) & 0xFFFF));
               atomicExch(&sh->abort, DF_STALL);
               sh->status = EST_DF_STALL;
             }
@@ -779,6 +793,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
       }
       a.total[bi] = total;
       a.ncand[bi] = cnt;
+      if (status == EST_DF_STALL) {  // where the watchdog fired (host message)
+        a.cost[bi] = sh->stall_at;
+        a.total[bi] = (double)sh->stall_val;
+      }
     }
     __syncthreads();
   }
