@@ -10,30 +10,35 @@
 // depends on its predecessors' final lists (HaploPair.cpp:35-89), so here the
 // block's waves run different loci at once:
 //
-//   A (wave 0) walks the loci in order.  A lane takes a state of the current
+//   A (waves 0..NA-1) walk the loci in order, each over a fixed share of
+//     every locus's states (blocks of 64 of the chain list and of the state
+//     range, block k to wave k % NA).  A lane takes a state of the current
 //     locus — the chains first, longest first (the record's chain list), then
 //     the other states — and, once every predecessor it reads is final (one
 //     bit per state of the previous locus), builds the state's list exactly as
 //     phase A does: the ordered forward sum, the extension constructor and the
 //     appends that fit.  A list that is complete is final at once; a chain's
 //     state goes to the chain queue.
-//   B (waves 1..NW-1) cut into segments of S lanes (two links per lane) or 2S
+//   B (waves NA..NW-1) cut into segments of S lanes (two links per lane) or 2S
 //     lanes; a segment takes the next chain from the queue, whatever its locus,
 //     and runs its adds with the libstdc++-exact segmented selection
 //     (coop_select.hpp), then marks the state final.
 //
-// Locus j's frontier lives in ring slot j % R (R >= 3).  A opens locus j only
-// when locus j-R+1 — the last reader of the slot's previous occupant, locus
-// j-R — is complete, so A runs up to R-2 loci ahead of the oldest open chain.
-// Every list is built by the same operations in the same order as in
+// Locus j's frontier lives in ring slot j % R (R >= 3).  The first A wave to
+// reach locus j opens it (trace record, flags, then the slot published) once
+// locus j-R+1 — the last reader of the slot's previous occupant, locus j-R —
+// is complete; A runs up to R-2 loci ahead of the oldest open chain.  Every
+// list is built by the same operations in the same order as in
 // estep_values, so the frontiers, the trace store and the results are
 // identical; only the interleaving across states changes.
 //
-// Queue: a ring of `qcap` words in LDS.  B segments take tickets (an LDS
-// counter); A writes the entry of ticket t into slot t % qcap once the slot is
-// empty, tagged with the lap t / qcap so a segment never takes an entry of
-// another lap.  After the last locus (or an abort) A queues one END entry per
-// segment, so every ticket taken is served and the queue is empty again.
+// Queue: a ring of `qcap` words in LDS.  A waves take tickets for their
+// entries and B segments tickets to serve (two LDS counters).  The entry of
+// ticket t goes to slot t % qcap once the slot holds the empty mark of lap
+// t / qcap, which the taker of ticket t - qcap leaves; entries carry their lap
+// too, so a segment never takes an entry of another lap and a producer never
+// overtakes an earlier lap's.  After the last locus (or an abort) the last A
+// wave queues one END entry per segment, so every ticket taken is served.
 #include "hmc_internal.hpp"
 #include "select.hpp"
 #include "coop_select.hpp"
@@ -236,7 +241,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
   const int sb = sg.g * 2 * S;
   const LinkList W{(double *)(smem + plan.o_slik), (uint32_t *)(smem + plan.o_smeta), 1};  // final selection
 
-  for (int i = tid; i < qcap; i += blockDim.x) queue[i] = 0u;
   __syncthreads();
   auto next_q = [&]() -> int {
     __syncthreads();
@@ -264,6 +268,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
       continue;
     }
     const unsigned long long *roff = a.rec_off + (size_t)bi * (L + 1);
+    for (int i = tid; i < qcap; i += blockDim.x) queue[i] = 0u;  // every slot free for lap 0
     if (tid == 0) {
       sh->q_head = 0;
       sh->q_tail = 0;
@@ -296,7 +301,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           const uint32_t t = (uint32_t)t0 + (uint32_t)__popcll(m & lanemask_lt());
           uint32_t *slot = queue + (t & (uint32_t)qmask);
           int guard = 0;
-          while (ld_vol(slot) != 0u) {  // ticket t - qcap not taken yet
+          // the slot is free for ticket t once ticket t - qcap was taken: the
+          // taker leaves the next lap's empty mark (several A waves write
+          // out of ticket order, so "empty" alone would let ticket t + qcap in first)
+          while (ld_vol(slot) != ((t >> qlog) & 63u) << QE_LAP) {
             if (++guard > DF_SPIN_MAX || ld_vol(&sh->abort) == DF_STALL) {
               if (guard > DF_SPIN_MAX) stall_note(3, 0, (int)t);
               atomicExch(&sh->abort, DF_STALL);
@@ -649,7 +657,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           }
           wave_lds_sync();  // the descriptor is read before its slot can be reused
           if (got) {
-            if (sg.k == 0) st_vol(queue + (tk & qmask), 0u);  // only the segment's first lane read the entry
+            if (sg.k == 0)  // (only the segment's first lane read the entry) free for ticket tk + qcap
+              st_vol(queue + (tk & qmask), ((((uint32_t)tk >> qlog) + 1u) & 63u) << QE_LAP);
             if (!done) {
               const DfRing &g = sh->ring[cs];
               const int F = g.F;
