@@ -133,9 +133,11 @@ int Ctx::estep(double *ll_out, int *H_out, uint64_t *re_out) {
             freeb / 1e9, d_trace.n * 4 / 1e9, d_rec.n * 4 / 1e9, trace_budget * 4 / 1e9, rec_budget * 4 / 1e9);
   // Stores sized by an earlier E-step when more HBM was free (E1, before an
   // exact M-step's tables) shrink to this E-step's budgets: the pass
-  // scratch is allocated from what they leave free.
-  if (d_trace.n > trace_budget) d_trace.release();
-  if (d_rec.n > rec_budget) d_rec.release();
+  // scratch is allocated from what they leave free.  (Past the budget by more
+  // than 1/8 only: the budgets move by a few GB with the M-step's buffers,
+  // and re-mapping a store of ~100 GB costs seconds.)
+  if (d_trace.n > trace_budget + trace_budget / 8) d_trace.release();
+  if (d_rec.n > rec_budget + rec_budget / 8) d_rec.release();
   h_total.assign(n, 0.0);
   h_ncand.assign(n, 0);
   h_status.assign(n, 0);
