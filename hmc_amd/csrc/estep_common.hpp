@@ -68,4 +68,31 @@ __device__ inline void copy_extended(const double *xl, const uint32_t *xm, doubl
   }
 }
 
+// copy_extended on the compact frontier (value_front.hpp): the predecessor's
+// homozygous flags as a bit mask xhm, the new flags into *yhm; the link words
+// go to the trace record tl only.
+template <int GRP = 4>
+__device__ inline void copy_extended_hm(const double *xl, unsigned long long xhm, double *yl, unsigned long long &yhm,
+                                        int k0, int ns, uint32_t s, double tpv, bool rev, bool differ, uint32_t *tl) {
+  for (int k = 0; k < ns; k += GRP) {
+    double v[GRP];
+#pragma unroll
+    for (int u = 0; u < GRP; ++u)
+      if (k + u < ns) v[u] = xl[k + u];
+#pragma unroll
+    for (int u = 0; u < GRP; ++u)
+      if (k + u < ns) {
+        double lk = v[u] * tpv;
+        bool homo = (xhm >> (k + u)) & 1ull;
+        if (differ && homo) {
+          if (rev) lk = 0.0;
+          homo = false;
+        }
+        yl[k0 + k + u] = lk;
+        yhm |= (unsigned long long)homo << (k0 + k + u);
+        tl[k0 + k + u] = meta_pack(s, (uint32_t)(k + u), rev, homo, false);
+      }
+  }
+}
+
 }  // namespace hmc

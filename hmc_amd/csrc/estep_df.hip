@@ -139,7 +139,7 @@ __host__ __device__ inline DfPlan df_plan(int S, int fc, int na, int nb, bool pa
 // likelihoods of every state; [0, fc) in LDS, the rest in HBM.  The link
 // words themselves live only in the trace record (the traceback reads them
 // there; a chain's partial list is read back from it): per state 24 + 8 S
-// bytes instead of the locus-synchronous pass's 16 + 12 S.
+// bytes, as the locus-synchronous pass (value_front.hpp).
 struct DfFront {
   unsigned char *l, *g;
   int fc, fcap, S;

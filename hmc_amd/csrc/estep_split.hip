@@ -1247,8 +1247,8 @@ __host__ __device__ inline K2Plan k2_plan(int S, int fc, int nw, bool pair = fal
   p.o_slik = take(nw * sl * 8);
   p.o_smeta = take(nw * sl * 4);
   p.o_bs = take((int)sizeof(K2Shared));
-  p.o_front[0] = take(fc * (16 + 12 * S));
-  p.o_front[1] = take(fc * (16 + 12 * S));
+  p.o_front[0] = take(fc * (24 + 8 * S));  // value_front.hpp: 24 + 8 S bytes per state
+  p.o_front[1] = take(fc * (24 + 8 * S));
   p.bytes = o;
   return p;
 }
@@ -1293,43 +1293,6 @@ __device__ inline void k2_trace_end(const ValueArgs &a, const TraceRec &tr, int 
     a.trace[tr.off] = (uint32_t)F;
     a.loc_off[(size_t)bi * (a.L + 1) + j] = tr.off;
   }
-}
-
-// The finished k-best lists of locus j into the trace store (same layout as
-// the fused kernel: [F][headers][pad][F x S link words]).
-__device__ inline bool k2_write_trace(const ValueArgs &a, K2Shared *bs, const VFront &Y, const uint32_t *Rhd, int F,
-                                      int j, int bi, unsigned long long &cur, unsigned long long &end) {
-  const int S = a.S, NT = (int)blockDim.x;
-  const unsigned long long words = trace_locus_words((unsigned long long)F, S);
-  const unsigned long long off = k2_trace_alloc(a, bs, cur, end, words);
-  if (off + words > a.trace_cap) return false;
-  uint32_t *hdr = a.trace + off + 1;
-  uint32_t *lnk = a.trace + trace_links(off, (uint32_t)F);
-#ifndef HMC_TRACE_PER_STATE
-  for (int t = threadIdx.x; t < F; t += NT) hdr[t] = (Rhd[t] & 0xFFFFu) | *Y.nl(t) << 16;
-  // the link block is the frontier's meta array in state order (LDS tier,
-  // then HBM tier), links past a list's length zeroed: one coalesced word
-  // per thread and step
-  const uint32_t nlw = (uint32_t)F * (uint32_t)S;
-  for (uint32_t w = threadIdx.x; w < nlw; w += (uint32_t)NT) {
-    const uint32_t t = w / (uint32_t)S, k = w - t * (uint32_t)S;
-    const uint32_t n = *Y.nl((int)t);
-    lnk[w] = k < n ? Y.meta((int)t)[k] : 0u;
-  }
-#else  // one thread per state, S words each
-  for (int t = threadIdx.x; t < F; t += NT) {
-    const uint32_t n = *Y.nl(t);
-    hdr[t] = (Rhd[t] & 0xFFFFu) | n << 16;
-    const uint32_t *pm = Y.meta(t);
-    uint32_t *dst = lnk + (size_t)t * S;
-    for (int k = 0; k < S; ++k) dst[k] = (uint32_t)k < n ? pm[k] : 0u;
-  }
-#endif
-  if (threadIdx.x == 0) {
-    a.trace[off] = (uint32_t)F;
-    a.loc_off[(size_t)bi * (a.L + 1) + j] = off;
-  }
-  return true;
 }
 
 }  // namespace
@@ -1434,16 +1397,25 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
     {
       const double *Rtp = (const double *)(R + 4);
       const uint32_t *Rhd = R + 4 + 2 * Fp;
-      for (int t = tid; t < Fp; t += NT) {
-        const bool homo = (Rhd[t] >> 24) & 1u;
-        const double tpv = Rtp[t];
-        *X.fwd(t) = homo ? tpv : tpv * 2.0;
-        X.lik(t)[0] = tpv;
-        X.meta(t)[0] = meta_pack(0, 0, false, homo, true);
-        *X.nl(t) = 1;
+      TraceRec tr;
+      if (!k2_trace_begin(a, bs, Fp, tcur, tend, tr)) {
+        status = EST_OVERFLOW_TRACE;
+      } else {
+        for (int t = tid; t < Fp; t += NT) {
+          const bool homo = (Rhd[t] >> 24) & 1u;
+          const double tpv = Rtp[t];
+          *X.fwd(t) = homo ? tpv : tpv * 2.0;
+          X.lik(t)[0] = tpv;
+          *X.hm(t) = homo ? 1ull : 0ull;
+          *X.nl(t) = 1;
+          tr.hdr[t] = (Rhd[t] & 0xFFFFu) | 1u << 16;
+          uint32_t *tl = tr.lnk + (size_t)t * S;
+          tl[0] = meta_pack(0, 0, false, homo, true);
+          for (int k = 1; k < S; ++k) tl[k] = 0u;
+        }
+        k2_trace_end(a, tr, Fp, hl, bi);
       }
       __syncthreads();
-      if (!k2_write_trace(a, bs, X, Rhd, Fp, hl, bi, tcur, tend)) status = EST_OVERFLOW_TRACE;
     }
 
     // ---- forward over loci ----------------------------------------------------
@@ -1496,17 +1468,17 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
         uint32_t w = Rct[cb];
         uint32_t s = cw_state(w), ns = cw_ns(w);
         double *yl = Y.lik(t);
-        uint32_t *ym = Y.meta(t);
+        unsigned long long yhm = 0ull;
         uint32_t *tl = tr.lnk + (size_t)t * S;
-        copy_extended<HMC_PA_UNROLL>(X.lik((int)s), X.meta((int)s), yl, ym, 0, (int)ns, s, tpv, cw_rev(w), differ, tl);
+        copy_extended_hm<HMC_PA_UNROLL>(X.lik((int)s), *X.hm((int)s), yl, yhm, 0, (int)ns, s, tpv, cw_rev(w), differ, tl);
         int k = (int)ns, r0 = ce;
         for (int r = cb + 1; r < ce; ++r) {
           w = Rct[r];
           s = cw_state(w);
           ns = cw_ns(w);
           if (k + (int)ns <= S) {
-            copy_extended<HMC_PA_UNROLL>(X.lik((int)s), X.meta((int)s), yl, ym, k, (int)ns, s, tpv, cw_rev(w), differ,
-                                         tl);
+            copy_extended_hm<HMC_PA_UNROLL>(X.lik((int)s), *X.hm((int)s), yl, yhm, k, (int)ns, s, tpv, cw_rev(w), differ,
+                                            tl);
             k += (int)ns;
           } else {
             r0 = r;
@@ -1518,6 +1490,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
         }
         tr.hdr[t] = (hd & 0xFFFFu) | (uint32_t)k << 16;
         *Y.fwd(t) = fwd;
+        *Y.hm(t) = yhm;  // (a chain's state: the flags of its partial list; the chain's end rewrites them)
         *Y.nl(t) = (uint32_t)k;
         *Y.r0(t) = (uint32_t)r0;
         if (!(fwd > 0.0) && j < L && !pruned) bs->flag = 1;
@@ -1567,14 +1540,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
                 k0 = (int)*Y.nl(st);
                 wc = Rct[r];
                 wn = r + 1 < re_ ? Rct[r + 1] : 0u;
+                // the partial list: likelihoods in the frontier, link words in the trace record
+                const uint32_t *pl = tr.lnk + (size_t)st * S;
                 if constexpr (WIDE) {
                   for (int kk = sg.k; kk < k0; kk += WAVE) {
                     slot_l[kk - sg.k] = Y.lik(st)[kk];
-                    slot_m[kk - sg.k] = Y.meta(st)[kk];
+                    slot_m[kk - sg.k] = pl[kk];
                   }
                 } else if (sg.k < k0) {
                   *slot_l = Y.lik(st)[sg.k];
-                  *slot_m = Y.meta(st)[sg.k];
+                  *slot_m = pl[sg.k];
                 }
               } else {
                 done = true;
@@ -1592,10 +1567,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
             auto extend = [&](int kk) {
               const int qk = kk - k0;
               double lk;
-              uint32_t pm;
-              X.ld_link((int)s, qk, lk, pm);
+              unsigned long long xhm;
+              X.ld_link((int)s, qk, lk, xhm);
               lk *= tpv;
-              bool homo = meta_homo(pm);
+              bool homo = (xhm >> qk) & 1ull;
               if (differ && homo) {
                 if (rev) lk = 0.0;
                 homo = false;
@@ -1639,19 +1614,23 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
               if (FAST && tie_v != 0.0 && tie_v == ss.slik[sg.base + S - 1]) bs->tie = 1;
               tie_v = 0.0;
               uint32_t *tl = tr.lnk + (size_t)st * S;
+              // (every lane of the segment is here: its positions < S are k, and for
+              // WIDE k + 64 >= S) the final list's homozygous flags, bit k = position k
+              const uint32_t fm = sg.k < S ? slot_m[0] : 0u;
+              const unsigned long long hb = (wave_ballot(sg.k < S && meta_homo(fm)) >> sg.base) &
+                                            (S >= 64 ? ~0ull : ((1ull << S) - 1ull));
               if constexpr (WIDE) {
                 for (int kk = sg.k; kk < S; kk += WAVE) {
                   Y.lik(st)[kk] = slot_l[kk - sg.k];
-                  Y.meta(st)[kk] = slot_m[kk - sg.k];
                   tl[kk] = slot_m[kk - sg.k];
                 }
               } else if (sg.k < S) {
                 Y.lik(st)[sg.k] = *slot_l;
-                Y.meta(st)[sg.k] = *slot_m;
                 tl[sg.k] = *slot_m;
               }
               if (sg.k == 0) {
                 *Y.nl(st) = (uint32_t)S;
+                *Y.hm(st) = hb;
                 tr.hdr[st] = (Rhd[st] & 0xFFFFu) | (uint32_t)S << 16;
               }
               ci = -1;
@@ -1693,7 +1672,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           const uint32_t n = *X.nl(t);
           for (uint32_t k = 0; k < n; ++k) {
             double lk = X.lik(t)[k];
-            const bool homo = meta_homo(X.meta(t)[k]);
+            const bool homo = (*X.hm(t) >> k) & 1ull;
             if (!homo) lk *= 2.0;
             W.set(cnt++, lk, meta_pack((uint32_t)t, k, false, homo, false));
           }
