@@ -73,6 +73,7 @@ _SIGS = [
     ("hmc_set_value_pass", _i, [_vp, _i, _i]),
     ("hmc_set_structure_pass", _i, [_vp, _i]),
     ("hmc_set_dataflow_waves", _i, [_vp, _i]),
+    ("hmc_set_end_order", _i, [_vp, _i]),
     ("hmc_set_exact_walk", _i, [_vp, _i]),
     ("hmc_last_value_pass", _i, [_vp, _P(_i)]),
     ("hmc_mine_level", _i, [_vp, _i, _i, _P(C.c_int32), _P(C.c_int32), _P(_d), _P(_u64)]),

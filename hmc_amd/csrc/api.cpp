@@ -229,6 +229,12 @@ int hmc_set_value_pass(hmc_ctx *h, int mode, int ring) {
   return HMC_OK;
 }
 
+int hmc_set_end_order(hmc_ctx *h, int on) {
+  if (!h || on < 0 || on > 1) return HMC_EARG;
+  h->c.end_order = on != 0;
+  return HMC_OK;
+}
+
 int hmc_set_dataflow_waves(hmc_ctx *h, int a_waves) {
   if (!h || a_waves < 0 || a_waves > 8) return HMC_EARG;
   h->c.df_na = a_waves;  // 0: by the launch shape

@@ -315,6 +315,15 @@ struct Ctx {
   DevBuf<double> t_freq, t_prefix, t_tp;
   DevBuf<uint8_t> t_last;
   DevBuf<uint32_t> t_succ, d_head_ids, d_head_pat0;
+  // The table in end-locus order for the structure pass (gmodel.hip), rebuilt
+  // on the first E-step after every change of the model (model_gen, below).
+  DevBuf<uint32_t> g_gid, g_inv, g_succ, g_keys;
+  DevBuf<double> g_tp;
+  DevBuf<uint8_t> g_last;
+  DevBuf<char> g_temp;
+  uint64_t gmodel_gen = ~0ull;  // the model_gen the end-order table was built for
+  bool end_order = true;        // hmc_set_end_order
+  int ensure_gmodel();
   int n_head = 0;
   // Table generations: every new table gets a new number; the candidate tree
   // (n_* arrays: the allele strings of a mined table) belongs to tree_gen.

@@ -369,6 +369,10 @@ int Ctx::estep_fused(const std::vector<int32_t> &order) {
 
 int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
   const int S = this->S(), n = nloc(), L = pan.L;
+  {
+    const int rc0 = ensure_gmodel();
+    if (rc0) return rc0;
+  }
   int32_t *dstatus = exact ? d_xstatus.p : d_status.p;
   int dev_cu = 256;
   hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, device);
@@ -889,7 +893,53 @@ DevModel Ctx::dev_model() const {
     m.hf_status = d_hf_status.p;
     m.head_al = d_head_al.p;
   }
+  if (end_order && gmodel_gen == model_gen && P > 0) {
+    m.gsucc = g_succ.p;
+    m.gtp = g_tp.p;
+    m.glast = g_last.p;
+    m.gid = g_gid.p;
+    m.ginv = g_inv.p;
+  }
   return m;
+}
+
+// The end-locus-ordered table of the current model (gmodel.hip): sorted ids,
+// their inverse, successors / tp / last alleles by g.  Without the HBM for it
+// the structure pass keeps the id-ordered table (same records).
+int Ctx::ensure_gmodel() {
+  if (!end_order || gmodel_gen == model_gen || P <= 0) return HMC_OK;
+  const int A = pan.amax;
+  const size_t tb = gmodel_sort_bytes(P, pan.L);
+  hipError_t e;
+  if ((e = g_gid.ensure(P)) || (e = g_inv.ensure(P)) || (e = g_succ.ensure((size_t)P * A)) || (e = g_keys.ensure(3 * (size_t)P)) ||
+      (e = g_tp.ensure(P)) || (e = g_last.ensure(P)) || (e = g_temp.ensure(std::max<size_t>(tb, 1)))) {
+    if (e != hipErrorOutOfMemory) return hipfail(e, "end-order table");
+    (void)hipGetLastError();
+    g_gid.release(), g_inv.release(), g_succ.release(), g_keys.release(), g_tp.release(), g_last.release(), g_temp.release();
+    return HMC_OK;  // gmodel_gen stays stale: the id-ordered table
+  }
+  GModelArgs g;
+  g.P = P;
+  g.A = A;
+  g.L = pan.L;
+  g.start = t_start.p;
+  g.len = t_len.p;
+  g.succ = t_succ.p;
+  g.tp = t_tp.p;
+  g.last = t_last.p;
+  g.key_in = g_keys.p;
+  g.key_out = g_keys.p + P;
+  g.id_in = g_keys.p + 2 * (size_t)P;
+  g.temp = g_temp.p;
+  g.temp_bytes = g_temp.n;
+  g.gid = g_gid.p;
+  g.inv = g_inv.p;
+  g.gsucc = g_succ.p;
+  g.gtp = g_tp.p;
+  g.glast = g_last.p;
+  if ((e = build_gmodel(g, st))) return hipfail(e, "end-order table");
+  gmodel_gen = model_gen;
+  return HMC_OK;
 }
 
 int Ctx::resolutions_idx(std::vector<uint8_t> &out) {

@@ -310,6 +310,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
   const uint64_t lt = lanemask_lt();
   const Blk<NW> B{(int *)(smem + plan.o_red), tid, lane, wv};
   const int S = a.S, L = a.pan.L, amax = a.pan.amax, hl = a.mod.head_len;
+  // the pattern table in end-locus order when the host built it (gmodel.hip):
+  // frontier states carry g instead of pattern ids, and one locus's lookups
+  // fall in one block of the table
+  const bool gsp = a.mod.gsucc != nullptr;
+  const uint32_t *SUCC = gsp ? a.mod.gsucc : a.mod.succ;
+  const double *TP = gsp ? a.mod.gtp : a.mod.tp;
+  const uint8_t *LAST = gsp ? a.mod.glast : a.mod.last;
+  auto to_g = [&](uint32_t id) -> uint32_t { return gsp ? a.mod.ginv[id] : id; };
+  auto to_id = [&](uint32_t gv) -> uint32_t { return gsp ? a.mod.gid[gv] : gv; };
   int *pr_off = (int *)(smem + plan.o_pairs);  // [npm+2]; [npm+1] = npairs
   uint8_t *pr_x = (uint8_t *)(pr_off + npm + 2);
   uint8_t *pr_y = pr_x + npm;
@@ -378,8 +387,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
       st0 = a.mod.hf_status[li];
       for (uint32_t t = a.mod.hf_off[li]; t < a.mod.hf_off[li + 1] && st0 == EST_OK; ++t) {
         if (Fp0 >= a.fcap) { st0 = EST_OVERFLOW_FRONTIER; break; }
-        *X.at(F_LO, Fp0) = a.mod.hf_pairs[2 * t];
-        *X.at(F_HI, Fp0) = a.mod.hf_pairs[2 * t + 1];
+        *X.at(F_LO, Fp0) = to_g(a.mod.hf_pairs[2 * t]);
+        *X.at(F_HI, Fp0) = to_g(a.mod.hf_pairs[2 * t + 1]);
         *X.at(F_NL, Fp0) = 1;
         ++Fp0;
       }
@@ -409,8 +418,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
           if (hq == NONE) { st0 = EST_NO_HEAD_PATTERN; break; }
           if (hq < head) continue;  // hp->id() >= head->id()
           if (Fp0 >= a.fcap) { st0 = EST_OVERFLOW_FRONTIER; break; }
-          *X.at(F_LO, Fp0) = head;
-          *X.at(F_HI, Fp0) = hq;
+          *X.at(F_LO, Fp0) = to_g(head);  // (head <= hq by id, so by g: both end at locus 0)
+          *X.at(F_HI, Fp0) = to_g(hq);
           *X.at(F_NL, Fp0) = 1;
           ++Fp0;
         }
@@ -435,12 +444,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         uint32_t *Rhd = R + 4 + 2 * Fp, *Rcb = Rhd + Fp;
         for (int t = tid; t < Fp; t += NT) {
           const uint32_t lo = *X.at(F_LO, t), hi = *X.at(F_HI, t);
-          Rtp[t] = a.mod.freq[lo] * a.mod.freq[hi];  // HaploPair.cpp:27
-          Rhd[t] = (uint32_t)a.mod.last[lo] | (uint32_t)a.mod.last[hi] << 8 | 1u << 16 | (lo == hi ? 1u << 24 : 0u);
+          Rtp[t] = a.mod.freq[to_id(lo)] * a.mod.freq[to_id(hi)];  // HaploPair.cpp:27
+          Rhd[t] = (uint32_t)LAST[lo] | (uint32_t)LAST[hi] << 8 | 1u << 16 | (lo == hi ? 1u << 24 : 0u);
           Rcb[t] = 0;
           if (a.exact) {  // head pairs' pattern ids (their alleles before head_len)
-            Rcb[Fp + 1 + t] = lo;
-            Rcb[2 * Fp + 1 + t] = hi;
+            Rcb[Fp + 1 + t] = to_id(lo);
+            Rcb[2 * Fp + 1 + t] = to_id(hi);
           }
         }
         if (tid == 0) {
@@ -458,7 +467,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     if (a.prune && status == EST_OK) {  // head pairs' forward likelihoods (HaploPair.cpp:27-32)
       for (int t = tid; t < Fp; t += NT) {
         const uint32_t lo = *X.at(F_LO, t), hi = *X.at(F_HI, t);
-        const double tpv = a.mod.freq[lo] * a.mod.freq[hi];
+        const double tpv = a.mod.freq[to_id(lo)] * a.mod.freq[to_id(hi)];
         fwx[t] = lo == hi ? tpv : tpv * 2.0;
       }
       B.sync();
@@ -522,8 +531,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
               g_s[q] = pr_o[p] == 2 ? (uint32_t)(local >> 1) : (uint32_t)local;
               const uint32_t x = o ? pr_y[p] : pr_x[p];
               const uint32_t y = o ? pr_x[p] : pr_y[p];
-              g_sa[q] = a.mod.succ[(size_t)*X.at(F_LO, (int)g_s[q]) * amax + x];
-              g_sb[q] = a.mod.succ[(size_t)*X.at(F_HI, (int)g_s[q]) * amax + y];
+              g_sa[q] = SUCC[(size_t)*X.at(F_LO, (int)g_s[q]) * amax + x];
+              g_sb[q] = SUCC[(size_t)*X.at(F_HI, (int)g_s[q]) * amax + y];
             }
           }
         }
@@ -635,10 +644,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
           *Y.at(F_NL, t) = nl;
           re += nl;
           if (!counting) {
-            Rtp[t] = a.mod.tp[lo] * a.mod.tp[hi];  // m_transition_prob, HaploPair.cpp:42
+            Rtp[t] = TP[lo] * TP[hi];  // m_transition_prob, HaploPair.cpp:42
             // bit 27: the state's adds overflow S (a chain; the dataflow value pass
             // takes the chains first, estep_df.hip)
-            Rhd[t] = (uint32_t)a.mod.last[lo] | (uint32_t)a.mod.last[hi] << 8 | nl << 16 | (nsum > (uint32_t)S ? HDR_CHAIN : 0u);
+            Rhd[t] = (uint32_t)LAST[lo] | (uint32_t)LAST[hi] << 8 | nl << 16 | (nsum > (uint32_t)S ? HDR_CHAIN : 0u);
             Rcb[t] = *Y.at(F_CB, t);
           }
           if (!counting && nsum > (uint32_t)S) {  // bucket 0 = most contributions

@@ -96,7 +96,32 @@ struct DevModel {
   const uint32_t *hf_pairs = nullptr;  // [2 x total] (head id, matching pattern id)
   const int32_t *hf_status = nullptr;  // [n] EST_OK or EST_NO_HEAD_PATTERN
   const uint8_t *head_al = nullptr;    // [P][head_len] alleles of the start-0 length-head_len patterns
+  // the same table in end-locus order (gmodel.hip), when built: g = position
+  // of a pattern among those sorted by (end locus, id); the structure pass
+  // (estep_structure) then carries g instead of ids
+  const uint32_t *gsucc = nullptr;  // [P][amax] g of the successor, NONE
+  const double *gtp = nullptr;      // [P] by g
+  const uint8_t *glast = nullptr;   // [P] by g
+  const uint32_t *gid = nullptr;    // [P] g -> id
+  const uint32_t *ginv = nullptr;   // [P] id -> g
 };
+
+// Build of the end-locus-ordered table (gmodel.hip): sort temporaries and outputs.
+struct GModelArgs {
+  int P = 0, A = 0, L = 0;
+  const int32_t *start = nullptr, *len = nullptr;
+  const uint32_t *succ = nullptr;
+  const double *tp = nullptr;
+  const uint8_t *last = nullptr;
+  uint32_t *key_in = nullptr, *key_out = nullptr, *id_in = nullptr;  // [P] each
+  void *temp = nullptr;
+  size_t temp_bytes = 0;
+  uint32_t *gid = nullptr, *inv = nullptr, *gsucc = nullptr;
+  double *gtp = nullptr;
+  uint8_t *glast = nullptr;
+};
+size_t gmodel_sort_bytes(int P, int L);
+hipError_t build_gmodel(const GModelArgs &g, hipStream_t st);
 
 struct EstepArgs {
   DevPanel pan;

@@ -252,6 +252,11 @@ class HaploModel:
         (3 or 4, 0 = 3).  Results are identical."""
         self._check(lib().hmc_set_value_pass(self._h, {"auto": 0, "classic": 1, "dataflow": 2}[mode], int(ring)))
 
+    def set_end_order(self, on: bool):
+        """Structure pass over the pattern table in end-locus order
+        (hmc_set_end_order; default on) or in id order.  Results are identical."""
+        self._check(lib().hmc_set_end_order(self._h, int(bool(on))))
+
     def set_dataflow_waves(self, a_waves: int):
         """A waves of the dataflow value pass (hmc_set_dataflow_waves): 1..8,
         0 = by the launch shape.  Results are identical."""

@@ -363,6 +363,11 @@ int hmc_set_structure_pass(hmc_ctx *ctx, int version);
  * states), 1..8 and fewer than the waves per individual; 0 = by the launch
  * shape.  Results are identical. */
 int hmc_set_dataflow_waves(hmc_ctx *ctx, int a_waves);
+/* Structure pass over the pattern table in end-locus order (1, default) or
+ * in the table's id order (0): the successor lookups of one locus fall in one
+ * block of the table instead of lines spread over all of it.  Results are
+ * identical. */
+int hmc_set_end_order(hmc_ctx *ctx, int on);
 /* Exact M-step trie walk: pattern-tree items (individual, start locus) per
  * wavefront, 1 (64 lanes each) or 4 (16 lanes each); 0 = automatic.  The
  * frequency sums are fixed-point integer adds, identical for any order. */

@@ -235,6 +235,26 @@ def test_structure_pass_v2(oracle_mod, name, shape, S):
         m.close()
 
 
+@pytest.mark.parametrize("name,S", [("a3miss5", 10), ("n300", 10), ("a8", 3), ("cfg1", 10), ("a4", 40)])
+def test_structure_end_order(oracle_mod, name, S):
+    """hmc_set_end_order: the structure pass over the pattern table sorted by
+    (end locus, id) (gmodel.hip) and over the id-ordered table give the same
+    E-step as HaploModel::resolveAll on the M0 model (the full-EM tests run
+    with it on: the default)."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=S)
+    o.find_patterns()
+    o.reset_counters()
+    ll1 = o.resolve_all()
+    for on in (True, False):
+        m = gpu_model(p, S)
+        m.set_end_order(on)
+        m.find_patterns()
+        ll_g, H, re_g = m.resolve_all()
+        assert_estep_equal(m, o, ll_g, ll1, H, re_g)
+        m.close()
+
+
 @pytest.mark.parametrize("name", ["n60", "miss2"])
 def test_structure_pass_v2_exact_em(oracle_mod, name):
     """The exact M-step's records (forward links in extendAll order, pair
