@@ -1,6 +1,7 @@
 """A/B of the value-pass schedules along the converged chain (E1, M1, E2, M2,
-E3 from M0): per configuration "mode:ring:vnw:vipc[:sv[:na]]" (mode classic | dataflow | fused,
-0 = automatic; sv = structure pass version 1 or 2; na = A waves of the dataflow pass) the chain restarts from M0 (hmc_em_rewind) and each E-step's
+E3 from M0): per configuration "mode:ring:vnw:vipc[:sv[:na[:eo]]]" (mode classic | dataflow | fused,
+0 = automatic; sv = structure pass version 1 or 2; na = A waves of the dataflow pass;
+eo = 0: structure pass over the id-ordered pattern table, 1 (default): end-locus order) the chain restarts from M0 (hmc_em_rewind) and each E-step's
 device ms of the passes is printed.  LL and R_E must not depend on the
 schedule.
 
@@ -29,6 +30,7 @@ for c in confs:
     mode, ring, vnw, vipc = f[:4]
     m.set_structure_pass(int(f[4]) if len(f) > 4 else 1)
     m.set_dataflow_waves(int(f[5]) if len(f) > 5 else 0)
+    m.set_end_order(int(f[6]) if len(f) > 6 else 1)
     m.set_estep_mode(1 if mode == "fused" else 0)  # fused: the single-pass kernel (no record store)
     m.set_value_pass("classic" if mode == "fused" else mode, int(ring))
     m.set_pass_shapes(0, 0, int(vnw), int(vipc))
