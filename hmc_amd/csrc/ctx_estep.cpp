@@ -786,6 +786,7 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
         hipEventElapsedTime(&ms, ev[0], ev[1]);
         ms_s2 += ms;
         ms_order += ms;
+        ++n_value_passes;  // (every value-kernel launch counts: the PMC pairing in tools/pmc_traffic.py)
       }
       h_redo.clear();
       for (size_t q = 0; q < k; ++q) {
@@ -833,6 +834,7 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
         if ((rc = read_status(sset, (int)k, true))) return rc;
         hipEventElapsedTime(&ms, ev[0], ev[1]);
         ms_fb += ms;
+        ++n_value_passes;
         for (int r : h_redo)
           if (h_status[r] != EST_OK && h_status[r] != EST_UNRESOLVED)
             return fail(HMC_EHIP, "underflow re-run: value status %d (individual %d)", h_status[r], i0 + r);
