@@ -134,58 +134,9 @@ __host__ __device__ inline DfPlan df_plan(int S, int fc, int na, int nb, bool pa
   return p;
 }
 
-// A ring slot's frontier: forward likelihood, list length, first add that
-// overflows, the homozygous flags of the list's links (bit k), and the S
-// likelihoods of every state; [0, fc) in LDS, the rest in HBM.  The link
-// words themselves live only in the trace record (the traceback reads them
-// there; a chain's partial list is read back from it): per state 24 + 8 S
-// bytes, as the locus-synchronous pass (value_front.hpp).
-struct DfFront {
-  unsigned char *l, *g;
-  int fc, fcap, S;
-  __device__ double *fwd(int t) const { return t < fc ? (double *)l + t : (double *)g + (t - fc); }
-  __device__ uint32_t *nl(int t) const {
-    return t < fc ? (uint32_t *)(l + (size_t)fc * 8) + t : (uint32_t *)(g + (size_t)fcap * 8) + (t - fc);
-  }
-  __device__ uint32_t *r0(int t) const {
-    return t < fc ? (uint32_t *)(l + (size_t)fc * 12) + t : (uint32_t *)(g + (size_t)fcap * 12) + (t - fc);
-  }
-  __device__ unsigned long long *hm(int t) const {
-    return t < fc ? (unsigned long long *)(l + (size_t)fc * 16) + t
-                  : (unsigned long long *)(g + (size_t)fcap * 16) + (t - fc);
-  }
-  __device__ double *lik(int t) const {
-    return t < fc ? (double *)(l + (size_t)fc * 24) + t * S : (double *)(g + (size_t)fcap * 24) + (size_t)(t - fc) * S;
-  }
-};
-__host__ __device__ inline size_t df_front_bytes(int fcap, int S) { return al256((size_t)fcap * (24 + 8 * S)); }
-
-// Copy the first ns links of predecessor s (likelihoods xl, homozygous flags
-// xhm) into a list at position k0, transformed as by the extension
-// constructor / add (HaploPair.cpp:35-80, as copy_extended); the link words
-// go to the trace record tl, the new flags into *yhm.
-__device__ inline void df_copy_extended(const double *xl, unsigned long long xhm, double *yl, unsigned long long &yhm,
-                                        int k0, int ns, uint32_t s, double tpv, bool rev, bool differ, uint32_t *tl) {
-  for (int k = 0; k < ns; k += 4) {
-    double v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (k + u < ns) v[u] = xl[k + u];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (k + u < ns) {
-        double lk = v[u] * tpv;
-        bool homo = (xhm >> (k + u)) & 1ull;
-        if (differ && homo) {
-          if (rev) lk = 0.0;
-          homo = false;
-        }
-        yl[k0 + k + u] = lk;
-        yhm |= (unsigned long long)homo << (k0 + k + u);
-        tl[k0 + k + u] = meta_pack(s, (uint32_t)(k + u), rev, homo, false);
-      }
-  }
-}
+// A ring slot's frontier: the value pass's compact frontier (value_front.hpp,
+// VFront): [0, fc) in LDS, the rest in HBM.
+__host__ __device__ inline size_t df_front_bytes(int fcap, int S) { return k2_front_bytes(fcap, S); }
 
 __device__ inline int ld_vol(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ inline uint32_t ld_vol(const uint32_t *p) {
@@ -223,7 +174,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
   char *sp = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
   const size_t hbm_slot = df_front_bytes(a.fcap, S);
   auto front = [&](int slot) {
-    return DfFront{smem + plan.o_front + (size_t)slot * plan.front_stride, (unsigned char *)sp + (size_t)slot * hbm_slot,
+    return VFront{smem + plan.o_front + (size_t)slot * plan.front_stride, (unsigned char *)sp + (size_t)slot * hbm_slot,
                   a.lds_fc, a.fcap, S};
   };
   auto flags = [&](int slot) { return (uint32_t *)(smem + plan.o_flags) + (size_t)slot * plan.flag_words; };
@@ -376,7 +327,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
         const int F = (int)Rh[0];
         const double *Rtp = (const double *)(Rh + 4);
         const uint32_t *Rhd = Rh + 4 + 2 * F;
-        const DfFront Y = front(b);
+        const VFront Y = front(b);
         const unsigned long long off = sh->ring[b].tr;
         uint32_t *thd = a.trace + off + 1, *tln = a.trace + trace_links(off, (uint32_t)F);
         for (int t = lane; t < F; t += WAVE) {
@@ -427,7 +378,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           break;
         }
         acq_wg();
-        const DfFront X = front(bx), Y = front(b);
+        const VFront X = front(bx), Y = front(b);
         const uint32_t *xfl = flags(bx);
         uint32_t *yfl = flags(b);
         const uint32_t *Rj = a.rec + roff[j];
@@ -550,14 +501,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
             double *yl = Y.lik(t);
             unsigned long long yhm = 0ull;
             uint32_t *tl = tln + (size_t)t * S;
-            df_copy_extended(X.lik((int)s), *X.hm((int)s), yl, yhm, 0, (int)ns, s, tpv, cw_rev(w), differ, tl);
+            copy_extended_hm<4>(X.lik((int)s), *X.hm((int)s), yl, yhm, 0, (int)ns, s, tpv, cw_rev(w), differ, tl);
             int k = (int)ns, r0 = ce;
             for (int r = cb + 1; r < ce; ++r) {
               w = Rct[r];
               s = cw_state(w);
               ns = cw_ns(w);
               if (k + (int)ns <= S) {
-                df_copy_extended(X.lik((int)s), *X.hm((int)s), yl, yhm, k, (int)ns, s, tpv, cw_rev(w), differ, tl);
+                copy_extended_hm<4>(X.lik((int)s), *X.hm((int)s), yl, yhm, k, (int)ns, s, tpv, cw_rev(w), differ, tl);
                 k += (int)ns;
               } else {
                 r0 = r;
@@ -662,7 +613,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
             if (!done) {
               const DfRing &g = sh->ring[cs];
               const int F = g.F;
-              const DfFront Y = front(cs);
+              const VFront Y = front(cs);
               if (sg.k < k0) {  // the partial list: likelihoods here, link words in the trace record
                 *slot_l = Y.lik(st)[sg.k];
                 *slot_m = a.trace[trace_links(g.tr, (uint32_t)F) + (size_t)st * S + sg.k];
@@ -687,7 +638,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
         idle = 0;
         int n = 0;
         if (have) {
-          const DfFront X = front((cs + R - 1) % R);
+          const VFront X = front((cs + R - 1) % R);
           const unsigned long long xhm = *X.hm((int)cw_state(wc));
           const uint32_t s = cw_state(wc), ns = cw_ns(wc);
           const bool rev = cw_rev(wc);
@@ -723,7 +674,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
           k0 = S;
           if (++r == re_) {  // the chain's list is final
             const DfRing &g = sh->ring[cs];
-            const DfFront Y = front(cs);
+            const VFront Y = front(cs);
             const uint32_t *Rj = a.rec + g.rec;
             const int F = g.F;
             const uint32_t *Rhd = Rj + 4 + 2 * F;
@@ -760,7 +711,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
       int status = sh->status;
       int cnt = 0;
       double total = 0.0;
-      const DfFront X = front(L % R);
+      const VFront X = front(L % R);
       const int Fp = sh->ring[L % R].F;
       if (status == EST_OK) {
         for (int t = 0; t < Fp; ++t) {
