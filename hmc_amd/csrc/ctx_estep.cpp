@@ -688,11 +688,13 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
       // individuals: more selection segments and LDS per individual.
       const int per_cu = (int)((k + dev_cu - 1) / dev_cu);
       const bool small_heavy = heavy && per_cu < 4;
-      // (heavy groups filling the GPU: 8 waves x 2 per CU, cfg 3 E1 values
-      // 2.95 -> 2.68 s against 4 x 4, profiles/r03/e1/e1_wide.log)
+      // (heavy groups filling the GPU: 4 waves x 4 per CU since the compact
+      // frontier, cfg 3 E1 values 2 192 -> 2 134 ms against 8 x 2,
+      // profiles/r04/shapes/value_shapes_cfg3.log; with the round-3 frontier
+      // 8 x 2 had won, 2.95 -> 2.68 s, profiles/r03/e1/e1_wide.log)
       int vnw = vp_nw > 0 ? vp_nw
                           : (small_heavy ? 16 / per_cu
-                                         : (heavy ? 8 : ((int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3))));
+                                         : (heavy ? 4 : ((int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3))));
       int vipc = vp_ipc > 0 ? vp_ipc
                             : (small_heavy ? per_cu
                                            : (vnw == 1 ? 20 : (vnw >= 8 ? 2 : (vnw >= 4 ? 4 : 8))));  // a half-given shape completes by the same rule
