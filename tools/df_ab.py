@@ -1,7 +1,8 @@
 """A/B of the value-pass schedules along the converged chain (E1, M1, E2, M2,
-E3 from M0): per configuration "mode:ring:vnw:vipc[:sv[:na[:eo]]]" (mode classic | dataflow | fused,
+E3 from M0): per configuration "mode:ring:vnw:vipc[:sv[:na[:eo[:snw:sipc]]]]" (mode classic | dataflow | fused,
 0 = automatic; sv = structure pass version 1 or 2; na = A waves of the dataflow pass;
-eo = 0: structure pass over the id-ordered pattern table, 1 (default): end-locus order) the chain restarts from M0 (hmc_em_rewind) and each E-step's
+eo = 0: structure pass over the id-ordered pattern table, 1 (default): end-locus order;
+snw / sipc: structure-pass waves per individual / individuals per CU) the chain restarts from M0 (hmc_em_rewind) and each E-step's
 device ms of the passes is printed.  LL and R_E must not depend on the
 schedule.
 
@@ -33,7 +34,7 @@ for c in confs:
     m.set_end_order(int(f[6]) if len(f) > 6 else 1)
     m.set_estep_mode(1 if mode == "fused" else 0)  # fused: the single-pass kernel (no record store)
     m.set_value_pass("classic" if mode == "fused" else mode, int(ring))
-    m.set_pass_shapes(0, 0, int(vnw), int(vipc))
+    m.set_pass_shapes(int(f[7]) if len(f) > 7 else 0, int(f[8]) if len(f) > 8 else 0, int(vnw), int(vipc))
     m.em_rewind()
     line = []
     for k in range(1, 4):
