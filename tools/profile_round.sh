@@ -26,7 +26,7 @@ FC=$(find "$OUT/pmc_fetch" -name "*counter_collection.csv" | head -n 1)
 WC=$(find "$OUT/pmc_write" -name "*counter_collection.csv" | head -n 1)
 python3 tools/pmc_traffic.py "$FC" "$WC" $K "$DEST/pmc_${K}_cfg$CFG.json" \
   "rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE (separate passes) --kernel-include-regex $K -- python3 $BENCH" \
-  "$OUT/pmc_fetch.json"
+  "$OUT/pmc_fetch.json" "$OUT/pmc_write.json"
 cp "$FC" "$DEST/pmc_fetch_size_cfg$CFG.csv"
 cp "$WC" "$DEST/pmc_write_size_cfg$CFG.csv"
 echo "[profile] kernel trace" >&2
