@@ -941,7 +941,9 @@ int Ctx::ensure_gmodel() {
   g.gsucc = g_succ.p;
   g.gtp = g_tp.p;
   g.glast = g_last.p;
-  if ((e = build_gmodel(g, st))) return hipfail(e, "end-order table");
+  if ((e = build_gmodel(g, st)) || (e = hipStreamSynchronize(st))) return hipfail(e, "end-order table");
+  g_keys.release();  // sort keys and scratch: only the build needs them (cfg 4's 720 M patterns: ~10 GB)
+  g_temp.release();
   gmodel_gen = model_gen;
   return HMC_OK;
 }
