@@ -942,8 +942,10 @@ int Ctx::ensure_gmodel() {
   g.gtp = g_tp.p;
   g.glast = g_last.p;
   if ((e = build_gmodel(g, st)) || (e = hipStreamSynchronize(st))) return hipfail(e, "end-order table");
-  g_keys.release();  // sort keys and scratch: only the build needs them (cfg 4's 720 M patterns: ~10 GB)
-  g_temp.release();
+  if (g_keys.n * 4 + g_temp.n > (2ull << 30)) {  // only the build needs them: give large ones back (cfg 4's
+    g_keys.release();                              // 720 M patterns: ~10 GB); small ones stay mapped (re-mapping
+    g_temp.release();                              // costs more than the next model's build)
+  }
   gmodel_gen = model_gen;
   return HMC_OK;
 }
