@@ -123,10 +123,13 @@ int Ctx::estep(double *ll_out, int *H_out, uint64_t *re_out) {
   // (cfg 3's E1 with the M0 model needs ~2x HBM in records + traces; larger
   // stores (fewer groups) measured no faster and crowd out the next M0.  The
   // trace cap keeps cfg 3's E2.. (~90 GB of traces) in one value pass.)
-  trace_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.42), 120ull << 30),
+  // (round 4, compact value frontier: 130 / 88 GiB gives cfg 3's E1 five
+  // groups instead of five or six, E1 3.47 -> 3.36 s; 145 / 98 and 110 / 74
+  // measured slower, profiles/r04/shapes/store_ab_cfg3.log)
+  trace_budget = std::max<uint64_t>(trace_bytes ? trace_bytes : std::min<uint64_t>((uint64_t)(avail * 0.46), 130ull << 30),
                                     1ull << 16) / 4;
   rec_budget = std::max<uint64_t>(rec_bytes ? rec_bytes : trace_bytes ? trace_bytes
-                                  : std::min<uint64_t>((uint64_t)(avail * 0.28), 80ull << 30),
+                                  : std::min<uint64_t>((uint64_t)(avail * 0.31), 88ull << 30),
                                   1ull << 16) / 4;
   if (debug_mem)
     fprintf(stderr, "[hmc] E-step: free %.1f GB, stores %.1f + %.1f GB, budgets trace %.1f rec %.1f GB\n",
