@@ -589,7 +589,9 @@ __global__ __launch_bounds__(64) void bench_seg2(int S, int adds, double *out) {
   if (lane == 0) out[blockIdx.x] = acc;
 }
 
-// mode 5: two elements per lane, S lanes per list (seg2_nth_slots)
+// mode 5: two elements per lane, S lanes per list (seg2_nth_slots); mode 8:
+// the same (the round-4 A/B of the cut from the swap count, now the only one)
+template <bool KCUT>
 __global__ __launch_bounds__(64) void bench_seg2e(int S, int adds, double *out) {
   extern __shared__ unsigned char sm[];
   const int lane = threadIdx.x;
@@ -612,6 +614,7 @@ __global__ __launch_bounds__(64) void bench_seg2e(int S, int adds, double *out) 
       ss.smeta[sb + S + sg.k] = 64u * r + sg.k;
     }
     wave_lds_sync();
+    (void)KCUT;
     seg2_nth_slots(in ? 2 * S : 0, S - 1, sg, ss);
   }
   double acc = 0.0;
@@ -651,19 +654,19 @@ int main(int argc, char **argv) {
   // mode 2/3 with wpc / (32 / S) process the same lists.
   const int G = 64 / (2 * S);
   const int lists = mode == 2 || mode == 3 ? cu * wpc * 64 : cu * wpc * G;
-  if (mode < 0 || mode == 1 || mode > 7) return 1;
+  if (mode < 0 || mode == 1 || mode > 8) return 1;
   const int G5 = 64 / S, G6 = 64 / ((2 * S + 3) / 4);
   int grid = mode == 0 ? cu * wpc
                        : (mode == 4 ? cu * wpc / 2
-                                    : (mode == 5 || mode == 7 ? (lists + G5 - 1) / G5
+                                    : (mode == 5 || mode == 7 || mode == 8 ? (lists + G5 - 1) / G5
                                                               : (mode == 6 ? (lists + G6 - 1) / G6 : (lists + 63) / 64)));
-  size_t lds = mode == 2 || mode == 3 ? (size_t)2 * S * 64 * 12 : (mode == 4 ? 4096 : (mode == 5 || mode == 7 ? 4608 : (mode == 6 ? 8448 : 2048)));
+  size_t lds = mode == 2 || mode == 3 ? (size_t)2 * S * 64 * 12 : (mode == 4 ? 4096 : (mode == 5 || mode == 7 || mode == 8 ? 4608 : (mode == 6 ? 8448 : 2048)));
   void (*kern)(int, int, double *) =
       mode == 0 ? bench_seg
                 : (mode == 2 ? bench_lane<false>
                              : (mode == 3 ? bench_lane<true>
                                           : (mode == 4 ? bench_seg2
-                                                       : (mode == 5 ? bench_seg2e : (mode == 6 ? bench_seg4e : bench_seg2m)))));
+                                                       : (mode == 5 ? bench_seg2e<false> : (mode == 8 ? bench_seg2e<true> : (mode == 6 ? bench_seg4e : bench_seg2m))))));
   if (lds > 65536) (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   double *out;
   (void)hipMalloc(&out, grid * sizeof(double));
