@@ -700,7 +700,10 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
                                          : (heavy ? 4 : ((int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3))));
       int vipc = vp_ipc > 0 ? vp_ipc
                             : (small_heavy ? per_cu
-                                           : (vnw == 1 ? 20 : (vnw >= 8 ? 2 : (vnw >= 4 ? 4 : 8))));  // a half-given shape completes by the same rule
+                                           : (vnw == 1 ? 16 : (vnw >= 8 ? 2 : (vnw >= 4 ? 4 : 8))));  // a half-given shape completes by the same rule
+      // (one wave per individual: 16 per CU on the 4-wave build since the
+      // swap-count cut, cfg 3 E3 values 507 -> 479 ms, E2 equal; 20 on the
+      // 5-wave build before, profiles/r04/shapes/one_wave_16_vs_20_cfg3.log)
       // the HBM tier of the value frontiers holds the group's largest
       // frontier (pass 1 measured it), not the structure pass's capacity
       int fgrp = 1;
