@@ -409,7 +409,12 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
       // measured individuals nearest in cost (cfg 3 E1 after E5: 7.1 -> 5.9 s,
       // deferred 1 713 -> 12 per group, profiles/r02/e1_groups/)
       if (!have_est) {  // nothing measured yet: 4 per CU share the store evenly
-        k = std::min(np, 4 * dev_cu);
+        // (a model smaller than the panel — cfg 3's E2 after the M0-based E1 —
+        // gives every individual a share: its records fit, and the E-step runs
+        // in one group instead of a sample group and the rest; the M0 model's
+        // E1 needs more per individual than an even share, so it samples first)
+        const bool light = exact ? false : (double)P <= (double)pan.N * (double)pan.L;
+        k = light ? np : std::min(np, 4 * dev_cu);
         if (np > k) {  // every np/k-th of the heaviest-first list
           std::vector<int32_t> pick, other;
           pick.reserve(k);
