@@ -51,15 +51,16 @@ from hmc_amd import synth  # noqa: E402
 
 METRIC = "individuals×loci/sec per EM iter, synthetic panel, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E (spec)
-PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r04", "r03")]  # newest profile of the workload first
+PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r05", "r04", "r03")]  # newest profile of the workload first
 DBL_MAX = sys.float_info.max
 # What bounds estep_values (SQ counters under profiles/): the
-# roofline above prices it against HBM, but the kernel moves ~1/30 of peak —
-# its waves are parked on dependent LDS round trips and barriers.
+# roofline prices it against HBM as the contract asks, but the kernel moves a
+# few % of peak; its VALU issue (SQ_INSTS_VALU, tools/sq_summary.py) is the
+# roof it runs against.
 # The sampled CPU estimate checked against the whole single-thread chain at
 # cfg 2 (bench.py --config 2 --cpu-validate on a GPU box, same run).
 VALIDATION_NOTE = "profiles/r04/cpu_validate_cfg2.json"
-LIMITER = "issue/latency: dependent selection steps and per-locus barriers (SQ counters, DESIGN.md 9), not HBM bandwidth"
+LIMITER = "VALU issue of the segmented k-best selection (SQ_INSTS_VALU x 4 cycles over the SIMDs' issue capacity, DESIGN.md 9), not HBM bandwidth"
 
 
 def parse():
@@ -237,6 +238,7 @@ def main():
         wall = time.perf_counter() - t_s
         t = m.timings()
         sp = m.estep_split_stats()
+        ms_stats = m.mine_stats() if go or force_m else {"reduction_ms": 0.0, "reduction_levels": 0}
         run_log.append([int(log["r_e"]), int(sp["value_passes"])])
         progress(f"EM iteration {it}: LL {log['log_likelihood']:.6f}, R_E {log['r_e']}, "
                  f"E {t['estep_forward_ms'] + t['estep_traceback_ms']:.0f} ms "
@@ -249,7 +251,8 @@ def main():
                     values_ms=sp["values_ms"], fallback_ms=sp["fallback_ms"], n_fallback=sp["n_fallback"],
                     struct_passes=sp["structure_passes"], value_passes=sp["value_passes"],
                     tb_ms=t["estep_traceback_ms"], mstep_ms=t["mstep_ms"] if go or force_m else 0.0,
-                    value_dataflow=m.last_value_pass_dataflow())
+                    value_dataflow=m.last_value_pass_dataflow(), reduction_ms=ms_stats["reduction_ms"],
+                    reduction_levels=ms_stats["reduction_levels"])
 
     for _ in range(args.warmup):
         em_step()
@@ -308,7 +311,16 @@ def main():
     r_m_all = sum_over_ranks(float(sum(s["r_m"] for s in steps)))  # each rank scans its own samples
     b_iter = (2.0 * N * L * args.steps + 2.0 * H_all * L + 8.0 * r_e_all + r_m_all) / args.steps
     ach_iter = b_iter / (elapsed / args.steps) / 1e9
-    pmc = pmc_summary(args.tag)
+    pmc = pmc_summary(args.tag, ident)
+    sq = sq_summary(args.tag, ident)
+    # the bound from the evidence: the fraction of the VALU issue roof the SQ
+    # pass measured against the fraction of HBM bandwidth the PMC pass measured
+    hbm_frac_meas = None
+    if pmc and pmc.get("hbm_bytes_per_launch") and val_ms > 0 and n_launch:
+        hbm_frac_meas = pmc["hbm_bytes_per_launch"] / (val_ms * 1e-3 / n_launch) / 1e9 / HBM_PEAK_GBS
+    bound = "hbm"
+    if sq and sq.get("valu_issue_frac") is not None:
+        bound = "valu-issue" if sq["valu_issue_frac"] > (hbm_frac_meas or achieved / HBM_PEAK_GBS) else "hbm"
 
     if rank == 0:
         line = {
@@ -341,11 +353,19 @@ def main():
                       "ms_per_iteration": chain_s / chain_iters * 1e3 if chain_iters else None},
             "value_steady": steady,
             "roofline": {
-                "bound": "hbm", "kernel": "estep_values",
+                "bound": bound, "kernel": "estep_values",
                 "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
-                "traffic_over_alg": pmc.get("traffic_over_alg") if pmc else None,
+                "traffic": pmc.get("hbm_bytes_per_launch") if pmc and pmc["same_build"] else None,
+                "traffic_over_alg": pmc.get("traffic_over_alg") if pmc and pmc["same_build"] else None,
                 "traffic_source": pmc.get("source") if pmc else None,
+                "traffic_same_build": pmc["same_build"] if pmc else None,
+                "hbm_frac_measured": hbm_frac_meas if pmc and pmc["same_build"] else None,
+                "valu_issue_frac": sq["valu_issue_frac"] if sq and sq["same_build"] else None,
+                "valu_issue_frac_2cyc": sq["valu_issue_frac_2cyc"] if sq and sq["same_build"] else None,
+                "lds_bank_conflict_ratio": sq["lds_bank_conflict_ratio"] if sq and sq["same_build"] else None,
+                "valu_issue_source": sq.get("source") if sq else None,
+                "valu_issue_same_build": sq["same_build"] if sq else None,
+                "valu_issue_formula": "SQ_INSTS_VALU * 4 cycles / (1024 SIMDs * 2.4 GHz * kernel time of the SQ pass)",
                 "limiter": LIMITER,
                 "alg_bytes_per_launch": 8.0 * r_e_all / world / max(1, n_launch),
                 "avg_launch_ms": val_ms / max(1, n_launch),
@@ -369,21 +389,43 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_summary(tag):
-    """rocprofv3 PMC summary (HBM bytes per estep_values launch) of this
-    workload, committed under profiles/rNN/ by tools/profile_round.sh (the
-    newest round that has one); None when this configuration has not been
-    profiled."""
+def _profile_json(name, ident):
+    """The newest committed profile summary `name` under profiles/rNN/
+    (tools/profile_round.sh), with `same_build`: whether it was measured on
+    the library this process loaded (SHA-256 prefix).  Counters of another
+    build are reported as null in the line, not paired with this run's times."""
     for d in PMC_DIRS:
-        p = os.path.join(d, f"pmc_estep_values_{tag}.json")
+        p = os.path.join(d, name)
         try:
             with open(p) as f:
                 out = json.load(f)
-            out["source"] = os.path.relpath(p, ROOT)
-            return out
         except (OSError, ValueError):
             continue
+        out["source"] = os.path.relpath(p, ROOT)
+        lib = out.get("library") or {}
+        out["same_build"] = bool(lib) and lib.get("sha256_16") == ident.get("sha256_16")
+        return out
     return None
+
+
+def pmc_summary(tag, ident):
+    """rocprofv3 PMC summary (HBM bytes per estep_values launch) of this workload."""
+    return _profile_json(f"pmc_estep_values_{tag}.json", ident)
+
+
+def sq_summary(tag, ident):
+    """SQ summary of estep_values (tools/sq_summary.py): VALU issue fraction and
+    LDS bank-conflict ratio summed over the instantiations the pass launched."""
+    d = _profile_json(f"sq_estep_values_{tag}.json", ident)
+    if not d or not d.get("kernels"):
+        return None
+    ks = d["kernels"].values()
+    t = sum(k["kernel_seconds"] for k in ks)
+    cap = 1024 * 2.4e9 * t
+    valu = sum(k["valu_insts"] for k in ks)
+    lds_conf = max(k["lds_bank_conflict_ratio"] for k in ks)
+    return {"valu_issue_frac": 4.0 * valu / cap if cap else None, "valu_issue_frac_2cyc": 2.0 * valu / cap if cap else None,
+            "lds_bank_conflict_ratio": lds_conf, "source": d["source"], "same_build": d["same_build"]}
 
 
 def cpu_baseline(m, panel, args):

@@ -106,6 +106,7 @@ _SIGS = [
     ("hmc_set_mine_memory", _i, [_vp, C.c_uint64]),
     ("hmc_last_estep_frontier", _i, [_vp, _P(C.c_int), _P(C.c_int)]),
     ("hmc_last_mine_stats", _i, [_vp, _P(_i), _P(C.c_int64), _P(_d)]),
+    ("hmc_last_mine_reduction", _i, [_vp, _P(_d), _P(_i)]),
     ("hmc_model_save", _i, [_vp]),
     ("hmc_em_rewind", _i, [_vp]),
     ("hmc_build_info", _cp, []),

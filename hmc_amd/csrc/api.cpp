@@ -340,6 +340,13 @@ int hmc_last_mine_stats(const hmc_ctx *h, int *blocks, int64_t *nodes, double *n
   return HMC_OK;
 }
 
+int hmc_last_mine_reduction(const hmc_ctx *h, double *ms, int *levels) {
+  if (!h) return HMC_EARG;
+  if (ms) *ms = h->c.ms_red;
+  if (levels) *levels = h->c.n_red_levels;
+  return HMC_OK;
+}
+
 int hmc_model_save(hmc_ctx *h) { return h ? h->c.model_save() : HMC_EARG; }
 int hmc_em_rewind(hmc_ctx *h) { return h ? h->c.em_rewind() : HMC_EARG; }
 

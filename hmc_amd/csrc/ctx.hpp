@@ -397,7 +397,13 @@ struct Ctx {
   int n_order_redo = 0;  // individuals re-run on the exact value pass (ties) by the last E-step
 
   // timings
-  hipEvent_t ev[6] = {};
+  hipEvent_t ev[8] = {};
+  // cross-rank reduction of the last pattern search: device ms between the
+  // first and the last collective of each mining level (the ordered chain's
+  // mine_sum launches included), and the levels reduced
+  double ms_red = 0;
+  int n_red_levels = 0;
+  bool red_timed = false;
   double ms_fwd = 0, ms_tb = 0, ms_m = 0;
   double ms_s1 = 0, ms_s2 = 0, ms_fb = 0;  // split E-step: structure, values, fused fallback
   double ms_order = 0;                     // part of ms_s2: exact value pass re-runs
@@ -472,6 +478,68 @@ struct Ctx {
     if (rc) return rc;
     if ((e = hipMemcpyAsync(h, tmp.p, n * 8, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
       return hipfail(e, "bcast_host");
+    return HMC_OK;
+  }
+
+  // The ordered reduction's chain (RED_ORDERED): rank 0's `d` holds its local
+  // sums (the caller computed them); rank r > 0 receives the running sums of
+  // ranks 0..r-1 into `d` from rank r-1, runs `cont` (which continues them over
+  // its own items in order), and passes them to rank r+1; rank W-1 broadcasts
+  // the finals.  W-1 point-to-point hops plus one broadcast per call, instead
+  // of one broadcast from every rank (W broadcasts of W-1 hops each).  The
+  // host-callback transport has only an all-reduce: there each hop is an
+  // all-reduce in which one rank contributes (the same chain, W collectives).
+  int ordered_chain(double *d, size_t n, const std::function<int()> &cont) {
+    if (!multi() || n == 0) return HMC_OK;
+    int rc;
+    if (host_fn) {
+      for (int r = 0; r < world; ++r) {
+        if (r == rank && r > 0 && (rc = cont())) return rc;
+        if ((rc = bcast(d, n, r))) return rc;
+      }
+      return HMC_OK;
+    }
+    ncclResult_t x;
+    if (rank > 0) {
+      if ((x = ncclRecv(d, n, ncclDouble, rank - 1, comm, st)) != ncclSuccess)
+        return fail(HMC_ERCCL, "ncclRecv: %s", ncclGetErrorString(x));
+      if ((rc = cont())) return rc;
+    }
+    if (rank < world - 1 && (x = ncclSend(d, n, ncclDouble, rank + 1, comm, st)) != ncclSuccess)
+      return fail(HMC_ERCCL, "ncclSend: %s", ncclGetErrorString(x));
+    return bcast(d, n, world - 1);
+  }
+  // The same chain over a small host vector (LL, total weight): `cont` runs on
+  // the host over the running sums received.
+  int ordered_chain_host(double *h, size_t n, const std::function<void(double *)> &cont) {
+    if (!multi() || n == 0) {
+      cont(h);
+      return HMC_OK;
+    }
+    if (host_fn) {
+      for (int r = 0; r < world; ++r) {
+        if (r == rank) cont(h);
+        int rc = bcast_host(h, n, r);
+        if (rc) return rc;
+      }
+      return HMC_OK;
+    }
+    DevBuf<double> tmp;
+    hipError_t e = tmp.ensure(n);
+    if (e) return hipfail(e, "ordered_chain_host");
+    if (rank == 0) cont(h);
+    if ((e = hipMemcpyAsync(tmp.p, h, n * 8, hipMemcpyHostToDevice, st))) return hipfail(e, "ordered_chain_host");
+    int rc = ordered_chain(tmp.p, n, [&]() -> int {
+      hipError_t e2;
+      if ((e2 = hipMemcpyAsync(h, tmp.p, n * 8, hipMemcpyDeviceToHost, st)) || (e2 = hipStreamSynchronize(st)))
+        return hipfail(e2, "ordered_chain_host");
+      cont(h);
+      if ((e2 = hipMemcpyAsync(tmp.p, h, n * 8, hipMemcpyHostToDevice, st))) return hipfail(e2, "ordered_chain_host");
+      return HMC_OK;
+    });
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(h, tmp.p, n * 8, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+      return hipfail(e, "ordered_chain_host");
     return HMC_OK;
   }
 

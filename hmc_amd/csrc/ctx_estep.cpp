@@ -211,11 +211,8 @@ int Ctx::estep(double *ll_out, int *H_out, uint64_t *re_out) {
     acc[0] = ll;
     acc[1] = tw;
   };
-  if (multi() && reduction == RED_ORDERED) {
-    for (int r = 0; r < world; ++r) {  // the chain continues rank by rank
-      if (r == rank) local_sums(red);
-      if ((rc = bcast_host(red, 2, r))) return rc;
-    }
+  if (multi() && reduction == RED_ORDERED) {  // the chain continues rank by rank
+    if ((rc = ordered_chain_host(red, 2, local_sums))) return rc;
   } else {
     local_sums(red);
     if ((rc = allreduce_host(red, 2))) return rc;

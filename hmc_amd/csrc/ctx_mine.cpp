@@ -87,6 +87,8 @@ int Ctx::mine_impl_body(int *P_out, uint64_t *rm_out, int bynum_rounds) {
   const int L = pan.L;
   hipError_t e;
   hipEventRecord(ev[4], st);
+  ms_red = 0;
+  n_red_levels = 0;
   // PatternManager::findPatternByFreq argument normalisation (PatternManager.cpp:29-32)
   int mxl = max_len <= 0 ? L : max_len;
   int mnl = std::max(min_len, 1);
@@ -280,10 +282,14 @@ int Ctx::mine_block(int lo, int hi, int mxl, int mnl, double mf, int bynum_round
       // then rank r continues every child's sum from ranks 0..r-1 (items in
       // order) over its lists and passes it on
       if ((e = launch_mine_count(a, level, (int)pbeg, (int)pend, st))) return hipfail(e, "mine_count");
-      for (int r = 0; r < world; ++r) {
-        if (r == rank && r > 0 && (e = launch_mine_sum(a, (int)cb, (int)ce, st))) return hipfail(e, "mine_sum");
-        if ((rc = bcast(n_sum.p + (cb - wbase), nlev, r))) return rc;
-      }
+      hipEventRecord(ev[6], st);
+      if ((rc = ordered_chain(n_sum.p + (cb - wbase), nlev, [&]() -> int {
+             hipError_t e2 = launch_mine_sum(a, (int)cb, (int)ce, st);
+             return e2 ? hipfail(e2, "mine_sum") : HMC_OK;
+           })))
+        return rc;
+      hipEventRecord(ev[7], st);
+      red_timed = true;
     } else if ((e = launch_mine_count(a, level, (int)pbeg, (int)pend, st))) {
       return hipfail(e, "mine_count");
     }
@@ -323,7 +329,12 @@ int Ctx::mine_block(int lo, int hi, int mxl, int mnl, double mf, int bynum_round
       hipEventDestroy(dm0);
       hipEventDestroy(dm1);
     }
-    if (!(multi() && reduction == RED_ORDERED) && (rc = allreduce_sum(n_sum.p + (cb - wbase), nlev))) return rc;
+    if (!(multi() && reduction == RED_ORDERED) && multi()) {
+      hipEventRecord(ev[6], st);
+      if ((rc = allreduce_sum(n_sum.p + (cb - wbase), nlev))) return rc;
+      hipEventRecord(ev[7], st);
+      red_timed = true;
+    }
     if ((e = s_ext.ensure(nlev)) || (e = s_child.ensure(nlev))) return hipfail(e, "mine");
     const size_t tmpb = mine_scan_tmp_bytes(nlev);
     if ((e = s_tmp.ensure(tmpb))) return hipfail(e, "mine");
@@ -333,6 +344,13 @@ int Ctx::mine_block(int lo, int hi, int mxl, int mnl, double mf, int bynum_round
     const unsigned long long *tot = h_totals.p;
     if ((e = hipMemcpyAsync(h_totals.p, d_totals.p, 16, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
       return hipfail(e, "mine");
+    if (red_timed) {  // this level's cross-rank reduction (the stream has drained)
+      float ms = 0;
+      hipEventElapsedTime(&ms, ev[6], ev[7]);
+      ms_red += ms;
+      ++n_red_levels;
+      red_timed = false;
+    }
     next_total = tot[0];  // list slots the next level's children need
     if (tot[1] > (unsigned long long)INT32_MAX - (unsigned long long)ce)
       return fail(HMC_EUNSUPPORTED, "candidate tree exceeds 2^31 nodes at length %d", level + 1);
@@ -648,13 +666,15 @@ int Ctx::mine_level(int level, int n, const int32_t *start, const int32_t *allel
   MineArgs a = mine_args(genotype);
   int rc;
   if (multi() && reduction == RED_ORDERED) {
-    for (int r = 0; r < world; ++r) {
-      if (r == rank) {
-        a.seeded = r > 0;
-        if ((e = launch_mine_scan(a, level, n, d_lv_start.p, d_lv_al.p, d_lv_sum.p, st))) return hipfail(e, "mine_scan");
-      }
-      if ((rc = bcast(d_lv_sum.p, n, r))) return rc;
-    }
+    a.seeded = false;
+    if (rank == 0 && (e = launch_mine_scan(a, level, n, d_lv_start.p, d_lv_al.p, d_lv_sum.p, st)))
+      return hipfail(e, "mine_scan");
+    if ((rc = ordered_chain(d_lv_sum.p, n, [&]() -> int {
+           a.seeded = true;
+           hipError_t e2 = launch_mine_scan(a, level, n, d_lv_start.p, d_lv_al.p, d_lv_sum.p, st);
+           return e2 ? hipfail(e2, "mine_scan") : HMC_OK;
+         })))
+      return rc;
   } else {
     if ((e = launch_mine_scan(a, level, n, d_lv_start.p, d_lv_al.p, d_lv_sum.p, st))) return hipfail(e, "mine_scan");
     if ((rc = allreduce_sum(d_lv_sum.p, n))) return rc;

@@ -189,7 +189,10 @@ class HaploModel:
     def mine_stats(self) -> dict:
         b, n, g = C.c_int(), C.c_int64(), C.c_double()
         self._check(lib().hmc_last_mine_stats(self._h, C.byref(b), C.byref(n), C.byref(g)))
-        return dict(blocks=b.value, nodes=n.value, node_window_gb=g.value)
+        ms, lv = C.c_double(), C.c_int()
+        self._check(lib().hmc_last_mine_reduction(self._h, C.byref(ms), C.byref(lv)))
+        return dict(blocks=b.value, nodes=n.value, node_window_gb=g.value, reduction_ms=ms.value,
+                    reduction_levels=lv.value)
 
     def model_save(self):
         """Keep a device copy of the current pattern table (hmc_model_save)."""

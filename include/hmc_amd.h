@@ -160,6 +160,12 @@ int hmc_set_mine_memory(hmc_ctx *ctx, uint64_t list_bytes);
 /* Last search: blocks, candidate nodes created (all blocks) and the size of
  * the node arrays kept (GB, ~70 B per node). */
 int hmc_last_mine_stats(const hmc_ctx *ctx, int *blocks, int64_t *nodes, double *node_window_gb);
+/* Cross-rank reduction of the last pattern search (multi-rank contexts):
+ * device ms from the first to the last collective of each mining level,
+ * summed (the ordered chain's mine_sum launches included), and the number of
+ * levels reduced.  0 / 0 on one rank.  Replaces no reference interface
+ * (the reference is single-process). */
+int hmc_last_mine_reduction(const hmc_ctx *ctx, double *ms, int *levels);
 /* Pattern table in id order (HaploPattern.h:16-98).  succ[P][max_alleles]
  * holds pattern ids (-1 = none); alleles[P][maxlen] symbols (-1 padding).
  * Any output pointer may be NULL. */

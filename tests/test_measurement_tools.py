@@ -59,3 +59,24 @@ def test_sq_summary_shares(tmp_path):
                         str(tmp_path / "b.csv")], capture_output=True, text=True, check=True)
     row = [ln for ln in r.stdout.splitlines() if "estep_values<false, 5" in ln][0]
     assert "| 40 % | 25 % | 35 % | 2.00 : 0.50" in row and "| 50 % |" in row
+
+
+def test_sq_summary_issue_fraction_json(tmp_path):
+    """valu_issue_frac = SQ_INSTS_VALU * 4 / (1024 SIMDs * 2.4 GHz * kernel seconds of the pass);
+    the JSON carries the profiled run's library identity for bench.py's same-build check."""
+    k = "void hmc::estep_values<false, 4, false, true>(hmc::ValueArgs)"
+    write_counters(tmp_path / "a.csv", [(1, k, "SQ_WAVE_CYCLES", 100.0), (1, k, "SQ_INSTS_VALU", 2.4e3),
+                                        (2, k, "SQ_INSTS_VALU", 2.4e3)])
+    write_counters(tmp_path / "b.csv", [(1, k, "SQ_LDS_BANK_CONFLICT", 30.0), (1, k, "SQ_ACTIVE_INST_LDS", 60.0)])
+    with open(tmp_path / "bench.json", "w") as f:
+        f.write("progress\n" + json.dumps({"library": {"sha256_16": "abc"}}) + "\n")
+    out = tmp_path / "sq.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "sq_summary.py"), str(tmp_path / "a.csv"),
+                    str(tmp_path / "b.csv"), "estep_values", str(out), str(tmp_path / "bench.json")],
+                   capture_output=True, text=True, check=True)
+    d = json.load(open(out))
+    kk = d["kernels"]["hmc::estep_values<false, 4, false, true>"]
+    assert kk["launches"] == 2 and abs(kk["kernel_seconds"] - 2e-9) < 1e-18
+    assert abs(kk["valu_issue_frac"] - 4 * 4.8e3 / (1024 * 2.4e9 * 2e-9)) < 1e-9
+    assert abs(kk["lds_bank_conflict_ratio"] - 0.5) < 1e-12
+    assert d["library"] == {"sha256_16": "abc"}

@@ -1,8 +1,10 @@
-"""A/B of library builds over cfg 3's converged chain: M0 once, then twice
-(hmc_em_rewind) E1, M1, E2, M2, E3 with device ms of every E-step's passes.
-Pick the build with HMC_AMD_LIB; LL and R_E must not change between builds.
+"""A/B of library builds or E-step options over a config's converged chain:
+M0 once, then twice (hmc_em_rewind) E1, M1, E2, M2, E3 with device ms of
+every E-step's passes.  Pick the build with HMC_AMD_LIB and the value mode
+with HMC_VALUE_MODE (exact | fast: value-only k-best lists, the exact pass
+re-run only for individuals with ties); LL and R_E must not change.
 
-    HMC_AMD_LIB=... python tools/chain_ab.py TAG [CFG]
+    HMC_AMD_LIB=... HMC_VALUE_MODE=fast python tools/chain_ab.py TAG [CFG]
 """
 import os
 import sys
@@ -14,12 +16,16 @@ from hmc_amd import synth  # noqa: E402
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "run"
 cfg = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+vmode = os.environ.get("HMC_VALUE_MODE", "exact")
 m = hmc_amd.HaploModel()
+m.set_value_mode(vmode)
 m.load(hmc_amd.GenoData.from_panel(synth.config_panel(cfg)))
 t0 = time.perf_counter()
 P, _ = m.find_patterns()
-print(f"{tag}: M0 {P} patterns {time.perf_counter() - t0:.1f} s lib {hmc_amd.lib_identity()}", flush=True)
+print(f"{tag}: cfg {cfg} value mode {vmode}: M0 {P} patterns {time.perf_counter() - t0:.1f} s "
+      f"lib {hmc_amd.lib_identity()}", flush=True)
 m.model_save()
+n = m.i1 - m.i0
 for rep in range(2):
     m.em_rewind()
     for k in range(1, 4):
@@ -29,6 +35,7 @@ for rep in range(2):
         s = m.estep_split_stats()
         print(f"{tag} chain {rep} E{k}: wall {wall * 1e3:.0f} ms structure {s['structure_ms']:.0f} ms "
               f"({s['structure_passes']}) values {s['values_ms']:.0f} ms ({s['value_passes']}) "
+              f"order re-runs {s['n_order_rerun']} of {n} ({s['order_ms']:.0f} ms) "
               f"ll={ll!r} R_E={re}", flush=True)
         if k < 3:
             m.find_patterns()

@@ -58,6 +58,10 @@ def run_alg(path):
 
 
 if len(sys.argv) > 6:
+    try:  # the profiled build: bench.py reports traffic only for the library it loads itself
+        out["library"] = json.loads(open(sys.argv[6]).read().strip().splitlines()[-1]).get("library")
+    except (OSError, ValueError, IndexError):
+        out["library"] = None
     alg, nl = run_alg(sys.argv[6])
     alg_w, nl_w = run_alg(sys.argv[7]) if len(sys.argv) > 7 else (alg, nl)
     out["alg_bytes_per_launch"] = alg / max(1, nl)

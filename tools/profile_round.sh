@@ -44,4 +44,6 @@ for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
     python3 $SHORT > "$OUT/sq_$N.json" 2> "$OUT/sq_$N.err"
   cp "$(find "$OUT/sq_$N" -name "*counter_collection.csv" | head -n 1)" "$DEST/sq_${N}_cfg$CFG.csv"
 done
+python3 tools/sq_summary.py "$DEST/sq_SQ_WAVES_cfg$CFG.csv" "$DEST/sq_SQ_INSTS_LDS_cfg$CFG.csv" $K \
+  "$DEST/sq_${K}_cfg$CFG.json" "$OUT/sq_SQ_WAVES.json"
 echo "[profile] done" >&2
