@@ -66,17 +66,18 @@ LIMITER = "VALU issue of the segmented k-best selection (SQ_INSTS_VALU x 4 cycle
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 5],
-                    help="BASELINE config (synth.CONFIGS); the options below override it")
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 20; cfg 4: 3, one chain)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 5; cfg 4: 1)")
+    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5],
+                    help="BASELINE config (synth.CONFIGS); the options below override it.  cfg 4 (50 000 x 5 000) is "
+                         "the 8-GPU configuration: --gpus 8 gives each rank ~6 250 individuals")
     ap.add_argument("--individuals", type=int, default=0, help="total individuals (all ranks)")
     ap.add_argument("--loci", type=int, default=0)
     ap.add_argument("--alleles", type=int, default=0, help="alleles per locus of the synthetic panel (cfg 5: 8)")
     ap.add_argument("--missing", type=float, default=0.0, help="missing-allele rate of the synthetic panel")
     ap.add_argument("--seed", type=int, default=0, help="panel seed (default = config index)")
     ap.add_argument("--sample-size", type=int, default=10)
-    ap.add_argument("--steady-steps", type=int, default=8,
+    ap.add_argument("--steady-steps", type=int, default=None,
                     help="forced iterations after the chain's end, timed for value_steady (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-indiv", type=int, default=20, help="individuals per CPU E-step sample (E_k, k >= 2)")
@@ -92,6 +93,12 @@ def parse():
                     help="M-step collective: RCCL (the product), or a gloo host all-reduce with every rank on "
                          "GPU LOCAL_RANK %% device_count (rehearses the multi-rank bench on one GPU; not a measurement)")
     a = ap.parse_args()
+    big = a.config == 4  # an E1 of ~25 s per rank at 8 ranks: one chain, no steady leg, no CPU sample
+    a.steps = a.steps if a.steps is not None else (3 if big else 20)
+    a.warmup = a.warmup if a.warmup is not None else (1 if big else 5)
+    a.steady_steps = a.steady_steps if a.steady_steps is not None else (0 if big else 8)
+    if big:
+        a.no_cpu_baseline = True
     c = synth.CONFIGS[a.config]
     a.N = a.individuals or c["N"]
     a.L = a.loci or c["L"]
@@ -239,6 +246,7 @@ def main():
         t = m.timings()
         sp = m.estep_split_stats()
         ms_stats = m.mine_stats() if go or force_m else {"reduction_ms": 0.0, "reduction_levels": 0}
+        win = m.estep_windows()
         run_log.append([int(log["r_e"]), int(sp["value_passes"])])
         progress(f"EM iteration {it}: LL {log['log_likelihood']:.6f}, R_E {log['r_e']}, "
                  f"E {t['estep_forward_ms'] + t['estep_traceback_ms']:.0f} ms "
@@ -252,7 +260,8 @@ def main():
                     struct_passes=sp["structure_passes"], value_passes=sp["value_passes"],
                     tb_ms=t["estep_traceback_ms"], mstep_ms=t["mstep_ms"] if go or force_m else 0.0,
                     value_dataflow=m.last_value_pass_dataflow(), reduction_ms=ms_stats["reduction_ms"],
-                    reduction_levels=ms_stats["reduction_levels"])
+                    reduction_levels=ms_stats["reduction_levels"], windows=win["windows"],
+                    recompute_ms=win["recompute_ms"])
 
     for _ in range(args.warmup):
         em_step()

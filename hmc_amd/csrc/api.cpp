@@ -186,6 +186,25 @@ int hmc_shard_range(const hmc_ctx *h, int *i0, int *i1) {
   return HMC_OK;
 }
 
+int hmc_set_shard(hmc_ctx *h, int i0, int i1) {
+  if (!h) return HMC_EARG;
+  hmc::Ctx &c = h->c;
+  if (!c.have_panel) return c.fail(HMC_EARG, "no panel");
+  if (c.world != 1 || i0 < 0 || i1 <= i0 || i1 > c.pan.N)
+    return c.fail(HMC_EARG, "shard [%d, %d) of a %d-rank context over %d individuals", i0, i1, c.world, c.pan.N);
+  c.i0 = i0;
+  c.i1 = i1;
+  // nothing learned about the old shard carries over: no samples, no E-step,
+  // no accepted resolutions, no per-individual costs or store estimates
+  c.have_samples = c.have_estep = c.have_best = c.best_on_host = false;
+  c.hf_valid = false;
+  c.H = 0;
+  c.h_cost.clear();
+  c.prev_rneed.clear();
+  c.prev_P = 0;
+  return HMC_OK;
+}
+
 int hmc_set_estep_mode(hmc_ctx *h, int mode) {
   if (!h || mode < 0 || mode > 1) return HMC_EARG;
   h->c.estep_mode = mode;
@@ -217,8 +236,8 @@ int hmc_last_exact_stats(const hmc_ctx *h, int *rounds, uint64_t *candidates, do
 }
 
 int hmc_set_value_mode(hmc_ctx *h, int mode) {
-  if (!h || mode < 0 || mode > 1) return HMC_EARG;  // 0: value-only + re-runs, 1: libstdc++ permutations
-  h->c.value_fast = mode == 0;
+  if (!h || mode < 0 || mode > 2) return HMC_EARG;  // 0: value-only + re-runs, 1: libstdc++ permutations, 2: automatic
+  h->c.value_mode = mode;
   return HMC_OK;
 }
 
@@ -262,6 +281,22 @@ int hmc_last_value_pass(const hmc_ctx *h, int *dataflow) {
 int hmc_set_value_layout(hmc_ctx *h, int mode) {
   if (!h || mode < 0 || mode > 2) return HMC_EARG;  // 0 never, 1 heavy groups, 2 every group
   h->c.value_pair = mode;
+  return HMC_OK;
+}
+
+int hmc_set_estep_windows(hmc_ctx *h, int mode, int window_loci) {
+  if (!h || mode < 0 || mode > 2 || window_loci < 0) return HMC_EARG;
+  h->c.window_mode = mode;  // 0 automatic, 1 never, 2 always
+  h->c.window_loci = window_loci;
+  return HMC_OK;
+}
+
+int hmc_last_estep_windows(const hmc_ctx *h, int *windows, int *window_loci, int *groups, double *recompute_ms) {
+  if (!h) return HMC_EARG;
+  if (windows) *windows = h->c.last_windows;
+  if (window_loci) *window_loci = h->c.last_window_loci;
+  if (groups) *groups = h->c.last_window_groups;
+  if (recompute_ms) *recompute_ms = h->c.ms_ck;
   return HMC_OK;
 }
 

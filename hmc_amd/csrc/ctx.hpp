@@ -283,7 +283,17 @@ struct Ctx {
   bool debug_mem = false, diag_mine = false;
   bool check_records = false;  // HMC_CHECK_RECORDS: validate each structure pass's records on the host
   int validate_records(const int32_t *ids, int np_, int i0);
-  bool value_fast = false;   // value-only k-best lists first, the exact pass for ties only (hmc_set_value_mode)
+  // Value-pass mode (hmc_set_value_mode): value-only k-best lists first and
+  // the exact pass for the individuals with ties (fast), the exact pass for
+  // everyone, or automatic — fast on multi-allelic panels once the model is
+  // smaller than the panel (cfg 5's E2 / E3: values 792 -> 616 ms and 734 ->
+  // 594 ms with 25 % of the individuals re-run; cfg 3's biallelic E2: 452 ->
+  // 683 ms with 52 % re-run, profiles/r05/value_mode/), until an E-step re-runs
+  // more than 35 % of its individuals.
+  enum { VM_FAST = 0, VM_EXACT = 1, VM_AUTO = 2 };
+  int value_mode = VM_AUTO;
+  bool fast_off = false;     // auto: a value-only E-step re-ran too many individuals (reset by a panel load)
+  bool last_fast = false;    // the last E-step ran the value-only pass
   int value_pair = 2;        // two links per lane in phase B: 0 never, 1 heavy groups, 2 every group (hmc_set_value_layout)
   uint64_t trace_bytes = 0, rec_bytes = 0;  // E-step store budgets (0 = automatic)
 
@@ -888,6 +898,37 @@ struct Ctx {
   // records with forward links, then exact_fb + exact_walk per group instead
   // of the value pass and traceback; E-step outputs are left untouched).
   int estep_split(const std::vector<int32_t> &order, bool exact = false);
+
+  // ---- checkpoint-and-recompute E-step (ctx_window.cpp) -----------------
+  // When an individual's records and traces for all loci are too large for
+  // the stores to hold more than a few hundred individuals at once (cfg 4's
+  // per-rank E1 on the genotype-mined M0: ~250 MB of records and ~390 MB of
+  // traces per individual, groups of ~280 on 256 CUs), the loci are cut into
+  // windows.  Forward: per window, the structure pass and the value pass over
+  // the whole group, each starting from the frontier the window before left in
+  // a checkpoint (pattern pairs and list lengths; forward likelihoods and the
+  // k-best lists) and saving its own last frontier; the last window makes the
+  // final selection and traces its candidates back to its first locus.
+  // Backward: every earlier window, last to first, is recomputed from its
+  // checkpoint (records and traces of that window only) and the traceback
+  // continues through it from the cursor the window above left
+  // (HaploPair::getGenotype, HaploPair.cpp:91-124).  Bit-identical to the
+  // classic passes: every window replays the same arithmetic in the same order.
+  enum { WIN_AUTO = 0, WIN_NEVER = 1, WIN_ALWAYS = 2 };
+  int window_mode = WIN_AUTO;  // hmc_set_estep_windows
+  int window_loci = 0;         // record indices per window (0 = from the budgets)
+  DevBuf<uint32_t> d_ck;
+  DevBuf<unsigned long long> d_ck_off, d_ck_cursor;
+  DevBuf<uint32_t> d_cur_state, d_cur_idx;
+  DevBuf<uint8_t> d_cur_swap;
+  int last_windows = 0, last_window_loci = 0, last_window_groups = 0;  // hmc_last_estep_windows
+  double ms_ck = 0;  // device ms of the backward (recompute) passes, part of ms_s1 / ms_s2
+  // A probe of the first loci of a sample decides: WIN_DECLINED when the
+  // classic passes fit groups of at least two individuals per CU (or the
+  // whole shard).
+  static constexpr int WIN_DECLINED = 2;
+  int estep_windowed(const std::vector<int32_t> &order);
+  bool windows_allowed() const;
 
   // PatternManager::checkFrequency (PatternManager.cpp:146-193) of n given
   // candidates of one length against the current items (genotypes while no

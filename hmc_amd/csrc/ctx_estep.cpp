@@ -1,5 +1,6 @@
 // ctx_estep.cpp — Ctx members: the E-step: HaploModel::resolveAll through the structure and value passes.
 #include "ctx.hpp"
+#include "plan.hpp"
 
 namespace hmc {
 
@@ -167,7 +168,8 @@ int Ctx::estep(double *ll_out, int *H_out, uint64_t *re_out) {
   if ((e = hipMemcpyAsync(d_cost.p, h_cost.data(), (size_t)n * 4, hipMemcpyHostToDevice, st)))
     return hipfail(e, "estep");
   ms_fwd = ms_tb = 0;
-  ms_s1 = ms_s2 = ms_fb = ms_order = 0;
+  ms_s1 = ms_s2 = ms_fb = ms_order = ms_ck = 0;
+  last_windows = last_window_loci = last_window_groups = 0;
   n_fallback = n_order_redo = 0;
   n_struct_passes = n_value_passes = 0;
   int rc = 0;
@@ -177,6 +179,7 @@ int Ctx::estep(double *ll_out, int *H_out, uint64_t *re_out) {
   }
   if (rc) return rc;
   if (estep_mode == ESTEP_SPLIT) ms_fwd = ms_s1 + ms_s2 + ms_fb;
+  if (last_fast && value_mode == VM_AUTO && (double)n_order_redo > 0.35 * (double)n) fast_off = true;
   // samples in the reference's order: individuals in order, candidates in
   // order, h0 then h1 (HaploModel.cpp:105-106)
   std::vector<int32_t> rowmap;
@@ -374,11 +377,25 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
     if (rc0) return rc0;
   }
   int32_t *dstatus = exact ? d_xstatus.p : d_status.p;
+  // value-only lists first (hmc_set_value_mode; lists longer than a wavefront:
+  // exact order only)
+  const bool light_model = (double)P <= (double)pan.N * (double)pan.L;
+  const bool vfast = !exact && S <= 32 &&
+                     (value_mode == VM_FAST || (value_mode == VM_AUTO && pan.amax > 2 && light_model && !fast_off));
+  if (!exact) last_fast = vfast;
   int dev_cu = 256;
   hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, device);
   const int G = std::max(1, std::min(waves > 0 ? waves : dev_cu * std::max(8, lds_waves_per_cu), n));
   hipError_t e;
   float ms = 0;
+  // Loci in windows with checkpoints (ctx_window.cpp) when the first E-step
+  // on a model larger than the panel would otherwise run in groups too small
+  // to fill the GPU (cfg 4's per-rank E1); a probe of the first loci decides.
+  if (!exact && windows_allowed() &&
+      (window_mode == WIN_ALWAYS || ((double)P > (double)pan.N * (double)pan.L && n > 2 * dev_cu))) {
+    const int rw_ = estep_windowed(order);
+    if (rw_ != WIN_DECLINED) return rw_;
+  }
   std::vector<int32_t> pending(order), sset, rest;
   std::vector<unsigned long long> rneed(n, 0), tneed(n, 0), base(n, 0), rsz(n, 0);
   std::vector<int32_t> fbig(n, 0);  // largest frontier of each individual (structure pass)
@@ -400,69 +417,26 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
     // ---- pass 1: structure records --------------------------------------
     int np = (int)pending.size();
     {
-      uint64_t r = 0, t = 0;
-      int k = 0;
-      // the first pass spans the whole cost range and later estimates use the
+      // (the first pass spans the whole cost range and later estimates use the
       // measured individuals nearest in cost (cfg 3 E1 after E5: 7.1 -> 5.9 s,
-      // deferred 1 713 -> 12 per group, profiles/r02/e1_groups/)
-      if (!have_est) {  // nothing measured yet: 4 per CU share the store evenly
-        // (a model smaller than the panel — cfg 3's E2 after the M0-based E1 —
-        // gives every individual a share: its records fit, and the E-step runs
-        // in one group instead of a sample group and the rest; the M0 model's
-        // E1 needs more per individual than an even share, so it samples first)
-        const bool light = exact ? false : (double)P <= (double)pan.N * (double)pan.L;
-        k = light ? np : std::min(np, 4 * dev_cu);
-        if (np > k) {  // every np/k-th of the heaviest-first list
-          std::vector<int32_t> pick, other;
-          pick.reserve(k);
-          other.reserve(np - k);
-          for (int q = 0; q < np; ++q)
-            ((int64_t)q * k / np != (int64_t)(q - 1) * k / np || q == 0 ? pick : other).push_back(pending[q]);
-          pending = pick;
-          pending.insert(pending.end(), other.begin(), other.end());
-          k = (int)pick.size();
-        }
-        // (at most 8 192 words per locus, or the store already allocated:
-        // mapping the whole budget, tens of GB, costs seconds per E-step on a
-        // fresh context; a region too small only defers its individual)
-        const uint64_t cap = std::max<uint64_t>(d_rec.n / (uint64_t)k, std::max<uint64_t>(1ull << 22, 8192ull * (uint64_t)L));
-        const uint64_t share = std::min<uint64_t>(rec_budget / (uint64_t)k, cap);
-        for (int q = 0; q < k; ++q) {
-          base[pending[q]] = (uint64_t)q * share;
-          rsz[pending[q]] = share;
-        }
-        r = share * (uint64_t)k;
-      } else {  // the prefix whose regions (and measured traces) fit the budgets
-        uint64_t r_est = 0;
-        while (k < np) {
-          const int bi = pending[k];
-          const uint64_t need = exact_need[bi] ? rneed[bi] : std::min<uint64_t>(est[bi], rec_budget);
-          // (estimated traces are not counted: groups cut by records and then
-          // split by exact traces measured faster at cfg 3's E1)
-          const uint64_t tn = exact_need[bi] ? tneed[bi] : 0;
-          if (k > 0 && (r + need > rec_budget || t + tn > trace_budget)) break;
-          rsz[bi] = need;
-          r += need;
-          t += tn;
-          r_est += exact_need[bi] ? 0 : need;
-          ++k;
-        }
-        // the store left over goes to the estimated regions (up to 3x), so
-        // fewer individuals are deferred to a pass of their own (A/B on one
-        // box, cfg 3: E1 value passes 3.88 -> 3.60 s, E2 structure 218 -> 177 ms)
-        // (within the store as allocated, or 1.25x the estimates: growing the
-        // allocation to the budget only for headroom costs its mapping time)
-        const uint64_t room = std::min<uint64_t>(rec_budget, std::max<uint64_t>(d_rec.n, r + r / 4));
-        const double grow = r_est > 0 && r < room ? std::min(3.0, 1.0 + (double)(room - r) / (double)r_est) : 1.0;
-        r = 0;
-        for (int q = 0; q < k; ++q) {
-          const int bi = pending[q];
-          if (!exact_need[bi]) rsz[bi] = std::min<uint64_t>((uint64_t)((double)rsz[bi] * grow), rec_budget);
-          if (r + rsz[bi] > rec_budget) rsz[bi] = rec_budget - r;
-          base[bi] = r;
-          r += rsz[bi];
-        }
-      }
+      // deferred 1 713 -> 12 per group, profiles/r02/e1_groups/); a model
+      // smaller than the panel — cfg 3's E2 after the M0-based E1 — gives every
+      // individual a share: its records fit, and the E-step runs in one group;
+      // the first pass caps a share at 8 192 words per locus or the store
+      // already allocated: mapping the whole budget, tens of GB, costs seconds
+      // per E-step on a fresh context; a region too small only defers its
+      // individual; the store left over goes to the estimated regions (A/B on
+      // one box, cfg 3: E1 value passes 3.88 -> 3.60 s, E2 structure 218 -> 177 ms))
+      RegionPlanIn pin;
+      pin.have_est = have_est;
+      pin.light = exact ? false : (double)P <= (double)pan.N * (double)pan.L;
+      pin.dev_cu = dev_cu;
+      pin.L = L;
+      pin.rec_budget = rec_budget;
+      pin.trace_budget = trace_budget;
+      pin.rec_alloc = d_rec.n;
+      uint64_t r = 0;
+      const int k = plan_record_regions(pin, pending, exact_need, rneed, tneed, est, base, rsz, &r);
       np = k;
       rec_words = r;
       std::vector<unsigned long long> rb(n, 0), rs(n, 0);
@@ -644,12 +618,7 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
     size_t pos = 0;
     while (pos < sset.size()) {
       uint64_t t = 0;
-      size_t k = 0;
-      while (pos + k < sset.size() && (k == 0 || t + tneed[sset[pos + k]] <= trace_budget)) {
-        base[sset[pos + k]] = t;
-        t += tneed[sset[pos + k]];
-        ++k;
-      }
+      size_t k = plan_trace_group(sset, pos, tneed, trace_budget, base, &t);
       // traces over the budget by a few individuals while structure groups
       // still follow: those join the next group (re-walked there, exact sizes
       // known) instead of a value pass of their own, which would cost one
@@ -712,11 +681,11 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
       for (size_t q = 0; q < k; ++q) fgrp = std::max(fgrp, (int)fbig[sset[pos + q]]);
       fgrp = std::min(fcap, (fgrp + 63) & ~63);
       // two links per lane (cfg 3: E1 values 2.68 -> 2.34 s, E2 ~3 % less)
-      const bool pair = !value_fast && S <= 16 && (value_pair == 2 || (value_pair == 1 && heavy));
+      const bool pair = !vfast && S <= 16 && (value_pair == 2 || (value_pair == 1 && heavy));
       // Dataflow value pass (estep_df.hip): one wave walks the loci and
       // builds the lists, the others run the chains of adds of any open locus.
       DfShape df;
-      const bool use_df = !value_fast && S <= 32 && (value_pass == VP_DATAFLOW || (value_pass == VP_AUTO && df_auto(heavy))) &&
+      const bool use_df = !vfast && S <= 32 && (value_pass == VP_DATAFLOW || (value_pass == VP_AUTO && df_auto(heavy))) &&
                           df_shape(S, pair, heavy, small_heavy, per_cu, fgrp, df);
       if (use_df) {
         vnw = df.nw;
@@ -758,7 +727,7 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
       v.stamps = d_stamps.p;
       v.next_q = d_nextq.p + 1;
       if ((e = hipMemsetAsync(d_nextq.p + 1, 0, 4, st))) return hipfail(e, "estep");
-      const bool fast = value_fast && S <= 32;  // lists longer than a wavefront: exact order only
+      const bool fast = vfast;
       hipEventRecord(ev[0], st);
       if (use_df) {
         if ((e = launch_estep_values_df(v, grid2, vnw, df.na, vwpe, pair, df.R, df.qcap, st)))

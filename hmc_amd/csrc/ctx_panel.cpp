@@ -27,6 +27,7 @@ void Ctx::shard(int N, int L) {
 int Ctx::upload_panel() {
   const int N = pan.N, L = pan.L, A = pan.amax;
   shard(N, L);
+  fast_off = false;
   std::vector<uchar2> im((size_t)N * L), lm((size_t)L * N);
   for (int i = 0; i < N; ++i)
     for (int k = 0; k < L; ++k) {

@@ -795,10 +795,16 @@ __global__ __launch_bounds__(256) void estep_traceback(TracebackArgs a) {
   const size_t h0 = (size_t)a.sample_base[bi] + 2 * c;
   uint8_t *row[2] = {a.rows + h0 * L, a.rows + (h0 + 1) * L};
   const unsigned long long *lo = a.loc_off + (size_t)bi * (L + 1);
-  uint32_t st = a.cand_state[(size_t)bi * S_MAX + c];
-  uint32_t idx = a.cand_idx[(size_t)bi * S_MAX + c];
+  // locus window of trace indices [wlo, whi): from the candidates (the last
+  // window) or from the cursor the window above left
+  const int wlo = a.win_hi > 0 ? a.win_lo : a.head_len, whi = a.win_hi > 0 ? a.win_hi : L + 1;
+  const size_t cs = (size_t)bi * S_MAX + c;
+  const bool first = whi == L + 1;
+  uint32_t st = first ? a.cand_state[cs] : a.cur_state[cs];
+  uint32_t idx = first ? a.cand_idx[cs] : a.cur_idx[cs];
   int ra = 0, rb = 1;
-  for (int j = L; j > a.head_len; --j) {
+  if (!first && a.cur_swap[cs]) { ra = 1; rb = 0; }
+  for (int j = whi - 1; j > a.head_len && j >= wlo; --j) {
     const uint32_t *r = a.trace + lo[j];
     const uint32_t F = r[0];
     const uint32_t hdr = r[1 + st];
@@ -808,6 +814,12 @@ __global__ __launch_bounds__(256) void estep_traceback(TracebackArgs a) {
     if (meta_rev(m)) { int t = ra; ra = rb; rb = t; }
     st = meta_pred(m);
     idx = meta_idx(m);
+  }
+  if (wlo > a.head_len) {  // the window below continues from here
+    a.cur_state[cs] = st;
+    a.cur_idx[cs] = idx;
+    a.cur_swap[cs] = (uint8_t)ra;
+    return;
   }
   const uint32_t hdr = a.trace[lo[a.head_len] + 1 + st];
   row[ra][a.head_len - 1] = (uint8_t)(hdr & 0xFF);

@@ -310,6 +310,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
   const uint64_t lt = lanemask_lt();
   const Blk<NW> B{(int *)(smem + plan.o_red), tid, lane, wv};
   const int S = a.S, L = a.pan.L, amax = a.pan.amax, hl = a.mod.head_len;
+  // locus window of record indices [wlo, whi) (classic: the head to L)
+  const int wlo = a.w.hi > 0 ? a.w.lo : hl, whi = a.w.hi > 0 ? a.w.hi : L + 1;
+  const bool from_ck = wlo > hl;
   // the pattern table in end-locus order when the host built it (gmodel.hip):
   // frontier states carry g instead of pattern ids, and one locus's lookups
   // fall in one block of the table
@@ -380,9 +383,24 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     IdFront X = FA, Y = FB;
 
     // ---- initHeadList (HaploBuilder.cpp:153-224) ----------------------------
-    // head_len == 1 on the device; longer heads from the host's list
+    // head_len == 1 on the device; longer heads from the host's list.  A locus
+    // window after the first starts from its checkpoint (the frontier after
+    // record index wlo - 1) instead.
     int Fp0 = 0, st0 = EST_OK;
-    if (tid == 0 && hl > 1) {
+    if (from_ck) {
+      const uint32_t *ck = a.w.ck_store + a.w.ck_off[(size_t)bi * (a.w.nwin + 1) + a.w.win];
+      Fp0 = (int)ck[0];
+      if (Fp0 > a.fcap) {
+        st0 = EST_OVERFLOW_FRONTIER;
+      } else {
+        for (int t = tid; t < Fp0; t += NT) {
+          *X.at(F_LO, t) = ck[2 + t];
+          *X.at(F_HI, t) = ck[2 + Fp0 + t];
+          *X.at(F_NL, t) = ck[2 + 2 * Fp0 + t];
+        }
+      }
+    }
+    if (!from_ck && tid == 0 && hl > 1) {
       const int li = gi - a.mod.hf_base;
       st0 = a.mod.hf_status[li];
       for (uint32_t t = a.mod.hf_off[li]; t < a.mod.hf_off[li + 1] && st0 == EST_OK; ++t) {
@@ -393,7 +411,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         ++Fp0;
       }
     }
-    if (tid == 0 && hl == 1) {
+    if (!from_ck && tid == 0 && hl == 1) {
       const uchar2 g0 = g[0];
       const bool m0 = g0.x == MISSING, m1 = g0.y == MISSING;
       for (int hix = 0; hix < a.mod.n_head; ++hix) {
@@ -430,7 +448,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     status = B.bcast(st0);
     int fbig = Fp;  // the head frontier counts too: the value pass sizes its HBM tier by this
     B.sync();
-    if (status == EST_OK) {
+    if (status == EST_OK && !from_ck) {
       const unsigned long long words = 4 + 4ull * Fp + 1 + (a.exact ? 2ull * Fp : 0ull);
       rneed += (words + 1) & ~1ull;
       tneed += a.exact ? 4ull * Fp + 2 : trace_locus_words((unsigned long long)Fp, S);
@@ -474,7 +492,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     }
     // ---- structure of the forward over loci (HaploBuilder.cpp:47-82) -------
     S1_ST(5);
-    for (int i = hl; i < L && status == EST_OK; ++i) {
+    for (int i = from_ck ? wlo - 1 : hl; i < whi - 1 && status == EST_OK; ++i) {
       if (Fp == 0) { status = EST_UNRESOLVED; break; }
       const uchar2 gg = g[i];
       if (tid == 0) {  // allele-pair list in extendAll call order
@@ -738,7 +756,34 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
       S1_ST(4);
     }
     if (status == EST_OK && Fp == 0) status = EST_UNRESOLVED;
-    if (counting && status != EST_OVERFLOW_FRONTIER && status != EST_OVERFLOW_CONTRIB && status != EST_NO_HEAD_PATTERN)
+    // the window's last frontier is the next window's checkpoint (also while
+    // counting: the frontier is exact, only the records were not stored)
+    if (status == EST_OK && whi <= L && a.w.ck_write) {
+      const unsigned long long words = ck_words((unsigned long long)Fp, S);
+      unsigned long long o = 0;
+      if (tid == 0) {
+        o = atomicAdd(a.w.ck_cursor, words);
+        if (o + words > a.w.ck_cap) o = REC_NONE;
+        a.w.ck_off[(size_t)bi * (a.w.nwin + 1) + a.w.win + 1] = o;
+      }
+      o = B.bcast64(o);
+      if (o == REC_NONE) {
+        status = EST_OVERFLOW_CKPT;
+      } else {
+        uint32_t *ck = a.w.ck_store + o;
+        if (tid == 0) {
+          ck[0] = (uint32_t)Fp;
+          ck[1] = 0;
+        }
+        for (int t = tid; t < Fp; t += NT) {
+          ck[2 + t] = *X.at(F_LO, t);
+          ck[2 + Fp + t] = *X.at(F_HI, t);
+          ck[2 + 2 * Fp + t] = *X.at(F_NL, t);
+        }
+      }
+    }
+    if (counting && status != EST_OVERFLOW_FRONTIER && status != EST_OVERFLOW_CONTRIB && status != EST_NO_HEAD_PATTERN &&
+        status != EST_OVERFLOW_CKPT)
       status = EST_OVERFLOW_REC;
     fbig = Fp > fbig ? Fp : fbig;
     if (status < 0) reset_tables();  // aborted mid-locus: keys may be left
@@ -748,7 +793,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
       a.rec_need[bi] = rneed;
       a.trace_need[bi] = tneed;
       a.status[bi] = status;
-      a.re_count[bi] = re;
+      if (a.re_mode == 0) a.re_count[bi] = re;
+      else if (a.re_mode == 1) a.re_count[bi] += re;
       a.fmax[bi] = fbig;
       atomicMax(a.max_states, (unsigned)fbig);
     }
@@ -1352,6 +1398,9 @@ template <bool FAST, int WPE, bool WIDE = false, bool PAIR = false>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) void estep_values(ValueArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int S = a.S, L = a.L, hl = a.head_len;
+  // locus window of trace indices [wlo, whi) (classic: the head to L)
+  const int wlo = a.w.hi > 0 ? a.w.lo : hl, whi = a.w.hi > 0 ? a.w.hi : L + 1;
+  const bool from_ck = wlo > hl, last_win = whi == L + 1;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;
   const int NT = blockDim.x, NW = NT / WAVE;
   const K2Plan plan = k2_plan(S, a.lds_fc, NW, PAIR);
@@ -1401,9 +1450,26 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
     VFront X = FA, Y = FB;
 
     // ---- head list (HaploPair.cpp:14-33) -----------------------------------
-    const uint32_t *R = a.rec + roff[hl];
-    int Fp = (int)R[0];
-    {
+    // (a locus window after the first: the frontier its checkpoint holds)
+    const uint32_t *R = from_ck ? a.rec : a.rec + roff[hl];
+    int Fp = 0;
+    if (from_ck) {
+      const uint32_t *ck = a.w.ck_store + a.w.ck_off[(size_t)bi * (a.w.nwin + 1) + a.w.win];
+      Fp = (int)ck[0];
+      const double *cf = (const double *)(ck + ck_value_off((unsigned long long)Fp));
+      const unsigned long long *ch = (const unsigned long long *)(cf + Fp);
+      const double *cl = (const double *)(ch + Fp);
+      for (int t = tid; t < Fp; t += NT) {
+        const uint32_t n = ck[2 + 2 * Fp + t];
+        *X.fwd(t) = cf[t];
+        *X.hm(t) = ch[t];
+        *X.nl(t) = n;
+        double *xl = X.lik(t);
+        for (uint32_t k = 0; k < n; ++k) xl[k] = cl[(size_t)t * S + k];
+      }
+      __syncthreads();
+    } else {
+      Fp = (int)R[0];
       const double *Rtp = (const double *)(R + 4);
       const uint32_t *Rhd = R + 4 + 2 * Fp;
       TraceRec tr;
@@ -1428,7 +1494,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
     }
 
     // ---- forward over loci ----------------------------------------------------
-    for (int j = hl + 1; j <= L && status == EST_OK; ++j) {
+    for (int j = from_ck ? wlo : hl + 1; j < whi && status == EST_OK; ++j) {
       R = a.rec + roff[j];
       const int F = (int)R[0], C = (int)R[1], NCH = (int)R[2];
       const double *Rtp = (const double *)(R + 4);
@@ -1666,11 +1732,35 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
       Fp = F;
     }
 
-    // ---- final selection (HaploBuilder.cpp:87-116) ------------------------
+    // ---- a window before the last: its last frontier (values) goes to the
+    // next window's checkpoint, which the structure pass allocated ----------
     __syncthreads();
+    if (!last_win) {
+      if (status == EST_OK && a.w.ck_write) {
+        uint32_t *ck = a.w.ck_store + a.w.ck_off[(size_t)bi * (a.w.nwin + 1) + a.w.win + 1];
+        double *cf = (double *)(ck + ck_value_off((unsigned long long)Fp));
+        unsigned long long *ch = (unsigned long long *)(cf + Fp);
+        double *cl = (double *)(ch + Fp);
+        for (int t = tid; t < Fp; t += NT) {
+          const uint32_t n = *X.nl(t);
+          cf[t] = *X.fwd(t);
+          ch[t] = *X.hm(t);
+          const double *xl = X.lik(t);
+          for (uint32_t k = 0; k < n; ++k) cl[(size_t)t * S + k] = xl[k];
+        }
+      }
+      if (tid == 0) {
+        if (a.w.ck_write) a.cost[bi] += (int32_t)((__builtin_amdgcn_s_memtime() - t_indiv) >> 10);
+        a.status[bi] = status;
+      }
+      __syncthreads();
+      continue;
+    }
+    // ---- final selection (HaploBuilder.cpp:87-116) ------------------------
     K2_ST(4);
     if (tid == 0) {
-      a.cost[bi] = (int32_t)((__builtin_amdgcn_s_memtime() - t_indiv) >> 10);
+      const int32_t spent = (int32_t)((__builtin_amdgcn_s_memtime() - t_indiv) >> 10);
+      a.cost[bi] = a.w.windowed() ? a.cost[bi] + spent : spent;
       int cnt = 0;
       double total = 0.0;
       if (status == EST_OK) {

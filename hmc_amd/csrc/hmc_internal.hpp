@@ -60,6 +60,7 @@ enum EStatus : int32_t {
   EST_OVERFLOW_REC = -4,       // structure-record store exhausted (split E-step)
   EST_OVERFLOW_CONTRIB = -5,   // more contributions at a locus than the structure pass's capacity
   EST_DF_STALL = -6,           // dataflow value pass: a wait made no progress (watchdog; a bug, reported)
+  EST_OVERFLOW_CKPT = -7,      // windowed E-step: the checkpoint store is full
   EST_NEEDS_EXACT = 2,         // split E-step: a forward likelihood underflowed to 0 before
                                // the last locus, so extend() would skip that pair
                                // (HaploBuilder.cpp:237) — re-run on the fused kernel
@@ -158,6 +159,26 @@ struct EstepArgs {
   int diag_indiv;                // diagnostic build: stamp only this batch index (-1: all)
 };
 
+// Locus window of the checkpoint-and-recompute E-step (see StructArgs).
+// Checkpoint of an individual's frontier after record index j (window start
+// j + 1), at word ck_off[b * (nwin + 1) + win] of ck_store (even):
+//   [F][0] | lo u32[F] hi u32[F] nl u32[F] (structure: pattern g / ids and list
+//   lengths) | pad to even | fwd f64[F] hm u64[F] lik f64[F][S] (value pass)
+struct WinArgs {
+  int lo = 0, hi = 0;             // record / trace indices [lo, hi); hi == L + 1: the last window
+  int win = 0, nwin = 1;
+  uint32_t *ck_store = nullptr;
+  unsigned long long ck_cap = 0;  // words
+  unsigned long long *ck_cursor = nullptr;
+  unsigned long long *ck_off = nullptr;  // [batch][nwin + 1]
+  bool ck_write = false;          // save the window's last frontier (forward passes)
+  __host__ __device__ bool windowed() const { return ck_store != nullptr; }
+};
+__host__ __device__ inline unsigned long long ck_value_off(unsigned long long F) { return (2ull + 3ull * F + 1ull) & ~1ull; }
+__host__ __device__ inline unsigned long long ck_words(unsigned long long F, int S) {
+  return ck_value_off(F) + 4ull * F + 2ull * F * (unsigned long long)S;
+}
+
 // Split E-step, pass 1 (estep_structure): the value-independent part of
 // resolve() — frontier pattern-id pairs, successor keys, m_best_pair dedup in
 // creation order, per-state contribution lists and k-best list lengths — as
@@ -201,8 +222,16 @@ struct StructArgs {
   // EST_NEEDS_EXACT); status EST_OK_PRUNED.  Scratch: estep_s1_scratch_bytes(.., prune)
   bool prune = false;
   int32_t *next_q;                // dynamic schedule: order entries taken after the first gridDim.x (zeroed)
+  // Locus windows (checkpoint-and-recompute E-step, Ctx::estep_windowed):
+  // records of indices [win_lo, win_hi) only — win_lo == head_len starts
+  // with the head pairs, else from the frontier the checkpoint of window
+  // `win` holds (ck_off[b][win]); a window that ends before L+1 saves its
+  // last frontier as window win+1's checkpoint when ck_write (allocating it
+  // from ck_cursor).  Classic passes: win_lo = head_len, win_hi = L + 1.
+  WinArgs w;
   int32_t *status;                // [batch]
-  unsigned long long *re_count;   // [batch]
+  unsigned long long *re_count;   // [batch] (re_mode: 0 written, 1 added to, 2 untouched)
+  int re_mode = 0;
   int32_t *fmax;                  // [batch]
   unsigned int *max_states;
   unsigned long long *stamps;     // diagnostic build: [16] shader cycles per phase / counters
@@ -236,6 +265,7 @@ struct ValueArgs {
   double *prior, *posterior, *weight;
   int32_t *cost;
   unsigned long long *stamps;  // diagnostic build: [16] block-critical-path cycles per phase
+  WinArgs w;                   // locus window (StructArgs::w); cost is added to over the forward windows
 };
 
 struct TracebackArgs {
@@ -251,6 +281,13 @@ struct TracebackArgs {
   const int32_t *sample_base;  // [batch] first sample row of each individual
   uint8_t *rows;               // [H][L] sample-major haplotypes (allele index)
   double *w_out;               // [H]
+  // Locus window [win_lo, win_hi) of trace indices (checkpoint-and-recompute
+  // E-step): the walk starts from the candidates (win_hi == L + 1) or from
+  // the cursor the window above left (state, index, haplotype swap), and leaves
+  // one for the window below; classic: win_lo = head_len, win_hi = L + 1.
+  int win_lo = 0, win_hi = 0;
+  uint32_t *cur_state = nullptr, *cur_idx = nullptr;  // [batch][S_MAX]
+  uint8_t *cur_swap = nullptr;                        // [batch][S_MAX]
 };
 
 size_t estep_scratch_bytes(int fcap, int hcap, int S, int nw);

@@ -237,11 +237,28 @@ class HaploModel:
                                          _p(alleles, C.c_int32), _p(freq, C.c_double), C.byref(sc)))
         return freq, sc.value
 
+    def set_shard(self, i0: int, i1: int):
+        """One-rank measurement hook (hmc_set_shard): later E- and M-steps cover
+        individuals [i0, i1) of the loaded panel with the current model."""
+        self._check(lib().hmc_set_shard(self._h, int(i0), int(i1)))
+        self.i0, self.i1 = int(i0), int(i1)
+
+    def set_estep_windows(self, mode: str = "auto", window_loci: int = 0):
+        """Checkpoint-and-recompute E-step (hmc_set_estep_windows): "auto",
+        "never" or "always"; window_loci = loci per window (0: from the store
+        budgets).  Results are identical."""
+        self._check(lib().hmc_set_estep_windows(self._h, {"auto": 0, "never": 1, "always": 2}[mode], int(window_loci)))
+
+    def estep_windows(self) -> dict:
+        w, wl, g, ms = C.c_int(), C.c_int(), C.c_int(), C.c_double()
+        self._check(lib().hmc_last_estep_windows(self._h, C.byref(w), C.byref(wl), C.byref(g), C.byref(ms)))
+        return dict(windows=w.value, window_loci=wl.value, groups=g.value, recompute_ms=ms.value)
+
     def set_value_mode(self, mode: str):
         """Value pass of the split E-step: "fast" (value-only k-best lists, the
         libstdc++ permutations only for individuals with ties) or "exact" (the
         permutations for everyone; default).  Results are identical."""
-        self._check(lib().hmc_set_value_mode(self._h, {"fast": 0, "exact": 1}[mode]))
+        self._check(lib().hmc_set_value_mode(self._h, {"fast": 0, "exact": 1, "auto": 2}[mode]))
 
     def set_value_layout(self, mode: int):
         """Phase-B layout of the value pass (hmc_set_value_layout): two links

@@ -118,6 +118,13 @@ int hmc_panel_info(const hmc_ctx *ctx, int *N, int *L, int *max_alleles);
 /* This rank's individuals [i0, i1): contiguous blocks balanced by E-step cost
  * (L/8 + heterozygous-or-missing loci per individual); [0, N) on one rank. */
 int hmc_shard_range(const hmc_ctx *ctx, int *i0, int *i1);
+/* Measurement hook of a one-rank context: from here on the E-step and the
+ * M-step's scans cover individuals [i0, i1) of the loaded panel only, with
+ * the current model (e.g. the M0 mined over the whole panel) — rank r's own
+ * E-step work of an N-rank run, on one GPU (tools/cfg4_rank.py).  Drops the
+ * samples and every per-individual estimate.  Replaces no reference
+ * interface. */
+int hmc_set_shard(hmc_ctx *ctx, int i0, int i1);
 /* Per-locus allele tables: num[L], sym[L][max_alleles], freq[L][max_alleles]
  * (GenoData::allele_num / allele_symbol / allele_frequency, GenoData.h:43-49). */
 int hmc_allele_table(const hmc_ctx *ctx, int32_t *num, int32_t *sym, double *freq);
@@ -338,10 +345,14 @@ int hmc_last_estep_passes(const hmc_ctx *ctx, int *structure_passes, int *value_
  * (a non-zero likelihood tied across some list's S-cut — the set
  * std::nth_element keeps then depends on the list order, HaploPair.cpp:85-88 —
  * or final candidates with equal or zero priors, HaploBuilder.cpp:101-105) is
- * re-run with the libstdc++ permutations.  Mode 1 (default): every individual
- * with the libstdc++ permutations.  Results are identical; mode 0 pays off
- * only where few individuals have such ties (at BASELINE config 3 about half
- * of them have final candidates with equal priors, and mode 1 is faster). */
+ * re-run with the libstdc++ permutations.  Mode 1: every individual with the
+ * libstdc++ permutations.  Mode 2 (default): automatic — mode 0 on panels with
+ * more than two alleles per locus once the model is smaller than the panel,
+ * mode 1 otherwise and for the rest of the context once a mode-0 E-step
+ * re-ran more than 35 % of its individuals.  Results are identical in every
+ * mode; mode 0 pays off only where few individuals have such ties (at
+ * BASELINE config 3 about half of them have final candidates with equal
+ * priors, and mode 1 is faster; at config 5's later E-steps a quarter). */
 int hmc_set_value_mode(hmc_ctx *ctx, int mode);
 /* Phase-B layout of the value pass (results identical): the overflowing adds'
  * selections with two links per lane (S lanes and 64 / S lists per
@@ -380,6 +391,20 @@ int hmc_set_end_order(hmc_ctx *ctx, int on);
 int hmc_set_exact_walk(hmc_ctx *ctx, int items_per_wave);
 /* 1 when the last value-pass launch ran the dataflow schedule. */
 int hmc_last_value_pass(const hmc_ctx *ctx, int *dataflow);
+/* Checkpoint-and-recompute E-step (SURVEY §7 hard part 4): the loci in
+ * windows, each window's last frontier saved as the next one's checkpoint;
+ * the forward keeps one window of records and traces per individual, the
+ * traceback recomputes each earlier window from its checkpoint.  Results are
+ * identical to the classic passes.  mode 0 (default): automatic — when the
+ * first loci of a sample show that the classic passes could hold fewer than
+ * two individuals per CU in a group (cfg 4's per-rank E1); 1 never; 2 always
+ * (tests).  window_loci: loci per window (0: from the store budgets).
+ * Replaces no reference interface (HaploBuilder::resolve keeps every locus's
+ * pairs alive, HaploBuilder.cpp:35-126). */
+int hmc_set_estep_windows(hmc_ctx *ctx, int mode, int window_loci);
+/* The last E-step's windows (0 = classic passes), loci per window, groups of
+ * individuals, and device ms of the recompute (backward) passes. */
+int hmc_last_estep_windows(const hmc_ctx *ctx, int *windows, int *window_loci, int *groups, double *recompute_ms);
 /* Individuals the last E-step re-ran with the libstdc++ permutations (mode 0)
  * and the device time of those re-runs (ms, part of values_ms). */
 int hmc_last_estep_order(const hmc_ctx *ctx, int *n_rerun, double *rerun_ms);

@@ -1,0 +1,126 @@
+"""GPU parity of the checkpoint-and-recompute E-step (ctx_window.cpp,
+hmc_set_estep_windows): the loci cut into windows, each window's last frontier
+saved as the next one's checkpoint, the traceback recomputing every earlier
+window from its checkpoint.  Forced on small panels with tiny windows (down to
+one locus), it must equal the CPU restatement bit for bit — the same bar as
+the classic passes (tolerance 0 for every integer and double)."""
+import numpy as np
+import pytest
+
+import hmc_amd
+from hmc_amd import synth
+
+from test_gpu_parity import PANELS, assert_estep_equal, gpu_model, last_symbols, panel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name,wl", [(n, w) for n in sorted(PANELS) for w in (1, 7)] + [("n300", 64), ("a4", 33)])
+def test_windowed_estep_on_reference_model(oracle_mod, name, wl):
+    """E-step on the restatement's M0 table in windows of `wl` loci ==
+    HaploModel::resolveAll: LL, R_E, totals, candidates, priors, posteriors,
+    samples, weights, resolutions."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
+    o.find_patterns()
+    pt = o.patterns()
+    m = gpu_model(p)
+    m.set_estep_windows("always", wl)
+    m.set_patterns(pt["start"], pt["len"], pt["freq"], pt["tp"], pt["succ"], last_symbols(pt))
+    ll_g, H, re_g = m.resolve_all()
+    w = m.estep_windows()
+    assert w["windows"] == -(-(p.L) // wl), w
+    o.reset_counters()
+    assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
+
+
+@pytest.mark.parametrize("name,wl", [("cfg1", 3), ("n60", 5), ("miss2", 11), ("a3miss5", 2), ("a8", 4)])
+def test_windowed_full_em(oracle_mod, name, wl):
+    """HaploModel::run with every E-step in windows: iteration count,
+    per-iteration LL / R_E / R_M / pattern counts, HaploComp and the accepted
+    pair of every individual."""
+    p = panel(name)
+    m = gpu_model(p, max_iteration=30)
+    m.set_estep_windows("always", wl)
+    res = m.run()
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10, max_iter=30)
+    r = o.run()
+    assert m.iterations == r["iterations"]
+    assert [x["ll"] for x in m.log] == r["ll"].tolist()
+    assert [x["r_e"] for x in m.log] == r["R_E"].tolist()
+    for k in range(r["iterations"] - 1):
+        assert m.log[k]["r_m"] == r["R_M"][k + 1]
+    assert np.array_equal(res, r["resolutions"])
+    np.testing.assert_array_equal(np.array([x["haplocomp"] for x in m.log]), r["haplocomp"])
+
+
+@pytest.mark.parametrize("S,wl", [(1, 3), (3, 1), (17, 4), (40, 6)])
+def test_windowed_sample_sizes(oracle_mod, S, wl):
+    """Windows with lists of one link, of an odd width, past 16 (one link per
+    lane) and past 32 (a list over two lanes' slots)."""
+    p = panel("a3miss5")
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=S)
+    o.find_patterns()
+    m = gpu_model(p, S)
+    m.set_estep_windows("always", wl)
+    m.find_patterns()
+    ll_g, H, re_g = m.resolve_all()
+    o.reset_counters()
+    assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
+
+
+@pytest.mark.parametrize("model,order", [("MC", 2), ("MA", 1)])
+def test_windowed_head_len_models(oracle_mod, model, order):
+    """Models whose head patterns span several loci (MC order 2: head_len 3):
+    the first window starts at the head pairs, the traceback ends in them."""
+    p = panel("n60")
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10, max_iter=6)
+    o.set_model(model, order)
+    r = o.run()
+    m = gpu_model(p, max_iteration=6, model=model, mc_order=order)
+    m.set_estep_windows("always", 4)
+    res = m.run()
+    assert m.iterations == r["iterations"]
+    assert [x["ll"] for x in m.log] == r["ll"].tolist()
+    assert np.array_equal(res, r["resolutions"])
+
+
+def test_windowed_underflow_hands_over(oracle_mod):
+    """Individuals whose forward likelihoods underflow leave the windows and
+    are re-run by the classic passes with extend()'s forward test
+    (HaploBuilder.cpp:237): same LL (-inf) and resolutions as the reference."""
+    rng = np.random.default_rng(5)
+    a = (rng.integers(0, 2, (6, 2, 2500)) + ord("1")).astype(np.int32)
+    o = oracle_mod.Oracle(a, "S" * 2500, sample_size=4, max_iter=3)
+    r = o.run()
+    m = hmc_amd.HaploModel()
+    m.set_estep_windows("always", 300)
+    m.sample_size = 4
+    m.max_iteration = 3
+    res = m.run(hmc_amd.GenoData(a, "S" * 2500))
+    assert [x["ll"] for x in m.log] == r["ll"].tolist()
+    assert np.array_equal(res, r["resolutions"])
+    assert m.estep_split_stats()["n_fallback"] > 0
+
+
+def test_windowed_equals_classic_cfg2():
+    """cfg 2 (1 000 x 500): E1 on the genotype-mined M0 and E2 in automatic
+    windows of the store budgets and in windows of 50 loci equal the classic
+    passes bit for bit (LL, R_E, samples, weights)."""
+    p = synth.config_panel(2)
+    runs = []
+    for mode, wl in (("never", 0), ("always", 50), ("always", 0)):
+        m = gpu_model(p)
+        m.set_estep_windows(mode, wl)
+        m.find_patterns()
+        out = []
+        for _ in range(2):
+            ll, H, re = m.resolve_all()
+            al, w, tw = m.samples(H)
+            out.append((float(ll).hex(), H, re, al.tobytes(), w.tobytes(), float(tw).hex()))
+            if mode == "always":
+                assert m.estep_windows()["windows"] >= 1
+            m.find_patterns()
+        runs.append(out)
+        m.close()
+    assert runs[0] == runs[1] == runs[2]
