@@ -18,41 +18,21 @@
 #include <vector>
 
 #include "../include/hmc_amd.h"
+#include "hmc_options.hpp"
 
 int main(int argc, char **argv) {
-  double min_freq_abs = 1.5, min_freq = -1.0;
-  int max_iteration = 1, sample_size = 10, min_len = 1, max_len = 30, device = 0;
-  std::vector<std::string> files;
-  std::string model = "MV", format = "PHASE";
-  int mc_order = 1, num_patterns = -1;
-  bool exact = false, output_patterns = false;
-  for (int i = 1; i < argc; ++i) {
-    std::string a = argv[i];
-    auto next = [&]() -> const char * {
-      if (i + 1 >= argc) { fprintf(stderr, "missing value for %s\n", a.c_str()); exit(1); }
-      return argv[++i];
-    };
-    if (a == "-a" || a == "--min-freq-abs") min_freq_abs = atof(next());
-    else if (a == "-r" || a == "--min-freq-rel") { min_freq = atof(next()); min_freq_abs = 0; }
-    else if (a == "-i" || a == "--max-iteration") max_iteration = atoi(next());
-    else if (a == "--sample-size") sample_size = atoi(next());
-    else if (a == "--min-pattern-len") min_len = atoi(next());
-    else if (a == "--max-pattern-len") max_len = atoi(next());
-    else if (a == "--device") device = atoi(next());
-    else if (a == "-d" || a == "--debug") (void)next();                 // Logger level (HMC.cpp:28)
-    else if (a == "-f" || a == "--input-format") format = next();      // HMC.cpp:29
-    else if (a == "--exact-estimate") exact = true;                      // HMC.cpp:42
-    else if (a == "--output-patterns") { (void)next(); output_patterns = true; }  // HMC.cpp:30, 229-232
-    else if (a == "-m" || a == "--model") model = next();             // HMC.cpp:35
-    else if (a == "-o" || a == "--mc-order") mc_order = atoi(next());  // HMC.cpp:41
-    else if (a == "-n" || a == "--num-patterns") num_patterns = atoi(next());  // HMC.cpp:38
-    else if (a[0] == '-') { fprintf(stderr, "unknown option %s\n", a.c_str()); return 1; }
-    else files.push_back(argv[i]);
-  }
-  if (files.empty()) {
-    fprintf(stderr, "Usage: hmc_resolve [option ...] datafiles\n");
+  hmc_cli::Options o;
+  std::string perr;
+  if (hmc_cli::parse_options(argc, argv, o, perr)) {
+    fprintf(stderr, "%s\n", perr.c_str());
     return 1;
   }
+  const double min_freq_abs = o.min_freq_abs, min_freq = o.min_freq;
+  const int max_iteration = o.max_iteration, sample_size = o.sample_size, min_len = o.min_len, max_len = o.max_len,
+            device = o.device, mc_order = o.mc_order, num_patterns = o.num_patterns;
+  const std::vector<std::string> &files = o.files;
+  const std::string &model = o.model, &format = o.format;
+  const bool exact = o.exact, output_patterns = o.output_patterns;
   hmc_ctx *ctx = nullptr;
   int rc = hmc_ctx_create(device, &ctx);
   auto die = [&](const char *what) {
