@@ -205,8 +205,21 @@ int hmc_set_shard(hmc_ctx *h, int i0, int i1) {
   return HMC_OK;
 }
 
+// The kernels measured slower than the automatic paths (the fused E-step,
+// the dataflow value pass, the three-scan structure pass, the four-item exact
+// walk) are built into libhmc_amd_variants.so only (make variants); the
+// product library refuses to select them.
+#ifdef HMC_VARIANTS
+static int variant_ok(hmc_ctx *) { return HMC_OK; }
+#else
+static int variant_ok(hmc_ctx *h) {
+  return h->c.fail(HMC_EUNSUPPORTED, "this kernel variant is built into libhmc_amd_variants.so only (make variants)");
+}
+#endif
+
 int hmc_set_estep_mode(hmc_ctx *h, int mode) {
   if (!h || mode < 0 || mode > 1) return HMC_EARG;
+  if (mode == 1 && variant_ok(h)) return HMC_EUNSUPPORTED;
   h->c.estep_mode = mode;
   return HMC_OK;
 }
@@ -243,6 +256,7 @@ int hmc_set_value_mode(hmc_ctx *h, int mode) {
 
 int hmc_set_value_pass(hmc_ctx *h, int mode, int ring) {
   if (!h || mode < 0 || mode > 2 || ring < 0 || ring == 1 || ring == 2 || ring > 4) return HMC_EARG;
+  if (mode == 2 && variant_ok(h)) return HMC_EUNSUPPORTED;
   h->c.value_pass = mode;  // 0 automatic, 1 locus-synchronous (estep_values), 2 dataflow (estep_values_df)
   h->c.df_ring = ring ? ring : 3;
   return HMC_OK;
@@ -262,12 +276,14 @@ int hmc_set_dataflow_waves(hmc_ctx *h, int a_waves) {
 
 int hmc_set_exact_walk(hmc_ctx *h, int items_per_wave) {
   if (!h || (items_per_wave != 0 && items_per_wave != 1 && items_per_wave != 4)) return HMC_EARG;
+  if (items_per_wave == 4 && variant_ok(h)) return HMC_EUNSUPPORTED;
   h->c.exact_ipw = items_per_wave == 0 ? 1 : items_per_wave;
   return HMC_OK;
 }
 
 int hmc_set_structure_pass(hmc_ctx *h, int version) {
   if (!h || version < 0 || version > 2) return HMC_EARG;  // 0 = automatic
+  if (version == 2 && variant_ok(h)) return HMC_EUNSUPPORTED;
   h->c.structure_pass_version = version == 0 ? 1 : version;
   return HMC_OK;
 }
@@ -386,7 +402,11 @@ int hmc_model_save(hmc_ctx *h) { return h ? h->c.model_save() : HMC_EARG; }
 int hmc_em_rewind(hmc_ctx *h) { return h ? h->c.em_rewind() : HMC_EARG; }
 
 const char *hmc_build_info(void) {
-  return "hmc_amd 0.3 gfx950 -O3 -ffp-contract=off, built " __DATE__ " " __TIME__;
+#ifdef HMC_VARIANTS
+  return "hmc_amd 0.4+variants gfx950 -O3 -ffp-contract=off, built " __DATE__ " " __TIME__;
+#else
+  return "hmc_amd 0.4 gfx950 -O3 -ffp-contract=off, built " __DATE__ " " __TIME__;
+#endif
 }
 
 int hmc_load_phase(hmc_ctx *h, const char *path) {

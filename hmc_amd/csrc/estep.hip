@@ -326,6 +326,7 @@ size_t estep_lds_bytes(int S, int fc, int hc, int nw, int amax) {
 #define STAMP_FLUSH
 #endif
 
+#ifdef HMC_VARIANTS  // (the fused single-pass kernel: tests of the variants library only)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void estep_forward(EstepArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   STAMP_DECL
@@ -780,6 +781,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void e
   STAMP_FLUSH
 }
 
+#endif  // HMC_VARIANTS
+
 // Traceback (HaploPair::getGenotype, HaploPair.cpp:91-124): 16, 32 or 64
 // lanes per individual, one per candidate; walks the trace store from locus L back to
 // the head locus and writes both haplotypes as sample rows.
@@ -1022,20 +1025,23 @@ hipError_t launch_test_coop_nth(double *lik, uint32_t *tag, const int *off, cons
   return hipGetLastError();
 }
 
+#ifdef HMC_VARIANTS
 hipError_t launch_estep(const EstepArgs &a, int grid, int nw, hipStream_t st) {
   if (a.S < 1 || a.S > 32 || a.pan.amax > A_MAX || a.fcap > F_MAX || (a.hcap & (a.hcap - 1)) ||
       a.lds_hc < 1 || (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || nw < 1 || nw > 4)
     return hipErrorInvalidValue;
   const size_t lds = estep_lds_bytes(a.S, a.lds_fc, a.lds_hc, nw, a.pan.amax);
-  static size_t lds_attr = 0;
-  if (lds > 65536 && lds > lds_attr) {
+  if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute((const void *)estep_forward, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    lds_attr = lds;
   }
   hipLaunchKernelGGL(estep_forward, dim3(grid), dim3(WAVE * nw), lds, st, a);
   return hipGetLastError();
 }
+
+#else
+hipError_t launch_estep(const EstepArgs &, int, int, hipStream_t) { return hipErrorNotSupported; }
+#endif
 
 hipError_t launch_traceback(const TracebackArgs &a, int, hipStream_t st) {
   if (a.nbatch <= 0) return hipSuccess;

@@ -45,6 +45,7 @@
 #include "estep_common.hpp"
 #include "value_front.hpp"
 
+#ifdef HMC_VARIANTS  // (measured slower than estep_values: the variants library only)
 namespace hmc {
 
 namespace {
@@ -772,14 +773,12 @@ hipError_t launch_estep_values_df(const ValueArgs &a, int grid, int nw, int na, 
   const DfPlan plan = df_plan(a.S, a.lds_fc, na, nw - na, pair, R, qcap, a.fcap);
   const size_t lds = (size_t)plan.bytes;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  static size_t lds_attr = 0;
-  if (lds > 65536 && lds > lds_attr) {
+  if (lds > 65536) {
     for (const void *f : {(const void *)estep_values_df<4, true>, (const void *)estep_values_df<4, false>,
                           (const void *)estep_values_df<5, true>, (const void *)estep_values_df<5, false>}) {
       hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
     }
-    lds_attr = lds;
   }
   const dim3 g(grid), b(WAVE * nw);
   if (pair) {
@@ -793,3 +792,12 @@ hipError_t launch_estep_values_df(const ValueArgs &a, int grid, int nw, int na, 
 }
 
 }  // namespace hmc
+#else
+namespace hmc {
+size_t estep_df_lds_bytes(int, int, int, int, bool, int, int, int) { return 0; }
+size_t estep_df_scratch_bytes(int, int, int) { return 0; }
+hipError_t launch_estep_values_df(const ValueArgs &, int, int, int, int, bool, int, int, hipStream_t) {
+  return hipErrorNotSupported;
+}
+}  // namespace hmc
+#endif  // HMC_VARIANTS

@@ -803,6 +803,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
   S1_FLUSH
 }
 
+#ifdef HMC_VARIANTS  // (estep_structure2: measured slower, the variants library only)
 // ======================================================= pass 1, v2 ======
 //
 // The same structure records with fewer block-wide hand-offs per locus
@@ -1266,6 +1267,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     }
   }
 }
+
+#endif  // HMC_VARIANTS
 
 // ============================================================ pass 2 ======
 
@@ -1822,6 +1825,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
   K2_FLUSH
 }
 
+#ifdef HMC_VARIANTS
 hipError_t launch_estep_structure2(const StructArgs &a, int grid, int nw, hipStream_t st) {
   if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > F_MAX || (a.hcap & (a.hcap - 1)) || a.lds_hc < 1 ||
       (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || a.lds_cc < 0 || a.ccap < 1 || a.mod.head_len < 1 ||
@@ -1830,15 +1834,12 @@ hipError_t launch_estep_structure2(const StructArgs &a, int grid, int nw, hipStr
       (nw != 1 && nw != 4 && nw != 8 && nw != 16))
     return hipErrorInvalidValue;
   const size_t lds = estep_s1v2_lds_bytes(a.lds_fc, a.lds_hc, a.lds_cc, a.pan.amax, nw);
-  static size_t lds_attr[4] = {0, 0, 0, 0};
-  const int ix = nw == 16 ? 3 : (nw == 8 ? 2 : (nw == 4 ? 1 : 0));
   const void *f = nw == 16 ? (const void *)estep_structure2<16>
                            : (nw == 8 ? (const void *)estep_structure2<8>
                                       : (nw == 4 ? (const void *)estep_structure2<4> : (const void *)estep_structure2<1>));
-  if (lds > 65536 && lds > lds_attr[ix]) {
+  if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    lds_attr[ix] = lds;
   }
   if (nw == 16) hipLaunchKernelGGL(estep_structure2<16>, dim3(grid), dim3(16 * WAVE), lds, st, a);
   else if (nw == 8) hipLaunchKernelGGL(estep_structure2<8>, dim3(grid), dim3(8 * WAVE), lds, st, a);
@@ -1846,6 +1847,12 @@ hipError_t launch_estep_structure2(const StructArgs &a, int grid, int nw, hipStr
   else hipLaunchKernelGGL(estep_structure2<1>, dim3(grid), dim3(WAVE), lds, st, a);
   return hipGetLastError();
 }
+
+#else
+// the product library: estep_structure2 is built into libhmc_amd_variants.so only
+size_t estep_s1v2_lds_bytes(int, int, int, int, int) { return 0; }
+hipError_t launch_estep_structure2(const StructArgs &, int, int, hipStream_t) { return hipErrorNotSupported; }
+#endif
 
 hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStream_t st) {
   if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > F_MAX || (a.hcap & (a.hcap - 1)) || a.lds_hc < 1 ||
@@ -1855,15 +1862,12 @@ hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStre
       (nw != 1 && nw != 4 && nw != 8 && nw != 16))
     return hipErrorInvalidValue;
   const size_t lds = estep_s1_lds_bytes(a.lds_fc, a.lds_hc, a.lds_cc, a.pan.amax, nw);
-  static size_t lds_attr[4] = {0, 0, 0, 0};
-  const int ix = nw == 16 ? 3 : (nw == 8 ? 2 : (nw == 4 ? 1 : 0));
   const void *f = nw == 16 ? (const void *)estep_structure<16>
                            : (nw == 8 ? (const void *)estep_structure<8>
                                       : (nw == 4 ? (const void *)estep_structure<4> : (const void *)estep_structure<1>));
-  if (lds > 65536 && lds > lds_attr[ix]) {
+  if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    lds_attr[ix] = lds;
   }
   if (nw == 16) hipLaunchKernelGGL(estep_structure<16>, dim3(grid), dim3(16 * WAVE), lds, st, a);
   else if (nw == 8) hipLaunchKernelGGL(estep_structure<8>, dim3(grid), dim3(8 * WAVE), lds, st, a);
@@ -1877,30 +1881,16 @@ hipError_t launch_estep_values(const ValueArgs &a, int grid, int nw, bool fast, 
       (a.S > 32 && fast) || (pair && (fast || a.S > 16)))
     return hipErrorInvalidValue;
   const size_t lds = estep_s2_lds_bytes(a.S, a.lds_fc, nw, pair);
-  static size_t lds_attr = 0;
-  if (lds > 65536 && lds > lds_attr) {
-    for (const void *f : {(const void *)estep_values<true, 4>, (const void *)estep_values<false, 4>,
-                          (const void *)estep_values<true, 5>, (const void *)estep_values<false, 5>,
-                          (const void *)estep_values<false, 4, true>, (const void *)estep_values<false, 4, false, true>,
-                          (const void *)estep_values<false, 5, false, true>}) {
-      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) return e;
-    }
-    lds_attr = lds;
+  void (*k)(ValueArgs);
+  if (a.S > 32) k = estep_values<false, 4, true>;  // lists of more than one wavefront: exact order only
+  else if (pair) k = wpe == 5 ? estep_values<false, 5, false, true> : estep_values<false, 4, false, true>;
+  else if (wpe == 5) k = fast ? estep_values<true, 5> : estep_values<false, 5>;
+  else k = fast ? estep_values<true, 4> : estep_values<false, 4>;
+  if (lds > 65536) {  // (per device: set on every launch that needs it)
+    hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
   }
-  const dim3 g(grid), b(WAVE * nw);
-  if (a.S > 32) {  // lists of more than one wavefront: exact order only
-    hipLaunchKernelGGL((estep_values<false, 4, true>), g, b, lds, st, a);
-  } else if (pair) {
-    if (wpe == 5) hipLaunchKernelGGL((estep_values<false, 5, false, true>), g, b, lds, st, a);
-    else hipLaunchKernelGGL((estep_values<false, 4, false, true>), g, b, lds, st, a);
-  } else if (wpe == 5) {
-    if (fast) hipLaunchKernelGGL((estep_values<true, 5>), g, b, lds, st, a);
-    else hipLaunchKernelGGL((estep_values<false, 5>), g, b, lds, st, a);
-  } else {
-    if (fast) hipLaunchKernelGGL((estep_values<true, 4>), g, b, lds, st, a);
-    else hipLaunchKernelGGL((estep_values<false, 4>), g, b, lds, st, a);
-  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(WAVE * nw), lds, st, a);
   return hipGetLastError();
 }
 

@@ -515,16 +515,17 @@ hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st, int i
   if (a.width < 1 || a.width > 64 || (items_per_wave != 1 && items_per_wave != 4)) return hipErrorInvalidValue;
   const size_t lds = exact_walk_lds_bytes(a.max_depth, a.fmax) * (size_t)items_per_wave;
   if (lds > EXACT_WALK_LDS_MAX) return hipErrorInvalidValue;  // the host reports it (exact_walk_group)
-  const void *f = items_per_wave == 4 ? (const void *)exact_walk<16> : (const void *)exact_walk<WAVE>;
-  static size_t lds_attr[2] = {0, 0};
-  const int ix = items_per_wave == 4 ? 1 : 0;
-  if (lds > 65536 && lds > lds_attr[ix]) {  // wide frontiers: a larger reached-state bitmap, fewer waves per CU
-    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+#ifdef HMC_VARIANTS
+  void (*k)(ExactArgs) = items_per_wave == 4 ? exact_walk<16> : exact_walk<WAVE>;
+#else
+  if (items_per_wave != 1) return hipErrorNotSupported;  // (four items per wave: the variants library only)
+  void (*k)(ExactArgs) = exact_walk<WAVE>;
+#endif
+  if (lds > 65536) {  // wide frontiers: a larger reached-state bitmap, fewer waves per CU (set per launch: per device)
+    hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    lds_attr[ix] = lds;
   }
-  if (items_per_wave == 4) hipLaunchKernelGGL(exact_walk<16>, dim3(grid), dim3(WAVE), lds, st, a);
-  else hipLaunchKernelGGL(exact_walk<WAVE>, dim3(grid), dim3(WAVE), lds, st, a);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(WAVE), lds, st, a);
   return hipGetLastError();
 }
 

@@ -680,12 +680,10 @@ hipError_t launch_mine_sum(const MineArgs &a, int cb, int ce, hipStream_t st) {
 hipError_t launch_mine_count(const MineArgs &a, int level, int pbeg, int pend, hipStream_t st) {
   if (pend <= pbeg) return hipSuccess;
   const size_t lds = (size_t)mine_count_bufs(a.amax) * ((size_t)a.amax * CROW * 8 + (size_t)a.amax * WAVE * 4);
-  static size_t lds_attr = 0;
-  if (lds > 65536 - 1024 && lds > lds_attr) {  // many alleles: opt in to the CU's full LDS
+  if (lds > 65536 - 1024) {  // many alleles: opt in to the CU's full LDS (per device: set on every launch)
     hipError_t e = hipFuncSetAttribute((const void *)mine_count, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds + 1024);
     if (e != hipSuccess) return e;
-    lds_attr = lds;
   }
   hipLaunchKernelGGL(mine_count, dim3(pend - pbeg), dim3(WAVE), lds, st, a, level, pbeg, pend);
   return hipGetLastError();

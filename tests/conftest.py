@@ -10,6 +10,19 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
+    config.addinivalue_line("markers", "variants: the kernels measured slower than the automatic paths, built into "
+                                       "libhmc_amd_variants.so only (HMC_AMD_LIB=hmc_amd/libhmc_amd_variants.so -m variants)")
+
+
+def pytest_collection_modifyitems(config, items):
+    """Tests of the variant kernels run only against the variants library:
+    the product library refuses to select them (HMC_EUNSUPPORTED)."""
+    if "variants" in os.path.basename(os.environ.get("HMC_AMD_LIB", "")):
+        return
+    skip = pytest.mark.skip(reason="variant kernels: HMC_AMD_LIB=hmc_amd/libhmc_amd_variants.so pytest -m variants")
+    for it in items:
+        if "variants" in it.keywords:
+            it.add_marker(skip)
 
 
 @pytest.fixture(scope="session")
