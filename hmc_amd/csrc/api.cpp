@@ -275,8 +275,8 @@ int hmc_set_dataflow_waves(hmc_ctx *h, int a_waves) {
 }
 
 int hmc_set_exact_walk(hmc_ctx *h, int items_per_wave) {
-  if (!h || (items_per_wave != 0 && items_per_wave != 1 && items_per_wave != 4)) return HMC_EARG;
-  if (items_per_wave == 4 && variant_ok(h)) return HMC_EUNSUPPORTED;
+  if (!h || (items_per_wave != 0 && items_per_wave != 1 && items_per_wave != 2 && items_per_wave != 4)) return HMC_EARG;
+  if (items_per_wave >= 2 && variant_ok(h)) return HMC_EUNSUPPORTED;
   h->c.exact_ipw = items_per_wave == 0 ? 1 : items_per_wave;
   return HMC_OK;
 }
@@ -297,6 +297,15 @@ int hmc_last_value_pass(const hmc_ctx *h, int *dataflow) {
 int hmc_set_value_layout(hmc_ctx *h, int mode) {
   if (!h || mode < 0 || mode > 2) return HMC_EARG;  // 0 never, 1 heavy groups, 2 every group
   h->c.value_pair = mode;
+  return HMC_OK;
+}
+
+int hmc_last_exact_walk(const hmc_ctx *h, int64_t *units, int64_t *launches, int64_t *deferred, int *pruned) {
+  if (!h) return HMC_EARG;
+  if (units) *units = h->c.xw_units;
+  if (launches) *launches = h->c.xw_launches;
+  if (deferred) *deferred = h->c.xw_defers;
+  if (pruned) *pruned = h->c.exact_pruned;
   return HMC_OK;
 }
 

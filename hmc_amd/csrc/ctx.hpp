@@ -709,6 +709,16 @@ struct Ctx {
   int exact_group(const int32_t *ids, int k, const std::function<int(std::vector<int32_t> &)> &rerun = nullptr);
   // The trie walk of one group (the current round's trie).
   int exact_walk_group(ExactArgs &x, int k, int dev_cu);
+  // Breadth-first (default): work units of one trie node each, lane by lane
+  // (exact_walk_units), level by level over batches of items.
+  int exact_walk_bfs(ExactArgs &x, int k, int dev_cu);
+  DevBuf<int32_t> d_xu_q, d_xu_start, d_xu_node, d_xdef, d_xidx;
+  DevBuf<double> d_xu_freq, d_xe_w, d_xlacc;
+  DevBuf<unsigned long long> d_xu_e0, d_xcur;
+  DevBuf<uint32_t> d_xu_ne, d_xe_t, d_xlbits;
+  DevBuf<int> d_xndef;
+  long long xw_units = 0, xw_launches = 0, xw_defers = 0;  // walk statistics of the last exact M-step
+  int exact_pruned = 0;  // individuals the last exact M-step walked over pruned records (underflow)
   double ms_walk = 0;
   // Rounds of one exact M-step share the E-step model: when a round's
   // individuals ran as one structure pass and one group, the next rounds walk
@@ -919,8 +929,9 @@ struct Ctx {
   int window_loci = 0;         // record indices per window (0 = from the budgets)
   DevBuf<uint32_t> d_ck;
   DevBuf<unsigned long long> d_ck_off, d_ck_cursor;
-  DevBuf<uint32_t> d_cur_state, d_cur_idx;
-  DevBuf<uint8_t> d_cur_swap;
+  DevBuf<uint32_t> d_nodes, d_bnd_n, d_gc_scr;  // trace survivors (3 words per node), boundary list lengths, collection scratch
+  DevBuf<unsigned long long> d_bnd_off, d_node_cursor;
+  double win_scale = 1.0;  // shrinks the windows after a trace store overflow (the E-step restarts)
   int last_windows = 0, last_window_loci = 0, last_window_groups = 0;  // hmc_last_estep_windows
   double ms_ck = 0;  // device ms of the backward (recompute) passes, part of ms_s1 / ms_s2
   // A probe of the first loci of a sample decides: WIN_DECLINED when the
@@ -944,7 +955,9 @@ struct Ctx {
   // frontier, key slots (2x, power of two), contributions per locus (2x).
   // structure pass: 2 = estep_structure2 (fewer block hand-offs per locus), 1 = estep_structure
   int structure_pass_version = 1;  // hmc_set_structure_pass
-  int exact_ipw = 1;               // exact_walk items per wavefront, 1 or 4 (hmc_set_exact_walk)
+  // exact M-step walk (hmc_set_exact_walk): 1 breadth-first lane units
+  // (default), 2 / 4 depth-first, one / four items per wavefront (variants)
+  int exact_ipw = 1;
   static void s1_tier(int budget, int amax, int nw, int &fc, int &hc, int &cc, bool v2 = false) {
     for (int f = 2048; f >= 16; f -= 16) {
       const int h = next_pow2(2 * f), c = 2 * f;

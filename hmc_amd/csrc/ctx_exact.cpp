@@ -216,6 +216,7 @@ int Ctx::exact_group(const int32_t *ids, int k, const std::function<int(std::vec
     if (xs[ids[q]] == EST_NEEDS_EXACT) redo.push_back(ids[q]);
   if (!redo.empty()) {  // their records again, pruned, then their fwd/bwd sums
     if (!rerun) return fail(HMC_EHIP, "exact M-step: a forward likelihood underflows (individual %d)", i0 + redo[0]);
+    exact_pruned += (int)redo.size();
     int rc;
     if ((rc = rerun(redo))) return rc;
     const int nr = (int)redo.size();
@@ -242,12 +243,13 @@ int Ctx::exact_group(const int32_t *ids, int k, const std::function<int(std::vec
 }
 
 int Ctx::exact_walk_group(ExactArgs &x, int k, int dev_cu) {
+  if (exact_ipw == 1) return exact_walk_bfs(x, k, dev_cu);
   const int L = pan.L;
   hipError_t e;
   if (exact_walk_lds_bytes(tr_maxd, x.fmax) > EXACT_WALK_LDS_MAX)
     return fail(HMC_EUNSUPPORTED, "exact M-step: a frontier of %d states (trie depth %d) exceeds the walk's LDS bitmap",
                 x.fmax, tr_maxd);
-  // items per wavefront: 4 (16 lanes each) when their LDS fits, else 1
+  // (variants) items per wavefront: 4 (16 lanes each) when their LDS fits, else 1
   const int ipw = exact_ipw == 4 && exact_walk_lds_bytes(tr_maxd, x.fmax) * 4 <= EXACT_WALK_LDS_MAX ? 4 : 1;
   x.scratch_stride = exact_walk_scratch_doubles(tr_maxd, x.fmax, x.width);
   const long long items = (long long)k * L;
@@ -277,6 +279,109 @@ int Ctx::exact_walk_group(ExactArgs &x, int k, int dev_cu) {
     if (debug_mem && items > 16 * (long long)grid)
       fprintf(stderr, "[hmc] exact walk: items %lld..%lld of %lld (%d individuals), %.1f ms\n", i0, x.item1, items, k, ms);
   }
+  return HMC_OK;
+}
+
+int Ctx::exact_walk_bfs(ExactArgs &x, int k, int dev_cu) {
+  const int L = pan.L, fmax = std::max(x.fmax, 1);
+  const long long items = (long long)k * L;
+  hipError_t e;
+  // lanes: 8 waves per CU; each owns [a side | b side][3][fmax] accumulators and a state bitmap
+  const int grid = dev_cu * 2, nthr = grid * 256;
+  const size_t lacc = 6 * (size_t)fmax, lbits = (size_t)fmax / 32 + 2;
+  // unit and entry pools: a third of what is free (entries 28 B, units 32 B)
+  size_t freeb = 0, totb = 0;
+  hipMemGetInfo(&freeb, &totb);
+  const double scratch_b = (double)nthr * (lacc * 8 + lbits * 4);
+  const double pool_b = std::max(256e6, std::min(24e9, ((double)freeb - scratch_b) / 3.0));
+  const unsigned long long ecap = (unsigned long long)(pool_b * 0.8 / 28.0), ucap = (unsigned long long)(pool_b * 0.2 / 32.0);
+  const long long batch = std::max<long long>(1, std::min<long long>({items, (long long)(ecap / (2ull * (unsigned long long)fmax)),
+                                                                        (long long)ucap / 2, 1ll << 30}));
+  if ((e = d_xu_q.ensure(ucap)) || (e = d_xu_start.ensure(ucap)) || (e = d_xu_node.ensure(ucap)) || (e = d_xu_freq.ensure(ucap)) ||
+      (e = d_xu_e0.ensure(ucap)) || (e = d_xu_ne.ensure(ucap)) || (e = d_xe_t.ensure(ecap)) || (e = d_xe_w.ensure(3 * ecap)) ||
+      (e = d_xcur.ensure(2)) || (e = d_xndef.ensure(1)) || (e = d_xdef.ensure(std::max<size_t>((size_t)batch, ucap))) ||
+      (e = d_xidx.ensure(std::max<size_t>((size_t)batch, ucap))) || (e = d_xlacc.ensure((size_t)nthr * lacc)) ||
+      (e = d_xlbits.ensure((size_t)nthr * lbits)) || (e = hipMemsetAsync(d_xlacc.p, 0, (size_t)nthr * lacc * 8, st)) ||
+      (e = hipMemsetAsync(d_xlbits.p, 0, (size_t)nthr * lbits * 4, st)))
+    return hipfail(e, "exact walk pools");
+  XWalkArgs w;
+  w.u.q = d_xu_q.p;
+  w.u.start = d_xu_start.p;
+  w.u.node = d_xu_node.p;
+  w.u.freq = d_xu_freq.p;
+  w.u.e0 = d_xu_e0.p;
+  w.u.ne = d_xu_ne.p;
+  w.e_t = d_xe_t.p;
+  w.e_w = d_xe_w.p;
+  w.e_cap = ecap;
+  w.u_cap = ucap;
+  w.cursor = d_xcur.p;
+  w.defer = d_xdef.p;
+  w.n_defer = d_xndef.p;
+  w.lacc = d_xlacc.p;
+  w.lbits = d_xlbits.p;
+  w.lacc_stride = lacc;
+  w.lbits_stride = lbits;
+  x.scratch = nullptr;
+  hipEventRecord(ev[0], st);
+  // One level: the units [in_base, in_base + n) (or the listed ones) at
+  // `depth`, outputs from (u_top, e_top); then the next level over those
+  // outputs, then — with the pools above free again — the deferred units.
+  std::function<int(int, bool, unsigned long long, const std::vector<int32_t> *, int, unsigned long long, unsigned long long)> level;
+  level = [&](int depth, bool roots, unsigned long long in_base, const std::vector<int32_t> *idx, int n,
+              unsigned long long u_top, unsigned long long e_top) -> int {
+    hipError_t e2;
+    const unsigned long long cur0[2] = {u_top, e_top};
+    const int zero = 0;
+    if ((e2 = hipMemcpyAsync(d_xcur.p, cur0, 16, hipMemcpyHostToDevice, st)) ||
+        (e2 = hipMemcpyAsync(d_xndef.p, &zero, 4, hipMemcpyHostToDevice, st)) ||
+        (idx && (e2 = hipMemcpyAsync(d_xidx.p, idx->data(), idx->size() * 4, hipMemcpyHostToDevice, st))))
+      return hipfail(e2, "exact walk");
+    XWalkArgs w2 = w;
+    w2.in_base = in_base;
+    w2.idx = idx ? d_xidx.p : nullptr;
+    w2.n_in = n;
+    w2.depth = depth;
+    w2.roots = roots;
+    if ((e2 = launch_exact_walk_units(x, w2, std::max(1, std::min(grid, (n + 255) / 256)), st)))
+      return hipfail(e2, "exact_walk_units");
+    unsigned long long cur[2];
+    int nd = 0;
+    if ((e2 = hipMemcpyAsync(cur, d_xcur.p, 16, hipMemcpyDeviceToHost, st)) ||
+        (e2 = hipMemcpyAsync(&nd, d_xndef.p, 4, hipMemcpyDeviceToHost, st)) || (e2 = hipStreamSynchronize(st)))
+      return hipfail(e2, "exact walk");
+    ++xw_launches;
+    xw_units += n;
+    std::vector<int32_t> def((size_t)nd);
+    if (nd && ((e2 = hipMemcpyAsync(def.data(), d_xdef.p, (size_t)nd * 4, hipMemcpyDeviceToHost, st)) ||
+               (e2 = hipStreamSynchronize(st))))
+      return hipfail(e2, "exact walk");
+    const unsigned long long u_end = std::min(cur[0], ucap), e_end = std::min(cur[1], ecap);
+    if (nd == n && u_end == u_top)
+      return fail(HMC_ENOMEM, "exact M-step: one trie node's children exceed the walk's pools (%llu units, %llu entries)",
+                  ucap, ecap);
+    int rc2;
+    if (u_end > u_top && (rc2 = level(depth + 1, false, u_top, nullptr, (int)(u_end - u_top), u_end, e_end))) return rc2;
+    if (nd) {
+      xw_defers += nd;
+      std::sort(def.begin(), def.end());  // (any order gives the same sums: fixed-point adds)
+      if ((rc2 = level(depth, roots, in_base, &def, nd, u_top, e_top))) return rc2;
+    }
+    return HMC_OK;
+  };
+  for (long long b = 0; b < items; b += batch) {
+    const int nb = (int)std::min<long long>(batch, items - b);
+    int rc = level(0, true, (unsigned long long)b, nullptr, nb, 0, 0);
+    if (rc) return rc;
+  }
+  hipEventRecord(ev[1], st);
+  if ((e = hipStreamSynchronize(st))) return hipfail(e, "exact walk");
+  float ms = 0;
+  hipEventElapsedTime(&ms, ev[0], ev[1]);
+  ms_walk += ms;
+  if (debug_mem)
+    fprintf(stderr, "[hmc] exact walk (breadth-first): %lld items, %d individuals, %.1f ms; %lld units in %lld launches, "
+            "%lld deferred; pools %llu units / %llu entries\n", items, k, ms, xw_units, xw_launches, xw_defers, ucap, ecap);
   return HMC_OK;
 }
 
@@ -395,6 +500,8 @@ int Ctx::estimate_patterns(int *P_out, uint64_t *rm_out) {
   exact_rounds = 0;
   exact_candidates = 0;
   ms_walk = 0;
+  xw_units = xw_launches = xw_defers = 0;
+  exact_pruned = 0;
   xc_reuse = false;
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };

@@ -1,17 +1,24 @@
-// ctx_window.cpp — Ctx members: the checkpoint-and-recompute E-step (locus
-// windows, SURVEY §7 hard part 4) for panels whose per-individual records and
-// traces leave the stores room for only a few hundred individuals at a time.
+// ctx_window.cpp — Ctx members: the windowed E-step (locus windows with
+// frontier checkpoints and trace garbage collection, SURVEY §7 hard part 4) for
+// panels whose per-individual records and traces leave the stores room for
+// only a few hundred individuals at a time (cfg 4's per-rank E1: ~250 MB of
+// records and ~390 MB of traces per individual).
 //
 // HaploBuilder::resolve (HaploBuilder.cpp:35-126) walks the loci once forward
 // and the traceback (HaploPair::getGenotype, HaploPair.cpp:91-124) once
-// backward; the forward state at a locus is the frontier alone (pattern pairs,
-// list lengths, forward likelihoods, k-best lists).  So the record indices
-// hl..L are cut into windows: the forward saves each window's last frontier
-// (a checkpoint of ~(7 + 2S) words per state) and keeps no records or traces
-// past the window; the backward recomputes each window from its checkpoint —
-// the same passes over the same records, so the same traces — and continues
-// the traceback through it.  Records and traces then take one window's worth
-// per individual, and the whole shard runs as one group that fills the GPU.
+// backward from the final candidates.  The forward state at a window boundary
+// is the frontier alone (pattern pairs and list lengths; forward likelihoods
+// and k-best lists): each window's passes start from the checkpoint the
+// window before left, so records are kept for one window only.  The traces
+// needed later are only those reachable backward from the final candidates,
+// and the k-best links coalesce within a few dozen loci (cfg 2's E1: the
+// ~1 000-2 300 list entries of a locus reach ~10 entries 50 loci back): after
+// each window, the window before it is collected — its entries reachable from
+// any entry at the current window's end become survivor nodes
+// (estep_trace_gc) — so full traces are kept for two windows only.  The
+// traceback walks the two full windows and then the survivors' chains.  Every
+// pass runs the same arithmetic on the same inputs in the same order as the
+// classic passes, so the results are bit-identical.
 #include "ctx.hpp"
 
 namespace hmc {
@@ -45,8 +52,10 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   std::vector<unsigned long long> rw, tw;  // exact needs per individual and window
   std::vector<int32_t> fw;                 // largest frontier per individual and window
 
+  unsigned long long ck_cap[2] = {0, 0};  // checkpoint slots: [0, half) and [half, end)
+  bool bump = false;            // records from the store's bump allocator (the windows), else the regions rb / rs (the probe)
   // Structure pass of the record indices [bound[w], bound[w + 1]) over
-  // ids[0, np_) in the regions rb / rs.
+  // ids[0, np_).
   auto structure = [&](int w, const int32_t *ids, int np_, bool ck_write, int re_mode, bool fwd) -> int {
     const int nw1 = s1_nw > 0 ? s1_nw : (heavy_model ? (np_ <= dev_cu ? 16 : 4) : 1);
     const int bpc1 = s1_ipc > 0 ? s1_ipc
@@ -78,8 +87,8 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     s1.rec = d_rec.p;
     s1.rec_cap = d_rec.n;
     s1.rec_cursor = d_rec_cursor.p;
-    s1.rec_base = d_rbase.p;
-    s1.rec_size = d_recsz.p;
+    s1.rec_base = bump ? nullptr : d_rbase.p;
+    s1.rec_size = bump ? nullptr : d_recsz.p;
     s1.rec_off = d_rec_off.p;
     s1.rec_need = d_rneed.p;
     s1.trace_need = d_tneed.p;
@@ -97,8 +106,8 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     s1.w.win = w;
     s1.w.nwin = nwin;
     s1.w.ck_store = d_ck.p;
-    s1.w.ck_cap = d_ck.n;
-    s1.w.ck_cursor = d_ck_cursor.p;
+    s1.w.ck_cap = ck_cap[(w + 1) & 1];
+    s1.w.ck_cursor = d_ck_cursor.p + ((w + 1) & 1);
     s1.w.ck_off = d_ck_off.p;
     s1.w.ck_write = ck_write;
     hipEventRecord(ev[0], st);
@@ -162,20 +171,23 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   if (rl <= 0) return fail(HMC_EHIP, "windowed E-step without a measured individual");
 
   // ---- plan: window length and group size --------------------------------
-  // Every individual of a group gets an even share of each store per window,
-  // sized for the heaviest probed one with 25 % headroom; one whose window
-  // needs more runs that window again with its exact size.
-  const double fmax_est = std::max(1.0, (tl - 2.0) / (1.0 + S));  // states per locus of the heaviest
-  const double ckw = (double)ck_words((unsigned long long)fmax_est, S) + 2.0;
+  // The group's records (one window, bump-allocated) and traces (two windows)
+  // are sized by the probe's mean per-locus needs with 25 % headroom; an
+  // individual whose window records do not fit runs that window again.
+  const double fmean = std::max(1.0, (tmean - 2.0) / (1.0 + S));  // states per locus, mean
+  const double ckw = (double)ck_words((unsigned long long)fmean, S) + 4.0;
+  (void)rl;
+  (void)tl;
   int k = n, WL = 0;
   for (int div = 1;; ++div) {
     k = (n + div - 1) / div;
-    const double wl_r = (double)rbud / ((double)k * rl * 1.25), wl_t = (double)tbud / ((double)k * tl * 1.25);
-    WL = window_loci > 0 ? window_loci : (int)std::max(1.0, std::min(wl_r, wl_t));
+    const double wl_r = (double)rbud / ((double)k * rmean * 1.25), wl_t = (double)tbud / (2.0 * (double)k * tmean * 1.25);
+    WL = window_loci > 0 ? window_loci : (int)std::max(1.0, std::min(wl_r, wl_t) * win_scale);
     WL = std::min(WL, NR);
-    nwin = (NR + WL - 1) / WL;
-    if ((double)k * (nwin - 1) * ckw <= (double)cbud || k == 1) break;
+    if ((window_loci > 0 || WL >= 16) && 2.0 * (double)k * ckw * 1.5 <= (double)cbud) break;
+    if (k == 1) break;
   }
+  nwin = (NR + WL - 1) / WL;
   WL = (NR + nwin - 1) / nwin;  // even windows
   bound.assign(nwin + 1, 0);
   for (int w = 0; w <= nwin; ++w) bound[w] = hl + std::min(NR, w * WL);
@@ -184,35 +196,39 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   last_window_loci = WL;
   last_window_groups = ngroups;
   if (debug_mem)
-    fprintf(stderr, "[hmc] windowed E-step: %d individuals in %d group(s) of <= %d, %d windows of %d loci; "
-            "per locus %.0f record / %.0f trace words (heaviest), budgets rec %.1f trace %.1f ckpt %.1f GB\n",
-            n, ngroups, k, nwin, WL, rl, tl, rbud * 4e-9, tbud * 4e-9, cbud * 4e-9);
-  // ---- buffers ------------------------------------------------------------
-  const uint64_t ck_need = nwin > 1 ? (uint64_t)((double)k * (nwin - 1) * ckw * 1.25) + 1024 : 1024;
-  if (d_ck.n < ck_need) {
+    fprintf(stderr, "[hmc] windowed E-step: %d individuals in %d group(s) of <= %d, %d windows of %d loci; per locus "
+            "%.0f record / %.0f trace words (mean), budgets rec %.1f trace %.1f ckpt %.1f GB\n",
+            n, ngroups, k, nwin, WL, rmean, tmean, rbud * 4e-9, tbud * 4e-9, cbud * 4e-9);
+  // ---- buffers: checkpoints in two slots (the window's input and output)
+  const uint64_t ck_half = std::max<uint64_t>(1024, (uint64_t)((double)k * ckw * 1.5));
+  if (d_ck.n < 2 * ck_half) {
     d_ck.release();
-    e = d_ck.ensure(std::min<uint64_t>(ck_need, std::max<uint64_t>(cbud, 1024)));
+    e = d_ck.ensure(2 * ck_half);
     if (e == hipErrorOutOfMemory) {  // the stores are dead here: they give way
       (void)hipGetLastError();
       d_trace.release();
       d_rec.release();
-      e = d_ck.ensure(std::min<uint64_t>(ck_need, std::max<uint64_t>(cbud, 1024)));
+      e = d_ck.ensure(2 * ck_half);
     }
     if (e) return hipfail(e, "checkpoint store");
   }
-  if ((e = d_ck_off.ensure((size_t)n * (nwin + 1))) || (e = d_ck_cursor.ensure(1)) ||
-      (e = d_cur_state.ensure((size_t)n * S_MAX)) || (e = d_cur_idx.ensure((size_t)n * S_MAX)) ||
-      (e = d_cur_swap.ensure((size_t)n * S_MAX)) || (e = hipMemsetAsync(d_re.p, 0, (size_t)n * 8, st)) ||
+  ck_cap[0] = d_ck.n / 2;
+  ck_cap[1] = d_ck.n;
+  bump = true;
+  const unsigned long long zero64 = 0;
+  if ((e = d_ck_off.ensure((size_t)n * (nwin + 1))) || (e = d_ck_cursor.ensure(2)) || (e = d_bnd_off.ensure(n)) ||
+      (e = d_bnd_n.ensure(n)) || (e = d_node_cursor.ensure(1)) || (e = hipMemsetAsync(d_re.p, 0, (size_t)n * 8, st)) ||
       (e = hipMemsetAsync(d_cost.p, 0, (size_t)n * 4, st)))
     return hipfail(e, "windowed E-step alloc");
   rw.assign((size_t)n * nwin, 0);
   tw.assign((size_t)n * nwin, 0);
   fw.assign((size_t)n * nwin, 0);
   std::vector<int32_t> underflow;  // individuals whose likelihoods underflow: the classic passes (prune mode)
+  // trace store: even windows fill it from the bottom, odd windows from the top
+  uint64_t tr_lo = 0, tr_hi = 0;
 
-  // Value pass of window w over ids[0, k_) (trace regions in tbv), then the
-  // traceback through the window when `tb`.
-  auto values = [&](int w, const int32_t *ids, int k_, bool ck_write, bool tb, bool fwd) -> int {
+  // Value pass of window w over ids[0, k_) (trace regions in tbv).
+  auto values = [&](int w, const int32_t *ids, int k_) -> int {
     hipError_t e2;
     int rc2;
     double rsum = 0;
@@ -270,33 +286,199 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     v.w.win = w;
     v.w.nwin = nwin;
     v.w.ck_store = d_ck.p;
-    v.w.ck_cap = d_ck.n;
-    v.w.ck_cursor = d_ck_cursor.p;
+    v.w.ck_cap = ck_cap[(w + 1) & 1];
+    v.w.ck_cursor = d_ck_cursor.p + ((w + 1) & 1);
     v.w.ck_off = d_ck_off.p;
-    v.w.ck_write = ck_write;
+    v.w.ck_write = true;
     hipEventRecord(ev[0], st);
     if ((e2 = launch_estep_values(v, grid2, vnw, false, vwpe, st, pair))) return hipfail(e2, "estep_values launch");
     hipEventRecord(ev[1], st);
     if ((rc2 = read_status({}, 0, true))) return rc2;
     hipEventElapsedTime(&ms, ev[0], ev[1]);
     ms_s2 += ms;
-    if (!fwd) ms_ck += ms;
     ++n_value_passes;
     if (debug_mem)
-      fprintf(stderr, "[hmc] window %d/%d %s: value pass %d individuals, %d x %d per CU, %.1f ms\n", w + 1, nwin,
-              fwd ? "forward" : "recompute", k_, vnw, vipc, ms);
+      fprintf(stderr, "[hmc] window %d/%d: value pass %d individuals, %d x %d per CU, %.1f ms\n", w + 1, nwin, k_, vnw, vipc, ms);
     for (int q = 0; q < k_; ++q) {
-      const int s = h_status[ids[q]];
-      if (s == EST_OVERFLOW_TRACE) return fail(HMC_EHIP, "trace store overflow with exact sizes (window %d)", w);
-      if (s != EST_OK && s != EST_UNRESOLVED && s != EST_NEEDS_EXACT)
-        return fail(HMC_EHIP, "windowed value pass: status %d (individual %d, window %d)", s, i0 + ids[q], w);
+      const int s2 = h_status[ids[q]];
+      if (s2 == EST_OVERFLOW_TRACE) return fail(HMC_EHIP, "trace store overflow with exact sizes (window %d)", w);
+      if (s2 != EST_OK && s2 != EST_UNRESOLVED && s2 != EST_NEEDS_EXACT)
+        return fail(HMC_EHIP, "windowed value pass: status %d (individual %d, window %d)", s2, i0 + ids[q], w);
     }
-    if (tb) {
+    return HMC_OK;
+  };
+
+  // One window over the group `grp`: the structure pass (records bump-allocated
+  // from the record store), then the value passes; an individual whose window
+  // records did not fit runs the window again once the others' records are
+  // dead.  Traces go to the window's half of the trace store.  Individuals
+  // that die (no resolution) or underflow leave `grp`.
+  auto window = [&](int w, std::vector<int32_t> &grp) -> int {
+    std::vector<int32_t> todo(grp), dead;
+    bool first = true;
+    if ((e = hipMemcpyAsync(d_ck_cursor.p + ((w + 1) & 1), (w + 1) & 1 ? &ck_cap[0] : &zero64, 8, hipMemcpyHostToDevice, st)))
+      return hipfail(e, "windowed E-step");
+    if (w % 2 == 0) tr_lo = 0;
+    else tr_hi = d_trace.n;
+    while (!todo.empty()) {
+      if ((e = hipMemsetAsync(d_rec_cursor.p, 0, 8, st))) return hipfail(e, "windowed E-step");
+      if ((rc = structure(w, todo.data(), (int)todo.size(), first, first ? 1 : 2, true))) return rc;
+      std::vector<int32_t> ok, deferred;
+      for (int bi : todo) {
+        const int s = h_status[bi];
+        if ((rc = restart_status(s))) return rc;
+        if (s == EST_OVERFLOW_CKPT) return fail(HMC_ENOMEM, "checkpoint store too small (window %d)", w);
+        if (first) {
+          rw[(size_t)bi * nwin + w] = hr[bi];
+          tw[(size_t)bi * nwin + w] = ht[bi];
+          fw[(size_t)bi * nwin + w] = hf[bi];
+        }
+        (s == EST_OVERFLOW_REC ? deferred : ok).push_back(bi);
+      }
+      // traces of this window: exact sizes, bottom-up (even windows) or
+      // top-down (odd) in the store, clear of the window before
+      uint64_t t = 0;
+      for (int bi : ok) t += tw[(size_t)bi * nwin + w];
+      if (tr_lo + t > tr_hi) {  // two windows of traces do not fit: smaller windows, the E-step again
+        win_scale *= 0.6;
+        if (debug_mem) fprintf(stderr, "[hmc] windowed E-step: traces of two windows exceed the store; windows x0.6, restart\n");
+        return ESTEP_RESTART;
+      }
+      std::fill(tbv.begin(), tbv.end(), 0ull);
+      for (int bi : ok) {
+        const uint64_t need = tw[(size_t)bi * nwin + w];
+        if (w % 2 == 0) {
+          tbv[bi] = tr_lo;
+          tr_lo += need;
+        } else {
+          tr_hi -= need;
+          tbv[bi] = tr_hi;
+        }
+      }
+      if (!ok.empty() && (rc = values(w, ok.data(), (int)ok.size()))) return rc;
+      for (int bi : ok) {
+        const int s2 = h_status[bi];
+        if (s2 == EST_NEEDS_EXACT) underflow.push_back(bi);
+        if (s2 != EST_OK) dead.push_back(bi);
+      }
+      if (!first && deferred.size() == todo.size())
+        return fail(HMC_ENOMEM, "windowed E-step: one individual's records of window %d exceed the record store", w);
+      todo.swap(deferred);
+      first = false;
+    }
+    if (!dead.empty()) {  // out of the later windows and the collections
+      std::vector<char> gone(n, 0);
+      for (int bi : dead) gone[bi] = 1;
+      std::vector<int32_t> keep;
+      for (int bi : grp)
+        if (!gone[bi]) keep.push_back(bi);
+      grp.swap(keep);
+    }
+    return HMC_OK;
+  };
+
+  // Collection of window w - 1 (the survivors of every list entry at the end
+  // of window w) over `grp`; a node store that fills up grows and the
+  // individuals that did not fit run again.
+  auto collect = [&](int w, std::vector<int32_t> &grp) -> int {
+    const int lo0 = bound[w - 1], mid = bound[w], hi1 = bound[w + 1];
+    uint64_t mwords = 0;
+    int fb = 1;
+    for (int bi : grp) {
+      mwords = std::max<uint64_t>(mwords, (tw[(size_t)bi * nwin + w - 1] + tw[(size_t)bi * nwin + w]) / 32);
+      fb = std::max(fb, std::max(fw[(size_t)bi * nwin + w - 1], fw[(size_t)bi * nwin + w]));
+    }
+    const int max_words = (int)(((uint64_t)fb * S + 31) / 32) + 1;
+    const size_t stride = (size_t)(hi1 - lo0 + 1) + 2 * (size_t)(max_words + 1) + mwords + (size_t)(hi1 - lo0) + 64;
+    std::vector<int32_t> todo(grp);
+    while (!todo.empty()) {
+      const int grid = std::max(1, std::min((int)todo.size(), dev_cu * 4));
+      hipError_t e2;
+      int rc2;
+      if ((e2 = d_gc_scr.ensure(stride * grid)) || (e2 = hipMemsetAsync(d_nextq.p, 0, 4, st))) return hipfail(e2, "trace collection");
+      if ((rc2 = upload_order(d_order, todo.data(), (int)todo.size()))) return rc2;
+      TraceGcArgs g;
+      g.L = L;
+      g.S = S;
+      g.head_len = hl;
+      g.order = d_order.p;
+      g.n_order = (int)todo.size();
+      g.next_q = d_nextq.p;
+      g.trace = d_trace.p;
+      g.loc_off = d_loc_off.p;
+      g.lo0 = lo0;
+      g.mid = mid;
+      g.hi1 = hi1;
+      g.scratch = d_gc_scr.p;
+      g.scratch_stride = stride;
+      g.max_words = max_words;
+      g.nodes = d_nodes.p;
+      g.node_cap = d_nodes.n / 3;
+      g.node_cursor = d_node_cursor.p;
+      g.bnd_off = d_bnd_off.p;
+      g.bnd_n = d_bnd_n.p;
+      g.status = d_status.p;
+      hipEventRecord(ev[0], st);
+      if ((e2 = launch_estep_trace_gc(g, grid, st))) return hipfail(e2, "estep_trace_gc launch");
+      hipEventRecord(ev[1], st);
+      if ((rc2 = read_status({}, 0, false))) return rc2;
+      hipEventElapsedTime(&ms, ev[0], ev[1]);
+      ms_ck += ms;
+      ms_s2 += ms;
+      std::vector<int32_t> again;
+      for (int bi : todo) {
+        if (h_status[bi] == EST_GC_MISS) return fail(HMC_EHIP, "trace collection: a survivor's predecessor is missing (individual %d)", i0 + bi);
+        if (h_status[bi] == EST_OVERFLOW_NODES) again.push_back(bi);
+      }
+      if (debug_mem)
+        fprintf(stderr, "[hmc] window %d/%d: collected window %d for %zu individuals, %.1f ms%s\n", w + 1, nwin, w,
+                todo.size(), ms, again.empty() ? "" : " (node store full: grows)");
+      if (!again.empty()) {  // grow the node store (contents kept) and run those again
+        unsigned long long used = 0;
+        if ((e2 = hipMemcpyAsync(&used, d_node_cursor.p, 8, hipMemcpyDeviceToHost, st)) || (e2 = hipStreamSynchronize(st)))
+          return hipfail(e2, "trace collection");
+        used = std::min<unsigned long long>(used, d_nodes.n / 3);
+        if ((e2 = hipMemcpyAsync(d_node_cursor.p, &used, 8, hipMemcpyHostToDevice, st)) ||
+            (e2 = d_nodes.grow_keep(d_nodes.n * 2, used * 3, st)))
+          return hipfail(e2, "trace survivor nodes");
+        for (int bi : again) h_status[bi] = EST_OK;
+        if ((e2 = hipMemcpyAsync(d_status.p, h_status.data(), (size_t)n * 4, hipMemcpyHostToDevice, st))) return hipfail(e2, "trace collection");
+      }
+      todo.swap(again);
+    }
+    return HMC_OK;
+  };
+
+  std::vector<unsigned long long> rec_all(n, 0);
+  for (int g = 0; g < ngroups; ++g) {
+    std::vector<int32_t> grp(order.begin() + (std::ptrdiff_t)g * k, order.begin() + std::min<size_t>(order.size(), (size_t)(g + 1) * k));
+    const unsigned long long node0 = 0;
+    if ((e = hipMemcpyAsync(d_node_cursor.p, &node0, 8, hipMemcpyHostToDevice, st))) return hipfail(e, "windowed E-step");
+    if (nwin >= 3 && d_nodes.n == 0 && (e = d_nodes.ensure(std::max<size_t>(3 << 20, (size_t)3 * grp.size() * NR * 16))))
+      return hipfail(e, "trace survivor nodes");
+    {  // the record store (one window, bump-allocated) and the trace store (two windows)
+      double tsum = 0;
+      for (int bi : grp) (void)bi;
+      tsum = 2.0 * (double)grp.size() * WL * tmean * 1.35 + 4.0 * (1 << 20);
+      if ((rc = ensure_store(d_rec, (uint64_t)std::min<double>((double)rbud, (double)grp.size() * WL * rmean * 1.3 + (1 << 22)), rbud,
+                             "record store")) ||
+          (rc = ensure_store(d_trace, (uint64_t)std::min<double>((double)tbud, tsum), tbud, "trace store")))
+        return rc;
+    }
+    tr_lo = 0;
+    tr_hi = d_trace.n;
+    for (int w = 0; w < nwin; ++w) {
+      if ((rc = window(w, grp))) return rc;
+      if (w >= 1 && w < nwin - 1 && (rc = collect(w, grp))) return rc;
+    }
+    // the traceback: the last two windows' traces, then the survivors' chains
+    if (!grp.empty()) {
       TracebackArgs t;
       t.L = L;
       t.S = S;
       t.head_len = hl;
-      t.nbatch = k_;
+      t.nbatch = (int)grp.size();
+      if ((rc = upload_order(d_order2, grp.data(), (int)grp.size()))) return rc;
       t.order = d_order2.p;
       t.indiv_begin = i0;
       t.mod = dev_model();
@@ -309,112 +491,17 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
       t.sample_base = d_sbase.p;
       t.rows = d_rows.p;
       t.w_out = d_wslot.p;
-      t.win_lo = bound[w];
-      t.win_hi = bound[w + 1];
-      t.cur_state = d_cur_state.p;
-      t.cur_idx = d_cur_idx.p;
-      t.cur_swap = d_cur_swap.p;
+      t.full_lo = nwin >= 3 ? bound[nwin - 2] : 0;
+      t.nodes = d_nodes.p;
+      t.bnd_off = d_bnd_off.p;
+      t.bnd_n = d_bnd_n.p;
       hipEventRecord(ev[2], st);
-      if ((e2 = launch_traceback(t, 0, st))) return hipfail(e2, "traceback");
+      if ((e = launch_traceback(t, 0, st))) return hipfail(e, "traceback");
       hipEventRecord(ev[3], st);
-      if ((e2 = hipStreamSynchronize(st))) return hipfail(e2, "traceback");
+      if ((e = hipStreamSynchronize(st))) return hipfail(e, "traceback");
       hipEventElapsedTime(&ms, ev[2], ev[3]);
       ms_tb += ms;
     }
-    return HMC_OK;
-  };
-
-  // One window over the group `grp` (forward or recompute): structure pass,
-  // then value passes (and tracebacks) in sub-groups whose traces fit; an
-  // individual whose window records overflowed its share runs again with its
-  // exact size.  Individuals that die (no resolution) or underflow leave `grp`.
-  auto window = [&](int w, std::vector<int32_t> &grp, bool fwd, bool tb) -> int {
-    std::vector<int32_t> todo(grp), dead;
-    bool first = true;
-    while (!todo.empty()) {
-      std::fill(rb.begin(), rb.end(), 0ull);
-      std::fill(rs.begin(), rs.end(), 0ull);
-      int np = 0;
-      uint64_t r = 0;
-      if (fwd && first) {  // an even share each
-        const uint64_t share = std::max<uint64_t>(2, (rbud / (uint64_t)todo.size()) & ~1ull);
-        for (int bi : todo) {
-          rb[bi] = r;
-          rs[bi] = share;
-          r += share;
-        }
-        np = (int)todo.size();
-      } else {  // exact sizes: the prefix that fits
-        for (int bi : todo) {
-          const uint64_t need = std::max<uint64_t>(rw[(size_t)bi * nwin + w], 2);
-          if (np > 0 && r + need > rbud) break;
-          rb[bi] = r;
-          rs[bi] = need;
-          r += need;
-          ++np;
-        }
-      }
-      if ((rc = ensure_store(d_rec, r, std::max<uint64_t>(rbud, r), "record store"))) return rc;
-      if ((rc = structure(w, todo.data(), np, fwd && first, fwd && first ? 1 : 2, fwd))) return rc;
-      std::vector<int32_t> ok, deferred;
-      for (int q = 0; q < np; ++q) {
-        const int bi = todo[q], s = h_status[bi];
-        if ((rc = restart_status(s))) return rc;
-        if (s == EST_OVERFLOW_CKPT) return fail(HMC_ENOMEM, "checkpoint store too small (window %d)", w);
-        if (!fwd && s == EST_OVERFLOW_REC) return fail(HMC_EHIP, "record store overflow with exact sizes (window %d)", w);
-        if (fwd && first) {
-          rw[(size_t)bi * nwin + w] = hr[bi];
-          tw[(size_t)bi * nwin + w] = ht[bi];
-          fw[(size_t)bi * nwin + w] = hf[bi];
-        }
-        (s == EST_OVERFLOW_REC ? deferred : ok).push_back(bi);
-      }
-      for (int q = np; q < (int)todo.size(); ++q) deferred.push_back(todo[q]);
-      // value passes in sub-groups whose traces fit the budget
-      size_t pos = 0;
-      while (pos < ok.size()) {
-        uint64_t t = 0;
-        size_t kk = 0;
-        std::fill(tbv.begin(), tbv.end(), 0ull);
-        while (pos + kk < ok.size()) {
-          const int bi = ok[pos + kk];
-          const uint64_t need = tw[(size_t)bi * nwin + w];
-          if (kk > 0 && t + need > tbud) break;
-          tbv[bi] = t;
-          t += need;
-          ++kk;
-        }
-        if ((rc = ensure_store(d_trace, std::max<uint64_t>(t, 1), std::max<uint64_t>(tbud, t), "trace store"))) return rc;
-        if ((rc = values(w, ok.data() + pos, (int)kk, fwd, tb, fwd))) return rc;
-        for (size_t q = 0; q < kk; ++q) {
-          const int bi = ok[pos + q], s = h_status[bi];
-          if (s == EST_NEEDS_EXACT) underflow.push_back(bi);
-          if (s != EST_OK) dead.push_back(bi);
-        }
-        pos += kk;
-      }
-      todo.swap(deferred);
-      first = false;
-    }
-    if (!dead.empty()) {  // out of the later windows and the recompute
-      std::vector<char> gone(n, 0);
-      for (int bi : dead) gone[bi] = 1;
-      std::vector<int32_t> keep;
-      for (int bi : grp)
-        if (!gone[bi]) keep.push_back(bi);
-      grp.swap(keep);
-    }
-    return HMC_OK;
-  };
-
-  std::vector<unsigned long long> rec_all(n, 0);
-  for (int g = 0; g < ngroups; ++g) {
-    std::vector<int32_t> grp(order.begin() + (std::ptrdiff_t)g * k, order.begin() + std::min<size_t>(order.size(), (size_t)(g + 1) * k));
-    if ((e = hipMemsetAsync(d_ck_cursor.p, 0, 8, st))) return hipfail(e, "windowed E-step");
-    for (int w = 0; w < nwin; ++w)  // forward; the last window traces back through itself
-      if ((rc = window(w, grp, true, w == nwin - 1))) return rc;
-    for (int w = nwin - 2; w >= 0; --w)  // backward: recompute and trace back
-      if ((rc = window(w, grp, false, true))) return rc;
     for (int q = g * k; q < std::min(n, (g + 1) * k); ++q) {
       const int bi = order[q];
       for (int w = 0; w < nwin; ++w) rec_all[bi] += rw[(size_t)bi * nwin + w];

@@ -798,16 +798,12 @@ __global__ __launch_bounds__(256) void estep_traceback(TracebackArgs a) {
   const size_t h0 = (size_t)a.sample_base[bi] + 2 * c;
   uint8_t *row[2] = {a.rows + h0 * L, a.rows + (h0 + 1) * L};
   const unsigned long long *lo = a.loc_off + (size_t)bi * (L + 1);
-  // locus window of trace indices [wlo, whi): from the candidates (the last
-  // window) or from the cursor the window above left
-  const int wlo = a.win_hi > 0 ? a.win_lo : a.head_len, whi = a.win_hi > 0 ? a.win_hi : L + 1;
-  const size_t cs = (size_t)bi * S_MAX + c;
-  const bool first = whi == L + 1;
-  uint32_t st = first ? a.cand_state[cs] : a.cur_state[cs];
-  uint32_t idx = first ? a.cand_idx[cs] : a.cur_idx[cs];
+  uint32_t st = a.cand_state[(size_t)bi * S_MAX + c];
+  uint32_t idx = a.cand_idx[(size_t)bi * S_MAX + c];
   int ra = 0, rb = 1;
-  if (!first && a.cur_swap[cs]) { ra = 1; rb = 0; }
-  for (int j = whi - 1; j > a.head_len && j >= wlo; --j) {
+  // trace indices still in the store: from L down to full_lo (windowed E-step), else to the head
+  const int jstop = a.full_lo > a.head_len ? a.full_lo : a.head_len + 1;
+  for (int j = L; j >= jstop; --j) {
     const uint32_t *r = a.trace + lo[j];
     const uint32_t F = r[0];
     const uint32_t hdr = r[1 + st];
@@ -818,13 +814,29 @@ __global__ __launch_bounds__(256) void estep_traceback(TracebackArgs a) {
     st = meta_pred(m);
     idx = meta_idx(m);
   }
-  if (wlo > a.head_len) {  // the window below continues from here
-    a.cur_state[cs] = st;
-    a.cur_idx[cs] = idx;
-    a.cur_swap[cs] = (uint8_t)ra;
-    return;
+  uint32_t hdr;  // the head pair's alleles at locus head_len - 1
+  if (a.full_lo > a.head_len) {  // the survivor nodes below full_lo: the boundary list, then the chain
+    const unsigned long long ob = a.bnd_off[bi];
+    const uint32_t on = a.bnd_n[bi], key = st << 8 | idx;
+    uint32_t l0 = 0, l1 = on;
+    while (l0 < l1) {
+      const uint32_t md = (l0 + l1) >> 1;
+      if (a.nodes[3 * (ob + md)] < key) l0 = md + 1;
+      else l1 = md;
+    }
+    unsigned long long nd = ob + l0;  // (present: the collection kept every entry reachable from the candidates' locus)
+    for (int j = a.full_lo - 1; j > a.head_len; --j) {
+      const uint32_t *x = a.nodes + 3 * nd;
+      row[ra][j - 1] = (uint8_t)(x[1] & 0xFF);
+      row[rb][j - 1] = (uint8_t)((x[1] >> 8) & 0xFF);
+      if ((x[1] >> 16) & 1u) { int t = ra; ra = rb; rb = t; }
+      nd = x[2];
+    }
+    st = a.nodes[3 * nd] >> 8;  // the head pair (HaploPair.cpp:112-120)
+    hdr = a.nodes[3 * nd + 1];
+  } else {
+    hdr = a.trace[lo[a.head_len] + 1 + st];
   }
-  const uint32_t hdr = a.trace[lo[a.head_len] + 1 + st];
   row[ra][a.head_len - 1] = (uint8_t)(hdr & 0xFF);
   row[rb][a.head_len - 1] = (uint8_t)((hdr >> 8) & 0xFF);
   if (a.head_len > 1) {  // the head pair's patterns cover loci 0..head_len-1 (HaploPair.cpp:112-120)

@@ -1854,6 +1854,171 @@ size_t estep_s1v2_lds_bytes(int, int, int, int, int) { return 0; }
 hipError_t launch_estep_structure2(const StructArgs &, int, int, hipStream_t) { return hipErrorNotSupported; }
 #endif
 
+
+// ---- trace garbage collection (windowed E-step, TraceGcArgs) ----------------
+// HaploPair::getGenotype (HaploPair.cpp:91-124) only ever follows links from
+// the final candidates, and the k-best lists' links coalesce fast: on cfg 2's
+// E1 the ~1 000-2 300 list entries of the last locus reach ~10 entries 50 loci
+// back.  A block per individual marks, in one bitmap per locus (F x S bits),
+// the entries of [lo0, hi1) reachable from every entry at hi1 - 1, then writes
+// the marked entries of [lo0, mid) as nodes (ascending key per locus; the
+// predecessor's node by a prefix popcount of the locus below, or by a binary
+// search of the boundary list of the window before).
+__global__ __launch_bounds__(256) void estep_trace_gc(TraceGcArgs a) {
+  __shared__ unsigned long long red64[16];  // Blk<4>: 2 x 4 + 8 ints, then 4 u64 (8-byte aligned)
+  __shared__ int sq;
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;
+  const Blk<4> B{(int *)red64, tid, lane, wv};
+  const int S = a.S, L = a.L, hl = a.head_len;
+  const int nloc = a.hi1 - a.lo0;
+  uint32_t *moff = a.scratch + (size_t)blockIdx.x * a.scratch_stride;  // [nloc + 1]
+  uint32_t *preA = moff + nloc + 1, *preB = preA + a.max_words + 1;
+  uint32_t *M = preB + a.max_words + 1;
+  for (int q = blockIdx.x; q < a.n_order;) {
+    const int bi = a.order[q];
+    const unsigned long long *lo = a.loc_off + (size_t)bi * (L + 1);
+    auto words_at = [&](int j) -> uint32_t { return (a.trace[lo[j]] * (uint32_t)S + 31u) >> 5; };
+    // ---- bitmap offsets per locus
+    uint32_t acc = 0;
+    for (int c0 = 0; c0 < nloc; c0 += 256) {
+      const int c = c0 + tid;
+      const int w = c < nloc ? (int)words_at(a.lo0 + c) : 0;
+      int tot = 0;
+      const int ex = B.scan(w, &tot);
+      if (c < nloc) moff[c] = acc + (uint32_t)ex;
+      acc += (uint32_t)tot;
+    }
+    B.sync();
+    for (uint32_t w = tid; w < acc; w += 256) M[w] = 0u;
+    B.sync();
+    // ---- every list entry of the last locus, then backward along the links
+    {
+      const int j = a.hi1 - 1;
+      const uint32_t F = a.trace[lo[j]];
+      const uint32_t *hdr = a.trace + lo[j] + 1;
+      uint32_t *Mj = M + moff[j - a.lo0];
+      for (uint32_t t = tid; t < F; t += 256) {
+        const uint32_t n = (hdr[t] >> 16) & 0xFFu;
+        for (uint32_t k = 0; k < n; ++k) {
+          const uint32_t bit = t * (uint32_t)S + k;
+          atomicOr(Mj + (bit >> 5), 1u << (bit & 31u));
+        }
+      }
+    }
+    B.sync();
+    for (int j = a.hi1 - 1; j > a.lo0; --j) {
+      const uint32_t F = a.trace[lo[j]];
+      const uint32_t *links = a.trace + trace_links(lo[j], F);
+      const uint32_t *Mj = M + moff[j - a.lo0];
+      uint32_t *Mp = M + moff[j - 1 - a.lo0];
+      const uint32_t nw = (F * (uint32_t)S + 31u) >> 5;
+      for (uint32_t w = tid; w < nw; w += 256)
+        for (uint32_t b = Mj[w]; b; b &= b - 1u) {
+          const uint32_t bit = w * 32u + (uint32_t)__builtin_ctz(b);
+          const uint32_t m = links[bit];
+          if (meta_head(m)) continue;
+          const uint32_t pb = meta_pred(m) * (uint32_t)S + meta_idx(m);
+          atomicOr(Mp + (pb >> 5), 1u << (pb & 31u));
+        }
+      B.sync();
+    }
+    // ---- the survivors of [lo0, mid) as nodes
+    unsigned long long cnt = 0;
+    for (uint32_t w = tid; w < moff[a.mid - a.lo0]; w += 256) cnt += (unsigned long long)__popc(M[w]);
+    const unsigned long long total = B.reduce_u64(cnt);
+    unsigned long long base = 0;
+    if (tid == 0) {
+      base = atomicAdd(a.node_cursor, total);
+      if (base + total > a.node_cap) base = ~0ull;
+    }
+    base = B.bcast64(base);
+    if (base == ~0ull) {
+      if (tid == 0) a.status[bi] = EST_OVERFLOW_NODES;
+    } else {
+      const unsigned long long ob = a.bnd_off[bi];
+      const uint32_t on = a.lo0 > hl ? a.bnd_n[bi] : 0u;
+      unsigned long long nb = base, nb_prev = base;
+      uint32_t cnt_last = 0;
+      int miss = 0;
+      uint32_t *Pc = preA, *Pp = preB;
+      for (int j = a.lo0; j < a.mid; ++j) {
+        const uint32_t F = a.trace[lo[j]];
+        const uint32_t *hdr = a.trace + lo[j] + 1;
+        const uint32_t *links = a.trace + trace_links(lo[j], F);
+        const uint32_t *Mj = M + moff[j - a.lo0];
+        const uint32_t nw = (F * (uint32_t)S + 31u) >> 5;
+        uint32_t acc2 = 0;
+        for (uint32_t c0 = 0; c0 < nw; c0 += 256) {
+          const uint32_t w = c0 + tid;
+          const int v = w < nw ? __popc(Mj[w]) : 0;
+          int tot = 0;
+          const int ex = B.scan(v, &tot);
+          if (w < nw) Pc[w] = acc2 + (uint32_t)ex;
+          acc2 += (uint32_t)tot;
+        }
+        B.sync();
+        const uint32_t *Mp = j > a.lo0 ? M + moff[j - 1 - a.lo0] : nullptr;
+        for (uint32_t w = tid; w < nw; w += 256) {
+          unsigned long long r = nb + Pc[w];
+          for (uint32_t b = Mj[w]; b; b &= b - 1u) {
+            const uint32_t bit = w * 32u + (uint32_t)__builtin_ctz(b);
+            const uint32_t t = bit / (uint32_t)S, k = bit - t * (uint32_t)S;
+            const uint32_t m = links[bit];
+            uint32_t pred = NONE;
+            if (!meta_head(m) && j > hl) {
+              const uint32_t pt = meta_pred(m), pk = meta_idx(m);
+              if (j > a.lo0) {
+                const uint32_t pb = pt * (uint32_t)S + pk;
+                pred = (uint32_t)(nb_prev + Pp[pb >> 5] + (uint32_t)__popc(Mp[pb >> 5] & ((1u << (pb & 31u)) - 1u)));
+              } else {  // the window before: its boundary list, ascending keys
+                const uint32_t key = pt << 8 | pk;
+                uint32_t l0 = 0, l1 = on;
+                while (l0 < l1) {
+                  const uint32_t md = (l0 + l1) >> 1;
+                  if (a.nodes[3 * (ob + md)] < key) l0 = md + 1;
+                  else l1 = md;
+                }
+                if (l0 < on && a.nodes[3 * (ob + l0)] == key) pred = (uint32_t)(ob + l0);
+                else miss = 1;
+              }
+            }
+            uint32_t *nd = a.nodes + 3 * r;
+            nd[0] = t << 8 | k;
+            nd[1] = (hdr[t] & 0xFFFFu) | (meta_rev(m) ? 1u << 16 : 0u);
+            nd[2] = pred;
+            ++r;
+          }
+        }
+        nb_prev = nb;
+        nb += acc2;
+        cnt_last = acc2;
+        uint32_t *const tp_ = Pc;
+        Pc = Pp;
+        Pp = tp_;
+        B.sync();
+      }
+      miss = B.reduce_u64((unsigned long long)miss) != 0;
+      if (tid == 0) {
+        a.bnd_off[bi] = nb_prev;
+        a.bnd_n[bi] = cnt_last;
+        if (miss) a.status[bi] = EST_GC_MISS;
+      }
+    }
+    B.sync();
+    if (tid == 0) sq = atomicAdd(a.next_q, 1) + (int)gridDim.x;
+    B.sync();
+    q = sq;
+  }
+}
+
+hipError_t launch_estep_trace_gc(const TraceGcArgs &a, int grid, hipStream_t st) {
+  if (a.n_order <= 0) return hipSuccess;
+  if (a.S < 1 || a.S > S_MAX || a.lo0 < a.head_len || a.mid <= a.lo0 || a.hi1 <= a.mid || a.hi1 > a.L + 1 || grid < 1)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(estep_trace_gc, dim3(grid), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_estep_structure(const StructArgs &a, int grid, int nw, hipStream_t st) {
   if (a.S < 1 || a.S > S_MAX || a.pan.amax > A_MAX || a.fcap > F_MAX || (a.hcap & (a.hcap - 1)) || a.lds_hc < 1 ||
       (a.lds_hc & (a.lds_hc - 1)) || a.lds_fc < 0 || a.lds_cc < 0 || a.ccap < 1 || a.mod.head_len < 1 ||

@@ -498,6 +498,263 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
   }
 }
 
+
+// ---- breadth-first walk ----------------------------------------------------
+// The depth-first walk above spends a wavefront and a dozen dependent,
+// barriered steps on every trie node, while a node's lists hold a handful of
+// non-zero states (300 x 200 panel, restatement counts: 14.9 M live nodes, 5.0
+// non-zero entries each).  Here a lane takes a whole node (a work unit,
+// XWalkArgs): it scatters the node's entries along their forward links
+// (HaploBuilder.cpp:369-427 scatters the same way) into private accumulators —
+// per reached state the lists of its a-allele child and of its b-allele child —
+// then adds every child's frequency (states ascending) and prefix term
+// (:437-441) and emits the children with non-zero lists that have children of
+// their own.  The host runs the levels depth by depth over batches of items;
+// a wave reserves its outputs with one atomic pair, and units whose outputs do
+// not fit are deferred and re-run once the deeper levels are done.
+__device__ inline unsigned long long wave_excl_u64(unsigned long long v, unsigned long long &total) {
+  const int lane = (int)(threadIdx.x & 63);
+  unsigned long long incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  total = __shfl(incl, 63);
+  return incl - v;
+}
+
+__global__ __launch_bounds__(256) void exact_walk_units(ExactArgs a, XWalkArgs x) {
+  const int gtid = blockIdx.x * blockDim.x + threadIdx.x, nthr = gridDim.x * blockDim.x;
+  const int lane = (int)(threadIdx.x & 63);
+  const int L = a.L, hl = a.head_len, W = a.width, fmax = a.fmax;
+  double *acc = x.lacc + (size_t)gtid * x.lacc_stride;  // [a side | b side][3][fmax]
+  uint32_t *bits = x.lbits + (size_t)gtid * x.lbits_stride;
+  const double *ew0 = x.e_w, *ew1 = x.e_w + x.e_cap, *ew2 = x.e_w + 2 * x.e_cap;
+  double *ow0 = x.e_w, *ow1 = x.e_w + x.e_cap, *ow2 = x.e_w + 2 * x.e_cap;
+  const int rounds = (x.n_in + nthr - 1) / nthr;  // wave-uniform: every lane joins its wave's reservation
+  for (int it = 0; it < rounds; ++it) {
+    const int j = it * nthr + gtid;
+    bool live = j < x.n_in;
+    unsigned long long u = 0;
+    int q = 0, start = 0, node = -1, bi = 0;
+    double pg = 0.0, pfreq = 1.0;
+    if (live) {
+      if (x.roots) {  // item j of the batch: its start locus's trie root, every state with its forward likelihood
+        const long long item = (long long)x.in_base + (x.idx ? x.idx[j] : j);
+        q = (int)(item / L);
+        start = (int)(item % L);
+        node = a.tr_root[start];
+      } else {
+        u = x.idx ? (unsigned long long)x.idx[j] : x.in_base + (unsigned long long)j;
+        node = x.u.node[u];
+        if (node >= 0) {
+          q = x.u.q[u];
+          start = x.u.start[u];
+          pfreq = x.u.freq[u];
+        }
+      }
+      live = node >= 0;
+    }
+    if (live) {
+      bi = a.order[q];
+      const int s0 = a.status[bi];
+      pg = a.gprob[bi];  // P(genotype) of the last E-step (HaploModel.cpp:109, HaploBuilder.cpp:294)
+      live = (s0 == EST_OK || s0 == EST_OK_PRUNED) && pg > 0.0;
+    }
+    unsigned long long cm = 0ull;  // alleles with a child
+    if (live)
+      for (int i = 0; i < W; ++i) cm |= (a.tr_child[(size_t)node * W + i] >= 0 ? 1ull : 0ull) << i;
+    live = live && cm != 0ull;
+    const int locus = start + x.depth;  // the children's allele is at this locus
+    const bool head = locus < hl;       // head pairs: their patterns' alleles, same states (HaploBuilder.cpp:340-367)
+    int FT = 0;
+    const double *bw = nullptr;
+    const uint32_t *thdr = nullptr, *plo = nullptr, *phi = nullptr;
+    // the children's two alleles of state t (a side, b side)
+    auto alleles = [&](uint32_t t, uint32_t &xa, uint32_t &xb) {
+      if (!head || hl == 1) {
+        xa = thdr[t] & 0xFFu;
+        xb = (thdr[t] >> 8) & 0xFFu;
+      } else {
+        xa = a.head_al[(size_t)plo[t] * hl + locus];
+        xb = a.head_al[(size_t)phi[t] * hl + locus];
+      }
+    };
+    if (live) {
+      const unsigned long long *roff = a.rec_off + (size_t)bi * (L + 1);
+      const unsigned long long *xo = a.x_off + (size_t)bi * (L + 1);
+      const int tix = head ? hl : locus + 1, pix = head ? hl : locus;  // the children's / the node's states
+      const RecView R(a.rec + roff[tix], head);
+      FT = R.F;
+      thdr = R.hdr;
+      if (head) {
+        plo = R.cb + FT + 1;
+        phi = plo + FT;
+      }
+      bw = (const double *)(a.x + xo[tix]) + FT;
+      const int FP = (int)a.rec[roff[pix]];
+      const double *fwp = (const double *)(a.x + xo[pix]);
+      const unsigned long long e0 = x.roots ? 0ull : x.u.e0[u];
+      const int ne = x.roots ? FP : (int)x.u.ne[u];
+      for (int k = 0; k < ne; ++k) {
+        const uint32_t s = x.roots ? (uint32_t)k : x.e_t[e0 + k];
+        const double w0 = x.roots ? fwp[s] : ew0[e0 + k];
+        const double w1 = x.roots ? 0.0 : ew1[e0 + k], w2 = x.roots ? 0.0 : ew2[e0 + k];
+        if (w0 == 0.0 && w1 == 0.0 && w2 == 0.0) continue;
+        if (head) {
+          uint32_t xa, xb;
+          alleles(s, xa, xb);
+          const bool ca = (cm >> xa) & 1ull, cb = xb != xa && ((cm >> xb) & 1ull);
+          if (!ca && !cb) continue;
+          bits[s >> 5] |= 1u << (s & 31u);
+          if (ca) {  // child xa: both sides when xb == xa, else the a side
+            double *A = acc + s;
+            if (xb == xa) {
+              A[0] = w0;
+              A[fmax] = w1;
+              A[2 * fmax] = w2;
+            } else {
+              A[fmax] = w0 * 0.5 + w1;
+            }
+          }
+          if (cb) acc[3 * (size_t)fmax + 2 * (size_t)fmax + s] = w0 * 0.5 + w2;  // child xb: the b side
+          continue;
+        }
+        uint32_t off = 0;
+        for (int p = 0; p < R.NP; ++p) {  // m_forward_links of the pair, in push order
+          const uint32_t no = R.npo[p];
+          for (uint32_t o = 0; o < no; ++o) {
+            const uint32_t w = R.out[off + s * no + o];
+            if (w == NONE) continue;
+            const uint32_t t = cw_state(w);
+            const bool rev = cw_rev(w);
+            uint32_t xa, xb;
+            alleles(t, xa, xb);
+            const bool ca = (cm >> xa) & 1ull, cb = xb != xa && ((cm >> xb) & 1ull);
+            if (!ca && !cb) continue;
+            bits[t >> 5] |= 1u << (t & 31u);
+            const double tp = R.tpv[t];
+            if (ca) {
+              double *A = acc + t;
+              walk_terms(true, xb == xa, rev, w0, w1, w2, tp, A[0], A[fmax], A[2 * fmax]);
+            }
+            if (cb) {
+              double *B = acc + 3 * (size_t)fmax + t;
+              walk_terms(false, true, rev, w0, w1, w2, tp, B[0], B[fmax], B[2 * fmax]);
+            }
+          }
+          off += (uint32_t)FP * no;
+        }
+      }
+    }
+    const int nwT = (FT + 31) >> 5;
+    // child i's lists at state t: the a-side accumulators when t's a allele is i, else the b side's
+    auto side = [&](uint32_t t, uint32_t i) -> const double * {
+      uint32_t xa, xb;
+      alleles(t, xa, xb);
+      return xa == i ? acc + t : (xb == i ? acc + 3 * (size_t)fmax + t : nullptr);
+    };
+    auto has_children = [&](int c) {
+      bool g = false;
+      for (int i = 0; i < W; ++i) g = g || a.tr_child[(size_t)c * W + i] >= 0;
+      return g;
+    };
+    // pass 1: the children this node emits and their entries
+    unsigned long long nu = 0, nent = 0;
+    if (live)
+      for (unsigned long long m = cm; m; m &= m - 1) {
+        const uint32_t i = (uint32_t)__builtin_ctzll(m);
+        const int child = a.tr_child[(size_t)node * W + i];
+        if (!has_children(child)) continue;
+        unsigned long long cnt = 0;
+        for (int w = 0; w < nwT; ++w)
+          for (uint32_t b = bits[w]; b; b &= b - 1u) {
+            const uint32_t t = (uint32_t)w * 32u + (uint32_t)__builtin_ctz(b);
+            const double *n = side(t, i);
+            if (n && (n[0] != 0.0 || n[fmax] != 0.0 || n[2 * fmax] != 0.0)) ++cnt;
+          }
+        if (cnt) {
+          ++nu;
+          nent += cnt;
+        }
+      }
+    // one reservation per wave
+    unsigned long long tu = 0, te = 0;
+    const unsigned long long xu = wave_excl_u64(nu, tu), xe = wave_excl_u64(nent, te);
+    unsigned long long bu = 0, be = 0;
+    if (lane == 0 && (tu | te)) {
+      bu = atomicAdd(x.cursor, tu);
+      be = atomicAdd(x.cursor + 1, te);
+    }
+    bu = __shfl(bu, 0) + xu;
+    be = __shfl(be, 0) + xe;
+    const bool ok = live && bu + nu <= x.u_cap && be + nent <= x.e_cap;
+    if (live && !ok) {  // re-run later: nothing of this node is added now
+      const int d = atomicAdd(x.n_defer, 1);
+      x.defer[d] = x.roots ? (x.idx ? x.idx[j] : (int32_t)j) : (int32_t)u;
+      for (unsigned long long k = bu; k < bu + nu && k < x.u_cap; ++k) x.u.node[k] = -1;  // holes
+    }
+    // pass 2: frequencies (hp->setFrequency, setPrefixFreq, HaploBuilder.cpp:437-441) and the emitted children
+    if (ok)
+      for (unsigned long long m = cm; m; m &= m - 1) {
+        const uint32_t i = (uint32_t)__builtin_ctzll(m);
+        const int child = a.tr_child[(size_t)node * W + i];
+        const bool gk = has_children(child);
+        double f = 0.0;
+        unsigned long long cnt = 0;
+        for (int w = 0; w < nwT; ++w)
+          for (uint32_t b = bits[w]; b; b &= b - 1u) {
+            const uint32_t t = (uint32_t)w * 32u + (uint32_t)__builtin_ctz(b);
+            const double *n = side(t, i);
+            if (!n) continue;
+            const double n0 = n[0], n1 = n[fmax], n2 = n[2 * fmax];
+            if (n0 == 0.0 && n1 == 0.0 && n2 == 0.0) continue;
+            f += ((n0 + n1) + n2) * bw[t];
+            if (gk) {
+              x.e_t[be + cnt] = t;
+              ow0[be + cnt] = n0;
+              ow1[be + cnt] = n1;
+              ow2[be + cnt] = n2;
+            }
+            ++cnt;
+          }
+        const double freq = f / pg;
+        const int pat = a.tr_data[child];
+        if (pat >= 0) {
+          atomicAdd(&a.acc_freq[pat], (unsigned long long)__double2ll_rn(freq * EXACT_FIXED_SCALE));
+          atomicAdd(&a.acc_prefix[pat], (unsigned long long)__double2ll_rn(pfreq * EXACT_FIXED_SCALE));
+        }
+        if (gk && cnt) {
+          x.u.q[bu] = q;
+          x.u.start[bu] = start;
+          x.u.node[bu] = child;
+          x.u.freq[bu] = freq;
+          x.u.e0[bu] = be;
+          x.u.ne[bu] = (uint32_t)cnt;
+          ++bu;
+          be += cnt;
+        }
+      }
+    // the accumulators and the bitmap back to zero
+    if (live)
+      for (int w = 0; w < nwT; ++w) {
+        for (uint32_t b = bits[w]; b; b &= b - 1u) {
+          const uint32_t t = (uint32_t)w * 32u + (uint32_t)__builtin_ctz(b);
+          for (int c = 0; c < 6; ++c) acc[(size_t)c * fmax + t] = 0.0;
+        }
+        bits[w] = 0u;
+      }
+  }
+}
+
+hipError_t launch_exact_walk_units(const ExactArgs &a, const XWalkArgs &x, int grid, hipStream_t st) {
+  if (x.n_in <= 0) return hipSuccess;
+  if (a.width < 1 || a.width > 64 || grid < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(exact_walk_units, dim3(grid), dim3(256), 0, st, a, x);
+  return hipGetLastError();
+}
+
 size_t exact_walk_scratch_doubles(int max_depth, int fmax, int width) {
   return (size_t)(max_depth + 1) * width * 3 * fmax + (size_t)(max_depth + 2) * width +
          ((size_t)(max_depth + 1) * fmax + 1) / 2;

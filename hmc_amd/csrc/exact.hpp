@@ -36,6 +36,39 @@ struct ExactArgs {
   long long item0 = 0, item1 = -1;  // walk items [item0, item1) of n_order x L (individual-major); -1 = all
 };
 
+// Breadth-first trie walk (exact_walk_units): one lane per work unit — a trie
+// node of one item (individual q of the group, start locus) at depth `depth`
+// with the non-zero entries of its three lists (state ascending; weights w0
+// both haplotypes match the node's pattern, w1 only the a side, w2 only the b
+// side).  A lane scatters the entries along the forward links into its
+// private accumulators, adds every child's frequency and prefix term, and
+// emits the children that have non-zero lists and children of their own as the
+// next level's units.  Roots (depth 0) carry no entries: every state after
+// max(start, head_len) loci with its forward likelihood.
+struct XUnits {
+  int32_t *q = nullptr, *start = nullptr, *node = nullptr;  // node < 0: a hole (skipped)
+  double *freq = nullptr;                                   // the node's frequency: its children's prefix term
+  unsigned long long *e0 = nullptr;                         // first entry in the pool
+  uint32_t *ne = nullptr;                                   // entries
+};
+struct XWalkArgs {
+  XUnits u;                       // the unit pool
+  uint32_t *e_t = nullptr;        // entry pool: state
+  double *e_w = nullptr;          // [3][e_cap] weights
+  unsigned long long e_cap = 0, u_cap = 0;
+  unsigned long long in_base = 0; // this level's units: [in_base, in_base + n_in), or idx[0, n_in) when idx
+  const int32_t *idx = nullptr;
+  int n_in = 0, depth = 0;
+  bool roots = false;
+  unsigned long long *cursor = nullptr;  // [2] next free unit, next free entry (outputs)
+  int32_t *defer = nullptr;       // input units whose outputs did not fit (re-run later)
+  int *n_defer = nullptr;
+  double *lacc = nullptr;         // per thread [2][3][fmax]: the a-allele and b-allele child of each state
+  uint32_t *lbits = nullptr;      // per thread reached-state bitmap [fmax / 32 + 1]
+  size_t lacc_stride = 0, lbits_stride = 0;  // doubles, words
+};
+hipError_t launch_exact_walk_units(const ExactArgs &a, const XWalkArgs &x, int grid, hipStream_t st);
+
 hipError_t launch_exact_fb(const ExactArgs &a, int grid, hipStream_t st);
 // items_per_wave 1 (64 lanes per item) or 4 (16 lanes each); scratch: grid x items x stride
 hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st, int items_per_wave = 1);

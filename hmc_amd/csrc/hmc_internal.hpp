@@ -61,6 +61,8 @@ enum EStatus : int32_t {
   EST_OVERFLOW_CONTRIB = -5,   // more contributions at a locus than the structure pass's capacity
   EST_DF_STALL = -6,           // dataflow value pass: a wait made no progress (watchdog; a bug, reported)
   EST_OVERFLOW_CKPT = -7,      // windowed E-step: the checkpoint store is full
+  EST_OVERFLOW_NODES = -8,     // windowed E-step: the trace-survivor node store is full
+  EST_GC_MISS = -9,            // windowed E-step: a survivor's predecessor is not in the boundary list (a bug)
   EST_NEEDS_EXACT = 2,         // split E-step: a forward likelihood underflowed to 0 before
                                // the last locus, so extend() would skip that pair
                                // (HaploBuilder.cpp:237) — re-run on the fused kernel
@@ -281,14 +283,44 @@ struct TracebackArgs {
   const int32_t *sample_base;  // [batch] first sample row of each individual
   uint8_t *rows;               // [H][L] sample-major haplotypes (allele index)
   double *w_out;               // [H]
-  // Locus window [win_lo, win_hi) of trace indices (checkpoint-and-recompute
-  // E-step): the walk starts from the candidates (win_hi == L + 1) or from
-  // the cursor the window above left (state, index, haplotype swap), and leaves
-  // one for the window below; classic: win_lo = head_len, win_hi = L + 1.
-  int win_lo = 0, win_hi = 0;
-  uint32_t *cur_state = nullptr, *cur_idx = nullptr;  // [batch][S_MAX]
-  uint8_t *cur_swap = nullptr;                        // [batch][S_MAX]
+  // Windowed E-step (trace garbage collection, TraceGcArgs): trace indices
+  // below full_lo are no longer in the trace store; the walk continues at
+  // index full_lo - 1 in the survivor nodes — the entry (state, list index)
+  // found by key in the individual's boundary list, then the nodes' chain.
+  // full_lo = 0: every trace index is in the store.
+  int full_lo = 0;
+  const uint32_t *nodes = nullptr;                // 3 words per node: key, alleles | rev << 16, predecessor node
+  const unsigned long long *bnd_off = nullptr;    // [batch] first node of the boundary list
+  const uint32_t *bnd_n = nullptr;                // [batch] its length
 };
+
+// Trace garbage collection of the windowed E-step (estep_trace_gc): the
+// k-best traces of loci [lo0, mid) (the older of two windows whose full traces
+// are in the store) shrink to their survivors — the list entries reachable
+// backward from any entry at the last locus of [mid, hi1).  Survivors become
+// nodes (key = state << 8 | list index, the pair's last alleles and the link's
+// reversed flag, the predecessor's node), locus by locus in key order; the
+// last locus's nodes are the individual's boundary list, through which the
+// next window's survivors and the final traceback find their predecessors.
+struct TraceGcArgs {
+  int L = 0, S = 1, head_len = 1;
+  const int32_t *order = nullptr;
+  int n_order = 0;
+  int32_t *next_q = nullptr;
+  const uint32_t *trace = nullptr;
+  const unsigned long long *loc_off = nullptr;
+  int lo0 = 0, mid = 0, hi1 = 0;
+  uint32_t *scratch = nullptr;  // per block: mark offsets, two prefix rows, the reached-entry bitmaps
+  size_t scratch_stride = 0;    // words
+  int max_words = 1;            // bitmap words of the largest locus (F x S bits)
+  uint32_t *nodes = nullptr;
+  unsigned long long node_cap = 0;       // nodes
+  unsigned long long *node_cursor = nullptr;
+  unsigned long long *bnd_off = nullptr;  // [batch]
+  uint32_t *bnd_n = nullptr;              // [batch]
+  int32_t *status = nullptr;              // EST_OVERFLOW_NODES: the node store is full (nothing changed)
+};
+hipError_t launch_estep_trace_gc(const TraceGcArgs &a, int grid, hipStream_t st);
 
 size_t estep_scratch_bytes(int fcap, int hcap, int S, int nw);
 size_t estep_lds_bytes(int S, int fc, int hc, int nw, int amax);

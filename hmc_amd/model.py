@@ -288,7 +288,9 @@ class HaploModel:
         self._check(lib().hmc_set_structure_pass(self._h, int(version)))
 
     def set_exact_walk(self, items_per_wave: int):
-        """Exact M-step walk items per wavefront (hmc_set_exact_walk): 1 or 4."""
+        """Exact M-step trie walk (hmc_set_exact_walk): 1 breadth-first lane
+        units (default); 2 / 4 the depth-first walk with one / four items per
+        wavefront (variants library)."""
         self._check(lib().hmc_set_exact_walk(self._h, int(items_per_wave)))
 
     def last_value_pass_dataflow(self) -> bool:
@@ -351,7 +353,10 @@ class HaploModel:
     def exact_stats(self) -> dict:
         r, c, ms = C.c_int(), C.c_uint64(), C.c_double()
         self._check(lib().hmc_last_exact_stats(self._h, C.byref(r), C.byref(c), C.byref(ms)))
-        return dict(rounds=r.value, candidates=c.value, walk_ms=ms.value)
+        u, la, de, pr = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int()
+        self._check(lib().hmc_last_exact_walk(self._h, C.byref(u), C.byref(la), C.byref(de), C.byref(pr)))
+        return dict(rounds=r.value, candidates=c.value, walk_ms=ms.value, walk_units=u.value, walk_launches=la.value,
+                    walk_deferred=de.value, pruned=pr.value)
 
     def head_len(self) -> int:
         """PatternManager::head_len of the current model (min pattern length)."""

@@ -103,6 +103,11 @@ int hmc_set_exact_estimate(hmc_ctx *ctx, int on);
 /* Last exact M-step: rounds of estimateFrequency, candidates estimated, and
  * device ms of the trie walks. */
 int hmc_last_exact_stats(const hmc_ctx *ctx, int *rounds, uint64_t *candidates, double *walk_ms);
+/* The last exact M-step's breadth-first walk: work units (trie nodes of an
+ * individual and start locus), kernel launches, units deferred for room, and
+ * the individuals walked over pruned records (forward likelihoods that
+ * underflow: extend()'s test, HaploBuilder.cpp:237, 291-314). */
+int hmc_last_exact_walk(const hmc_ctx *ctx, int64_t *units, int64_t *launches, int64_t *deferred, int *pruned);
 /* HaploModel::num_patterns (HMC.cpp:38): > 0 mines with
  * PatternManager::findPatternByNum (PatternManager.cpp:44-70, models MV/MA);
  * <= 0 (default) with findPatternByFreq. */

@@ -741,7 +741,10 @@ struct Model {
       for (int o = 0; o < (aeq(a1, a2) ? 1 : 2); ++o) {
         int x = o ? a2 : a1, y = o ? a1 : a2;
         const Pair &q = hp[locus][s];
-        if (q.fwd <= 0) continue;
+        if (q.fwd <= 0) {  // extend(): not extended (HaploBuilder.cpp:237); counted for the tests' panel search
+          ++n_skip;
+          continue;
+        }
         int sa = succOf(q.pa, x, P[q.pa].end);
         int sb = succOf(q.pb, y, P[q.pb].end);
         if (sa >= 0 && sb >= 0) addPair(locus, s, sa, sb, best);
@@ -903,6 +906,7 @@ struct Model {
   std::vector<Pat> *fpats = nullptr;
   double cur_gp = 1.0;
   uint64_t R_X = 0;  // trie-walk match-list entries visited (counter)
+  static thread_local uint64_t n_skip;  // pairs extend() skipped (forward likelihood 0) in this thread's resolves
 
   int fnew(int width) { fnodes.push_back(FNode{std::vector<int>(width, -1), -1}); return (int)fnodes.size() - 1; }
   // ForwardPatternTree::addPattern (PatternTree.cpp:188-212); a missing allele
@@ -1200,6 +1204,7 @@ thread_local std::vector<std::vector<double>> Model::uni;
 thread_local std::vector<std::vector<Pair>> Model::hp;
 thread_local int Model::S = 1;
 thread_local bool Model::track_links = false;
+thread_local uint64_t Model::n_skip = 0;
 
 }  // namespace ora
 
@@ -1555,6 +1560,20 @@ int ora_estimate_patterns(void *h, uint64_t *rx) {
 void ora_set_unphased(void *h, int n) { ((Model *)h)->unphased = n; }
 // HaploModel::num_patterns (HMC.cpp:38): > 0 selects findPatternByNum
 void ora_set_num_patterns(void *h, int n) { ((Model *)h)->prm.num_patterns = n; }
+// Pairs extend() skipped because their forward likelihood is 0 (HaploBuilder.cpp:237)
+// while resolving individuals [i0, i1) on this thread (diagnostic of the tests'
+// underflow panels).
+uint64_t ora_skip_count_range(void *h, int i0, int i1) {
+  Model *m = (Model *)h;
+  Model::n_skip = 0;
+  for (int i = i0; i < i1; ++i) {
+    std::vector<ora::Candidate> out;
+    std::vector<int> resol;
+    double gprob = 0.0;
+    m->resolve(i, out, resol, gprob, m->prm.sample_size);
+  }
+  return Model::n_skip;
+}
 // Tie diagnostics of the last resolveAll (see Model::tie_flags), [N].
 void ora_tie_flags(void *h, int *out) {
   Model *m = (Model *)h;

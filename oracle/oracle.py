@@ -36,6 +36,8 @@ def lib():
         L.ora_create_from_phase.restype = vp
         L.ora_create_from_phase.argtypes = [C.c_char_p]
         L.ora_destroy.argtypes = [vp]
+        L.ora_skip_count_range.restype = C.c_uint64
+        L.ora_skip_count_range.argtypes = [vp, C.c_int, C.c_int]
         L.ora_set_params.argtypes = [vp, d, i, i, i, i]
         L.ora_dims.argtypes = [vp, P(i), P(i), P(i)]
         L.ora_allele_table.argtypes = [vp, i, P(i), P(i), P(d)]
@@ -227,6 +229,12 @@ class Oracle:
     def set_num_patterns(self, n: int):
         """HaploModel::num_patterns: > 0 mines with findPatternByNum."""
         lib().ora_set_num_patterns(self.h, int(n))
+
+    def skip_counts(self) -> np.ndarray:
+        """Per individual: pairs extend() skipped because their forward
+        likelihood is 0 (HaploBuilder.cpp:237) when resolved with the current
+        model (diagnostic of the tests' underflow panels)."""
+        return np.array([lib().ora_skip_count_range(self.h, i, i + 1) for i in range(self.N)], np.uint64)
 
     def tie_flags(self) -> np.ndarray:
         """Per-individual tie diagnostics of the last E-step (Model::tie_flags)."""

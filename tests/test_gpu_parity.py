@@ -1183,12 +1183,13 @@ def test_exact_mstep_against_oracle(oracle_mod, name):
 @pytest.mark.variants
 @pytest.mark.parametrize("name", ["n60"])
 def test_exact_walk_four_items_per_wave(oracle_mod, name):
-    """hmc_set_exact_walk(4): four (individual, start locus) items per
-    wavefront, 16 lanes each — the fixed-point frequency sums are the same
-    integers, so the table equals the one-item walk's bit for bit."""
+    """hmc_set_exact_walk(4): the depth-first walk with four (individual, start
+    locus) items per wavefront, 16 lanes each — the fixed-point frequency sums
+    are the same integers, so the table equals the one-item walk's (mode 2)
+    bit for bit."""
     p = panel(name)
     tabs = []
-    for ipw in (1, 4):
+    for ipw in (2, 4):
         m = gpu_model(p)
         m.exact_estimate = True
         m.set_exact_walk(ipw)
@@ -1199,6 +1200,71 @@ def test_exact_walk_four_items_per_wave(oracle_mod, name):
         m.close()
     for k in ("start", "len", "alleles", "succ", "freq", "prefix", "tp"):
         assert np.array_equal(tabs[0][k], tabs[1][k]), k
+
+
+@pytest.mark.timeout(900)
+def test_exact_mstep_300x200_against_oracle(oracle_mod):
+    """The breadth-first walk on a 300 x 200 panel (the survey's probe size):
+    after M0 and E1, one exact M-step equals the restatement's table — same
+    patterns, order and successors, frequencies / prefix / tp within 1e-6."""
+    p = panel("n300")
+    oracle_mod.set_threads(16)
+    try:
+        o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
+        o.find_patterns()
+        o.resolve_all()
+        P_o, _ = o.estimate_patterns()
+        po = o.patterns()
+    finally:
+        oracle_mod.set_threads(1)
+    m = gpu_model(p)
+    m.exact_estimate = True
+    m.find_patterns()
+    m.resolve_all()
+    P_g, _ = m.find_patterns()
+    pg = m.patterns()
+    assert P_g == P_o
+    for k in ("start", "len", "alleles", "succ"):
+        assert np.array_equal(pg[k], po[k]), k
+    for k in ("freq", "prefix", "tp"):
+        assert _rel_close(pg[k], po[k]), (k, np.max(np.abs(pg[k] - po[k]) / np.maximum(np.abs(po[k]), 1e-300)))
+
+
+@pytest.mark.timeout(900)
+def test_exact_mstep_with_pruned_individual(oracle_mod):
+    """An individual some of whose pairs' forward likelihoods underflow to 0
+    (extend() skips them, HaploBuilder.cpp:237) while its genotype probability
+    stays positive — founder mosaic 60 x 1 600, seed 1, found with the
+    restatement's skip counter: E1 rebuilds it with the pruned structure pass
+    (n_fallback > 0) at a finite LL equal to the restatement's, and the exact
+    M-step walks its pruned records (HaploBuilder.cpp:291-314): the table
+    equals the restatement's within 1e-6."""
+    p = synth.founder_mosaic(60, 1600, A=2, seed=1)
+    oracle_mod.set_threads(16)
+    try:
+        o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
+        o.find_patterns()
+        ll_o = o.resolve_all()
+        _, gp = o.estep_summary()
+        sk = o.skip_counts()
+        assert np.isfinite(ll_o) and np.all(gp > 0) and np.any(sk > 0)
+        P_o, _ = o.estimate_patterns()
+        po = o.patterns()
+    finally:
+        oracle_mod.set_threads(1)
+    m = gpu_model(p)
+    m.exact_estimate = True
+    m.find_patterns()
+    ll_g, H, re = m.resolve_all()
+    assert ll_g == ll_o and m.estep_split_stats()["n_fallback"] > 0
+    P_g, _ = m.find_patterns()
+    assert m.exact_stats()["pruned"] > 0
+    pg = m.patterns()
+    assert P_g == P_o
+    for k in ("start", "len", "alleles", "succ"):
+        assert np.array_equal(pg[k], po[k]), k
+    for k in ("freq", "prefix", "tp"):
+        assert _rel_close(pg[k], po[k]), (k, np.max(np.abs(pg[k] - po[k]) / np.maximum(np.abs(po[k]), 1e-300)))
 
 
 def test_exact_single_allele_frequencies(oracle_mod):
