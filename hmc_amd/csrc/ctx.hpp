@@ -927,7 +927,7 @@ struct Ctx {
   enum { WIN_AUTO = 0, WIN_NEVER = 1, WIN_ALWAYS = 2 };
   int window_mode = WIN_AUTO;  // hmc_set_estep_windows
   int window_loci = 0;         // record indices per window (0 = from the budgets)
-  DevBuf<uint32_t> d_ck;
+  DevBuf<uint32_t> d_ck[2];  // checkpoint slots: window w reads slot w & 1, writes slot (w + 1) & 1
   DevBuf<unsigned long long> d_ck_off, d_ck_cursor;
   DevBuf<uint32_t> d_nodes, d_bnd_n, d_gc_scr;  // trace survivors (3 words per node), boundary list lengths, collection scratch
   DevBuf<unsigned long long> d_bnd_off, d_node_cursor;

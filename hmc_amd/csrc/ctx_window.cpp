@@ -37,7 +37,7 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   int rc;
   size_t freeb = 0, totb = 0;
   hipMemGetInfo(&freeb, &totb);
-  const double pool = (double)freeb + 4.0 * ((double)d_trace.n + (double)d_rec.n + (double)d_ck.n);
+  const double pool = (double)freeb + 4.0 * ((double)d_trace.n + (double)d_rec.n + (double)d_ck[0].n + (double)d_ck[1].n);
   const uint64_t rbud = (uint64_t)std::min(0.27 * pool, (double)(88ull << 30)) / 4;
   const uint64_t tbud = (uint64_t)std::min(0.40 * pool, (double)(130ull << 30)) / 4;
   const uint64_t cbud = (uint64_t)std::min(0.12 * pool, (double)(40ull << 30)) / 4;
@@ -52,7 +52,6 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   std::vector<unsigned long long> rw, tw;  // exact needs per individual and window
   std::vector<int32_t> fw;                 // largest frontier per individual and window
 
-  unsigned long long ck_cap[2] = {0, 0};  // checkpoint slots: [0, half) and [half, end)
   bool bump = false;            // records from the store's bump allocator (the windows), else the regions rb / rs (the probe)
   // Structure pass of the record indices [bound[w], bound[w + 1]) over
   // ids[0, np_).
@@ -105,9 +104,10 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     s1.w.hi = bound[w + 1];
     s1.w.win = w;
     s1.w.nwin = nwin;
-    s1.w.ck_store = d_ck.p;
-    s1.w.ck_cap = ck_cap[(w + 1) & 1];
-    s1.w.ck_cursor = d_ck_cursor.p + ((w + 1) & 1);
+    s1.w.ck_in = d_ck[w & 1].p;
+    s1.w.ck_out = d_ck[(w + 1) & 1].p;
+    s1.w.ck_cap = d_ck[(w + 1) & 1].n;
+    s1.w.ck_cursor = d_ck_cursor.p;
     s1.w.ck_off = d_ck_off.p;
     s1.w.ck_write = ck_write;
     hipEventRecord(ev[0], st);
@@ -176,6 +176,9 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   // individual whose window records do not fit runs that window again.
   const double fmean = std::max(1.0, (tmean - 2.0) / (1.0 + S));  // states per locus, mean
   const double ckw = (double)ck_words((unsigned long long)fmean, S) + 4.0;
+  // a checkpoint slot holds every individual's frontier at the heaviest probed size
+  // (a slot that fills up grows and the window's structure pass runs again)
+  const double ckw_max = (double)ck_words((unsigned long long)std::max(1.0, (tl - 2.0) / (1.0 + S) * 1.25), S) + 4.0;
   (void)rl;
   (void)tl;
   int k = n, WL = 0;
@@ -200,25 +203,24 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
             "%.0f record / %.0f trace words (mean), budgets rec %.1f trace %.1f ckpt %.1f GB\n",
             n, ngroups, k, nwin, WL, rmean, tmean, rbud * 4e-9, tbud * 4e-9, cbud * 4e-9);
   // ---- buffers: checkpoints in two slots (the window's input and output)
-  const uint64_t ck_half = std::max<uint64_t>(1024, (uint64_t)((double)k * ckw * 1.5));
-  if (d_ck.n < 2 * ck_half) {
-    d_ck.release();
-    e = d_ck.ensure(2 * ck_half);
-    if (e == hipErrorOutOfMemory) {  // the stores are dead here: they give way
-      (void)hipGetLastError();
-      d_trace.release();
-      d_rec.release();
-      e = d_ck.ensure(2 * ck_half);
+  const uint64_t ck_slot = std::max<uint64_t>(1024, (uint64_t)((double)k * ckw_max));
+  for (int sl = 0; sl < 2; ++sl)
+    if (d_ck[sl].n < ck_slot) {
+      d_ck[sl].release();
+      e = d_ck[sl].ensure(ck_slot);
+      if (e == hipErrorOutOfMemory) {  // the stores are dead here: they give way
+        (void)hipGetLastError();
+        d_trace.release();
+        d_rec.release();
+        e = d_ck[sl].ensure(ck_slot);
+      }
+      if (e) return hipfail(e, "checkpoint store");
     }
-    if (e) return hipfail(e, "checkpoint store");
-  }
-  ck_cap[0] = d_ck.n / 2;
-  ck_cap[1] = d_ck.n;
   bump = true;
   const unsigned long long zero64 = 0;
-  if ((e = d_ck_off.ensure((size_t)n * (nwin + 1))) || (e = d_ck_cursor.ensure(2)) || (e = d_bnd_off.ensure(n)) ||
-      (e = d_bnd_n.ensure(n)) || (e = d_node_cursor.ensure(1)) || (e = hipMemsetAsync(d_re.p, 0, (size_t)n * 8, st)) ||
-      (e = hipMemsetAsync(d_cost.p, 0, (size_t)n * 4, st)))
+  std::vector<unsigned long long> h_re_w(n), re_tot(n, 0);  // R_E per window (host sums: a pass can run twice)
+  if ((e = d_ck_off.ensure((size_t)n * (nwin + 1))) || (e = d_ck_cursor.ensure(1)) || (e = d_bnd_off.ensure(n)) ||
+      (e = d_bnd_n.ensure(n)) || (e = d_node_cursor.ensure(1)) || (e = hipMemsetAsync(d_cost.p, 0, (size_t)n * 4, st)))
     return hipfail(e, "windowed E-step alloc");
   rw.assign((size_t)n * nwin, 0);
   tw.assign((size_t)n * nwin, 0);
@@ -285,9 +287,10 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     v.w.hi = bound[w + 1];
     v.w.win = w;
     v.w.nwin = nwin;
-    v.w.ck_store = d_ck.p;
-    v.w.ck_cap = ck_cap[(w + 1) & 1];
-    v.w.ck_cursor = d_ck_cursor.p + ((w + 1) & 1);
+    v.w.ck_in = d_ck[w & 1].p;
+    v.w.ck_out = d_ck[(w + 1) & 1].p;
+    v.w.ck_cap = d_ck[(w + 1) & 1].n;
+    v.w.ck_cursor = d_ck_cursor.p;
     v.w.ck_off = d_ck_off.p;
     v.w.ck_write = true;
     hipEventRecord(ev[0], st);
@@ -316,18 +319,63 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   auto window = [&](int w, std::vector<int32_t> &grp) -> int {
     std::vector<int32_t> todo(grp), dead;
     bool first = true;
-    if ((e = hipMemcpyAsync(d_ck_cursor.p + ((w + 1) & 1), (w + 1) & 1 ? &ck_cap[0] : &zero64, 8, hipMemcpyHostToDevice, st)))
-      return hipfail(e, "windowed E-step");
+    if ((e = hipMemcpyAsync(d_ck_cursor.p, &zero64, 8, hipMemcpyHostToDevice, st))) return hipfail(e, "windowed E-step");
     if (w % 2 == 0) tr_lo = 0;
     else tr_hi = d_trace.n;
     while (!todo.empty()) {
       if ((e = hipMemsetAsync(d_rec_cursor.p, 0, 8, st))) return hipfail(e, "windowed E-step");
-      if ((rc = structure(w, todo.data(), (int)todo.size(), first, first ? 1 : 2, true))) return rc;
+      if ((rc = structure(w, todo.data(), (int)todo.size(), first, 0, true))) return rc;
+      if (first) {  // a checkpoint slot that filled up: twice the size, the pass again
+        bool ckf = false;
+        for (int bi : todo) ckf = ckf || h_status[bi] == EST_OVERFLOW_CKPT;
+        if (ckf) {
+          DevBuf<uint32_t> &o = d_ck[(w + 1) & 1];
+          const size_t want = o.n * 2;
+          o.release();
+          if ((e = o.ensure(want)) || (e = hipMemcpyAsync(d_ck_cursor.p, &zero64, 8, hipMemcpyHostToDevice, st)))
+            return hipfail(e, "checkpoint store");
+          if (debug_mem) fprintf(stderr, "[hmc] window %d/%d: checkpoint slot full, %.2f GB\n", w + 1, nwin, want * 4e-9);
+          continue;
+        }
+        // a frontier or contribution list past the pass's capacities: larger
+        // capacities and the window again (its checkpoints are intact)
+        bool grow = false;
+        for (int bi : todo) {
+          const int s = h_status[bi];
+          if (s == EST_NO_HEAD_PATTERN) return fail(HMC_ENOPATTERN, "Can not find matching pattern!");
+          if (s == EST_OVERFLOW_FRONTIER || s == EST_OVERFLOW_CONTRIB) grow = true;
+        }
+        if (grow) {
+          for (int bi : todo) {
+            const int s = h_status[bi];
+            if (s == EST_OVERFLOW_FRONTIER && fcap < F_MAX) {
+              fcap = (int)std::min<int64_t>(F_MAX, (int64_t)fcap * 4);
+              break;
+            }
+          }
+          for (int bi : todo)
+            if (h_status[bi] == EST_OVERFLOW_CONTRIB) {
+              ccap_mult *= 2;
+              break;
+            }
+          for (int bi : todo)
+            if ((h_status[bi] == EST_OVERFLOW_FRONTIER && fcap >= F_MAX) ||
+                (h_status[bi] == EST_OVERFLOW_CONTRIB && (int64_t)ccap_mult * fcap >= INT32_MAX))
+              return fail(HMC_EUNSUPPORTED, "frontier exceeds %d states", F_MAX);
+          if (debug_mem) fprintf(stderr, "[hmc] window %d/%d: capacities %d states x %d, the window again\n", w + 1, nwin, fcap, ccap_mult);
+          if ((e = hipMemcpyAsync(d_ck_cursor.p, &zero64, 8, hipMemcpyHostToDevice, st))) return hipfail(e, "windowed E-step");
+          continue;
+        }
+        if ((e = hipMemcpyAsync(h_re_w.data(), d_re.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
+            (e = hipStreamSynchronize(st)))
+          return hipfail(e, "windowed E-step");
+        for (int bi : todo) re_tot[bi] += h_re_w[bi];
+      }
       std::vector<int32_t> ok, deferred;
       for (int bi : todo) {
         const int s = h_status[bi];
         if ((rc = restart_status(s))) return rc;
-        if (s == EST_OVERFLOW_CKPT) return fail(HMC_ENOMEM, "checkpoint store too small (window %d)", w);
+        if (s == EST_OVERFLOW_CKPT) return fail(HMC_EHIP, "checkpoint slot overflow after growth (window %d)", w);
         if (first) {
           rw[(size_t)bi * nwin + w] = hr[bi];
           tw[(size_t)bi * nwin + w] = ht[bi];
@@ -507,6 +555,8 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
       for (int w = 0; w < nwin; ++w) rec_all[bi] += rw[(size_t)bi * nwin + w];
     }
   }
+  if ((e = hipMemcpyAsync(d_re.p, re_tot.data(), (size_t)n * 8, hipMemcpyHostToDevice, st)) || (e = hipStreamSynchronize(st)))
+    return hipfail(e, "windowed E-step");
   prev_rneed.swap(rec_all);  // record words per individual (the next E-step's estimates at this scale)
   prev_P = P;
   // individuals whose forward likelihoods underflow: the classic passes, which

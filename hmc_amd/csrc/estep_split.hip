@@ -388,7 +388,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     // record index wlo - 1) instead.
     int Fp0 = 0, st0 = EST_OK;
     if (from_ck) {
-      const uint32_t *ck = a.w.ck_store + a.w.ck_off[(size_t)bi * (a.w.nwin + 1) + a.w.win];
+      const uint32_t *ck = a.w.ck_in + a.w.ck_off[(size_t)bi * (a.w.nwin + 1) + a.w.win];
       Fp0 = (int)ck[0];
       if (Fp0 > a.fcap) {
         st0 = EST_OVERFLOW_FRONTIER;
@@ -770,7 +770,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
       if (o == REC_NONE) {
         status = EST_OVERFLOW_CKPT;
       } else {
-        uint32_t *ck = a.w.ck_store + o;
+        uint32_t *ck = a.w.ck_out + o;
         if (tid == 0) {
           ck[0] = (uint32_t)Fp;
           ck[1] = 0;
@@ -1457,7 +1457,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
     const uint32_t *R = from_ck ? a.rec : a.rec + roff[hl];
     int Fp = 0;
     if (from_ck) {
-      const uint32_t *ck = a.w.ck_store + a.w.ck_off[(size_t)bi * (a.w.nwin + 1) + a.w.win];
+      const uint32_t *ck = a.w.ck_in + a.w.ck_off[(size_t)bi * (a.w.nwin + 1) + a.w.win];
       Fp = (int)ck[0];
       const double *cf = (const double *)(ck + ck_value_off((unsigned long long)Fp));
       const unsigned long long *ch = (const unsigned long long *)(cf + Fp);
@@ -1740,7 +1740,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
     __syncthreads();
     if (!last_win) {
       if (status == EST_OK && a.w.ck_write) {
-        uint32_t *ck = a.w.ck_store + a.w.ck_off[(size_t)bi * (a.w.nwin + 1) + a.w.win + 1];
+        uint32_t *ck = a.w.ck_out + a.w.ck_off[(size_t)bi * (a.w.nwin + 1) + a.w.win + 1];
         double *cf = (double *)(ck + ck_value_off((unsigned long long)Fp));
         unsigned long long *ch = (unsigned long long *)(cf + Fp);
         double *cl = (double *)(ch + Fp);

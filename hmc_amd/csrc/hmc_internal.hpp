@@ -163,18 +163,19 @@ struct EstepArgs {
 
 // Locus window of the checkpoint-and-recompute E-step (see StructArgs).
 // Checkpoint of an individual's frontier after record index j (window start
-// j + 1), at word ck_off[b * (nwin + 1) + win] of ck_store (even):
+// j + 1), at word ck_off[b * (nwin + 1) + win] of ck_in / ck_out (even):
 //   [F][0] | lo u32[F] hi u32[F] nl u32[F] (structure: pattern g / ids and list
 //   lengths) | pad to even | fwd f64[F] hm u64[F] lik f64[F][S] (value pass)
 struct WinArgs {
   int lo = 0, hi = 0;             // record / trace indices [lo, hi); hi == L + 1: the last window
   int win = 0, nwin = 1;
-  uint32_t *ck_store = nullptr;
-  unsigned long long ck_cap = 0;  // words
-  unsigned long long *ck_cursor = nullptr;
+  const uint32_t *ck_in = nullptr;  // the checkpoints this window starts from (offsets ck_off[b][win])
+  uint32_t *ck_out = nullptr;       // the checkpoints it leaves (offsets ck_off[b][win + 1])
+  unsigned long long ck_cap = 0;  // words of ck_out
+  unsigned long long *ck_cursor = nullptr;  // next free word of ck_out
   unsigned long long *ck_off = nullptr;  // [batch][nwin + 1]
   bool ck_write = false;          // save the window's last frontier (forward passes)
-  __host__ __device__ bool windowed() const { return ck_store != nullptr; }
+  __host__ __device__ bool windowed() const { return ck_out != nullptr; }
 };
 __host__ __device__ inline unsigned long long ck_value_off(unsigned long long F) { return (2ull + 3ull * F + 1ull) & ~1ull; }
 __host__ __device__ inline unsigned long long ck_words(unsigned long long F, int S) {

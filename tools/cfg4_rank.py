@@ -2,8 +2,9 @@
 over all 50 000 individuals (the model every rank holds after the sharded
 M0), then the E-step over rank r's balanced shard only (hmc_set_shard) —
 exactly the E1 work of rank r in `bench.py --gpus 8 --config 4`.  Prints the
-E-step's device ms (structure / values / recompute), its windows, and a
-repeat's bit-identity.
+E-step's device ms (structure / values / trace collection), its windows, and
+that a repeat is bit-identical.  SHAPES = "s_nw:s_ipc:v_nw:v_ipc,..." runs
+the E-step once per pass-shape set (0 = automatic).
 
     python tools/cfg4_rank.py [RANK [WORLD [CFG]]]
 """
@@ -19,6 +20,7 @@ from hmc_amd.model import balanced_shard  # noqa: E402
 rank = int(sys.argv[1]) if len(sys.argv) > 1 else 0
 world = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 cfg = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+shapes = [tuple(int(x) for x in s.split(":")) for s in os.environ.get("SHAPES", "0:0:0:0,0:0:0:0").split(",")]
 t0 = time.perf_counter()
 p = synth.config_panel(cfg)
 print(f"cfg {cfg} panel {p.N} x {p.L} in {time.perf_counter() - t0:.1f} s", flush=True)
@@ -33,19 +35,22 @@ del p
 m.set_shard(i0, i1)
 print(f"rank {rank} of {world}: individuals [{i0}, {i1}) = {i1 - i0}", flush=True)
 ref = None
-for rep in range(2):
+for rep, sh in enumerate(shapes):
+    m.set_pass_shapes(*sh)
     t0 = time.perf_counter()
     ll, H, re = m.resolve_all()
     wall = time.perf_counter() - t0
     s = m.estep_split_stats()
     t = m.timings()
     w = m.estep_windows()
-    print(f"E1 run {rep}: wall {wall:.2f} s; device: structure {s['structure_ms']:.0f} ms ({s['structure_passes']} passes), "
-          f"values {s['values_ms']:.0f} ms ({s['value_passes']}), traceback {t['estep_traceback_ms']:.0f} ms, "
-          f"fallback {s['fallback_ms']:.0f} ms ({s['n_fallback']}); windows {w['windows']} of {w['window_loci']} loci in "
-          f"{w['groups']} group(s), recompute {w['recompute_ms']:.0f} ms; LL {ll!r} H {H} R_E {re}", flush=True)
+    fr = m.estep_frontier()
+    print(f"E1 run {rep} shapes {sh}: wall {wall:.2f} s; device: structure {s['structure_ms']:.0f} ms "
+          f"({s['structure_passes']} passes), values {s['values_ms']:.0f} ms ({s['value_passes']}; trace collection "
+          f"{w['recompute_ms']:.0f} of it), traceback {t['estep_traceback_ms']:.0f} ms, fallback {s['fallback_ms']:.0f} ms "
+          f"({s['n_fallback']}); windows {w['windows']} of {w['window_loci']} loci in {w['groups']} group(s); "
+          f"frontier {fr}; LL {ll!r} H {H} R_E {re}", flush=True)
     if ref is None:
         ref = (float(ll).hex(), H, re)
     else:
-        print(f"repeat identical: {(float(ll).hex(), H, re) == ref}", flush=True)
+        print(f"identical to run 0: {(float(ll).hex(), H, re) == ref}", flush=True)
 m.close()

@@ -28,6 +28,7 @@ P1, _ = m.find_patterns()
 dt = time.perf_counter() - t0
 st = m.exact_stats()
 print(f"exact M1: {P1} patterns, {st['rounds']} rounds, {st['candidates']} candidates, walk {st['walk_ms']:.1f} ms, "
-      f"device {m.timings()['mstep_ms']:.1f} ms, wall {dt * 1e3:.1f} ms", flush=True)
+      f"device {m.timings()['mstep_ms']:.1f} ms, wall {dt * 1e3:.1f} ms; ratio to sampling {dt * 1e3 / ts:.1f}x; {st}",
+      flush=True)
 ll2, H, re = m.resolve_all()
 print(f"E2 after exact M1: LL {ll2:.6f}, R_E {re}, {m.timings()['estep_forward_ms']:.1f} ms", flush=True)
