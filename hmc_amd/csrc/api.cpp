@@ -32,6 +32,7 @@ static int ctx_init(hmc_ctx *h, int device) {
   if ((e = hipStreamCreateWithFlags(&h->c.st, hipStreamNonBlocking))) return h->c.hipfail(e, "hipStreamCreate");
   for (auto &ev : h->c.ev)
     if ((e = hipEventCreate(&ev))) return h->c.hipfail(e, "hipEventCreate");
+
   return HMC_OK;
 }
 
@@ -133,6 +134,7 @@ void hmc_ctx_destroy(hmc_ctx *h) {
   if (h->c.comm && h->c.own_comm) ncclCommDestroy(h->c.comm);
   for (auto &ev : h->c.ev)
     if (ev) hipEventDestroy(ev);
+
   if (h->c.st) hipStreamDestroy(h->c.st);
   delete h;
 }

@@ -909,21 +909,20 @@ struct Ctx {
   // of the value pass and traceback; E-step outputs are left untouched).
   int estep_split(const std::vector<int32_t> &order, bool exact = false);
 
-  // ---- checkpoint-and-recompute E-step (ctx_window.cpp) -----------------
+  // ---- windowed E-step (ctx_window.cpp) ----------------------------------
   // When an individual's records and traces for all loci are too large for
-  // the stores to hold more than a few hundred individuals at once (cfg 4's
-  // per-rank E1 on the genotype-mined M0: ~250 MB of records and ~390 MB of
-  // traces per individual, groups of ~280 on 256 CUs), the loci are cut into
-  // windows.  Forward: per window, the structure pass and the value pass over
-  // the whole group, each starting from the frontier the window before left in
-  // a checkpoint (pattern pairs and list lengths; forward likelihoods and the
-  // k-best lists) and saving its own last frontier; the last window makes the
-  // final selection and traces its candidates back to its first locus.
-  // Backward: every earlier window, last to first, is recomputed from its
-  // checkpoint (records and traces of that window only) and the traceback
-  // continues through it from the cursor the window above left
-  // (HaploPair::getGenotype, HaploPair.cpp:91-124).  Bit-identical to the
-  // classic passes: every window replays the same arithmetic in the same order.
+  // the stores to hold more than a few groups at once (cfg 4's per-rank E1 on
+  // the genotype-mined M0: ~250 MB of records and ~390 MB of traces per
+  // individual, groups of ~280 on 256 CUs; cfg 3's E1: five groups), the loci
+  // are cut into windows.  Per window, the structure pass and the value pass
+  // over the whole group, each starting from the frontier the window before
+  // left in a checkpoint (pattern pairs and list lengths; forward likelihoods
+  // and the k-best lists) and saving its own last frontier; the last window
+  // makes the final selection.  Full traces are kept for two windows; after
+  // each window the one before it is collected into survivor nodes
+  // (estep_trace_gc), and the traceback (HaploPair::getGenotype,
+  // HaploPair.cpp:91-124) walks the last two windows' traces and then the
+  // nodes.  Bit-identical to the classic passes.
   enum { WIN_AUTO = 0, WIN_NEVER = 1, WIN_ALWAYS = 2 };
   int window_mode = WIN_AUTO;  // hmc_set_estep_windows
   int window_loci = 0;         // record indices per window (0 = from the budgets)
@@ -931,9 +930,10 @@ struct Ctx {
   DevBuf<unsigned long long> d_ck_off, d_ck_cursor;
   DevBuf<uint32_t> d_nodes, d_bnd_n, d_gc_scr;  // trace survivors (3 words per node), boundary list lengths, collection scratch
   DevBuf<unsigned long long> d_bnd_off, d_node_cursor;
+  DevBuf<int32_t> d_gc_order, d_gc_status, d_gc_nextq;  // the collection's own order, statuses and work counter
   double win_scale = 1.0;  // shrinks the windows after a trace store overflow (the E-step restarts)
   int last_windows = 0, last_window_loci = 0, last_window_groups = 0;  // hmc_last_estep_windows
-  double ms_ck = 0;  // device ms of the backward (recompute) passes, part of ms_s1 / ms_s2
+  double ms_ck = 0;  // device ms of the trace collections (part of ms_s2)
   // A probe of the first loci of a sample decides: WIN_DECLINED when the
   // classic passes fit groups of at least two individuals per CU (or the
   // whole shard).
@@ -955,8 +955,9 @@ struct Ctx {
   // frontier, key slots (2x, power of two), contributions per locus (2x).
   // structure pass: 2 = estep_structure2 (fewer block hand-offs per locus), 1 = estep_structure
   int structure_pass_version = 1;  // hmc_set_structure_pass
-  // exact M-step walk (hmc_set_exact_walk): 1 breadth-first lane units
-  // (default), 2 / 4 depth-first, one / four items per wavefront (variants)
+  // exact M-step walk (hmc_set_exact_walk): 1 depth-first, one item per
+  // wavefront (default); 4 four items per wavefront, 2 breadth-first lane
+  // units (both variants)
   int exact_ipw = 1;
   static void s1_tier(int budget, int amax, int nw, int &fc, int &hc, int &cc, bool v2 = false) {
     for (int f = 2048; f >= 16; f -= 16) {

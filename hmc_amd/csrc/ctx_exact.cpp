@@ -243,7 +243,7 @@ int Ctx::exact_group(const int32_t *ids, int k, const std::function<int(std::vec
 }
 
 int Ctx::exact_walk_group(ExactArgs &x, int k, int dev_cu) {
-  if (exact_ipw == 1) return exact_walk_bfs(x, k, dev_cu);
+  if (exact_ipw == 2) return exact_walk_bfs(x, k, dev_cu);  // (variants)
   const int L = pan.L;
   hipError_t e;
   if (exact_walk_lds_bytes(tr_maxd, x.fmax) > EXACT_WALK_LDS_MAX)
@@ -326,46 +326,53 @@ int Ctx::exact_walk_bfs(ExactArgs &x, int k, int dev_cu) {
   hipEventRecord(ev[0], st);
   // One level: the units [in_base, in_base + n) (or the listed ones) at
   // `depth`, outputs from (u_top, e_top); then the next level over those
-  // outputs, then — with the pools above free again — the deferred units.
-  std::function<int(int, bool, unsigned long long, const std::vector<int32_t> *, int, unsigned long long, unsigned long long)> level;
-  level = [&](int depth, bool roots, unsigned long long in_base, const std::vector<int32_t> *idx, int n,
+  // outputs, then — with the pools above free again — the deferred units (a
+  // loop at the same depth: the recursion is as deep as the trie only).
+  std::function<int(int, bool, unsigned long long, std::vector<int32_t> *, int, unsigned long long, unsigned long long)> level;
+  level = [&](int depth, bool roots, unsigned long long in_base, std::vector<int32_t> *idx0, int n,
               unsigned long long u_top, unsigned long long e_top) -> int {
-    hipError_t e2;
-    const unsigned long long cur0[2] = {u_top, e_top};
-    const int zero = 0;
-    if ((e2 = hipMemcpyAsync(d_xcur.p, cur0, 16, hipMemcpyHostToDevice, st)) ||
-        (e2 = hipMemcpyAsync(d_xndef.p, &zero, 4, hipMemcpyHostToDevice, st)) ||
-        (idx && (e2 = hipMemcpyAsync(d_xidx.p, idx->data(), idx->size() * 4, hipMemcpyHostToDevice, st))))
-      return hipfail(e2, "exact walk");
-    XWalkArgs w2 = w;
-    w2.in_base = in_base;
-    w2.idx = idx ? d_xidx.p : nullptr;
-    w2.n_in = n;
-    w2.depth = depth;
-    w2.roots = roots;
-    if ((e2 = launch_exact_walk_units(x, w2, std::max(1, std::min(grid, (n + 255) / 256)), st)))
-      return hipfail(e2, "exact_walk_units");
-    unsigned long long cur[2];
-    int nd = 0;
-    if ((e2 = hipMemcpyAsync(cur, d_xcur.p, 16, hipMemcpyDeviceToHost, st)) ||
-        (e2 = hipMemcpyAsync(&nd, d_xndef.p, 4, hipMemcpyDeviceToHost, st)) || (e2 = hipStreamSynchronize(st)))
-      return hipfail(e2, "exact walk");
-    ++xw_launches;
-    xw_units += n;
-    std::vector<int32_t> def((size_t)nd);
-    if (nd && ((e2 = hipMemcpyAsync(def.data(), d_xdef.p, (size_t)nd * 4, hipMemcpyDeviceToHost, st)) ||
-               (e2 = hipStreamSynchronize(st))))
-      return hipfail(e2, "exact walk");
-    const unsigned long long u_end = std::min(cur[0], ucap), e_end = std::min(cur[1], ecap);
-    if (nd == n && u_end == u_top)
-      return fail(HMC_ENOMEM, "exact M-step: one trie node's children exceed the walk's pools (%llu units, %llu entries)",
-                  ucap, ecap);
-    int rc2;
-    if (u_end > u_top && (rc2 = level(depth + 1, false, u_top, nullptr, (int)(u_end - u_top), u_end, e_end))) return rc2;
-    if (nd) {
+    std::vector<int32_t> idx_v;
+    if (idx0) idx_v.swap(*idx0);
+    bool listed = idx0 != nullptr;
+    while (n > 0) {
+      hipError_t e2;
+      const unsigned long long cur0[2] = {u_top, e_top};
+      const int zero = 0;
+      if ((e2 = hipMemcpyAsync(d_xcur.p, cur0, 16, hipMemcpyHostToDevice, st)) ||
+          (e2 = hipMemcpyAsync(d_xndef.p, &zero, 4, hipMemcpyHostToDevice, st)) ||
+          (listed && (e2 = hipMemcpyAsync(d_xidx.p, idx_v.data(), idx_v.size() * 4, hipMemcpyHostToDevice, st))) ||
+          (listed && (e2 = hipStreamSynchronize(st))))
+        return hipfail(e2, "exact walk");
+      XWalkArgs w2 = w;
+      w2.in_base = in_base;
+      w2.idx = listed ? d_xidx.p : nullptr;
+      w2.n_in = n;
+      w2.depth = depth;
+      w2.roots = roots;
+      if ((e2 = launch_exact_walk_units(x, w2, std::max(1, std::min(grid, (n + 255) / 256)), st)))
+        return hipfail(e2, "exact_walk_units");
+      unsigned long long cur[2];
+      int nd = 0;
+      if ((e2 = hipMemcpyAsync(cur, d_xcur.p, 16, hipMemcpyDeviceToHost, st)) ||
+          (e2 = hipMemcpyAsync(&nd, d_xndef.p, 4, hipMemcpyDeviceToHost, st)) || (e2 = hipStreamSynchronize(st)))
+        return hipfail(e2, "exact walk");
+      ++xw_launches;
+      xw_units += n;
+      std::vector<int32_t> def((size_t)nd);
+      if (nd && ((e2 = hipMemcpyAsync(def.data(), d_xdef.p, (size_t)nd * 4, hipMemcpyDeviceToHost, st)) ||
+                 (e2 = hipStreamSynchronize(st))))
+        return hipfail(e2, "exact walk");
+      const unsigned long long u_end = std::min(cur[0], ucap), e_end = std::min(cur[1], ecap);
+      if (nd == n && u_end == u_top)
+        return fail(HMC_ENOMEM, "exact M-step: one trie node's children exceed the walk's pools (%llu units, %llu entries)",
+                    ucap, ecap);
+      int rc2;
+      if (u_end > u_top && (rc2 = level(depth + 1, false, u_top, nullptr, (int)(u_end - u_top), u_end, e_end))) return rc2;
       xw_defers += nd;
       std::sort(def.begin(), def.end());  // (any order gives the same sums: fixed-point adds)
-      if ((rc2 = level(depth, roots, in_base, &def, nd, u_top, e_top))) return rc2;
+      idx_v.swap(def);
+      listed = true;
+      n = nd;
     }
     return HMC_OK;
   };

@@ -144,9 +144,8 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
 
   // ---- probe: the first loci of a sample spread over the cost order --------
   // (counting only: no records are stored) give each individual's record and
-  // trace words per locus; the classic passes run unless their groups would
-  // be too small to fill the GPU (more than one group of fewer than two
-  // individuals per CU)
+  // trace words per locus; the classic passes run unless they would need
+  // several groups (see below)
   const int LP = std::min(NR, window_loci > 0 ? std::max(window_loci, 64) : std::max(64, NR / 8));
   bound = {hl, hl + LP};
   const int kp = std::min(n, 4 * dev_cu);
@@ -167,7 +166,11 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   if (debug_mem)
     fprintf(stderr, "[hmc] window probe: %zu individuals x %d loci; per locus records %.0f (max %.0f), traces %.0f (max %.0f) "
             "words: classic groups of ~%.0f\n", pick.size(), LP, rmean, rl, tmean, tl, k_classic);
-  if (window_mode != WIN_ALWAYS && !(k_classic < 2.0 * dev_cu && (double)n > k_classic)) return WIN_DECLINED;
+  // windows when the classic groups would hold fewer than two individuals per
+  // CU, or when they would be three or more (cfg 3's E1: five groups, 3.41 s;
+  // windows 3.23 s — fewer pass tails; two groups: the same time either way)
+  if (window_mode != WIN_ALWAYS && !((double)n > k_classic && (k_classic < 2.0 * dev_cu || (double)n > 2.0 * k_classic)))
+    return WIN_DECLINED;
   if (rl <= 0) return fail(HMC_EHIP, "windowed E-step without a measured individual");
 
   // ---- plan: window length and group size --------------------------------
@@ -187,7 +190,9 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     const double wl_r = (double)rbud / ((double)k * rmean * 1.25), wl_t = (double)tbud / (2.0 * (double)k * tmean * 1.25);
     WL = window_loci > 0 ? window_loci : (int)std::max(1.0, std::min(wl_r, wl_t) * win_scale);
     WL = std::min(WL, NR);
-    if ((window_loci > 0 || WL >= 16) && 2.0 * (double)k * ckw * 1.5 <= (double)cbud) break;
+    // a fixed window length takes smaller groups until its records and traces fit
+    const bool fits = window_loci > 0 ? std::min(wl_r, wl_t) * win_scale >= (double)WL : WL >= 16;
+    if (fits && 2.0 * (double)k * ckw * 1.5 <= (double)cbud) break;
     if (k == 1) break;
   }
   nwin = (NR + WL - 1) / WL;
@@ -228,6 +233,9 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   std::vector<int32_t> underflow;  // individuals whose likelihoods underflow: the classic passes (prune mode)
   // trace store: even windows fill it from the bottom, odd windows from the top
   uint64_t tr_lo = 0, tr_hi = 0;
+
+  bool gc_pending = false;
+  std::vector<int32_t> gc_ids;  // the collection's individuals
 
   // Value pass of window w over ids[0, k_) (trace regions in tbv).
   auto values = [&](int w, const int32_t *ids, int k_) -> int {
@@ -389,6 +397,8 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
       for (int bi : ok) t += tw[(size_t)bi * nwin + w];
       if (tr_lo + t > tr_hi) {  // two windows of traces do not fit: smaller windows, the E-step again
         win_scale *= 0.6;
+        if (win_scale < 1e-3)
+          return fail(HMC_ENOMEM, "windowed E-step: the traces of one window of %d loci exceed the trace store", WL);
         if (debug_mem) fprintf(stderr, "[hmc] windowed E-step: traces of two windows exceed the store; windows x0.6, restart\n");
         return ESTEP_RESTART;
       }
@@ -426,9 +436,14 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   };
 
   // Collection of window w - 1 (the survivors of every list entry at the end
-  // of window w) over `grp`; a node store that fills up grows and the
-  // individuals that did not fit run again.
-  auto collect = [&](int w, std::vector<int32_t> &grp) -> int {
+  // of window w) over `grp`, after window w's value pass, a wavefront per
+  // individual.  (Run beside window w + 1's structure pass on a stream of its
+  // own it made that pass 50-60 % slower, more than the collection's own time:
+  // both are latency-bound on the same CUs.)  A node store that fills up is
+  // grown (contents kept) and the individuals that did not fit run again.
+  int gc_w = 0;
+  auto collect_launch = [&](int w, const std::vector<int32_t> &grp) -> int {
+    gc_w = w;
     const int lo0 = bound[w - 1], mid = bound[w], hi1 = bound[w + 1];
     uint64_t mwords = 0;
     int fb = 1;
@@ -436,63 +451,76 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
       mwords = std::max<uint64_t>(mwords, (tw[(size_t)bi * nwin + w - 1] + tw[(size_t)bi * nwin + w]) / 32);
       fb = std::max(fb, std::max(fw[(size_t)bi * nwin + w - 1], fw[(size_t)bi * nwin + w]));
     }
+    if (grp.empty()) return HMC_OK;
     const int max_words = (int)(((uint64_t)fb * S + 31) / 32) + 1;
     const size_t stride = (size_t)(hi1 - lo0 + 1) + 2 * (size_t)(max_words + 1) + mwords + (size_t)(hi1 - lo0) + 64;
-    std::vector<int32_t> todo(grp);
-    while (!todo.empty()) {
-      const int grid = std::max(1, std::min((int)todo.size(), dev_cu * 4));
-      hipError_t e2;
+    const int grid = std::max(1, std::min((int)grp.size(), dev_cu * 16));  // a wavefront per individual
+    gc_ids = grp;
+    hipError_t e2;
+    if ((e2 = d_gc_scr.ensure(stride * grid)) || (e2 = d_gc_order.ensure(n)) || (e2 = d_gc_status.ensure(n)) ||
+        (e2 = d_gc_nextq.ensure(1)) ||
+        (e2 = hipMemcpyAsync(d_gc_order.p, gc_ids.data(), gc_ids.size() * 4, hipMemcpyHostToDevice, st)) ||
+        (e2 = hipMemsetAsync(d_gc_status.p, 0, (size_t)n * 4, st)) || (e2 = hipMemsetAsync(d_gc_nextq.p, 0, 4, st)))
+      return hipfail(e2, "trace collection");
+    TraceGcArgs g;
+    g.L = L;
+    g.S = S;
+    g.head_len = hl;
+    g.order = d_gc_order.p;
+    g.n_order = (int)gc_ids.size();
+    g.next_q = d_gc_nextq.p;
+    g.trace = d_trace.p;
+    g.loc_off = d_loc_off.p;
+    g.lo0 = lo0;
+    g.mid = mid;
+    g.hi1 = hi1;
+    g.scratch = d_gc_scr.p;
+    g.scratch_stride = stride;
+    g.max_words = max_words;
+    g.nodes = d_nodes.p;
+    g.node_cap = d_nodes.n / 3;
+    g.node_cursor = d_node_cursor.p;
+    g.bnd_off = d_bnd_off.p;
+    g.bnd_n = d_bnd_n.p;
+    g.status = d_gc_status.p;
+    hipEventRecord(ev[4], st);
+    if ((e2 = launch_estep_trace_gc(g, grid, st, 1))) return hipfail(e2, "estep_trace_gc launch");
+    hipEventRecord(ev[5], st);
+    gc_pending = true;
+    if (debug_mem)
+      fprintf(stderr, "[hmc] window %d/%d: collection of window %d for %zu individuals\n", w + 1, nwin, w, gc_ids.size());
+    return HMC_OK;
+  };
+  std::function<int()> collect_finish;
+  collect_finish = [&]() -> int {
+    if (!gc_pending) return HMC_OK;
+    gc_pending = false;
+    hipError_t e2;
+    std::vector<int32_t> gs(n);
+    if ((e2 = hipMemcpyAsync(gs.data(), d_gc_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
+        (e2 = hipStreamSynchronize(st)))
+      return hipfail(e2, "trace collection");
+    hipEventElapsedTime(&ms, ev[4], ev[5]);
+    ms_ck += ms;
+    ms_s2 += ms;
+    std::vector<int32_t> again;  // node store full: grown (contents kept), those individuals again
+    for (int bi : gc_ids) {
+      if (gs[bi] == EST_GC_MISS) return fail(HMC_EHIP, "trace collection: a survivor's predecessor is missing (individual %d)", i0 + bi);
+      if (gs[bi] == EST_OVERFLOW_NODES) again.push_back(bi);
+    }
+    if (debug_mem)
+      fprintf(stderr, "[hmc] collection for %zu individuals: %.1f ms%s\n", gc_ids.size(), ms, again.empty() ? "" : " (node store full: grows)");
+    if (!again.empty()) {
+      unsigned long long used = 0;
+      if ((e2 = hipMemcpyAsync(&used, d_node_cursor.p, 8, hipMemcpyDeviceToHost, st)) || (e2 = hipStreamSynchronize(st)))
+        return hipfail(e2, "trace collection");
+      used = std::min<unsigned long long>(used, d_nodes.n / 3);
+      if ((e2 = hipMemcpyAsync(d_node_cursor.p, &used, 8, hipMemcpyHostToDevice, st)) ||
+          (e2 = d_nodes.grow_keep(d_nodes.n * 2, used * 3, st)))
+        return hipfail(e2, "trace survivor nodes");
       int rc2;
-      if ((e2 = d_gc_scr.ensure(stride * grid)) || (e2 = hipMemsetAsync(d_nextq.p, 0, 4, st))) return hipfail(e2, "trace collection");
-      if ((rc2 = upload_order(d_order, todo.data(), (int)todo.size()))) return rc2;
-      TraceGcArgs g;
-      g.L = L;
-      g.S = S;
-      g.head_len = hl;
-      g.order = d_order.p;
-      g.n_order = (int)todo.size();
-      g.next_q = d_nextq.p;
-      g.trace = d_trace.p;
-      g.loc_off = d_loc_off.p;
-      g.lo0 = lo0;
-      g.mid = mid;
-      g.hi1 = hi1;
-      g.scratch = d_gc_scr.p;
-      g.scratch_stride = stride;
-      g.max_words = max_words;
-      g.nodes = d_nodes.p;
-      g.node_cap = d_nodes.n / 3;
-      g.node_cursor = d_node_cursor.p;
-      g.bnd_off = d_bnd_off.p;
-      g.bnd_n = d_bnd_n.p;
-      g.status = d_status.p;
-      hipEventRecord(ev[0], st);
-      if ((e2 = launch_estep_trace_gc(g, grid, st))) return hipfail(e2, "estep_trace_gc launch");
-      hipEventRecord(ev[1], st);
-      if ((rc2 = read_status({}, 0, false))) return rc2;
-      hipEventElapsedTime(&ms, ev[0], ev[1]);
-      ms_ck += ms;
-      ms_s2 += ms;
-      std::vector<int32_t> again;
-      for (int bi : todo) {
-        if (h_status[bi] == EST_GC_MISS) return fail(HMC_EHIP, "trace collection: a survivor's predecessor is missing (individual %d)", i0 + bi);
-        if (h_status[bi] == EST_OVERFLOW_NODES) again.push_back(bi);
-      }
-      if (debug_mem)
-        fprintf(stderr, "[hmc] window %d/%d: collected window %d for %zu individuals, %.1f ms%s\n", w + 1, nwin, w,
-                todo.size(), ms, again.empty() ? "" : " (node store full: grows)");
-      if (!again.empty()) {  // grow the node store (contents kept) and run those again
-        unsigned long long used = 0;
-        if ((e2 = hipMemcpyAsync(&used, d_node_cursor.p, 8, hipMemcpyDeviceToHost, st)) || (e2 = hipStreamSynchronize(st)))
-          return hipfail(e2, "trace collection");
-        used = std::min<unsigned long long>(used, d_nodes.n / 3);
-        if ((e2 = hipMemcpyAsync(d_node_cursor.p, &used, 8, hipMemcpyHostToDevice, st)) ||
-            (e2 = d_nodes.grow_keep(d_nodes.n * 2, used * 3, st)))
-          return hipfail(e2, "trace survivor nodes");
-        for (int bi : again) h_status[bi] = EST_OK;
-        if ((e2 = hipMemcpyAsync(d_status.p, h_status.data(), (size_t)n * 4, hipMemcpyHostToDevice, st))) return hipfail(e2, "trace collection");
-      }
-      todo.swap(again);
+      if ((rc2 = collect_launch(gc_w, again))) return rc2;
+      return collect_finish();
     }
     return HMC_OK;
   };
@@ -517,7 +545,7 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     tr_hi = d_trace.n;
     for (int w = 0; w < nwin; ++w) {
       if ((rc = window(w, grp))) return rc;
-      if (w >= 1 && w < nwin - 1 && (rc = collect(w, grp))) return rc;
+      if (w >= 1 && w < nwin - 1 && ((rc = collect_launch(w, grp)) || (rc = collect_finish()))) return rc;
     }
     // the traceback: the last two windows' traces, then the survivors' chains
     if (!grp.empty()) {

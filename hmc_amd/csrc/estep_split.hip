@@ -134,10 +134,10 @@ __host__ __device__ inline K1Plan k1_plan(int fc, int hc, int cc, int npm, int n
 
 // Insert-or-find of the successor key: the first free or matching slot of its
 // LDS probe sequence, else the HBM table.  Slots never empty during a locus.
-__device__ inline uint32_t k1_key_slot(const K1Keys &K, unsigned long long key, uint32_t h0) {
+__device__ inline uint32_t k1_key_slot(const K1Keys &K, unsigned long long key, uint32_t h0, int probes = PROBE_LDS) {
   unsigned long long *lk = (unsigned long long *)K.l, *gk = (unsigned long long *)K.g;
   uint32_t h = h0 & (uint32_t)(K.hc - 1);
-  for (int p = 0; p < PROBE_LDS; ++p) {
+  for (int p = 0; p < probes; ++p) {
     const unsigned long long prev = atomicCAS(&lk[h], KEY_EMPTY, key);
     if (prev == KEY_EMPTY || prev == key) return h;
     h = (h + 1) & (uint32_t)(K.hc - 1);
@@ -574,7 +574,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
           hi = rev ? sa : sb;
         }
         if (valid) {
-          slot = k1_key_slot(K, ((unsigned long long)lo << 32) | hi, key_hash(lo, hi));
+          slot = k1_key_slot(K, ((unsigned long long)lo << 32) | hi, key_hash(lo, hi), a.probe_lds);
           atomicOr(K.lanes(slot) + wv, 1ull << lane);
         }
         S1_CNT(10, 1);
@@ -1864,11 +1864,13 @@ hipError_t launch_estep_structure2(const StructArgs &, int, int, hipStream_t) { 
 // the marked entries of [lo0, mid) as nodes (ascending key per locus; the
 // predecessor's node by a prefix popcount of the locus below, or by a binary
 // search of the boundary list of the window before).
-__global__ __launch_bounds__(256) void estep_trace_gc(TraceGcArgs a) {
-  __shared__ unsigned long long red64[16];  // Blk<4>: 2 x 4 + 8 ints, then 4 u64 (8-byte aligned)
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void estep_trace_gc(TraceGcArgs a) {
+  constexpr int NT = 64 * NW;
+  __shared__ unsigned long long red64[16];  // Blk<NW <= 4>: 2 NW + 8 ints, then NW u64 (8-byte aligned)
   __shared__ int sq;
   const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;
-  const Blk<4> B{(int *)red64, tid, lane, wv};
+  const Blk<NW> B{(int *)red64, tid, lane, wv};
   const int S = a.S, L = a.L, hl = a.head_len;
   const int nloc = a.hi1 - a.lo0;
   uint32_t *moff = a.scratch + (size_t)blockIdx.x * a.scratch_stride;  // [nloc + 1]
@@ -1880,7 +1882,7 @@ __global__ __launch_bounds__(256) void estep_trace_gc(TraceGcArgs a) {
     auto words_at = [&](int j) -> uint32_t { return (a.trace[lo[j]] * (uint32_t)S + 31u) >> 5; };
     // ---- bitmap offsets per locus
     uint32_t acc = 0;
-    for (int c0 = 0; c0 < nloc; c0 += 256) {
+    for (int c0 = 0; c0 < nloc; c0 += NT) {
       const int c = c0 + tid;
       const int w = c < nloc ? (int)words_at(a.lo0 + c) : 0;
       int tot = 0;
@@ -1889,7 +1891,7 @@ __global__ __launch_bounds__(256) void estep_trace_gc(TraceGcArgs a) {
       acc += (uint32_t)tot;
     }
     B.sync();
-    for (uint32_t w = tid; w < acc; w += 256) M[w] = 0u;
+    for (uint32_t w = tid; w < acc; w += NT) M[w] = 0u;
     B.sync();
     // ---- every list entry of the last locus, then backward along the links
     {
@@ -1897,7 +1899,7 @@ __global__ __launch_bounds__(256) void estep_trace_gc(TraceGcArgs a) {
       const uint32_t F = a.trace[lo[j]];
       const uint32_t *hdr = a.trace + lo[j] + 1;
       uint32_t *Mj = M + moff[j - a.lo0];
-      for (uint32_t t = tid; t < F; t += 256) {
+      for (uint32_t t = tid; t < F; t += NT) {
         const uint32_t n = (hdr[t] >> 16) & 0xFFu;
         for (uint32_t k = 0; k < n; ++k) {
           const uint32_t bit = t * (uint32_t)S + k;
@@ -1912,7 +1914,7 @@ __global__ __launch_bounds__(256) void estep_trace_gc(TraceGcArgs a) {
       const uint32_t *Mj = M + moff[j - a.lo0];
       uint32_t *Mp = M + moff[j - 1 - a.lo0];
       const uint32_t nw = (F * (uint32_t)S + 31u) >> 5;
-      for (uint32_t w = tid; w < nw; w += 256)
+      for (uint32_t w = tid; w < nw; w += NT)
         for (uint32_t b = Mj[w]; b; b &= b - 1u) {
           const uint32_t bit = w * 32u + (uint32_t)__builtin_ctz(b);
           const uint32_t m = links[bit];
@@ -1924,7 +1926,7 @@ __global__ __launch_bounds__(256) void estep_trace_gc(TraceGcArgs a) {
     }
     // ---- the survivors of [lo0, mid) as nodes
     unsigned long long cnt = 0;
-    for (uint32_t w = tid; w < moff[a.mid - a.lo0]; w += 256) cnt += (unsigned long long)__popc(M[w]);
+    for (uint32_t w = tid; w < moff[a.mid - a.lo0]; w += NT) cnt += (unsigned long long)__popc(M[w]);
     const unsigned long long total = B.reduce_u64(cnt);
     unsigned long long base = 0;
     if (tid == 0) {
@@ -1948,7 +1950,7 @@ __global__ __launch_bounds__(256) void estep_trace_gc(TraceGcArgs a) {
         const uint32_t *Mj = M + moff[j - a.lo0];
         const uint32_t nw = (F * (uint32_t)S + 31u) >> 5;
         uint32_t acc2 = 0;
-        for (uint32_t c0 = 0; c0 < nw; c0 += 256) {
+        for (uint32_t c0 = 0; c0 < nw; c0 += NT) {
           const uint32_t w = c0 + tid;
           const int v = w < nw ? __popc(Mj[w]) : 0;
           int tot = 0;
@@ -1958,7 +1960,7 @@ __global__ __launch_bounds__(256) void estep_trace_gc(TraceGcArgs a) {
         }
         B.sync();
         const uint32_t *Mp = j > a.lo0 ? M + moff[j - 1 - a.lo0] : nullptr;
-        for (uint32_t w = tid; w < nw; w += 256) {
+        for (uint32_t w = tid; w < nw; w += NT) {
           unsigned long long r = nb + Pc[w];
           for (uint32_t b = Mj[w]; b; b &= b - 1u) {
             const uint32_t bit = w * 32u + (uint32_t)__builtin_ctz(b);
@@ -2011,11 +2013,15 @@ __global__ __launch_bounds__(256) void estep_trace_gc(TraceGcArgs a) {
   }
 }
 
-hipError_t launch_estep_trace_gc(const TraceGcArgs &a, int grid, hipStream_t st) {
+hipError_t launch_estep_trace_gc(const TraceGcArgs &a, int grid, hipStream_t st, int nw) {
   if (a.n_order <= 0) return hipSuccess;
-  if (a.S < 1 || a.S > S_MAX || a.lo0 < a.head_len || a.mid <= a.lo0 || a.hi1 <= a.mid || a.hi1 > a.L + 1 || grid < 1)
+  if (a.S < 1 || a.S > S_MAX || a.lo0 < a.head_len || a.mid <= a.lo0 || a.hi1 <= a.mid || a.hi1 > a.L + 1 || grid < 1 ||
+      (nw != 1 && nw != 4))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(estep_trace_gc, dim3(grid), dim3(256), 0, st, a);
+  // nw = 1: a wavefront per individual — the marking walks the loci one after
+  // another, so more individuals in flight hide its latency
+  if (nw == 4) hipLaunchKernelGGL(estep_trace_gc<4>, dim3(grid), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(estep_trace_gc<1>, dim3(grid), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 

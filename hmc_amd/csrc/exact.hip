@@ -499,6 +499,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
 }
 
 
+#ifdef HMC_VARIANTS  // (the breadth-first walk: measured slower, the variants library only)
 // ---- breadth-first walk ----------------------------------------------------
 // The depth-first walk above spends a wavefront and a dozen dependent,
 // barriered steps on every trie node, while a node's lists hold a handful of
@@ -754,6 +755,9 @@ hipError_t launch_exact_walk_units(const ExactArgs &a, const XWalkArgs &x, int g
   hipLaunchKernelGGL(exact_walk_units, dim3(grid), dim3(256), 0, st, a, x);
   return hipGetLastError();
 }
+#else
+hipError_t launch_exact_walk_units(const ExactArgs &, const XWalkArgs &, int, hipStream_t) { return hipErrorNotSupported; }
+#endif
 
 size_t exact_walk_scratch_doubles(int max_depth, int fmax, int width) {
   return (size_t)(max_depth + 1) * width * 3 * fmax + (size_t)(max_depth + 2) * width +

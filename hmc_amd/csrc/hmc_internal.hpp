@@ -224,6 +224,7 @@ struct StructArgs {
   // For individuals whose likelihoods underflow (the value pass reports
   // EST_NEEDS_EXACT); status EST_OK_PRUNED.  Scratch: estep_s1_scratch_bytes(.., prune)
   bool prune = false;
+  int probe_lds = 16;  // LDS probes of the key table before the HBM table (PROBE_LDS)
   int32_t *next_q;                // dynamic schedule: order entries taken after the first gridDim.x (zeroed)
   // Locus windows (checkpoint-and-recompute E-step, Ctx::estep_windowed):
   // records of indices [win_lo, win_hi) only — win_lo == head_len starts
@@ -321,7 +322,7 @@ struct TraceGcArgs {
   uint32_t *bnd_n = nullptr;              // [batch]
   int32_t *status = nullptr;              // EST_OVERFLOW_NODES: the node store is full (nothing changed)
 };
-hipError_t launch_estep_trace_gc(const TraceGcArgs &a, int grid, hipStream_t st);
+hipError_t launch_estep_trace_gc(const TraceGcArgs &a, int grid, hipStream_t st, int nw = 1);
 
 size_t estep_scratch_bytes(int fcap, int hcap, int S, int nw);
 size_t estep_lds_bytes(int S, int fc, int hc, int nw, int amax);

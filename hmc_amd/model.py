@@ -288,9 +288,9 @@ class HaploModel:
         self._check(lib().hmc_set_structure_pass(self._h, int(version)))
 
     def set_exact_walk(self, items_per_wave: int):
-        """Exact M-step trie walk (hmc_set_exact_walk): 1 breadth-first lane
-        units (default); 2 / 4 the depth-first walk with one / four items per
-        wavefront (variants library)."""
+        """Exact M-step trie walk (hmc_set_exact_walk): 1 the depth-first walk,
+        one item per wavefront (default); 4 four items per wavefront and 2 the
+        breadth-first lane units (variants library)."""
         self._check(lib().hmc_set_exact_walk(self._h, int(items_per_wave)))
 
     def last_value_pass_dataflow(self) -> bool:

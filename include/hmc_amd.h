@@ -390,9 +390,12 @@ int hmc_set_dataflow_waves(hmc_ctx *ctx, int a_waves);
  * block of the table instead of lines spread over all of it.  Results are
  * identical. */
 int hmc_set_end_order(hmc_ctx *ctx, int on);
-/* Exact M-step trie walk: pattern-tree items (individual, start locus) per
- * wavefront, 1 (64 lanes each) or 4 (16 lanes each); 0 = automatic.  The
- * frequency sums are fixed-point integer adds, identical for any order. */
+/* Exact M-step trie walk (HaploBuilder.cpp:334-449 estimateFrequency): 0 or
+ * 1 = the depth-first walk, one (individual, start locus) item per wavefront
+ * (default); 4 = four items per wavefront (16 lanes each) and 2 = the
+ * breadth-first walk, one trie node per lane (both measured slower: the
+ * variants library only, HMC_EUNSUPPORTED in the product).  The frequency
+ * sums are fixed-point integer adds, identical for any order. */
 int hmc_set_exact_walk(hmc_ctx *ctx, int items_per_wave);
 /* 1 when the last value-pass launch ran the dataflow schedule. */
 int hmc_last_value_pass(const hmc_ctx *ctx, int *dataflow);

@@ -10,6 +10,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
+    config.addinivalue_line("markers", "slow: longer GPU parity combinations (still part of -m gpu)")
     config.addinivalue_line("markers", "variants: the kernels measured slower than the automatic paths, built into "
                                        "libhmc_amd_variants.so only (HMC_AMD_LIB=hmc_amd/libhmc_amd_variants.so -m variants)")
 

@@ -129,6 +129,28 @@ def test_estep_pass_shapes(oracle_mod, name, shape):
     assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
 
 
+# combinations cut from the matrix in round 4 (n60 and a8 panels with shapes
+# callers can still pick through hmc_set_pass_shapes)
+_SLOW_COMBOS = [("n60", (1, 12, 1, 20)), ("n60", (4, 2, 16, 1)), ("a8", (1, 12, 1, 20)), ("a8", (4, 2, 16, 1)),
+                ("a8", (16, 1, 8, 2)), ("n60", (4, 3, 4, 4))]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name,shape", _SLOW_COMBOS)
+def test_estep_pass_shapes_more_panels(oracle_mod, name, shape):
+    """The same check on the panels the round-4 matrix dropped (60 loci i.i.d.,
+    8 alleles per locus)."""
+    p = panel(name)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
+    o.find_patterns()
+    m = gpu_model(p)
+    m.set_pass_shapes(*shape)
+    m.find_patterns()
+    ll_g, H, re_g = m.resolve_all()
+    o.reset_counters()
+    assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
+
+
 @pytest.mark.parametrize("name,S", [("cfg1", 10), ("a3miss5", 3), ("a8", 10), ("n300", 3)])
 def test_value_only_mode_with_order_reruns(oracle_mod, name, S):
     """hmc_set_value_mode(0): value-only k-best lists (seg_rank_select), the
@@ -1185,11 +1207,13 @@ def test_exact_mstep_against_oracle(oracle_mod, name):
 def test_exact_walk_four_items_per_wave(oracle_mod, name):
     """hmc_set_exact_walk(4): the depth-first walk with four (individual, start
     locus) items per wavefront, 16 lanes each — the fixed-point frequency sums
-    are the same integers, so the table equals the one-item walk's (mode 2)
-    bit for bit."""
+    are the same integers, so the table equals the default walk's (mode 1) bit
+    for bit; (2) the breadth-first walk, one trie node per lane, sums each
+    child's frequency in state order instead of the wavefront's butterfly:
+    the same table within 1e-12."""
     p = panel(name)
     tabs = []
-    for ipw in (2, 4):
+    for ipw in (1, 4, 2):
         m = gpu_model(p)
         m.exact_estimate = True
         m.set_exact_walk(ipw)
@@ -1200,11 +1224,15 @@ def test_exact_walk_four_items_per_wave(oracle_mod, name):
         m.close()
     for k in ("start", "len", "alleles", "succ", "freq", "prefix", "tp"):
         assert np.array_equal(tabs[0][k], tabs[1][k]), k
+    for k in ("start", "len", "alleles", "succ"):
+        assert np.array_equal(tabs[0][k], tabs[2][k]), k
+    for k in ("freq", "prefix", "tp"):
+        assert np.allclose(tabs[0][k], tabs[2][k], rtol=1e-12, atol=1e-15), k
 
 
 @pytest.mark.timeout(900)
 def test_exact_mstep_300x200_against_oracle(oracle_mod):
-    """The breadth-first walk on a 300 x 200 panel (the survey's probe size):
+    """The exact M-step on a 300 x 200 panel (the survey's probe size):
     after M0 and E1, one exact M-step equals the restatement's table — same
     patterns, order and successors, frequencies / prefix / tp within 1e-6."""
     p = panel("n300")

@@ -1,9 +1,13 @@
-"""GPU parity of the checkpoint-and-recompute E-step (ctx_window.cpp,
-hmc_set_estep_windows): the loci cut into windows, each window's last frontier
-saved as the next one's checkpoint, the traceback recomputing every earlier
-window from its checkpoint.  Forced on small panels with tiny windows (down to
-one locus), it must equal the CPU restatement bit for bit — the same bar as
-the classic passes (tolerance 0 for every integer and double)."""
+"""GPU parity of the windowed E-step (ctx_window.cpp, hmc_set_estep_windows):
+the loci cut into windows, each window's last frontier saved as the next one's
+checkpoint, the records of one window at a time, the traces of two windows
+with the older one's live entries collected into survivor nodes.  Forced on
+small panels with tiny windows (down to one locus), it must equal the CPU
+restatement bit for bit — the same bar as the classic passes (tolerance 0 for
+every integer and double)."""
+import os
+import types
+
 import numpy as np
 import pytest
 
@@ -124,3 +128,39 @@ def test_windowed_equals_classic_cfg2():
         runs.append(out)
         m.close()
     assert runs[0] == runs[1] == runs[2]
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+@pytest.mark.skipif(os.environ.get("HMC_RUN_CFG4") != "1",
+                    reason="cfg 4 rank slice (~3 min, 50 000 x 5 000 panel): HMC_RUN_CFG4=1")
+def test_cfg4_rank0_real_shard_windowed_e1():
+    """Rank 0's real E1 of the 8-GPU cfg 4 run on one GPU: the global M0 over
+    all 50 000 individuals (what every rank holds after the sharded M0), then
+    the E-step over rank 0's balanced shard (hmc_set_shard).  It runs in
+    automatic windows (one group); the samples phase the genotypes, weights
+    sum to 1, priors are sorted; windows of 40 loci give the same LL, R_E,
+    samples and weights bit for bit."""
+    from hmc_amd.model import balanced_shard
+    from test_gpu_parity import _estep_properties
+
+    p = synth.config_panel(4)
+    m = gpu_model(p)
+    m.find_patterns()
+    i0, i1 = balanced_shard(p.alleles, 0, 8)
+    m.set_shard(i0, i1)
+    sub = types.SimpleNamespace(N=i1 - i0, alleles=p.alleles[i0:i1])
+    del p
+    out = []
+    for wl in (0, 40):
+        m.set_estep_windows("auto" if wl == 0 else "always", wl)
+        ll, H, re = m.resolve_all()
+        w = m.estep_windows()
+        assert w["windows"] >= 2 and (wl or w["groups"] == 1), w
+        if wl == 0:
+            _estep_properties(m, sub, ll, H)
+        al, wt, tw = m.samples(H)
+        out.append((float(ll).hex(), H, re, hash(al.tobytes()), wt.tobytes(), float(tw).hex()))
+        del al
+    assert out[0] == out[1]
+    m.close()

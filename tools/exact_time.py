@@ -4,12 +4,21 @@ total ms) next to the sampling M-step on the same E1 samples, and E2 after it.
 Env IPW: exact-walk items per wavefront (1 or 4)."""
 import os
 import sys
+import threading
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import hmc_amd  # noqa: E402
 from hmc_amd import synth  # noqa: E402
 
+def _beat():  # a line a minute: long exact M-steps print nothing else
+    t0 = time.time()
+    while True:
+        time.sleep(60)
+        print(f"  ... {time.time() - t0:.0f} s", flush=True)
+
+
+threading.Thread(target=_beat, daemon=True).start()
 p = synth.config_panel(int(os.environ.get("CFG", "2")))
 m = hmc_amd.HaploModel()
 m.set_exact_walk(int(os.environ.get("IPW", "1")))

@@ -3,7 +3,8 @@
 #   HBM traffic of the dominant kernel estep_values from two separate PMC
 #   passes (FETCH_SIZE, WRITE_SIZE) over the bench command itself, the
 #   kernel-trace stats of the same command, and SQ counter passes (instruction
-#   mix, LDS waits / bank conflicts, wave cycles) on a short run.
+#   mix, LDS waits / bank conflicts, wave cycles) of both E-step passes on a
+#   short run.
 # usage: bash tools/profile_round.sh OUTDIR TAG CONFIG
 #   -> OUTDIR/commit/TAG/ (copy to profiles/TAG afterwards); the PMC summary is
 #      profiles/TAG/pmc_estep_values_cfgCONFIG.json, which bench.py reads.
@@ -40,7 +41,7 @@ for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
          "SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM"; do
   N=$(echo "$P" | awk '{print $1}')
   echo "[profile] SQ pass $N" >&2
-  timeout -s KILL 300 rocprofv3 --pmc $P --kernel-include-regex $K --output-format csv -d "$OUT/sq_$N" -o s -- \
+  timeout -s KILL 300 rocprofv3 --pmc $P --kernel-include-regex "estep_values|estep_structure" --output-format csv -d "$OUT/sq_$N" -o s -- \
     python3 $SHORT > "$OUT/sq_$N.json" 2> "$OUT/sq_$N.err"
   cp "$(find "$OUT/sq_$N" -name "*counter_collection.csv" | head -n 1)" "$DEST/sq_${N}_cfg$CFG.csv"
 done
