@@ -390,7 +390,8 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
   float ms = 0;
   // Loci in windows with checkpoints (ctx_window.cpp) when the first E-step
   // on a model larger than the panel would otherwise run in groups too small
-  // to fill the GPU (cfg 4's per-rank E1); a probe of the first loci decides.
+  // to fill the GPU (cfg 4's per-rank E1) or in three or more groups (cfg 3's
+  // E1); a probe of the first loci decides.
   if (!exact && windows_allowed() &&
       (window_mode == WIN_ALWAYS || ((double)P > (double)pan.N * (double)pan.L && n > 2 * dev_cu))) {
     const int rw_ = estep_windowed(order);

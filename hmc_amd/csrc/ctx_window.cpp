@@ -38,9 +38,12 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   size_t freeb = 0, totb = 0;
   hipMemGetInfo(&freeb, &totb);
   const double pool = (double)freeb + 4.0 * ((double)d_trace.n + (double)d_rec.n + (double)d_ck[0].n + (double)d_ck[1].n);
-  const uint64_t rbud = (uint64_t)std::min(0.27 * pool, (double)(88ull << 30)) / 4;
-  const uint64_t tbud = (uint64_t)std::min(0.40 * pool, (double)(130ull << 30)) / 4;
-  const uint64_t cbud = (uint64_t)std::min(0.12 * pool, (double)(40ull << 30)) / 4;
+  // budgets (words) from the free HBM, within the caller's store caps when set
+  // (ranks sharing one GPU: hmc_set_store_budgets / hmc_set_tuning)
+  const bool capped = trace_bytes || rec_bytes;
+  const uint64_t rbud = std::min<uint64_t>((uint64_t)std::min(0.27 * pool, (double)(88ull << 30)) / 4, capped ? rec_budget : ~0ull);
+  const uint64_t tbud = std::min<uint64_t>((uint64_t)std::min(0.40 * pool, (double)(130ull << 30)) / 4, capped ? trace_budget : ~0ull);
+  const uint64_t cbud = std::min<uint64_t>((uint64_t)std::min(0.12 * pool, (double)(40ull << 30)) / 4, capped ? trace_budget / 3 : ~0ull);
   if ((e = d_nextq.ensure(2)) || (e = d_rec_off.ensure((size_t)n * (L + 1))) || (e = d_rec_cursor.ensure(1)))
     return hipfail(e, "windowed E-step alloc");
   std::vector<unsigned long long> hr(n), ht(n), rb(n, 0), rs(n, 0), tbv(n, 0);
@@ -146,9 +149,11 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   // (counting only: no records are stored) give each individual's record and
   // trace words per locus; the classic passes run unless they would need
   // several groups (see below)
-  const int LP = std::min(NR, window_loci > 0 ? std::max(window_loci, 64) : std::max(64, NR / 8));
+  // (at most 160 loci over two individuals per CU: one round of the pass, not
+  // a tail — cfg 4's probe of 625 loci over 1 024 took as long as a window)
+  const int LP = std::min(NR, window_loci > 0 ? std::max(window_loci, 64) : std::max(64, std::min(NR / 8, 160)));
   bound = {hl, hl + LP};
-  const int kp = std::min(n, 4 * dev_cu);
+  const int kp = std::min(n, 2 * dev_cu);
   std::vector<int32_t> pick;
   for (int q = 0; q < n; ++q)
     if ((int64_t)q * kp / n != (int64_t)(q - 1) * kp / n || q == 0) pick.push_back(order[q]);
@@ -241,19 +246,25 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   auto values = [&](int w, const int32_t *ids, int k_) -> int {
     hipError_t e2;
     int rc2;
-    double rsum = 0;
+    double rsum = 0, tsum = 0;
     int fgrp = 1;
     for (int q = 0; q < k_; ++q) {
       rsum += (double)rw[(size_t)ids[q] * nwin + w];
+      tsum += (double)tw[(size_t)ids[q] * nwin + w];
       fgrp = std::max(fgrp, (int)fw[(size_t)ids[q] * nwin + w]);
     }
     fgrp = std::min(fcap, (fgrp + 63) & ~63);
     const int wl = bound[w + 1] - bound[w];
     const bool heavy = rsum / ((double)k_ * wl) > 1500.0;
     const int per_cu = (k_ + dev_cu - 1) / dev_cu;
-    const bool small_heavy = heavy && per_cu < 4;
-    const int vnw = vp_nw > 0 ? vp_nw : (small_heavy ? 16 / per_cu : (heavy ? 4 : (k_ >= 32 * dev_cu ? 1 : (k_ >= 8 * dev_cu ? 2 : 3))));
-    const int vipc = vp_ipc > 0 ? vp_ipc : (small_heavy ? per_cu : (vnw == 1 ? 16 : (vnw >= 8 ? 2 : (vnw >= 4 ? 4 : 8))));
+    // heavy groups whose mean frontier is past twice the LDS tier of a 4 x 4
+    // block take a whole CU per individual (cfg 4's E1, ~1 700 states per
+    // locus: values 14.3 -> 13.7 s; cfg 3's E1, ~470: 4 x 4 stays)
+    const double fmean = (tsum / std::max(1.0, (double)k_ * wl) - 2.0) / (1.0 + S);
+    const bool small_heavy = heavy && (per_cu < 4 || (vp_nw == 0 && fmean > 2.0 * s2_tier(S, 4, 4, S <= 16)));
+    const int sh_ipc = per_cu < 4 ? per_cu : 1;
+    const int vnw = vp_nw > 0 ? vp_nw : (small_heavy ? 16 / sh_ipc : (heavy ? 4 : (k_ >= 32 * dev_cu ? 1 : (k_ >= 8 * dev_cu ? 2 : 3))));
+    const int vipc = vp_ipc > 0 ? vp_ipc : (small_heavy ? sh_ipc : (vnw == 1 ? 16 : (vnw >= 8 ? 2 : (vnw >= 4 ? 4 : 8))));
     const bool pair = S <= 16 && (value_pair == 2 || (value_pair == 1 && heavy));
     const int G2 = std::max(1, std::min(waves > 0 ? waves : dev_cu * vipc, n));
     const int vwpe = vnw * vipc > 16 && vnw * vipc <= 20 ? 5 : 4;
