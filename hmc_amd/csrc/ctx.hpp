@@ -681,6 +681,7 @@ struct Ctx {
   Cands ht;                    // that table, id order
   std::vector<int32_t> ht_succ;  // [P][amax]
   DevBuf<int32_t> d_tr_child, d_tr_data, d_tr_root, d_xstatus, d_xfmax;
+  DevBuf<unsigned> d_xspan;  // exact_span: the walk's largest per-item list span
   DevBuf<unsigned long long> d_xre, d_xacc;
   DevBuf<double> d_xscr;
   int tr_maxd = 0;

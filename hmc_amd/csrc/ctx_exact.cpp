@@ -251,7 +251,16 @@ int Ctx::exact_walk_group(ExactArgs &x, int k, int dev_cu) {
                 x.fmax, tr_maxd);
   // (variants) items per wavefront: 4 (16 lanes each) when their LDS fits, else 1
   const int ipw = exact_ipw == 4 && exact_walk_lds_bytes(tr_maxd, x.fmax) * 4 <= EXACT_WALK_LDS_MAX ? 4 : 1;
-  x.scratch_stride = exact_walk_scratch_doubles(tr_maxd, x.fmax, x.width);
+  {  // the largest list span of any item of the group (the per-wave scratch)
+    unsigned span = 0;
+    if ((e = d_xspan.ensure(1))) return hipfail(e, "exact_span");
+    x.span_max = d_xspan.p;
+    if ((e = hipMemsetAsync(d_xspan.p, 0, 4, st)) || (e = launch_exact_span(x, std::max(1, std::min(k, dev_cu * 8)), st)) ||
+        (e = hipMemcpyAsync(&span, d_xspan.p, 4, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+      return hipfail(e, "exact_span");
+    x.span = std::max<long long>(span, 1);
+  }
+  x.scratch_stride = exact_walk_scratch_doubles(tr_maxd, x.span, x.width);
   const long long items = (long long)k * L;
   // 28 waves per CU, fewer when the per-item lists would pass SCRATCH_MAX
   const long long by_mem = std::max<long long>(1, (long long)(SCRATCH_MAX / (x.scratch_stride * 8 * ipw)));
@@ -276,8 +285,10 @@ int Ctx::exact_walk_group(ExactArgs &x, int k, int dev_cu) {
     float ms = 0;
     hipEventElapsedTime(&ms, ev[0], ev[1]);
     ms_walk += ms;
-    if (debug_mem && items > 16 * (long long)grid)
-      fprintf(stderr, "[hmc] exact walk: items %lld..%lld of %lld (%d individuals), %.1f ms\n", i0, x.item1, items, k, ms);
+    if (debug_mem)
+      fprintf(stderr, "[hmc] exact walk: items %lld..%lld of %lld (%d individuals), %.1f ms; grid %d (%.1f waves per CU), "
+              "fmax %d, depth %d, %.1f MB per wave\n", i0, x.item1, items, k, ms, grid, (double)grid / dev_cu, x.fmax, tr_maxd,
+              x.scratch_stride * 8e-6);
   }
   return HMC_OK;
 }

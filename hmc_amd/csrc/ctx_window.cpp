@@ -56,15 +56,20 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   std::vector<int32_t> fw;                 // largest frontier per individual and window
 
   bool bump = false;            // records from the store's bump allocator (the windows), else the regions rb / rs (the probe)
+  // the structure pass's state capacity for the current window: twice the
+  // largest frontier of the window before (its key table, HBM tier included,
+  // stays small enough for the caches; cfg 4's E1 reaches 65 923 states at one
+  // locus, which sized every window's tables for 2^18 states)
+  int wfcap = fcap;
   // Structure pass of the record indices [bound[w], bound[w + 1]) over
   // ids[0, np_).
   auto structure = [&](int w, const int32_t *ids, int np_, bool ck_write, int re_mode, bool fwd) -> int {
     const int nw1 = s1_nw > 0 ? s1_nw : (heavy_model ? (np_ <= dev_cu ? 16 : 4) : 1);
     const int bpc1 = s1_ipc > 0 ? s1_ipc
                                 : (nw1 == 16 ? 1 : (nw1 == 4 ? 2 : (np_ > 8 * dev_cu ? 12 : (np_ > 4 * dev_cu ? 8 : 4))));
-    const int hcap1 = next_pow2(2 * fcap);
-    const int ccap1 = (int)std::min<int64_t>(INT32_MAX / 2, (int64_t)ccap_mult * fcap);
-    const size_t per1 = estep_s1_scratch_bytes(fcap, hcap1, ccap1, nw1, false);
+    const int hcap1 = next_pow2(2 * wfcap);
+    const int ccap1 = (int)std::min<int64_t>(INT32_MAX / 2, (int64_t)ccap_mult * wfcap);
+    const size_t per1 = estep_s1_scratch_bytes(wfcap, hcap1, ccap1, nw1, false);
     const int grid1 = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::min(np_, dev_cu * bpc1), SCRATCH_MAX / per1));
     hipError_t e2;
     int rc2;
@@ -82,7 +87,7 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     s1.n_order = np_;
     s1.scratch = d_scr1.p;
     s1.scratch_stride = per1;
-    s1.fcap = fcap;
+    s1.fcap = wfcap;
     s1.hcap = hcap1;
     s1.ccap = ccap1;
     s1_tier(160 * 1024 / bpc1 - 256, pan.amax, nw1, s1.lds_fc, s1.lds_hc, s1.lds_cc);
@@ -160,7 +165,9 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   std::fill(rs.begin(), rs.end(), 0ull);  // regions of size 0: counting only
   if ((rc = structure(0, pick.data(), (int)pick.size(), false, 2, true))) return rc;
   double rl = 0, tl = 0, rmean = 0, tmean = 0;
+  int probe_fmax = 1;
   for (int bi : pick) {
+    probe_fmax = std::max(probe_fmax, hf[bi]);
     if ((rc = restart_status(h_status[bi]))) return rc;
     rl = std::max(rl, (double)hr[bi] / LP);
     tl = std::max(tl, (double)ht[bi] / LP);
@@ -257,11 +264,12 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     const int wl = bound[w + 1] - bound[w];
     const bool heavy = rsum / ((double)k_ * wl) > 1500.0;
     const int per_cu = (k_ + dev_cu - 1) / dev_cu;
-    // heavy groups whose mean frontier is past twice the LDS tier of a 4 x 4
-    // block take a whole CU per individual (cfg 4's E1, ~1 700 states per
-    // locus: values 14.3 -> 13.7 s; cfg 3's E1, ~470: 4 x 4 stays)
+    // heavy groups whose mean frontier is past three times the LDS tier of a
+    // 4 x 4 block take a whole CU per individual (cfg 4's E1, ~1 600 states per
+    // locus: values 14.3 -> 13.4-13.7 s; cfg 3's E1, ~430: 4 x 4 stays — 16 x
+    // 1 there: 270-300 instead of ~215 ms per window)
     const double fmean = (tsum / std::max(1.0, (double)k_ * wl) - 2.0) / (1.0 + S);
-    const bool small_heavy = heavy && (per_cu < 4 || (vp_nw == 0 && fmean > 2.0 * s2_tier(S, 4, 4, S <= 16)));
+    const bool small_heavy = heavy && (per_cu < 4 || (vp_nw == 0 && fmean > 3.0 * s2_tier(S, 4, 4, S <= 16)));
     const int sh_ipc = per_cu < 4 ? per_cu : 1;
     const int vnw = vp_nw > 0 ? vp_nw : (small_heavy ? 16 / sh_ipc : (heavy ? 4 : (k_ >= 32 * dev_cu ? 1 : (k_ >= 8 * dev_cu ? 2 : 3))));
     const int vipc = vp_ipc > 0 ? vp_ipc : (small_heavy ? sh_ipc : (vnw == 1 ? 16 : (vnw >= 8 ? 2 : (vnw >= 4 ? 4 : 8))));
@@ -338,6 +346,12 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   auto window = [&](int w, std::vector<int32_t> &grp) -> int {
     std::vector<int32_t> todo(grp), dead;
     bool first = true;
+    {
+      int fprev = probe_fmax;
+      if (w > 0)
+        for (int bi : grp) fprev = std::max(fprev, fw[(size_t)bi * nwin + w - 1]);
+      wfcap = std::max(std::min(4096, fcap), std::min(fcap, next_pow2(2 * std::max(fprev, 1))));
+    }
     if ((e = hipMemcpyAsync(d_ck_cursor.p, &zero64, 8, hipMemcpyHostToDevice, st))) return hipfail(e, "windowed E-step");
     if (w % 2 == 0) tr_lo = 0;
     else tr_hi = d_trace.n;
@@ -367,8 +381,9 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
         if (grow) {
           for (int bi : todo) {
             const int s = h_status[bi];
-            if (s == EST_OVERFLOW_FRONTIER && fcap < F_MAX) {
-              fcap = (int)std::min<int64_t>(F_MAX, (int64_t)fcap * 4);
+            if (s == EST_OVERFLOW_FRONTIER && wfcap < F_MAX) {
+              wfcap = (int)std::min<int64_t>(F_MAX, (int64_t)wfcap * 4);
+              fcap = std::max(fcap, wfcap);
               break;
             }
           }
@@ -378,10 +393,10 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
               break;
             }
           for (int bi : todo)
-            if ((h_status[bi] == EST_OVERFLOW_FRONTIER && fcap >= F_MAX) ||
-                (h_status[bi] == EST_OVERFLOW_CONTRIB && (int64_t)ccap_mult * fcap >= INT32_MAX))
+            if ((h_status[bi] == EST_OVERFLOW_FRONTIER && wfcap >= F_MAX) ||
+                (h_status[bi] == EST_OVERFLOW_CONTRIB && (int64_t)ccap_mult * wfcap >= INT32_MAX))
               return fail(HMC_EUNSUPPORTED, "frontier exceeds %d states", F_MAX);
-          if (debug_mem) fprintf(stderr, "[hmc] window %d/%d: capacities %d states x %d, the window again\n", w + 1, nwin, fcap, ccap_mult);
+          if (debug_mem) fprintf(stderr, "[hmc] window %d/%d: capacities %d states x %d, the window again\n", w + 1, nwin, wfcap, ccap_mult);
           if ((e = hipMemcpyAsync(d_ck_cursor.p, &zero64, 8, hipMemcpyHostToDevice, st))) return hipfail(e, "windowed E-step");
           continue;
         }

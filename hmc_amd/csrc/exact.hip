@@ -170,6 +170,32 @@ __global__ __launch_bounds__(256) void exact_fb(ExactArgs a) {
   }
 }
 
+// The walk's largest per-item span (exact_walk's scratch layout): the states
+// of records max(s + d, head_len), d = 0..max_depth + 1, over every start
+// locus s of every individual of the group (block per individual).
+__global__ __launch_bounds__(256) void exact_span(ExactArgs a) {
+  const int tid = threadIdx.x, NT = blockDim.x;
+  const int L = a.L, hl = a.head_len;
+  for (int q = blockIdx.x; q < a.n_order; q += gridDim.x) {
+    const int bi = a.order[q];
+    const int st0 = a.status[bi];
+    if (st0 != EST_OK && st0 != EST_OK_PRUNED) continue;
+    const unsigned long long *roff = a.rec_off + (size_t)bi * (L + 1);
+    unsigned sp = 0;
+    for (int s0 = tid; s0 < L; s0 += NT) {
+      unsigned long long sum = 0;
+      for (int d = 0; d <= a.max_depth + 1; ++d) {
+        const int r = s0 + d > hl ? s0 + d : hl;
+        if (r > L) break;
+        sum += a.rec[roff[r]];
+      }
+      const unsigned v = (unsigned)(sum < 0xFFFFFFFFull ? sum : 0xFFFFFFFFull);
+      sp = v > sp ? v : sp;
+    }
+    atomicMax(a.span_max, sp);
+  }
+}
+
 // One contribution's terms into a child list set (HaploBuilder.cpp:375-427):
 // ma / mb = the child's allele is the pair's a / b allele at this locus.
 __device__ inline void walk_terms(bool ma, bool mb, bool rev, double w0, double w1, double w2, double tp, double &n0,
@@ -210,13 +236,17 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
   unsigned long long *stk64 = lds64 + (size_t)g * (exact_walk_lds_bytes(maxd, a.fmax) / 8);
   unsigned long long *sdesc = stk64, *smask = stk64 + D;
   int *snode = (int *)(stk64 + 2 * D), *snext = snode + D, *sslot = snext + D, *tcnt = sslot + D;
-  uint32_t *marks = (uint32_t *)(tcnt + D);  // [fmax/32 + 1] reached-state bitmap
+  int *sF = tcnt + D, *soff = sF + D;        // per depth: the states of its locus, their first entry in the item's layout
+  uint32_t *marks = (uint32_t *)(soff + D);  // [fmax/32 + 1] reached-state bitmap
   const int nwords = (a.fmax + 31) >> 5;
-  const size_t slot_doubles = (size_t)3 * a.fmax;
-  double *lists = a.scratch + ((size_t)blockIdx.x * NG + g) * a.scratch_stride;  // [maxd+1][W][3][fmax]
-  double *cfreq = lists + (size_t)(maxd + 1) * W * slot_doubles;          // [maxd+2][W]
-  uint32_t *touched = (uint32_t *)(cfreq + (size_t)(maxd + 2) * W);       // [maxd+1][fmax]
-  auto slot = [&](int d, int i) { return lists + ((size_t)d * W + i) * slot_doubles; };
+  // The item's lists: per depth d, W slots of three lists over the F_d states
+  // of d's locus (slot i of depth d at 3 (W soff[d] + i F_d)); the wave's
+  // region holds the largest such span of any item (ExactArgs::span)
+  double *lists = a.scratch + ((size_t)blockIdx.x * NG + g) * a.scratch_stride;  // [3 W span]
+  double *cfreq = lists + (size_t)3 * W * a.span;                          // [maxd+2][W]
+  uint32_t *touched = (uint32_t *)(cfreq + (size_t)(maxd + 2) * W);       // [span]: per depth at soff[d]
+  auto slot = [&](int d, int i) { return lists + (size_t)3 * ((size_t)W * soff[d] + (size_t)i * sF[d]); };
+  auto tch = [&](int d) { return touched + soff[d]; };
   for (int d = gl; d < D; d += GL) {
     tcnt[d] = 0;
     smask[d] = 0ull;
@@ -236,6 +266,27 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
     const unsigned long long *xo = a.x_off + (size_t)bi * (L + 1);
     const uint32_t *Rh = a.rec + roff[hl];
     const int Fh = (int)Rh[0];
+    {  // the item's layout: depth d's states are those of record max(start + d, head_len)
+      int carry = 0;
+      for (int d0 = 0; d0 < D; d0 += GL) {
+        const int dd = d0 + gl;
+        const int r = start + dd > hl ? start + dd : hl;
+        const int f = dd < D && r <= L ? (int)a.rec[roff[r]] : 0;
+        int incl = f;
+#pragma unroll
+        for (int o = 1; o < GL; o <<= 1) {
+          const int y = __shfl_up(incl, o, GL);
+          if (gl >= o) incl += y;
+        }
+        if (dd < D) {
+          sF[dd] = f;
+          soff[dd] = carry + incl - f;
+        }
+        carry += __shfl(incl, GL - 1, GL);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
     // depth 0: every state after max(start, head_len) loci, weight = forward likelihood
     {
       const int e0 = start > hl ? start : hl;
@@ -274,9 +325,10 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
         }
         const int locus = start + d;  // the children's allele is at this locus
         const double last_freq = d == 0 ? 1.0 : cfreq[(size_t)d * W + sslot[d]];  // prefix freq (HaploBuilder.cpp:305)
-        const double *P0 = slot(d, sslot[d]), *P1 = P0 + a.fmax, *P2 = P1 + a.fmax;
-        const uint32_t *Tp = touched + (size_t)d * a.fmax;
-        uint32_t *Tc = touched + (size_t)(d + 1) * a.fmax;
+        const int Fpd = sF[d], Fc = sF[d + 1];  // this depth's states, the children's
+        const double *P0 = slot(d, sslot[d]), *P1 = P0 + Fpd, *P2 = P1 + Fpd;
+        const uint32_t *Tp = tch(d);
+        uint32_t *Tc = tch(d + 1);
         {  // the previous sibling's children at depth d+1 back to zero
           const int nc = tcnt[d + 1];
           const unsigned long long wm = smask[d + 1];
@@ -285,8 +337,8 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
             for (unsigned long long m = wm; m; m &= m - 1) {
               double *C0 = slot(d + 1, __builtin_ctzll(m));
               C0[t] = 0.0;
-              C0[a.fmax + t] = 0.0;
-              C0[2 * a.fmax + t] = 0.0;
+              C0[Fc + t] = 0.0;
+              C0[2 * Fc + t] = 0.0;
             }
           }
         }
@@ -320,8 +372,8 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
               if (mb) n2 += w2;
               double *C0 = slot(d + 1, (int)i);
               C0[t] = n0;
-              C0[a.fmax + t] = n1;
-              C0[2 * a.fmax + t] = n2;
+              C0[Fc + t] = n1;
+              C0[2 * Fc + t] = n2;
             }
             Tc[t] = (uint32_t)t;
           }
@@ -396,14 +448,14 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
             if (ca) {
               double *C0 = slot(d + 1, (int)xa);
               C0[t] = a0;
-              C0[a.fmax + t] = a1;
-              C0[2 * a.fmax + t] = a2;
+              C0[Fc + t] = a1;
+              C0[2 * Fc + t] = a2;
             }
             if (cb) {
               double *C0 = slot(d + 1, (int)xb);
               C0[t] = b0;
-              C0[a.fmax + t] = b1;
-              C0[2 * a.fmax + t] = b2;
+              C0[Fc + t] = b1;
+              C0[2 * Fc + t] = b2;
             }
           }
         }
@@ -420,7 +472,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
           bool any = false;
           for (int j = gl; j < ntc; j += GL) {
             const uint32_t t = Tc[j];
-            const double n0 = C0[t], n1 = C0[a.fmax + t], n2 = C0[2 * a.fmax + t];
+            const double n0 = C0[t], n1 = C0[Fc + t], n2 = C0[2 * Fc + t];
             const double v = ((n0 + n1) + n2) * bw[t];
             if constexpr (NG == 1) {
               part[0] += v;
@@ -476,14 +528,15 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
     for (int dd = 0; dd <= maxd; ++dd) {
       const int nc = tcnt[dd];
       const unsigned long long wm = smask[dd];
-      const uint32_t *T = touched + (size_t)dd * a.fmax;
+      const uint32_t *T = tch(dd);
+      const int Fd = sF[dd];
       for (int j = gl; j < nc; j += GL) {
         const uint32_t t = T[j];
         for (unsigned long long m = wm; m; m &= m - 1) {
           double *D0 = slot(dd, __builtin_ctzll(m));
           D0[t] = 0.0;
-          D0[a.fmax + t] = 0.0;
-          D0[2 * a.fmax + t] = 0.0;
+          D0[Fd + t] = 0.0;
+          D0[2 * Fd + t] = 0.0;
         }
       }
     }
@@ -759,15 +812,21 @@ hipError_t launch_exact_walk_units(const ExactArgs &a, const XWalkArgs &x, int g
 hipError_t launch_exact_walk_units(const ExactArgs &, const XWalkArgs &, int, hipStream_t) { return hipErrorNotSupported; }
 #endif
 
-size_t exact_walk_scratch_doubles(int max_depth, int fmax, int width) {
-  return (size_t)(max_depth + 1) * width * 3 * fmax + (size_t)(max_depth + 2) * width +
-         ((size_t)(max_depth + 1) * fmax + 1) / 2;
+size_t exact_walk_scratch_doubles(int max_depth, long long span, int width) {
+  return (size_t)3 * width * (size_t)span + (size_t)(max_depth + 2) * width + ((size_t)span + 1) / 2;
 }
 
 
 hipError_t launch_exact_fb(const ExactArgs &a, int grid, hipStream_t st) {
   if (a.n_order <= 0) return hipSuccess;
   hipLaunchKernelGGL(exact_fb, dim3(grid), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_exact_span(const ExactArgs &a, int grid, hipStream_t st) {
+  if (a.n_order <= 0) return hipSuccess;
+  if (!a.span_max) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(exact_span, dim3(grid), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

@@ -32,6 +32,8 @@ struct ExactArgs {
   double *scratch;
   size_t scratch_stride;           // doubles
   int fmax;                        // most states of any locus of the group
+  long long span = 0;              // the walk's per-item list span: most states over max_depth + 2 consecutive depths
+  unsigned *span_max = nullptr;    // exact_span: atomicMax of each individual's largest span (zeroed by the host)
   unsigned long long *acc_freq, *acc_prefix;  // [candidates] fixed point
   long long item0 = 0, item1 = -1;  // walk items [item0, item1) of n_order x L (individual-major); -1 = all
 };
@@ -70,13 +72,15 @@ struct XWalkArgs {
 hipError_t launch_exact_walk_units(const ExactArgs &a, const XWalkArgs &x, int grid, hipStream_t st);
 
 hipError_t launch_exact_fb(const ExactArgs &a, int grid, hipStream_t st);
+// ExactArgs::span_max (atomicMax, zeroed by the caller) over the group
+hipError_t launch_exact_span(const ExactArgs &a, int grid, hipStream_t st);
 // items_per_wave 1 (64 lanes per item) or 4 (16 lanes each); scratch: grid x items x stride
 hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st, int items_per_wave = 1);
-size_t exact_walk_scratch_doubles(int max_depth, int fmax, int width);
-// LDS of one walked item: per depth two masks and four ints, the reached-state bitmap (8-byte multiple)
+size_t exact_walk_scratch_doubles(int max_depth, long long span, int width);
+// LDS of one walked item: per depth two masks and six ints, the reached-state bitmap (8-byte multiple)
 __host__ __device__ inline size_t exact_walk_lds_bytes(int max_depth, int fmax) {
   const size_t D = (size_t)max_depth + 2;
-  return (D * 16 + D * 16 + (size_t)((fmax + 31) / 32 + 1) * 4 + 7) & ~(size_t)7;
+  return (D * 16 + D * 24 + (size_t)((fmax + 31) / 32 + 1) * 4 + 7) & ~(size_t)7;
 }
 constexpr size_t EXACT_WALK_LDS_MAX = 160 * 1024;  // gfx950 LDS per workgroup
 

@@ -130,37 +130,63 @@ def test_windowed_equals_classic_cfg2():
     assert runs[0] == runs[1] == runs[2]
 
 
+def _heartbeat(path, stop):
+    """A line every 30 s under gpurun_out/ while a multi-minute test runs, so
+    that a runner watching its output directory sees progress."""
+    import threading
+    import time
+
+    def beat():
+        t0 = time.time()
+        while not stop.wait(30.0):
+            try:
+                os.makedirs(os.path.dirname(path), exist_ok=True)
+                with open(path, "a") as f:
+                    f.write(f"cfg 4 rank-0 test alive {time.time() - t0:.0f} s\n")
+            except OSError:
+                pass
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    return th
+
+
 @pytest.mark.slow
 @pytest.mark.timeout(900)
-@pytest.mark.skipif(os.environ.get("HMC_RUN_CFG4") != "1",
-                    reason="cfg 4 rank slice (~3 min, 50 000 x 5 000 panel): HMC_RUN_CFG4=1")
 def test_cfg4_rank0_real_shard_windowed_e1():
-    """Rank 0's real E1 of the 8-GPU cfg 4 run on one GPU: the global M0 over
-    all 50 000 individuals (what every rank holds after the sharded M0), then
-    the E-step over rank 0's balanced shard (hmc_set_shard).  It runs in
-    automatic windows (one group); the samples phase the genotypes, weights
-    sum to 1, priors are sorted; windows of 40 loci give the same LL, R_E,
+    """Rank 0's real E1 of the 8-GPU cfg 4 run on one GPU (~3 min): the global
+    M0 over all 50 000 individuals (what every rank holds after the sharded
+    M0), then the E-step over rank 0's balanced shard (hmc_set_shard).  It
+    runs in automatic windows (one group); the samples phase the genotypes,
+    weights sum to 1, priors are sorted; a second E1 repeats LL, H, R_E,
     samples and weights bit for bit."""
+    import threading
+
     from hmc_amd.model import balanced_shard
     from test_gpu_parity import _estep_properties
 
-    p = synth.config_panel(4)
-    m = gpu_model(p)
-    m.find_patterns()
-    i0, i1 = balanced_shard(p.alleles, 0, 8)
-    m.set_shard(i0, i1)
-    sub = types.SimpleNamespace(N=i1 - i0, alleles=p.alleles[i0:i1])
-    del p
-    out = []
-    for wl in (0, 40):
-        m.set_estep_windows("auto" if wl == 0 else "always", wl)
-        ll, H, re = m.resolve_all()
-        w = m.estep_windows()
-        assert w["windows"] >= 2 and (wl or w["groups"] == 1), w
-        if wl == 0:
-            _estep_properties(m, sub, ll, H)
-        al, wt, tw = m.samples(H)
-        out.append((float(ll).hex(), H, re, hash(al.tobytes()), wt.tobytes(), float(tw).hex()))
-        del al
-    assert out[0] == out[1]
-    m.close()
+    stop = threading.Event()
+    _heartbeat(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out",
+                            "heartbeat_cfg4_test"), stop)
+    try:
+        p = synth.config_panel(4)
+        m = gpu_model(p)
+        m.find_patterns()
+        i0, i1 = balanced_shard(p.alleles, 0, 8)
+        m.set_shard(i0, i1)
+        sub = types.SimpleNamespace(N=i1 - i0, alleles=p.alleles[i0:i1])
+        del p
+        out = []
+        for rep in range(2):
+            ll, H, re = m.resolve_all()
+            w = m.estep_windows()
+            assert w["windows"] >= 2 and w["groups"] == 1, w
+            if rep == 0:
+                _estep_properties(m, sub, ll, H)
+            al, wt, tw = m.samples(H)
+            out.append((float(ll).hex(), H, re, hash(al.tobytes()), wt.tobytes(), float(tw).hex()))
+            del al
+        assert out[0] == out[1]
+        m.close()
+    finally:
+        stop.set()
