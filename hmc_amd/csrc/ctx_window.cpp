@@ -264,12 +264,12 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     const int wl = bound[w + 1] - bound[w];
     const bool heavy = rsum / ((double)k_ * wl) > 1500.0;
     const int per_cu = (k_ + dev_cu - 1) / dev_cu;
-    // heavy groups whose mean frontier is past three times the LDS tier of a
-    // 4 x 4 block take a whole CU per individual (cfg 4's E1, ~1 600 states per
-    // locus: values 14.3 -> 13.4-13.7 s; cfg 3's E1, ~430: 4 x 4 stays — 16 x
-    // 1 there: 270-300 instead of ~215 ms per window)
+    // heavy groups whose mean frontier passes 1 000 states take a whole CU per
+    // individual (cfg 4's E1, ~1 600 states per locus: values 14.3 -> 13.4-13.7
+    // s; cfg 3's E1, ~430: 4 x 4 stays — 16 x 1 there: 270-300 instead of ~215
+    // ms per window, E1 values 2.10 -> 2.75 s)
     const double fmean = (tsum / std::max(1.0, (double)k_ * wl) - 2.0) / (1.0 + S);
-    const bool small_heavy = heavy && (per_cu < 4 || (vp_nw == 0 && fmean > 3.0 * s2_tier(S, 4, 4, S <= 16)));
+    const bool small_heavy = heavy && (per_cu < 4 || (vp_nw == 0 && fmean > 1000.0));
     const int sh_ipc = per_cu < 4 ? per_cu : 1;
     const int vnw = vp_nw > 0 ? vp_nw : (small_heavy ? 16 / sh_ipc : (heavy ? 4 : (k_ >= 32 * dev_cu ? 1 : (k_ >= 8 * dev_cu ? 2 : 3))));
     const int vipc = vp_ipc > 0 ? vp_ipc : (small_heavy ? sh_ipc : (vnw == 1 ? 16 : (vnw >= 8 ? 2 : (vnw >= 4 ? 4 : 8))));
