@@ -41,6 +41,9 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   // budgets (words) from the free HBM, within the caller's store caps when set
   // (ranks sharing one GPU: hmc_set_store_budgets / hmc_set_tuning)
   const bool capped = trace_bytes || rec_bytes;
+  // (pooling the two budgets and splitting them by need gave cfg 3's E1 8
+  // windows instead of 10 and 1 % — but stores past the classic E-step's
+  // budgets are re-mapped by the next E2, seconds per chain step: not kept)
   const uint64_t rbud = std::min<uint64_t>((uint64_t)std::min(0.27 * pool, (double)(88ull << 30)) / 4, capped ? rec_budget : ~0ull);
   const uint64_t tbud = std::min<uint64_t>((uint64_t)std::min(0.40 * pool, (double)(130ull << 30)) / 4, capped ? trace_budget : ~0ull);
   const uint64_t cbud = std::min<uint64_t>((uint64_t)std::min(0.12 * pool, (double)(40ull << 30)) / 4, capped ? trace_budget / 3 : ~0ull);
