@@ -26,9 +26,11 @@ WORLD_SIZE is not set and --gpus N > 1, by this script itself: it starts N
 fresh worker processes (rank env set, 127.0.0.1 rendezvous) before anything
 touches a GPU and exits with their status.  The panel is the same (strong
 scaling): individuals are sharded in contiguous blocks; the M-step's per-level
-candidate sums are reduced in rank order over RCCL inside libhmc_amd (chained
-ncclBroadcast of seeded partial sums: bit-identical to one GPU;
-hmc_set_reduction selects a single ncclAllReduce instead).  torch.distributed
+candidate sums are reduced in rank order over RCCL inside libhmc_amd (a
+point-to-point chain: rank r receives the running sums from r-1, continues
+them over its own items and sends them to r+1, then rank W-1 broadcasts the
+totals once — bit-identical to one GPU; hmc_set_reduction selects a single
+ncclAllReduce instead).  torch.distributed
 (gloo) only bootstraps the RCCL id, the barriers and the max-over-ranks time.
 """
 from __future__ import annotations
@@ -329,7 +331,10 @@ def main():
         hbm_frac_meas = pmc["hbm_bytes_per_launch"] / (val_ms * 1e-3 / n_launch) / 1e9 / HBM_PEAK_GBS
     bound = "hbm"
     if sq and sq.get("valu_issue_frac") is not None:
-        bound = "valu-issue" if sq["valu_issue_frac"] > (hbm_frac_meas or achieved / HBM_PEAK_GBS) else "hbm"
+        hbm_f = hbm_frac_meas or achieved / HBM_PEAK_GBS
+        bound = "valu-issue" if sq["valu_issue_frac"] > hbm_f else "hbm"
+        if max(sq["valu_issue_frac"], hbm_f) < 0.5:  # neither roof near: the waves wait (SQ_WAIT_ANY)
+            bound = "latency"
 
     if rank == 0:
         line = {
@@ -352,7 +357,7 @@ def main():
                             f"(E_k, accept, HaploComp, M_k while continuing; restart from M0 after the stop)",
                 "individuals": N, "loci": L, "sample_size": args.sample_size,
                 "min_freq_abs": 1.5, "pattern_len": [1, 30],
-                "parallelism": f"individual-sharded x{world}, " + ("ordered RCCL reduction (chained broadcasts)" if args.reduction == "ordered"
+                "parallelism": f"individual-sharded x{world}, " + ("ordered RCCL reduction (send/recv chain + one broadcast)" if args.reduction == "ordered"
                                                                      else "RCCL all-reduce") + " per mining level"
                                + (" [REHEARSAL: gloo host collective, ranks sharing GPUs - not a measurement]"
                                   if world > 1 and args.collective == "host" else ""),
