@@ -667,12 +667,18 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
       // frontier, cfg 3 E1 values 2 192 -> 2 134 ms against 8 x 2,
       // profiles/r04/shapes/value_shapes_cfg3.log; with the round-3 frontier
       // 8 x 2 had won, 2.95 -> 2.68 s, profiles/r03/e1/e1_wide.log)
+      // (five per CU: 4 waves x 5 on the 5-waves-per-SIMD build, one round
+      // instead of 1.2 — cfg 3's E1 on rank 0 of 8, 1 239 individuals: values
+      // 296 -> 262 ms; 3 x 5 and 2 x 8 383-386 ms; at ten per CU 4 x 4 stays:
+      // 481 ms against 583-869, profiles/r05/shards/)
+      const bool five_heavy = heavy && per_cu == 5;
       int vnw = vp_nw > 0 ? vp_nw
                           : (small_heavy ? 16 / per_cu
                                          : (heavy ? 4 : ((int)k >= 32 * dev_cu ? 1 : ((int)k >= 8 * dev_cu ? 2 : 3))));
       int vipc = vp_ipc > 0 ? vp_ipc
                             : (small_heavy ? per_cu
-                                           : (vnw == 1 ? 16 : (vnw >= 8 ? 2 : (vnw >= 4 ? 4 : 8))));  // a half-given shape completes by the same rule
+                                           : (five_heavy && vnw == 4 ? 5
+                                                                     : (vnw == 1 ? 16 : (vnw >= 8 ? 2 : (vnw >= 4 ? 4 : 8)))));  // a half-given shape completes by the same rule
       // (one wave per individual: 16 per CU on the 4-wave build since the
       // swap-count cut, cfg 3 E3 values 507 -> 479 ms, E2 equal; 20 on the
       // 5-wave build before, profiles/r04/shapes/one_wave_16_vs_20_cfg3.log)

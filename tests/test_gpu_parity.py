@@ -107,7 +107,7 @@ def _estep_on_reference_model(oracle_mod, name, S, mode):
 # shapes the rule never picks on the stress panel (3 alleles, 5 % missing)
 _AUTO_SHAPES = [(1, 12, 1, 20), (4, 2, 8, 2), (1, 8, 2, 8), (1, 4, 3, 8), (16, 1, 16, 1), (16, 1, 8, 2)]
 _STRESS_SHAPES = [(4, 3, 4, 4), (4, 1, 2, 8), (4, 2, 16, 1), (1, 8, 8, 2), (4, 2, 5, 3), (8, 2, 8, 2),
-                  (1, 16, 1, 20), (1, 20, 2, 8)]
+                  (1, 16, 1, 20), (1, 20, 2, 8), (4, 2, 4, 5)]
 
 
 @pytest.mark.parametrize("name,shape", [(n, s) for n in ("a3miss5", "n300") for s in _AUTO_SHAPES]
