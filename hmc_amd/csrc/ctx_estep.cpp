@@ -749,7 +749,8 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
       ms_s2 += ms;
       ++n_value_passes;
       if (debug_mem)
-        fprintf(stderr, "[hmc] value pass %d: %zu individuals, %.1f ms\n", n_value_passes, k, ms);
+        fprintf(stderr, "[hmc] value pass %d: %zu individuals, %d x %d per CU (%.0f record words per individual-locus), %.1f ms\n",
+                n_value_passes, k, vnw, vipc, rw / ((double)k * L), ms);
       // ---- ties: individuals whose result would depend on the libstdc++ list
       // order re-run on the exact value pass, in their own trace regions
       std::vector<int> h_order;
