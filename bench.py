@@ -263,7 +263,7 @@ def main():
                     tb_ms=t["estep_traceback_ms"], mstep_ms=t["mstep_ms"] if go or force_m else 0.0,
                     value_dataflow=m.last_value_pass_dataflow(), reduction_ms=ms_stats["reduction_ms"],
                     reduction_levels=ms_stats["reduction_levels"], windows=win["windows"],
-                    recompute_ms=win["recompute_ms"])
+                    collection_ms=win["collection_ms"])
 
     for _ in range(args.warmup):
         em_step()

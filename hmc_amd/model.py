@@ -244,7 +244,7 @@ class HaploModel:
         self.i0, self.i1 = int(i0), int(i1)
 
     def set_estep_windows(self, mode: str = "auto", window_loci: int = 0):
-        """Checkpoint-and-recompute E-step (hmc_set_estep_windows): "auto",
+        """Windowed E-step (hmc_set_estep_windows): "auto",
         "never" or "always"; window_loci = loci per window (0: from the store
         budgets).  Results are identical."""
         self._check(lib().hmc_set_estep_windows(self._h, {"auto": 0, "never": 1, "always": 2}[mode], int(window_loci)))
@@ -252,7 +252,7 @@ class HaploModel:
     def estep_windows(self) -> dict:
         w, wl, g, ms = C.c_int(), C.c_int(), C.c_int(), C.c_double()
         self._check(lib().hmc_last_estep_windows(self._h, C.byref(w), C.byref(wl), C.byref(g), C.byref(ms)))
-        return dict(windows=w.value, window_loci=wl.value, groups=g.value, recompute_ms=ms.value)
+        return dict(windows=w.value, window_loci=wl.value, groups=g.value, collection_ms=ms.value)
 
     def set_value_mode(self, mode: str):
         """Value pass of the split E-step: "fast" (value-only k-best lists, the

@@ -72,7 +72,8 @@ const char *hmc_ctx_error(const hmc_ctx *ctx);
  * continues each running sum of ranks 0..r-1 over its contiguous block of
  * items, which reproduces the reference's sequential sums
  * (PatternManager.cpp:254-262, HaploModel.cpp:110, HaploData.cpp:120-126) bit
- * for bit — W chained steps per mining level; 1 = all-reduce of per-rank
+ * for bit — a point-to-point chain per mining level (ncclRecv from r-1,
+ * the rank's adds, ncclSend to r+1; one ncclBroadcast from W-1); 1 = all-reduce of per-rank
  * partial sums (one collective, sums reassociated: last-bit drift, which can
  * flip a pattern at the min_freq threshold). */
 int hmc_set_reduction(hmc_ctx *ctx, int mode);
@@ -399,19 +400,21 @@ int hmc_set_end_order(hmc_ctx *ctx, int on);
 int hmc_set_exact_walk(hmc_ctx *ctx, int items_per_wave);
 /* 1 when the last value-pass launch ran the dataflow schedule. */
 int hmc_last_value_pass(const hmc_ctx *ctx, int *dataflow);
-/* Checkpoint-and-recompute E-step (SURVEY §7 hard part 4): the loci in
- * windows, each window's last frontier saved as the next one's checkpoint;
- * the forward keeps one window of records and traces per individual, the
- * traceback recomputes each earlier window from its checkpoint.  Results are
+/* Windowed E-step (SURVEY §7 hard part 4): the loci in windows, each
+ * window's last frontier saved as the next one's checkpoint; records are kept
+ * for one window and full traces for two, the older one collected into
+ * survivor nodes (the entries the traceback can still reach).  Results are
  * identical to the classic passes.  mode 0 (default): automatic — when the
  * first loci of a sample show that the classic passes could hold fewer than
- * two individuals per CU in a group (cfg 4's per-rank E1); 1 never; 2 always
- * (tests).  window_loci: loci per window (0: from the store budgets).
+ * two individuals per CU in a group (cfg 4's per-rank E1) or would need three
+ * or more groups (cfg 3's E1); 1 never; 2 always (tests).  window_loci: loci
+ * per window (0: from the store budgets).
  * Replaces no reference interface (HaploBuilder::resolve keeps every locus's
  * pairs alive, HaploBuilder.cpp:35-126). */
 int hmc_set_estep_windows(hmc_ctx *ctx, int mode, int window_loci);
 /* The last E-step's windows (0 = classic passes), loci per window, groups of
- * individuals, and device ms of the recompute (backward) passes. */
+ * individuals, and device ms of the trace collections (part of the value
+ * passes' time). */
 int hmc_last_estep_windows(const hmc_ctx *ctx, int *windows, int *window_loci, int *groups, double *recompute_ms);
 /* Individuals the last E-step re-ran with the libstdc++ permutations (mode 0)
  * and the device time of those re-runs (ms, part of values_ms). */

@@ -46,7 +46,7 @@ for rep, sh in enumerate(shapes):
     fr = m.estep_frontier()
     print(f"E1 run {rep} shapes {sh}: wall {wall:.2f} s; device: structure {s['structure_ms']:.0f} ms "
           f"({s['structure_passes']} passes), values {s['values_ms']:.0f} ms ({s['value_passes']}; trace collection "
-          f"{w['recompute_ms']:.0f} of it), traceback {t['estep_traceback_ms']:.0f} ms, fallback {s['fallback_ms']:.0f} ms "
+          f"{w['collection_ms']:.0f} of it), traceback {t['estep_traceback_ms']:.0f} ms, fallback {s['fallback_ms']:.0f} ms "
           f"({s['n_fallback']}); windows {w['windows']} of {w['window_loci']} loci in {w['groups']} group(s); "
           f"frontier {fr}; LL {ll!r} H {H} R_E {re}", flush=True)
     if ref is None:

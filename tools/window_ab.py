@@ -31,7 +31,7 @@ for mode, wl in sets:
         s = m.estep_split_stats()
         w = m.estep_windows()
         print(f"{mode}:{wl} run {rep}: wall {wall * 1e3:.0f} ms; structure {s['structure_ms']:.0f} ms ({s['structure_passes']}), "
-              f"values {s['values_ms']:.0f} ms ({s['value_passes']}; collection {w['recompute_ms']:.0f}), "
+              f"values {s['values_ms']:.0f} ms ({s['value_passes']}; collection {w['collection_ms']:.0f}), "
               f"traceback {m.timings()['estep_traceback_ms']:.0f} ms; windows {w['windows']} of {w['window_loci']} loci, "
               f"{w['groups']} group(s); LL {ll!r} R_E {re}", flush=True)
         key = (float(ll).hex(), H, re)
