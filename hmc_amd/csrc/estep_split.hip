@@ -1864,11 +1864,13 @@ hipError_t launch_estep_structure2(const StructArgs &, int, int, hipStream_t) { 
 // the marked entries of [lo0, mid) as nodes (ascending key per locus; the
 // predecessor's node by a prefix popcount of the locus below, or by a binary
 // search of the boundary list of the window before).
+constexpr uint32_t GC_LDS_WORDS = 1024;  // marks of loci up to 32 768 list entries in LDS (8 KB per block)
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void estep_trace_gc(TraceGcArgs a) {
   constexpr int NT = 64 * NW;
   __shared__ unsigned long long red64[16];  // Blk<NW <= 4>: 2 NW + 8 ints, then NW u64 (8-byte aligned)
   __shared__ int sq;
+  __shared__ uint32_t lmk[2][GC_LDS_WORDS];  // two loci's marks
   const int tid = threadIdx.x, lane = lane_id(), wv = tid / WAVE;
   const Blk<NW> B{(int *)red64, tid, lane, wv};
   const int S = a.S, L = a.L, hl = a.head_len;
@@ -1893,37 +1895,62 @@ __global__ __launch_bounds__(64 * NW) void estep_trace_gc(TraceGcArgs a) {
     B.sync();
     for (uint32_t w = tid; w < acc; w += NT) M[w] = 0u;
     B.sync();
-    // ---- every list entry of the last locus, then backward along the links
+    // ---- every list entry of the last locus, then backward along the links.
+    // A locus's marks live in one of two LDS buffers when they fit (LDS
+    // atomics instead of L2 atomics: the first loci back mark nearly every
+    // entry), else in its bitmap in M; marks of [lo0, mid) end up in M for
+    // the compaction below.
+    int cb = 0;  // the LDS buffer holding locus j's marks
     {
       const int j = a.hi1 - 1;
       const uint32_t F = a.trace[lo[j]];
       const uint32_t *hdr = a.trace + lo[j] + 1;
-      uint32_t *Mj = M + moff[j - a.lo0];
-      for (uint32_t t = tid; t < F; t += NT) {
-        const uint32_t n = (hdr[t] >> 16) & 0xFFu;
-        for (uint32_t k = 0; k < n; ++k) {
-          const uint32_t bit = t * (uint32_t)S + k;
-          atomicOr(Mj + (bit >> 5), 1u << (bit & 31u));
+      const uint32_t nw = (F * (uint32_t)S + 31u) >> 5;
+      uint32_t *C = nw <= GC_LDS_WORDS ? lmk[cb] : M + moff[j - a.lo0];
+      for (uint32_t w = tid; w < nw; w += NT) {  // word by word: entries (t, k < nl(t))
+        uint32_t word = 0u;
+        uint32_t t = w * 32u / (uint32_t)S, k = w * 32u - t * (uint32_t)S;
+        uint32_t n = t < F ? (hdr[t] >> 16) & 0xFFu : 0u;
+        for (uint32_t i = 0; i < 32u; ++i) {
+          if (t < F && k < n) word |= 1u << i;
+          if (++k == (uint32_t)S) {
+            k = 0;
+            ++t;
+            n = t < F ? (hdr[t] >> 16) & 0xFFu : 0u;
+          }
         }
+        C[w] = word;
       }
     }
     B.sync();
     for (int j = a.hi1 - 1; j > a.lo0; --j) {
       const uint32_t F = a.trace[lo[j]];
       const uint32_t *links = a.trace + trace_links(lo[j], F);
-      const uint32_t *Mj = M + moff[j - a.lo0];
-      uint32_t *Mp = M + moff[j - 1 - a.lo0];
       const uint32_t nw = (F * (uint32_t)S + 31u) >> 5;
+      const uint32_t nwp = (a.trace[lo[j - 1]] * (uint32_t)S + 31u) >> 5;
+      const uint32_t *Cj = nw <= GC_LDS_WORDS ? lmk[cb] : M + moff[j - a.lo0];
+      const bool pl = nwp <= GC_LDS_WORDS;
+      uint32_t *P = pl ? lmk[cb ^ 1] : M + moff[j - 1 - a.lo0];  // (M starts zeroed)
+      if (pl) {
+        for (uint32_t w = tid; w < nwp; w += NT) P[w] = 0u;
+        B.sync();
+      }
       for (uint32_t w = tid; w < nw; w += NT)
-        for (uint32_t b = Mj[w]; b; b &= b - 1u) {
+        for (uint32_t b = Cj[w]; b; b &= b - 1u) {
           const uint32_t bit = w * 32u + (uint32_t)__builtin_ctz(b);
           const uint32_t m = links[bit];
           if (meta_head(m)) continue;
           const uint32_t pb = meta_pred(m) * (uint32_t)S + meta_idx(m);
-          atomicOr(Mp + (pb >> 5), 1u << (pb & 31u));
+          atomicOr(P + (pb >> 5), 1u << (pb & 31u));
         }
       B.sync();
+      if (pl && j - 1 < a.mid) {  // the older window's marks, for the compaction
+        uint32_t *Mp = M + moff[j - 1 - a.lo0];
+        for (uint32_t w = tid; w < nwp; w += NT) Mp[w] = P[w];
+      }
+      cb ^= 1;
     }
+    B.sync();
     // ---- the survivors of [lo0, mid) as nodes
     unsigned long long cnt = 0;
     for (uint32_t w = tid; w < moff[a.mid - a.lo0]; w += NT) cnt += (unsigned long long)__popc(M[w]);
