@@ -280,6 +280,9 @@ struct Pair {
   // indices into the next locus, and m_backward_likelihood (default 1.0)
   std::vector<int> fl[2];
   double bwd = 1.0;
+  // exact M-step only: the pair's contributions in add order (predecessor,
+  // reversed) — the order HaploPair.cpp:42 / :66 sums its forward likelihood
+  std::vector<std::pair<int, bool>> in;
 };
 
 struct Sample {  // one weighted haplotype of HaploData (HaploData.h:57-65)
@@ -708,11 +711,13 @@ struct Model {
       if (!aeq(x.alA, x.alB))
         for (auto &l : x.links)
           if (l.homo) { if (rev) l.lik = 0; l.homo = false; }
+      if (track_links) x.in.emplace_back(predIdx, rev);
       nxt.push_back(std::move(x));
       best[key] = (int)nxt.size();
       uni_add((int)nxt.size() - 1, nxt.back().links.data(), (int)nxt.back().links.size());
     } else {
       Pair &x = nxt[it->second - 1];  // HaploPair::add, HaploPair.cpp:63-89
+      if (track_links) x.in.emplace_back(predIdx, rev);
       x.fwd += pred.fwd * x.tp;
       int k = (int)x.links.size();
       int n = (int)pred.links.size();
@@ -898,8 +903,8 @@ struct Model {
   // (PatternManager.cpp:347-438) over HaploBuilder::estimateFrequency
   // (HaploBuilder.cpp:263-450) and the ForwardPatternTree (PatternTree.cpp:179-212).
   // The reference sums the match lists over std::map<HaploPair*, double> in
-  // pointer (allocation) order; here the maps are keyed by state index
-  // (creation order), so sums agree to rounding, not bit for bit.
+  // pointer (allocation) order, which nothing reproduces; here the walk runs
+  // in the device walk's order (xwalk below), so the two agree bit for bit.
   struct FNode { std::vector<int> ch; int data = -1; };
   std::vector<FNode> fnodes;
   std::vector<int> froot;
@@ -933,64 +938,162 @@ struct Model {
           for (int t : x.fl[r]) x.bwd += hp[i + 1][t].bwd * hp[i + 1][t].tp;
       }
   }
-  typedef std::map<int, double> MList;  // state index -> weight
-  // HaploBuilder::estimateFrequency(node, ...) (:334-450); `locus` is the
-  // trie node's locus, lists hold states after locus-1 (heads while locus < head_len)
-  double fwalk(int node, int locus, int a, double last_freq, const MList last[3]) {
-    const int hl = head_len();
-    MList m[3];
-    if (locus < hl) {
-      const std::vector<Pair> &H = hp[hl];
-      for (auto &e : last[0]) {
-        const Pair &x = H[e.first];
-        const int pa = P[x.pa].al[locus], pb = P[x.pb].al[locus];
-        ++R_X;
-        if (aeq(pa, a)) {
-          if (aeq(pb, a)) m[0][e.first] += e.second;
-          else m[1][e.first] += e.second * 0.5;
-        } else if (aeq(pb, a)) {
-          m[2][e.first] += e.second * 0.5;
+  // The same walk (HaploBuilder.cpp:334-450) in the order of the device walk
+  // (hmc_amd/csrc/exact.hip, exact_walk), so that the two agree bit for bit:
+  // the reference sums its match lists in std::map<HaploPair*, double>
+  // pointer order, which no restatement reproduces, so any order is the
+  // reference's up to its allocator; this one is the device's.  All children
+  // of a trie node come from one pass: the states reached from the node's
+  // non-zero states along the forward links whose pair carries some child's
+  // allele, ascending; each gathers its contributions in add order (the
+  // terms of :375-427); a child's frequency is sum(((n0 + n1) + n2) * bwd)
+  // over those states, state j into partial j % 64, the 64 partials reduced
+  // by the butterfly x += x[lane ^ o], o = 32 .. 1; frequencies and prefix
+  // terms accumulate in 2^-44 fixed point (order-free).
+  static constexpr double XFIX = 17592186044416.0;  // 2^44
+  std::vector<uint64_t> xacc_f, xacc_p;
+  struct XLev {
+    std::vector<std::vector<double>> slot;  // [child allele][3 F]
+    std::vector<int> touched;
+  };
+  std::vector<XLev> xlev;
+  static void xterms(bool ma, bool mb, bool rev, double w0, double w1, double w2, double tp, double &n0, double &n1,
+                     double &n2) {
+    if (ma && mb) n0 += w0 * tp;
+    else if (ma) n1 += w0 * tp * 0.5;
+    else n2 += w0 * tp * 0.5;
+    if (!rev ? ma : mb) (!rev ? n1 : n2) += w1 * tp;
+    if (!rev ? mb : ma) (!rev ? n2 : n1) += w2 * tp;
+  }
+  // node at depth d of start locus `start`; its lists over the F states of
+  // record max(start + d, head_len): P[0..3F)
+  void xwalk(int node, int start, int d, int F, const double *P, double last_freq) {
+    const int hl = head_len(), W = g.maxnum();
+    const FNode &nd = fnodes[node];
+    uint64_t cm = 0;
+    for (int i = 0; i < (int)nd.ch.size(); ++i)
+      if (nd.ch[i] >= 0) cm |= 1ull << i;
+    if (!cm) return;
+    const int locus = start + d;
+    if ((int)xlev.size() < d + 2) xlev.resize(d + 2);
+    XLev &C = xlev[d + 1];
+    const bool head = locus < hl;
+    const std::vector<Pair> &Z = hp[head ? hl : locus + 1];
+    const int Fc = (int)Z.size();
+    C.slot.assign(W, std::vector<double>());
+    for (int i = 0; i < W; ++i)
+      if ((cm >> i) & 1ull) C.slot[i].assign(3 * (size_t)Fc, 0.0);
+    C.touched.clear();
+    auto alleles = [&](int t, int &xa, int &xb) {
+      if (head) {
+        xa = g.index(locus, P_al(Z[t].pa, locus));
+        xb = g.index(locus, P_al(Z[t].pb, locus));
+      } else {
+        xa = g.index(locus, Z[t].alA);
+        xb = g.index(locus, Z[t].alB);
+      }
+    };
+    if (head) {  // head pairs: their patterns' alleles, same states (:340-367)
+      for (int t = 0; t < Fc; ++t) {
+        int xa, xb;
+        alleles(t, xa, xb);
+        const double w0 = P[t], w1 = P[F + t], w2 = P[2 * F + t];
+        for (int i = 0; i < W; ++i) {
+          if (!((cm >> i) & 1ull)) continue;
+          const bool ma = xa == i, mb = xb == i;
+          double n0 = 0.0, n1 = 0.0, n2 = 0.0;
+          if (ma) {
+            if (mb) n0 = w0;
+            else n1 = w0 * 0.5;
+          } else if (mb) {
+            n2 = w0 * 0.5;
+          }
+          if (ma) n1 += w1;
+          if (mb) n2 += w2;
+          std::vector<double> &c = C.slot[i];
+          c[t] = n0;
+          c[Fc + t] = n1;
+          c[2 * (size_t)Fc + t] = n2;
+        }
+        C.touched.push_back(t);
+      }
+    } else {  // along the forward links into the states after `locus`
+      const std::vector<Pair> &X = hp[locus];
+      std::vector<char> mark(Fc, 0);
+      for (int s2 = 0; s2 < F; ++s2) {
+        if (P[s2] == 0.0 && P[F + s2] == 0.0 && P[2 * F + s2] == 0.0) continue;
+        for (int r = 0; r < 2; ++r)
+          for (int t : X[s2].fl[r]) {
+            int xa, xb;
+            alleles(t, xa, xb);
+            if (((cm >> xa) & 1ull) || ((cm >> xb) & 1ull)) mark[t] = 1;
+          }
+      }
+      for (int t = 0; t < Fc; ++t) {
+        if (!mark[t]) continue;
+        C.touched.push_back(t);
+        int xa, xb;
+        alleles(t, xa, xb);
+        const bool ca = (cm >> xa) & 1ull, cb = xb != xa && ((cm >> xb) & 1ull);
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, b0 = 0.0, b1 = 0.0, b2 = 0.0;
+        const double tp = Z[t].tp;
+        for (const auto &c : Z[t].in) {
+          const int s2 = c.first;
+          const double w0 = P[s2], w1 = P[F + s2], w2 = P[2 * F + s2];
+          if (ca) xterms(true, xb == xa, c.second, w0, w1, w2, tp, a0, a1, a2);
+          if (cb) xterms(false, true, c.second, w0, w1, w2, tp, b0, b1, b2);
+        }
+        if (ca) {
+          std::vector<double> &v = C.slot[xa];
+          v[t] = a0;
+          v[Fc + t] = a1;
+          v[2 * (size_t)Fc + t] = a2;
+        }
+        if (cb) {
+          std::vector<double> &v = C.slot[xb];
+          v[t] = b0;
+          v[Fc + t] = b1;
+          v[2 * (size_t)Fc + t] = b2;
         }
       }
-      for (auto &e : last[1]) { ++R_X; if (aeq(P[H[e.first].pa].al[locus], a)) m[1][e.first] += e.second; }
-      for (auto &e : last[2]) { ++R_X; if (aeq(P[H[e.first].pb].al[locus], a)) m[2][e.first] += e.second; }
-    } else {
-      const std::vector<Pair> &X = hp[locus], &Y = hp[locus + 1];
-      for (auto &e : last[0])
-        for (int r = 0; r < 2; ++r)
-          for (int t : X[e.first].fl[r]) {
-            const Pair &y = Y[t];
-            ++R_X;
-            if (aeq(y.alA, a)) {
-              if (aeq(y.alB, a)) m[0][t] += e.second * y.tp;
-              else m[1][t] += e.second * y.tp * 0.5;
-            } else if (aeq(y.alB, a)) {
-              m[2][t] += e.second * y.tp * 0.5;
-            }
-          }
-      for (auto &e : last[1]) {
-        for (int t : X[e.first].fl[0]) { ++R_X; if (aeq(Y[t].alA, a)) m[1][t] += e.second * Y[t].tp; }
-        for (int t : X[e.first].fl[1]) { ++R_X; if (aeq(Y[t].alB, a)) m[2][t] += e.second * Y[t].tp; }
+    }
+    // every child's frequency: hp->setFrequency(+freq), setPrefixFreq(+last_freq) (:437-441)
+    std::vector<double> cf(W, 0.0);
+    std::vector<char> desc(W, 0);
+    for (int i = 0; i < W; ++i) {
+      if (!((cm >> i) & 1ull)) continue;
+      const std::vector<double> &c = C.slot[i];
+      double part[64] = {0.0};
+      bool any = false;
+      for (size_t j = 0; j < C.touched.size(); ++j) {
+        const int t = C.touched[j];
+        const double n0 = c[t], n1 = c[Fc + t], n2 = c[2 * (size_t)Fc + t];
+        part[j % 64] += ((n0 + n1) + n2) * Z[t].bwd;
+        any = any || n0 != 0.0 || n1 != 0.0 || n2 != 0.0;
       }
-      for (auto &e : last[2]) {
-        for (int t : X[e.first].fl[0]) { ++R_X; if (aeq(Y[t].alB, a)) m[2][t] += e.second * Y[t].tp; }
-        for (int t : X[e.first].fl[1]) { ++R_X; if (aeq(Y[t].alA, a)) m[1][t] += e.second * Y[t].tp; }
+      for (int o = 32; o > 0; o >>= 1) {
+        double q[64];
+        for (int l = 0; l < 64; ++l) q[l] = part[l] + part[l ^ o];
+        for (int l = 0; l < 64; ++l) part[l] = q[l];
+      }
+      const double freq = part[0] / cur_gp;
+      cf[i] = freq;
+      desc[i] = any;
+      const int pat = fnodes[nd.ch[i]].data;
+      if (pat >= 0) {
+        xacc_f[pat] += (uint64_t)llrint(freq * XFIX);
+        xacc_p[pat] += (uint64_t)llrint(last_freq * XFIX);
       }
     }
-    const std::vector<Pair> &Z = hp[locus < hl ? hl : locus + 1];
-    double freq = 0;
-    for (int k = 0; k < 3; ++k)
-      for (auto &e : m[k]) freq += e.second * Z[e.first].bwd;
-    freq /= cur_gp;
-    if (fnodes[node].data >= 0) {
-      Pat &p = (*fpats)[fnodes[node].data];
-      p.freq += freq;
-      p.prefix += last_freq;
-    }
-    for (int i = 0; i < (int)fnodes[node].ch.size(); ++i)
-      if (fnodes[node].ch[i] >= 0) fwalk(fnodes[node].ch[i], locus + 1, g.symbol(locus + 1, i), freq, m);
-    return freq;
+    // descend into the children with non-zero lists, allele order
+    std::vector<std::vector<double>> lists(W);
+    for (int i = 0; i < W; ++i)
+      if (desc[i]) lists[i] = C.slot[i];  // (the level's buffers are reused below)
+    for (int i = 0; i < W; ++i)
+      if (desc[i]) xwalk(nd.ch[i], start, d + 1, Fc, lists[i].data(), cf[i]);
   }
+  int P_al(int pat, int locus) const { return P[pat].al[locus - P[pat].start]; }
+
   // HaploBuilder::estimateFrequency(patterns) (:274-332) for pats[b, e)
   void estimateFreqs(std::vector<Pat> &pats, size_t b, size_t e) {
     const int L = g.L, N = g.N, hl = head_len(), width = g.maxnum();
@@ -1003,6 +1106,8 @@ struct Model {
       pats[k].freq = 0;
       pats[k].prefix = 0;
     }
+    xacc_f.assign(pats.size(), 0);
+    xacc_p.assign(pats.size(), 0);
     std::vector<Candidate> out;
     std::vector<int> resol;
     for (int gi = 0; gi < N; ++gi) {
@@ -1012,20 +1117,21 @@ struct Model {
       track_links = false;
       calcBackward();
       cur_gp = gp[gi];  // (*m_genos)[geno].genotype_probability(): set by the last resolveAll (HaploModel.cpp:109)
+      if (!(cur_gp > 0.0)) continue;
       for (int start = 0; start < L; ++start) {
-        MList m[3];
+        // depth 0: every state after max(start, head_len) loci, weight = forward likelihood (:296-305)
         const int end = std::max(start, hl);
-        for (int i = 0; i < (int)hp[end].size(); ++i) m[0][i] = hp[end][i].fwd;
-        const FNode &r = fnodes[froot[start]];
-        for (int i = 0; i < (int)r.ch.size(); ++i)
-          if (r.ch[i] >= 0) fwalk(r.ch[i], start, g.symbol(start, i), 1.0, m);
+        const int F0 = (int)hp[end].size();
+        std::vector<double> l0(3 * (size_t)F0, 0.0);
+        for (int i = 0; i < F0; ++i) l0[i] = hp[end][i].fwd;
+        xwalk(froot[start], start, 0, F0, l0.data(), 1.0);
       }
     }
     hp.clear();
     for (size_t k = b; k < e; ++k) {
       Pat &p = pats[k];
-      double freq = std::min(p.freq, (double)N);
-      double pre = std::min(p.prefix, (double)N);
+      double freq = std::min((double)xacc_f[k] / XFIX, (double)N);
+      double pre = std::min((double)xacc_p[k] / XFIX, (double)N);
       freq = std::min(freq, pre);
       p.freq = freq / N;
       p.prefix = pre / N;

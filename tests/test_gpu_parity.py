@@ -1173,14 +1173,27 @@ def _rel_close(a, b, rtol=1e-6, atol=1e-12):
     return np.all(np.abs(a - b) <= atol + rtol * np.abs(b))
 
 
+def _assert_table_bits(pg, po):
+    """The exact M-step's table equals the restatement's bit for bit: the
+    restatement walks in the device walk's order (oracle/hmc_oracle.cpp
+    xwalk: gathers in add order, 64 strided partials and the butterfly, 2^-44
+    fixed-point totals) — the reference's own order is std::map pointer order,
+    reproducible by neither."""
+    for k in ("start", "len", "alleles", "succ"):
+        assert np.array_equal(pg[k], po[k]), k
+    for k in ("freq", "prefix", "tp"):
+        d = np.max(np.abs(pg[k] - po[k]) / np.maximum(np.abs(po[k]), 1e-300)) if len(po[k]) else 0.0
+        assert np.array_equal(pg[k], po[k]), (k, d, int(np.sum(pg[k] != po[k])))
+
+
 @pytest.mark.parametrize("name", EXACT_PANELS)
 def test_exact_mstep_against_oracle(oracle_mod, name):
     """--exact-estimate (PatternManager::estimatePatterns, HaploBuilder::
     estimateFrequency): after M0 and E1, one exact M-step gives the
     restatement's table — the same patterns in the same (candidate) order,
-    successors equal, frequencies / prefix frequencies / transition
-    probabilities within 1e-6 relative (the north star's bar: the reference
-    sums its match lists in pointer order)."""
+    successors, frequencies, prefix frequencies and transition probabilities
+    bit for bit (_assert_table_bits; the north star's bar is 1e-6: the
+    reference sums its match lists in pointer order)."""
     p = panel(name)
     o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
     o.find_patterns()
@@ -1196,10 +1209,7 @@ def test_exact_mstep_against_oracle(oracle_mod, name):
     st = m.exact_stats()
     assert st["rounds"] >= 1 and st["candidates"] >= P_g
     assert P_g == P_o
-    for k in ("start", "len", "alleles", "succ"):
-        assert np.array_equal(pg[k], po[k]), k
-    for k in ("freq", "prefix", "tp"):
-        assert _rel_close(pg[k], po[k]), (k, np.max(np.abs(pg[k] - po[k]) / np.maximum(np.abs(po[k]), 1e-300)))
+    _assert_table_bits(pg, po)
 
 
 @pytest.mark.variants
@@ -1234,7 +1244,7 @@ def test_exact_walk_four_items_per_wave(oracle_mod, name):
 def test_exact_mstep_300x200_against_oracle(oracle_mod):
     """The exact M-step on a 300 x 200 panel (the survey's probe size):
     after M0 and E1, one exact M-step equals the restatement's table — same
-    patterns, order and successors, frequencies / prefix / tp within 1e-6."""
+    patterns, order and successors, frequencies / prefix / tp bit for bit."""
     p = panel("n300")
     oracle_mod.set_threads(16)
     try:
@@ -1252,10 +1262,7 @@ def test_exact_mstep_300x200_against_oracle(oracle_mod):
     P_g, _ = m.find_patterns()
     pg = m.patterns()
     assert P_g == P_o
-    for k in ("start", "len", "alleles", "succ"):
-        assert np.array_equal(pg[k], po[k]), k
-    for k in ("freq", "prefix", "tp"):
-        assert _rel_close(pg[k], po[k]), (k, np.max(np.abs(pg[k] - po[k]) / np.maximum(np.abs(po[k]), 1e-300)))
+    _assert_table_bits(pg, po)
 
 
 @pytest.mark.timeout(900)
@@ -1266,7 +1273,7 @@ def test_exact_mstep_with_pruned_individual(oracle_mod):
     restatement's skip counter: E1 rebuilds it with the pruned structure pass
     (n_fallback > 0) at a finite LL equal to the restatement's, and the exact
     M-step walks its pruned records (HaploBuilder.cpp:291-314): the table
-    equals the restatement's within 1e-6."""
+    equals the restatement's bit for bit."""
     p = synth.founder_mosaic(60, 1600, A=2, seed=1)
     oracle_mod.set_threads(16)
     try:
@@ -1289,10 +1296,7 @@ def test_exact_mstep_with_pruned_individual(oracle_mod):
     assert m.exact_stats()["pruned"] > 0
     pg = m.patterns()
     assert P_g == P_o
-    for k in ("start", "len", "alleles", "succ"):
-        assert np.array_equal(pg[k], po[k]), k
-    for k in ("freq", "prefix", "tp"):
-        assert _rel_close(pg[k], po[k]), (k, np.max(np.abs(pg[k] - po[k]) / np.maximum(np.abs(po[k]), 1e-300)))
+    _assert_table_bits(pg, po)
 
 
 def test_exact_single_allele_frequencies(oracle_mod):
@@ -1320,8 +1324,8 @@ def test_exact_single_allele_frequencies(oracle_mod):
 def test_exact_mstep_after_find_pattern_by_num(oracle_mod, K, N, L, num):
     """--exact-estimate with num_patterns > 0: M0 by findPatternByNum, E1,
     then estimatePatterns at the search's last threshold (m_min_freq,
-    PatternManager.cpp:53-60, 364-408) — the restatement's table (ids,
-    strings, successors exact; frequencies 1e-6 relative) — and the whole EM."""
+    PatternManager.cpp:53-60, 364-408) — the restatement's table bit for bit
+    — and the whole EM (LL and resolutions bit for bit)."""
     p = synth.founder_mosaic(N, L, A=2, K=K, seed=5)
     o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
     o.set_num_patterns(num)
@@ -1336,10 +1340,7 @@ def test_exact_mstep_after_find_pattern_by_num(oracle_mod, K, N, L, num):
     P_g, _ = m.find_patterns()
     pg = m.patterns()
     assert P_g == P_o
-    for k in ("start", "len", "alleles", "succ"):
-        assert np.array_equal(pg[k], po[k]), k
-    for k in ("freq", "prefix", "tp"):
-        assert _rel_close(pg[k], po[k]), k
+    _assert_table_bits(pg, po)
     m2 = gpu_model(p, max_iteration=6, num_patterns=num)
     m2.exact_estimate = True
     res = m2.run()
@@ -1348,14 +1349,15 @@ def test_exact_mstep_after_find_pattern_by_num(oracle_mod, K, N, L, num):
     o2.set_exact(True)
     r = o2.run()
     assert m2.iterations == r["iterations"]
-    assert np.allclose([x["ll"] for x in m2.log], r["ll"], rtol=1e-9, atol=0)
-    assert np.mean(np.all(res == r["resolutions"], axis=(1, 2))) >= 0.99
+    assert [x["ll"] for x in m2.log] == r["ll"].tolist()
+    assert np.array_equal(res, r["resolutions"])
 
 
 @pytest.mark.parametrize("name", ["cfg1", "n60", "miss2"])
 def test_exact_em_against_oracle(oracle_mod, name):
-    """HaploModel::run with --exact-estimate: iteration count, per-iteration
-    LL to 1e-9 relative, and the accepted pairs."""
+    """HaploModel::run with --exact-estimate: iteration count, every
+    iteration's LL and the accepted pairs, bit for bit (the restatement walks
+    in the device walk's order, _assert_table_bits)."""
     p = panel(name)
     m = gpu_model(p, max_iteration=10)
     m.exact_estimate = True
@@ -1364,8 +1366,8 @@ def test_exact_em_against_oracle(oracle_mod, name):
     o.set_exact(True)
     r = o.run()
     assert m.iterations == r["iterations"]
-    assert np.allclose([x["ll"] for x in m.log], r["ll"], rtol=1e-9, atol=0)
-    assert np.mean(np.all(res == r["resolutions"], axis=(1, 2))) >= 0.99
+    assert [x["ll"] for x in m.log] == r["ll"].tolist()
+    assert np.array_equal(res, r["resolutions"])
 
 
 def test_exact_em_estep_after_store_shrink(oracle_mod):
