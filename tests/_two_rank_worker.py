@@ -32,6 +32,8 @@ def main():
     elif variant == "BYNUM":
         m.num_patterns, m.min_pattern_len = 150, 2
     m.load(hmc_amd.GenoData.from_panel(p))
+    if variant == "WIN":  # every E-step of each rank's shard in windows of 7 loci
+        m.set_estep_windows("always", 7)
     m.find_patterns()
     m0_freq = m.patterns()["freq"]
     m.clear_samples()

@@ -961,11 +961,12 @@ def _free_port():
 
 
 @pytest.mark.parametrize("reduction", ["ordered", "allreduce"])
-@pytest.mark.parametrize("variant", ["MV", "MC", "BYNUM"])
+@pytest.mark.parametrize("variant", ["MV", "MC", "BYNUM", "WIN"])
 def test_two_ranks_one_gpu_host_collective(oracle_mod, tmp_path, variant, reduction):
     """The sharded multi-rank path (individual shards, per-level cross-rank
     candidate sums, LL / total weight, the HaploComp counters) with 2 ranks on
-    one GPU and a gloo host collective, for MV, MC and findPatternByNum.
+    one GPU and a gloo host collective, for MV, MC, findPatternByNum and MV
+    with every E-step windowed (WIN: windows of 7 loci on each rank's shard).
     Ordered reduction (default) continues every sum rank by rank in the
     reference's item order: tolerance 0 — LL, every accepted pair and the
     HaploComp log equal the single-rank restatement's.  All-reduce mode
