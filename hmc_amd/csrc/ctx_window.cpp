@@ -349,6 +349,12 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
   auto window = [&](int w, std::vector<int32_t> &grp) -> int {
     std::vector<int32_t> todo(grp), dead;
     bool first = true;
+    // heaviest first within the window (each pass ends on its slowest
+    // individual): by the traces of the window before, a proxy for this one
+    if (w > 0)
+      std::stable_sort(todo.begin(), todo.end(), [&](int32_t x, int32_t y) {
+        return tw[(size_t)x * nwin + w - 1] > tw[(size_t)y * nwin + w - 1];
+      });
     {
       int fprev = probe_fmax;
       if (w > 0)
@@ -442,6 +448,10 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
           tbv[bi] = tr_hi;
         }
       }
+      // the value pass by this window's own record words, heaviest first
+      std::stable_sort(ok.begin(), ok.end(), [&](int32_t x, int32_t y) {
+        return rw[(size_t)x * nwin + w] > rw[(size_t)y * nwin + w];
+      });
       if (!ok.empty() && (rc = values(w, ok.data(), (int)ok.size()))) return rc;
       for (int bi : ok) {
         const int s2 = h_status[bi];
@@ -484,7 +494,10 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     const int max_words = (int)(((uint64_t)fb * S + 31) / 32) + 1;
     const size_t stride = (size_t)(hi1 - lo0 + 1) + 2 * (size_t)(max_words + 1) + mwords + (size_t)(hi1 - lo0) + 64;
     const int grid = std::max(1, std::min((int)grp.size(), dev_cu * 16));  // a wavefront per individual
-    gc_ids = grp;
+    gc_ids = grp;  // heaviest collections first: the traces of the two windows
+    std::stable_sort(gc_ids.begin(), gc_ids.end(), [&](int32_t x, int32_t y) {
+      return tw[(size_t)x * nwin + w - 1] + tw[(size_t)x * nwin + w] > tw[(size_t)y * nwin + w - 1] + tw[(size_t)y * nwin + w];
+    });
     hipError_t e2;
     if ((e2 = d_gc_scr.ensure(stride * grid)) || (e2 = d_gc_order.ensure(n)) || (e2 = d_gc_status.ensure(n)) ||
         (e2 = d_gc_nextq.ensure(1)) ||
