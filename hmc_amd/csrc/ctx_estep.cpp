@@ -630,6 +630,12 @@ int Ctx::estep_split(const std::vector<int32_t> &order, bool exact) {
         sset.resize(k);
       }
       if ((rc = ensure_store(d_trace, std::max<uint64_t>(t, 1), trace_budget, "trace store"))) return rc;
+      // the value pass heaviest first by the records the structure pass just
+      // measured (the group's end waits on its slowest individual; the
+      // genotype cost order only approximates the work)
+      if (!exact)
+        std::stable_sort(sset.begin() + (std::ptrdiff_t)pos, sset.begin() + (std::ptrdiff_t)(pos + k),
+                         [&](int32_t x, int32_t y) { return rneed[x] > rneed[y]; });
       std::vector<unsigned long long> tb(n, 0);
       for (size_t q = 0; q < k; ++q) tb[sset[pos + q]] = base[sset[pos + q]];
       if ((e = hipMemcpyAsync(d_tbase.p, tb.data(), (size_t)n * 8, hipMemcpyHostToDevice, st)))
