@@ -83,7 +83,8 @@ def parse():
                     help="forced iterations after the chain's end, timed for value_steady (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-indiv", type=int, default=20, help="individuals per CPU E-step sample (E_k, k >= 2)")
-    ap.add_argument("--cpu-indiv-e1", type=int, default=6, help="individuals of the CPU E_1 sample (M0 model)")
+    ap.add_argument("--cpu-indiv-e1", type=int, default=24,
+                    help="individuals of the CPU E_1 sample (M0 model); timed in two interleaved halves for the spread")
     ap.add_argument("--cpu-roots", type=int, default=30, help="start loci per CPU M-step sample")
     ap.add_argument("--cpu-validate", action="store_true",
                     help="also time the whole chain on the CPU restatement (1 thread) next to the sampled "
@@ -467,13 +468,26 @@ def cpu_baseline(m, panel, args):
     roots = (np.arange(kr) * L) // kr + L // (2 * kr)
     o = oracle.Oracle(panel.alleles, panel.types, sample_size=args.sample_size)
     old_ll, it, parts = -DBL_MAX, 1, []
+    e1_spread = None
     while True:
         pt = m.patterns(maxlen=30)
+        P = len(pt["start"])
         o.set_patterns(pt)
         del pt
         ids = strat_indiv(args.cpu_indiv_e1 if it == 1 else args.cpu_indiv)
-        te = o.time_resolve_list(ids)
+        if it == 1 and len(ids) >= 2:  # two interleaved halves of the stratified sample: the estimate's spread
+            ta, tb = o.time_resolve_list(ids[0::2]), o.time_resolve_list(ids[1::2])
+            te = ta + tb
+            e1_spread = {"half_a_scaled_s": ta * N / len(ids[0::2]), "half_b_scaled_s": tb * N / len(ids[1::2]),
+                         "rel_diff": abs(ta / len(ids[0::2]) - tb / len(ids[1::2])) / max(1e-12, te / len(ids))}
+        else:
+            te = o.time_resolve_list(ids)
         parts.append({"step": f"E{it}", "sample": len(ids), "seconds": te, "scale": N / len(ids)})
+        # HaploBuilder::initialize clears P maps before every individual
+        # (HaploBuilder.cpp:25-33); the restatement's resolve skips that, so it
+        # is timed on its own (one pass) and charged N times
+        tr = oracle.Oracle.time_best_pair_reset(P)
+        parts.append({"step": f"E{it} reset", "sample": 1, "seconds": tr, "scale": float(N), "patterns": P})
         ll, H, _ = m.resolve_all()  # the same E-step on the GPU (its samples feed the next M-step)
         go = ll >= old_ll and (old_ll - ll) / old_ll > 1e-4  # HaploModel.cpp:139
         if not go:
@@ -487,6 +501,7 @@ def cpu_baseline(m, panel, args):
         old_ll, it = ll, it + 1
     t_chain = sum(p["seconds"] * p["scale"] for p in parts)
     t_iter = t_chain / it
+    t_iter_port = sum(p["seconds"] * p["scale"] for p in parts if not p["step"].endswith("reset")) / it
     validation = None
     if args.cpu_validate:  # the same chain in full, M0 to the stop, one thread (HaploModel::run)
         oracle.set_threads(1)
@@ -494,16 +509,22 @@ def cpu_baseline(m, panel, args):
         n_e, n_m = len(full["t_e"]), max(0, full["iterations"] - 1)
         t_full = float(sum(full["t_e"][:n_e]) + sum(full["t_m"][:n_m]))
         validation = {"full_chain_iterations": int(full["iterations"]), "full_chain_seconds": t_full,
-                      "full_t_iter_s": t_full / full["iterations"], "sampled_t_iter_s": t_iter,
-                      "sampled_over_full": t_iter / (t_full / full["iterations"]),
+                      "full_t_iter_s": t_full / full["iterations"], "sampled_t_iter_s": t_iter_port,
+                      "sampled_over_full": t_iter_port / (t_full / full["iterations"]),
                       "full_parts_s": {"E": [float(x) for x in full["t_e"][:n_e]],
                                        "M": [float(x) for x in full["t_m"][:n_m]]}}
     return {
         "value": N * L / t_iter, "unit": "individual·loci/s", "cores": 1, "kind": "port",
+        "host_cores": os.cpu_count(),
+        "host_cores_note": "os.cpu_count() of the host; the reference and the restatement are single-threaded, so one "
+                           "core is timed (a box's CPU share for this job is 16)",
         "sample": f"converged chain of {it} EM iterations ({', '.join(p['step'] for p in parts)}): E_1 over "
                   f"{min(args.cpu_indiv_e1, N)} and E_k over {min(args.cpu_indiv, N)} individuals spread over the "
-                  f"cost order, M_k over {kr} start loci spread over [0, {L}), each scaled to the panel; "
+                  f"cost order, M_k over {kr} start loci spread over [0, {L}), each scaled to the panel; plus "
+                  f"HaploBuilder::initialize's per-individual clear of P maps (HaploBuilder.cpp:25-33), which the "
+                  f"restatement's resolve omits, timed once per E-step and charged N times; "
                   f"oracle/hmc_oracle.cpp g++ -O2, 1 thread",
+        "e1_spread": e1_spread,
         "parts": parts, "t_iter_s": t_iter, "sample_seconds": sum(p["seconds"] for p in parts),
         "validation": validation if validation else VALIDATION_NOTE,
     }

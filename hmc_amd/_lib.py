@@ -107,10 +107,14 @@ _SIGS = [
     ("hmc_last_estep_frontier", _i, [_vp, _P(C.c_int), _P(C.c_int)]),
     ("hmc_last_mine_stats", _i, [_vp, _P(_i), _P(C.c_int64), _P(_d)]),
     ("hmc_last_mine_reduction", _i, [_vp, _P(_d), _P(_i)]),
+    ("hmc_comm_stats", _i, [_vp, _P(C.c_int64), _P(C.c_int64), _P(C.c_uint64)]),
+    ("hmc_set_comm_timeout", _i, [_vp, _d]),
+    ("hmc_debug_stall", _i, [_vp, _d]),
     ("hmc_set_estep_windows", _i, [_vp, _i, _i]),
     ("hmc_set_shard", _i, [_vp, _i, _i]),
     ("hmc_last_exact_walk", _i, [_vp, _P(C.c_int64), _P(C.c_int64), _P(C.c_int64), _P(_i)]),
     ("hmc_last_estep_windows", _i, [_vp, _P(_i), _P(_i), _P(_i), _P(_d)]),
+    ("hmc_last_estep_restarts", _i, [_vp, _P(_i), _P(_d)]),
     ("hmc_model_save", _i, [_vp]),
     ("hmc_em_rewind", _i, [_vp]),
     ("hmc_build_info", _cp, []),

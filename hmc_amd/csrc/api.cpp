@@ -204,6 +204,7 @@ int hmc_set_shard(hmc_ctx *h, int i0, int i1) {
   c.h_cost.clear();
   c.prev_rneed.clear();
   c.prev_P = 0;
+  c.win_scale = 1.0;  // window shrinking learnt on the old shard does not carry over
   return HMC_OK;
 }
 
@@ -327,6 +328,13 @@ int hmc_last_estep_windows(const hmc_ctx *h, int *windows, int *window_loci, int
   return HMC_OK;
 }
 
+int hmc_last_estep_restarts(const hmc_ctx *h, int *restarts, double *window_scale) {
+  if (!h) return HMC_EARG;
+  if (restarts) *restarts = h->c.n_restarts;
+  if (window_scale) *window_scale = h->c.win_scale;
+  return HMC_OK;
+}
+
 int hmc_last_estep_order(const hmc_ctx *h, int *n_rerun, double *rerun_ms) {
   if (!h) return HMC_EARG;
   if (n_rerun) *n_rerun = h->c.n_order_redo;
@@ -406,6 +414,29 @@ int hmc_last_mine_reduction(const hmc_ctx *h, double *ms, int *levels) {
   if (!h) return HMC_EARG;
   if (ms) *ms = h->c.ms_red;
   if (levels) *levels = h->c.n_red_levels;
+  return HMC_OK;
+}
+
+int hmc_comm_stats(const hmc_ctx *h, int64_t *sends, int64_t *recvs, uint64_t *bytes_received) {
+  if (!h) return HMC_EARG;
+  if (sends) *sends = h->c.p2p_sends;
+  if (recvs) *recvs = h->c.p2p_recvs;
+  if (bytes_received) *bytes_received = h->c.p2p_bytes;
+  return HMC_OK;
+}
+
+int hmc_set_comm_timeout(hmc_ctx *h, double seconds) {
+  if (!h || !(seconds > 0)) return HMC_EARG;
+  h->c.comm_timeout_s = seconds;
+  return HMC_OK;
+}
+
+int hmc_debug_stall(hmc_ctx *h, double ms) {
+  if (!h || !(ms > 0) || ms > 60000) return HMC_EARG;
+  hmc::Ctx &c = h->c;
+  if (int rc = c.comm_ok()) return rc;
+  hipError_t e;
+  if ((e = hmc::launch_stall(ms, c.st)) || (e = c.sync_st())) return c.hipfail(e, "debug_stall");
   return HMC_OK;
 }
 
@@ -652,14 +683,14 @@ int hmc_get_patterns(hmc_ctx *h, int32_t *start, int32_t *len, double *freq, dou
       (prefix && (e = hipMemcpyAsync(prefix, c.t_prefix.p, (size_t)P * 8, hipMemcpyDeviceToHost, c.st))) ||
       (tp && (e = hipMemcpyAsync(tp, c.t_tp.p, (size_t)P * 8, hipMemcpyDeviceToHost, c.st))) ||
       (e = hipMemcpyAsync(last.data(), c.t_last.p, (size_t)P, hipMemcpyDeviceToHost, c.st)) ||
-      (e = hipStreamSynchronize(c.st)))
+      (e = c.sync_st()))
     return c.hipfail(e, "get_patterns");
   if (start) memcpy(start, st.data(), (size_t)P * 4);
   if (len) memcpy(len, ln.data(), (size_t)P * 4);
   if (succ) {
     std::vector<uint32_t> s((size_t)P * A);
     if ((e = hipMemcpyAsync(s.data(), c.t_succ.p, s.size() * 4, hipMemcpyDeviceToHost, c.st)) ||
-        (e = hipStreamSynchronize(c.st)))
+        (e = c.sync_st()))
       return c.hipfail(e, "get_patterns");
     for (size_t i = 0; i < s.size(); ++i) succ[i] = s[i] == hmc::NONE ? -1 : (int32_t)s[i];
   }
@@ -718,7 +749,7 @@ int hmc_set_patterns(hmc_ctx *h, int P, const int32_t *start, const int32_t *len
       (e = hipMemcpyAsync(c.t_last.p, last.data(), (size_t)P, hipMemcpyHostToDevice, c.st)) ||
       (e = hipMemcpyAsync(c.t_succ.p, s.data(), s.size() * 4, hipMemcpyHostToDevice, c.st)) ||
       (e = hipMemsetAsync(c.t_ppat.p, 0xFE, (size_t)P * 4, c.st)) ||  // prefixes unknown
-      (e = hipStreamSynchronize(c.st)))
+      (e = c.sync_st()))
     return c.hipfail(e, "set_patterns");
   c.P = P;
   c.head_len = hl;
@@ -752,7 +783,7 @@ int hmc_get_estep(hmc_ctx *h, double *total, int32_t *ncand, int32_t *status, do
   for (int q = 0; q < 3; ++q) {
     if (!outs[q]) continue;
     if ((e = hipMemcpyAsync(buf.data(), srcs[q], buf.size() * 8, hipMemcpyDeviceToHost, c.st)) ||
-        (e = hipStreamSynchronize(c.st)))
+        (e = c.sync_st()))
       return c.hipfail(e, "get_estep");
     for (int i = 0; i < n; ++i)
       for (int k = 0; k < S; ++k)
@@ -765,7 +796,7 @@ int hmc_get_estep_stats(hmc_ctx *h, int32_t *fmax) {
   if (!h || !h->c.have_estep || !fmax) return HMC_EARG;
   hipError_t e;
   if ((e = hipMemcpyAsync(fmax, h->c.d_fmax.p, (size_t)h->c.nloc() * 4, hipMemcpyDeviceToHost, h->c.st)) ||
-      (e = hipStreamSynchronize(h->c.st)))
+      (e = h->c.sync_st()))
     return h->c.hipfail(e, "get_estep_stats");
   return HMC_OK;
 }
@@ -781,7 +812,7 @@ int hmc_get_stamps(hmc_ctx *h, uint64_t *out40) {
   if (!h || !out40 || !h->c.d_stamps.p) return HMC_EARG;
   hipError_t e;
   if ((e = hipMemcpyAsync(out40, h->c.d_stamps.p, 40 * 8, hipMemcpyDeviceToHost, h->c.st)) ||
-      (e = hipStreamSynchronize(h->c.st)))
+      (e = h->c.sync_st()))
     return h->c.hipfail(e, "get_stamps");
   return HMC_OK;
 }
@@ -796,14 +827,14 @@ int hmc_get_samples(hmc_ctx *h, int32_t *alleles, double *weights, double *total
     for (int s = 0; s < H; ++s) top = std::max(top, c.h_rowmap[s] + 1);
     std::vector<uint8_t> rows((size_t)top * L);
     if ((e = hipMemcpyAsync(rows.data(), c.d_rows.p, rows.size(), hipMemcpyDeviceToHost, c.st)) ||
-        (e = hipStreamSynchronize(c.st)))
+        (e = c.sync_st()))
       return c.hipfail(e, "get_samples");
     for (int s = 0; s < H; ++s)
       for (int k = 0; k < L; ++k) alleles[(size_t)s * L + k] = c.pan.symbol(k, rows[(size_t)c.h_rowmap[s] * L + k]);
   }
   if (weights && H) {
     if ((e = hipMemcpyAsync(weights, c.d_w.p, (size_t)H * 8, hipMemcpyDeviceToHost, c.st)) ||
-        (e = hipStreamSynchronize(c.st)))
+        (e = c.sync_st()))
       return c.hipfail(e, "get_samples");
   }
   if (total_weight) *total_weight = c.total_weight;

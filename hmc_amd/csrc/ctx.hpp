@@ -19,6 +19,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hmc_amd.h"
@@ -261,6 +262,18 @@ struct Ctx {
   // unchanged, so the RCCL calls can be exercised on a one-GPU machine.
   bool force_coll = false;
   bool multi() const { return world > 1 || force_coll; }
+  // Point-to-point hops of the ordered chain issued by this context (sends,
+  // receives, bytes received) — hmc_comm_stats.
+  int64_t p2p_sends = 0, p2p_recvs = 0;
+  uint64_t p2p_bytes = 0;
+  DevBuf<double> d_chain_rx, d_chain_host;  // self-hop receive buffer; small host-vector collectives
+  // Bounded waits on an RCCL context (hmc_set_comm_timeout): a stream sync
+  // polls the communicator's asynchronous error and gives up after
+  // comm_timeout_s, aborting the communicator — a dead or stalled neighbour
+  // ends the run with HMC_ERCCL instead of a hang in ncclRecv.
+  double comm_timeout_s = 1800.0;
+  bool comm_dead = false;
+  std::string comm_msg;
   std::string err;
   // parameters (HaploModel.h:15-26 with the CLI defaults of HMC.cpp:35-47)
   double min_freq_abs = 1.5, min_freq = -1.0;
@@ -428,6 +441,7 @@ struct Ctx {
     return code;
   }
   int hipfail(hipError_t e, const char *where) {
+    if (comm_dead) return fail(HMC_ERCCL, "%s: %s", where, comm_msg.c_str());
     if (e == hipErrorOutOfMemory) return fail(HMC_ENOMEM, "%s: %s", where, hipGetErrorString(e));
     return fail(HMC_EHIP, "%s: %s", where, hipGetErrorString(e));
   }
@@ -436,17 +450,56 @@ struct Ctx {
   int S() const { return sample_size > 1 ? sample_size : 1; }  // HaploBuilder.cpp:44
 
   // ---------------------------------------------------------- collectives --
+  // Stream sync with a bounded wait.  Without an RCCL communicator (or on one
+  // rank without forced collectives) this is hipStreamSynchronize.  Otherwise
+  // the host polls the stream, checks ncclCommGetAsyncError between polls, and
+  // after comm_timeout_s (or on an asynchronous error) aborts the communicator
+  // — RCCL's kernels waiting in a receive see the abort flag and exit — and
+  // returns an error that hipfail() reports as HMC_ERCCL.
+  hipError_t sync_st() {
+    if (comm_dead) return hipErrorUnknown;
+    if (!comm || !multi()) return hipStreamSynchronize(st);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (long spin = 0;; ++spin) {
+      hipError_t q = hipStreamQuery(st);
+      if (q == hipSuccess) return hipSuccess;
+      if (q != hipErrorNotReady) return q;
+      ncclResult_t ar = ncclSuccess;
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      bool bad = ncclCommGetAsyncError(comm, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress;
+      if (bad || el > comm_timeout_s) {
+        char m[256];
+        if (bad)
+          snprintf(m, sizeof m, "RCCL asynchronous error: %s (communicator aborted)", ncclGetErrorString(ar));
+        else
+          snprintf(m, sizeof m, "rank %d: stream not drained after %.3g s (comm timeout; communicator aborted)", rank,
+                   comm_timeout_s);
+        comm_msg = m;
+        comm_dead = true;
+        ncclCommAbort(comm);  // releases kernels blocked on a peer, and frees the communicator
+        comm = nullptr;
+        (void)hipStreamSynchronize(st);
+        (void)hipGetLastError();
+        return hipErrorUnknown;
+      }
+      if (spin < 2000) std::this_thread::yield();
+      else std::this_thread::sleep_for(std::chrono::microseconds(spin < 20000 ? 20 : 200));
+    }
+  }
+  int comm_ok() { return comm_dead ? fail(HMC_ERCCL, "communicator aborted earlier: %s", comm_msg.c_str()) : HMC_OK; }
+
   int allreduce_sum(double *dptr, size_t n) {
     if (!multi() || n == 0) return HMC_OK;
     if (host_fn) {
       std::vector<double> h(n);
       hipError_t e;
-      if ((e = hipMemcpyAsync(h.data(), dptr, n * 8, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+      if ((e = hipMemcpyAsync(h.data(), dptr, n * 8, hipMemcpyDeviceToHost, st)) || (e = sync_st()))
         return hipfail(e, "allreduce");
       if (host_fn(h.data(), n, host_user) != 0) return fail(HMC_ERCCL, "host all-reduce callback failed");
       if ((e = hipMemcpyAsync(dptr, h.data(), n * 8, hipMemcpyHostToDevice, st))) return hipfail(e, "allreduce");
       return HMC_OK;
     }
+    if (int rc = comm_ok()) return rc;
     ncclResult_t r = ncclAllReduce(dptr, dptr, n, ncclDouble, ncclSum, comm, st);
     if (r != ncclSuccess) return fail(HMC_ERCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
     return HMC_OK;
@@ -460,13 +513,14 @@ struct Ctx {
       std::vector<double> h(n, 0.0);
       hipError_t e;
       if (rank == src && ((e = hipMemcpyAsync(h.data(), dptr, n * 8, hipMemcpyDeviceToHost, st)) ||
-                          (e = hipStreamSynchronize(st))))
+                          (e = sync_st())))
         return hipfail(e, "bcast");
       if (host_fn(h.data(), n, host_user) != 0) return fail(HMC_ERCCL, "host collective callback failed");
-      if ((e = hipMemcpyAsync(dptr, h.data(), n * 8, hipMemcpyHostToDevice, st)) || (e = hipStreamSynchronize(st)))
+      if ((e = hipMemcpyAsync(dptr, h.data(), n * 8, hipMemcpyHostToDevice, st)) || (e = sync_st()))
         return hipfail(e, "bcast");
       return HMC_OK;
     }
+    if (int rc = comm_ok()) return rc;
     ncclResult_t r = ncclBroadcast(dptr, dptr, n, ncclDouble, src, comm, st);
     if (r != ncclSuccess) return fail(HMC_ERCCL, "ncclBroadcast: %s", ncclGetErrorString(r));
     return HMC_OK;
@@ -480,13 +534,13 @@ struct Ctx {
       std::copy(v.begin(), v.end(), h);
       return HMC_OK;
     }
-    DevBuf<double> tmp;
+    DevBuf<double> &tmp = d_chain_host;
     hipError_t e = tmp.ensure(n);
     if (e) return hipfail(e, "bcast_host");
     if ((e = hipMemcpyAsync(tmp.p, h, n * 8, hipMemcpyHostToDevice, st))) return hipfail(e, "bcast_host");
     int rc = bcast(tmp.p, n, src);
     if (rc) return rc;
-    if ((e = hipMemcpyAsync(h, tmp.p, n * 8, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+    if ((e = hipMemcpyAsync(h, tmp.p, n * 8, hipMemcpyDeviceToHost, st)) || (e = sync_st()))
       return hipfail(e, "bcast_host");
     return HMC_OK;
   }
@@ -509,14 +563,44 @@ struct Ctx {
       }
       return HMC_OK;
     }
+    if ((rc = comm_ok())) return rc;
     ncclResult_t x;
+    if (world == 1) {
+      // One-rank test hook (force_coll): the chain's hop sent to this rank
+      // itself — the same ncclSend / ncclRecv calls, count, dtype and stream
+      // as a W > 1 hop, grouped (a self-send completes only with its receive
+      // in the same group).  The receive lands in a scratch buffer poisoned
+      // with NaN first, then replaces `d`: every running sum of the run has
+      // travelled through RCCL's point-to-point path.
+      hipError_t e;
+      if ((e = d_chain_rx.ensure(n)) || (e = hipMemsetAsync(d_chain_rx.p, 0xFF, n * 8, st)))
+        return hipfail(e, "ordered_chain self hop");
+      if ((x = ncclGroupStart()) != ncclSuccess) return fail(HMC_ERCCL, "ncclGroupStart: %s", ncclGetErrorString(x));
+      ncclResult_t xs = ncclSend(d, n, ncclDouble, 0, comm, st);
+      ncclResult_t xr = ncclRecv(d_chain_rx.p, n, ncclDouble, 0, comm, st);
+      x = ncclGroupEnd();
+      if (xs != ncclSuccess || xr != ncclSuccess || x != ncclSuccess)
+        return fail(HMC_ERCCL, "self send/recv: %s / %s / %s", ncclGetErrorString(xs), ncclGetErrorString(xr),
+                    ncclGetErrorString(x));
+      p2p_sends += 1;
+      p2p_recvs += 1;
+      p2p_bytes += n * 8;
+      if ((e = hipMemcpyAsync(d, d_chain_rx.p, n * 8, hipMemcpyDeviceToDevice, st)))
+        return hipfail(e, "ordered_chain self hop");
+      return bcast(d, n, 0);
+    }
     if (rank > 0) {
       if ((x = ncclRecv(d, n, ncclDouble, rank - 1, comm, st)) != ncclSuccess)
         return fail(HMC_ERCCL, "ncclRecv: %s", ncclGetErrorString(x));
+      p2p_recvs += 1;
+      p2p_bytes += n * 8;
       if ((rc = cont())) return rc;
     }
-    if (rank < world - 1 && (x = ncclSend(d, n, ncclDouble, rank + 1, comm, st)) != ncclSuccess)
-      return fail(HMC_ERCCL, "ncclSend: %s", ncclGetErrorString(x));
+    if (rank < world - 1) {
+      if ((x = ncclSend(d, n, ncclDouble, rank + 1, comm, st)) != ncclSuccess)
+        return fail(HMC_ERCCL, "ncclSend: %s", ncclGetErrorString(x));
+      p2p_sends += 1;
+    }
     return bcast(d, n, world - 1);
   }
   // The same chain over a small host vector (LL, total weight): `cont` runs on
@@ -534,21 +618,21 @@ struct Ctx {
       }
       return HMC_OK;
     }
-    DevBuf<double> tmp;
+    DevBuf<double> &tmp = d_chain_host;  // persistent: a hipFree per E-step would synchronise the device
     hipError_t e = tmp.ensure(n);
     if (e) return hipfail(e, "ordered_chain_host");
     if (rank == 0) cont(h);
     if ((e = hipMemcpyAsync(tmp.p, h, n * 8, hipMemcpyHostToDevice, st))) return hipfail(e, "ordered_chain_host");
     int rc = ordered_chain(tmp.p, n, [&]() -> int {
       hipError_t e2;
-      if ((e2 = hipMemcpyAsync(h, tmp.p, n * 8, hipMemcpyDeviceToHost, st)) || (e2 = hipStreamSynchronize(st)))
+      if ((e2 = hipMemcpyAsync(h, tmp.p, n * 8, hipMemcpyDeviceToHost, st)) || (e2 = sync_st()))
         return hipfail(e2, "ordered_chain_host");
       cont(h);
       if ((e2 = hipMemcpyAsync(tmp.p, h, n * 8, hipMemcpyHostToDevice, st))) return hipfail(e2, "ordered_chain_host");
       return HMC_OK;
     });
     if (rc) return rc;
-    if ((e = hipMemcpyAsync(h, tmp.p, n * 8, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+    if ((e = hipMemcpyAsync(h, tmp.p, n * 8, hipMemcpyDeviceToHost, st)) || (e = sync_st()))
       return hipfail(e, "ordered_chain_host");
     return HMC_OK;
   }
@@ -556,14 +640,14 @@ struct Ctx {
   int allreduce_host(double *h, size_t n) {  // small host vectors
     if (!multi() || n == 0) return HMC_OK;
     if (host_fn) return host_fn(h, n, host_user) == 0 ? HMC_OK : fail(HMC_ERCCL, "host all-reduce callback failed");
-    DevBuf<double> tmp;
+    DevBuf<double> &tmp = d_chain_host;
     hipError_t e = tmp.ensure(n);
     if (e) return hipfail(e, "allreduce_host");
     if ((e = hipMemcpyAsync(tmp.p, h, n * 8, hipMemcpyHostToDevice, st))) return hipfail(e, "allreduce_host");
     int rc = allreduce_sum(tmp.p, n);
     if (rc) return rc;
     if ((e = hipMemcpyAsync(h, tmp.p, n * 8, hipMemcpyDeviceToHost, st))) return hipfail(e, "allreduce_host");
-    if ((e = hipStreamSynchronize(st))) return hipfail(e, "allreduce_host");
+    if ((e = sync_st())) return hipfail(e, "allreduce_host");
     return HMC_OK;
   }
 
@@ -878,7 +962,7 @@ struct Ctx {
   int upload_order(DevBuf<int32_t> &d, const int32_t *v, int k) {
     hipError_t e;
     if (k > 0 && ((e = hipMemcpyAsync(d.p, v, (size_t)k * 4, hipMemcpyHostToDevice, st)) ||
-                  (e = hipStreamSynchronize(st))))
+                  (e = sync_st())))
       return hipfail(e, "estep order");
     return HMC_OK;
   }
@@ -892,7 +976,7 @@ struct Ctx {
     const int n = nloc();
     if ((e = hipMemcpyAsync(h_status.data(), dstatus ? dstatus : d_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
         (ncand && (e = hipMemcpyAsync(h_ncand.data(), d_ncand.p, (size_t)n * 4, hipMemcpyDeviceToHost, st))) ||
-        (e = hipStreamSynchronize(st)))
+        (e = sync_st()))
       return hipfail(e, "estep status");
     (void)ids;
     (void)k;
@@ -934,6 +1018,7 @@ struct Ctx {
   DevBuf<int32_t> d_gc_order, d_gc_status, d_gc_nextq;  // the collection's own order, statuses and work counter
   double win_scale = 1.0;  // shrinks the windows after a trace store overflow (the E-step restarts)
   int last_windows = 0, last_window_loci = 0, last_window_groups = 0;  // hmc_last_estep_windows
+  int n_restarts = 0;  // restarts of the last E-step (capacity growth, smaller windows): hmc_last_estep_restarts
   double ms_ck = 0;  // device ms of the trace collections (part of ms_s2)
   // A probe of the first loci of a sample decides: WIN_DECLINED when the
   // classic passes fit groups of at least two individuals per CU (or the
@@ -1043,7 +1128,7 @@ struct Ctx {
     hipError_t e;
     best_res.resize((size_t)nloc() * 2 * pan.L);
     if ((e = hipMemcpyAsync(best_res.data(), d_best.p, best_res.size(), hipMemcpyDeviceToHost, st)) ||
-        (e = hipStreamSynchronize(st)))
+        (e = sync_st()))
       return hipfail(e, "resolutions");
     best_on_host = true;
     return HMC_OK;

@@ -84,7 +84,7 @@ int Ctx::build_head_frontier() {
       (e = hipMemcpyAsync(d_hf_off.p, off.data(), (size_t)(n + 1) * 4, hipMemcpyHostToDevice, st)) ||
       (!pairs.empty() && (e = hipMemcpyAsync(d_hf_pairs.p, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, st))) ||
       (n && (e = hipMemcpyAsync(d_hf_status.p, status.data(), (size_t)n * 4, hipMemcpyHostToDevice, st))) ||
-      (e = hipStreamSynchronize(st)))
+      (e = sync_st()))
     return hipfail(e, "head frontier");
   hf_valid = true;
   return HMC_OK;
@@ -173,9 +173,11 @@ int Ctx::estep(double *ll_out, int *H_out, uint64_t *re_out) {
   n_fallback = n_order_redo = 0;
   n_struct_passes = n_value_passes = 0;
   int rc = 0;
+  n_restarts = 0;
   while (true) {  // a frontier overflow (fcap grows) restarts the E-step
     rc = estep_mode == ESTEP_SPLIT ? estep_split(order) : estep_fused(order);
     if (rc != ESTEP_RESTART) break;
+    ++n_restarts;
   }
   if (rc) return rc;
   if (estep_mode == ESTEP_SPLIT) ms_fwd = ms_s1 + ms_s2 + ms_fb;
@@ -197,11 +199,11 @@ int Ctx::estep(double *ll_out, int *H_out, uint64_t *re_out) {
       (e = hipMemcpyAsync(h_total.data(), d_total.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
       (e = hipMemcpyAsync(h_re.data(), d_re.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
       (e = hipMemcpyAsync(h_cost.data(), d_cost.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
-      (e = hipStreamSynchronize(st)))
+      (e = sync_st()))
     return hipfail(e, "estep");
   for (int h = 0; h < H; ++h) w[h] = wslot[rowmap[h]];
   if (H && ((e = hipMemcpyAsync(d_w.p, w.data(), (size_t)H * 8, hipMemcpyHostToDevice, st)) ||
-            (e = hipStreamSynchronize(st))))
+            (e = sync_st())))
     return hipfail(e, "estep");
   h_rowmap.swap(rowmap);
   // ll += log(genotype probability) in individual order (HaploModel.cpp:110);
@@ -305,7 +307,7 @@ int Ctx::traceback_group(int k) {
   hipEventRecord(ev[2], st);
   if ((e = launch_traceback(t, 0, st))) return hipfail(e, "traceback");
   hipEventRecord(ev[3], st);
-  if ((e = hipStreamSynchronize(st))) return hipfail(e, "traceback");
+  if ((e = sync_st())) return hipfail(e, "traceback");
   float ms = 0;
   hipEventElapsedTime(&ms, ev[2], ev[3]);
   ms_tb += ms;
@@ -932,7 +934,7 @@ int Ctx::ensure_gmodel() {
   g.gsucc = g_succ.p;
   g.gtp = g_tp.p;
   g.glast = g_last.p;
-  if ((e = build_gmodel(g, st)) || (e = hipStreamSynchronize(st))) return hipfail(e, "end-order table");
+  if ((e = build_gmodel(g, st)) || (e = sync_st())) return hipfail(e, "end-order table");
   if (g_keys.n * 4 + g_temp.n > (2ull << 30)) {  // only the build needs them: give large ones back (cfg 4's
     g_keys.release();                              // 720 M patterns: ~10 GB); small ones stay mapped (re-mapping
     g_temp.release();                              // costs more than the next model's build)
@@ -950,7 +952,7 @@ int Ctx::resolutions_idx(std::vector<uint8_t> &out) {
     return hipfail(e, "resolutions");
   out.resize((size_t)n * 2 * L);
   if ((e = hipMemcpyAsync(out.data(), d_res.p, out.size(), hipMemcpyDeviceToHost, st)) ||
-      (e = hipStreamSynchronize(st)))
+      (e = sync_st()))
     return hipfail(e, "resolutions");
   return HMC_OK;
 }
@@ -963,7 +965,7 @@ int Ctx::resolutions_idx(std::vector<uint8_t> &out) {
 // its individual and locus instead of letting a value pass walk bad records.
 int Ctx::validate_records(const int32_t *ids, int np_, int i0) {
   hipError_t e;
-  if ((e = hipStreamSynchronize(st))) return hipfail(e, "validate_records");
+  if ((e = sync_st())) return hipfail(e, "validate_records");
   const int L = pan.L, hl = head_len;
   std::vector<unsigned long long> off(d_rec_off.n);
   std::vector<uint32_t> rec(d_rec.n);

@@ -10,7 +10,7 @@ int Ctx::spell_table(const std::vector<int32_t> &ln, std::vector<int64_t> &off, 
   hipError_t e;
   if ((e = hipMemcpyAsync(pp.data(), t_ppat.p, (size_t)P * 4, hipMemcpyDeviceToHost, st)) ||
       (e = hipMemcpyAsync(last.data(), t_last.p, (size_t)P, hipMemcpyDeviceToHost, st)) ||
-      (e = hipStreamSynchronize(st)))
+      (e = sync_st()))
     return hipfail(e, "table strings");
   off.assign((size_t)P + 1, 0);
   for (int i = 0; i < P; ++i) off[i + 1] = off[i] + ln[i];
@@ -31,7 +31,7 @@ int Ctx::spell_table(const std::vector<int32_t> &ln, std::vector<int64_t> &off, 
     if (!tree_loaded) {
       node.resize(P);
       if ((e = hipMemcpyAsync(node.data(), t_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st)) ||
-          (e = hipStreamSynchronize(st)))
+          (e = sync_st()))
         return hipfail(e, "table strings");
       int nmax = 0;
       for (int k = 0; k < P; ++k) nmax = std::max(nmax, node[k] + 1);
@@ -39,7 +39,7 @@ int Ctx::spell_table(const std::vector<int32_t> &ln, std::vector<int64_t> &off, 
       alc.resize(nmax);
       if (nmax && ((e = hipMemcpyAsync(par.data(), n_parent.p, (size_t)nmax * 4, hipMemcpyDeviceToHost, st)) ||
                    (e = hipMemcpyAsync(alc.data(), n_allele.p, (size_t)nmax, hipMemcpyDeviceToHost, st)) ||
-                   (e = hipStreamSynchronize(st))))
+                   (e = sync_st())))
         return hipfail(e, "table strings");
       tree_loaded = true;
     }
@@ -69,7 +69,7 @@ int Ctx::table_to_host(Cands &c, std::vector<int32_t> &succ) {
       (e = hipMemcpyAsync(pre.data(), t_prefix.p, (size_t)P * 8, hipMemcpyDeviceToHost, this->st)) ||
       (e = hipMemcpyAsync(tp.data(), t_tp.p, (size_t)P * 8, hipMemcpyDeviceToHost, this->st)) ||
       (e = hipMemcpyAsync(su.data(), t_succ.p, su.size() * 4, hipMemcpyDeviceToHost, this->st)) ||
-      (e = hipStreamSynchronize(this->st)))
+      (e = this->sync_st()))
     return hipfail(e, "exact: table");
   std::vector<int64_t> off;
   std::vector<uint8_t> al;
@@ -145,7 +145,7 @@ int Ctx::estimate_round(Cands &c, size_t b, size_t e) {
   }
   std::vector<unsigned long long> acc(2 * nc);
   if ((er = hipMemcpyAsync(acc.data(), d_xacc.p, acc.size() * 8, hipMemcpyDeviceToHost, st)) ||
-      (er = hipStreamSynchronize(st)))
+      (er = sync_st()))
     return hipfail(er, "exact");
   if (multi()) {  // integer sums over ranks, exactly: 32-bit halves through the double collective
     std::vector<double> h(4 * nc);
@@ -209,7 +209,7 @@ int Ctx::exact_group(const int32_t *ids, int k, const std::function<int(std::vec
   std::vector<int32_t> xs(n), fm(n);
   if ((e = hipMemcpyAsync(xs.data(), d_xstatus.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
       (e = hipMemcpyAsync(fm.data(), d_xfmax.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
-      (e = hipStreamSynchronize(st)))
+      (e = sync_st()))
     return hipfail(e, "exact_fb");
   std::vector<int32_t> redo;
   for (int q = 0; q < k; ++q)
@@ -228,7 +228,7 @@ int Ctx::exact_group(const int32_t *ids, int k, const std::function<int(std::vec
     if ((e = launch_exact_fb(x2, std::max(1, std::min(nr, dev_cu * 8)), st))) return hipfail(e, "exact_fb");
     if ((e = hipMemcpyAsync(xs.data(), d_xstatus.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
         (e = hipMemcpyAsync(fm.data(), d_xfmax.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
-        (e = hipStreamSynchronize(st)))
+        (e = sync_st()))
       return hipfail(e, "exact_fb");
     for (int r : redo)
       if (xs[r] == EST_NEEDS_EXACT) return fail(HMC_EHIP, "exact M-step: pruned records still underflow (individual %d)", i0 + r);
@@ -256,7 +256,7 @@ int Ctx::exact_walk_group(ExactArgs &x, int k, int dev_cu) {
     if ((e = d_xspan.ensure(1))) return hipfail(e, "exact_span");
     x.span_max = d_xspan.p;
     if ((e = hipMemsetAsync(d_xspan.p, 0, 4, st)) || (e = launch_exact_span(x, std::max(1, std::min(k, dev_cu * 8)), st)) ||
-        (e = hipMemcpyAsync(&span, d_xspan.p, 4, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+        (e = hipMemcpyAsync(&span, d_xspan.p, 4, hipMemcpyDeviceToHost, st)) || (e = sync_st()))
       return hipfail(e, "exact_span");
     x.span = std::max<long long>(span, 1);
   }
@@ -281,7 +281,7 @@ int Ctx::exact_walk_group(ExactArgs &x, int k, int dev_cu) {
     hipEventRecord(ev[0], st);
     if ((e = launch_exact_walk(x, grid, st, ipw))) return hipfail(e, "exact_walk");
     hipEventRecord(ev[1], st);
-    if ((e = hipStreamSynchronize(st))) return hipfail(e, "exact_walk");
+    if ((e = sync_st())) return hipfail(e, "exact_walk");
     float ms = 0;
     hipEventElapsedTime(&ms, ev[0], ev[1]);
     ms_walk += ms;
@@ -352,7 +352,7 @@ int Ctx::exact_walk_bfs(ExactArgs &x, int k, int dev_cu) {
       if ((e2 = hipMemcpyAsync(d_xcur.p, cur0, 16, hipMemcpyHostToDevice, st)) ||
           (e2 = hipMemcpyAsync(d_xndef.p, &zero, 4, hipMemcpyHostToDevice, st)) ||
           (listed && (e2 = hipMemcpyAsync(d_xidx.p, idx_v.data(), idx_v.size() * 4, hipMemcpyHostToDevice, st))) ||
-          (listed && (e2 = hipStreamSynchronize(st))))
+          (listed && (e2 = sync_st())))
         return hipfail(e2, "exact walk");
       XWalkArgs w2 = w;
       w2.in_base = in_base;
@@ -365,13 +365,13 @@ int Ctx::exact_walk_bfs(ExactArgs &x, int k, int dev_cu) {
       unsigned long long cur[2];
       int nd = 0;
       if ((e2 = hipMemcpyAsync(cur, d_xcur.p, 16, hipMemcpyDeviceToHost, st)) ||
-          (e2 = hipMemcpyAsync(&nd, d_xndef.p, 4, hipMemcpyDeviceToHost, st)) || (e2 = hipStreamSynchronize(st)))
+          (e2 = hipMemcpyAsync(&nd, d_xndef.p, 4, hipMemcpyDeviceToHost, st)) || (e2 = sync_st()))
         return hipfail(e2, "exact walk");
       ++xw_launches;
       xw_units += n;
       std::vector<int32_t> def((size_t)nd);
       if (nd && ((e2 = hipMemcpyAsync(def.data(), d_xdef.p, (size_t)nd * 4, hipMemcpyDeviceToHost, st)) ||
-                 (e2 = hipStreamSynchronize(st))))
+                 (e2 = sync_st())))
         return hipfail(e2, "exact walk");
       const unsigned long long u_end = std::min(cur[0], ucap), e_end = std::min(cur[1], ecap);
       if (nd == n && u_end == u_top)
@@ -393,7 +393,7 @@ int Ctx::exact_walk_bfs(ExactArgs &x, int k, int dev_cu) {
     if (rc) return rc;
   }
   hipEventRecord(ev[1], st);
-  if ((e = hipStreamSynchronize(st))) return hipfail(e, "exact walk");
+  if ((e = sync_st())) return hipfail(e, "exact walk");
   float ms = 0;
   hipEventElapsedTime(&ms, ev[0], ev[1]);
   ms_walk += ms;
@@ -465,7 +465,7 @@ int Ctx::install_host_table(Cands &c, std::vector<int32_t> &succ) {
             (e = hipMemcpyAsync(t_last.p, last.data(), (size_t)P, hipMemcpyHostToDevice, st)) ||
             (e = hipMemcpyAsync(t_succ.p, su.data(), su.size() * 4, hipMemcpyHostToDevice, st)) ||
             (e = hipMemsetAsync(t_ppat.p, 0xFE, (size_t)P * 4, st)) ||  // alleles are kept on the host (ht)
-            (e = hipStreamSynchronize(st))))
+            (e = sync_st())))
     return hipfail(e, "exact: install table");
   this->P = P;
   // head list: start 0, length head_len, id order (PatternManager.cpp:304-306)
@@ -485,7 +485,7 @@ int Ctx::install_host_table(Cands &c, std::vector<int32_t> &succ) {
     }
   if (head_len > 1 && ((e = d_head_al.ensure(tab.size())) ||
                        (e = hipMemcpyAsync(d_head_al.p, tab.data(), tab.size(), hipMemcpyHostToDevice, st)) ||
-                       (e = hipStreamSynchronize(st))))
+                       (e = sync_st())))
     return hipfail(e, "exact: heads");
   if ((rc = set_heads(heads))) return rc;
   ht = c;
@@ -590,7 +590,7 @@ int Ctx::estimate_patterns(int *P_out, uint64_t *rm_out) {
   xc_reuse = false;
   hipEventRecord(ev[5], st);
   hipError_t e;
-  if ((e = hipStreamSynchronize(st))) return hipfail(e, "exact");
+  if ((e = sync_st())) return hipfail(e, "exact");
   // the walk's scratch (up to SCRATCH_MAX) and the tries go back to the E-step
   d_xscr.release();
   d_tr_child.release();

@@ -140,7 +140,7 @@ int Ctx::mine_impl_body(int *P_out, uint64_t *rm_out, int bynum_rounds) {
   }
   {  // before anything is committed: a failed successor walk leaves no table
     int merr = 0;
-    if ((e = hipMemcpyAsync(&merr, d_mine_err.p, 4, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+    if ((e = hipMemcpyAsync(&merr, d_mine_err.p, 4, hipMemcpyDeviceToHost, st)) || (e = sync_st()))
       return hipfail(e, "mine");
     if (merr) return fail(HMC_EUNSUPPORTED, "successor walk left the node window (blocks of %d start loci)", W);
   }
@@ -160,7 +160,7 @@ int Ctx::mine_impl_body(int *P_out, uint64_t *rm_out, int bynum_rounds) {
   if ((e = hipMemcpyAsync(rm_slots.data(), d_rm.p, rm_slots.size() * 8, hipMemcpyDeviceToHost, st)))
     return hipfail(e, "mine");
   hipEventRecord(ev[5], st);
-  if ((e = hipStreamSynchronize(st))) return hipfail(e, "mine");
+  if ((e = sync_st())) return hipfail(e, "mine");
   // The matching lists of the genotype branch (M0) reach tens of GB at
   // cfg 3 (R_M ~ 10^11 entries); give them back to the E-step's stores.
   for (int k = 0; k < 2; ++k) {
@@ -207,7 +207,7 @@ int Ctx::mine_block(int lo, int hi, int mxl, int mnl, double mf, int bynum_round
       if ((e2 = d_flag.ensure(1)) || (e2 = hipMemcpyAsync(d_flag.p, &f, 8, hipMemcpyHostToDevice, st)))
         return hipfail(e2, "mine");
       if (int r2 = allreduce_sum(d_flag.p, 1)) return r2;
-      if ((e2 = hipMemcpyAsync(&f, d_flag.p, 8, hipMemcpyDeviceToHost, st)) || (e2 = hipStreamSynchronize(st)))
+      if ((e2 = hipMemcpyAsync(&f, d_flag.p, 8, hipMemcpyDeviceToHost, st)) || (e2 = sync_st()))
         return hipfail(e2, "mine");
       oom = f > 0.0;
     }
@@ -295,7 +295,7 @@ int Ctx::mine_block(int lo, int hi, int mxl, int mnl, double mf, int bynum_round
     }
     if (diag_mine) {  // per-level list statistics of the parents (diagnostic)
       hipEventRecord(dm1, st);
-      hipStreamSynchronize(st);
+      sync_st();
       float ms = 0;
       hipEventElapsedTime(&ms, dm0, dm1);
       size_t tot_n = 0, max_n = 0, npar = 0;
@@ -342,7 +342,7 @@ int Ctx::mine_block(int lo, int hi, int mxl, int mnl, double mf, int bynum_round
     if ((e = launch_mine_offsets(a, (int)cb, (int)ce, s_ext.p, s_child.p, (int)ce, s_tmp.p, s_tmp.n, d_totals.p, st)))
       return hipfail(e, "mine_offsets");
     const unsigned long long *tot = h_totals.p;
-    if ((e = hipMemcpyAsync(h_totals.p, d_totals.p, 16, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+    if ((e = hipMemcpyAsync(h_totals.p, d_totals.p, 16, hipMemcpyDeviceToHost, st)) || (e = sync_st()))
       return hipfail(e, "mine");
     if (red_timed) {  // this level's cross-rank reduction (the stream has drained)
       float ms = 0;
@@ -380,7 +380,7 @@ int Ctx::mine_block(int lo, int hi, int mxl, int mnl, double mf, int bynum_round
     if ((e = launch_mine_root_size(a, d_rsize.p, lo, hi, st))) return hipfail(e, "mine_root_size");
     std::vector<uint32_t> rsize(hi - lo), rpos(hi - lo);
     if ((e = hipMemcpyAsync(rsize.data(), d_rsize.p + lo, rsize.size() * 4, hipMemcpyDeviceToHost, st)) ||
-        (e = hipStreamSynchronize(st)))
+        (e = sync_st()))
       return hipfail(e, "mine");
     uint64_t acc = (uint64_t)id_base;
     for (int s = hi - 1; s >= lo; --s) {  // roots popped from the back: start L-1 first
@@ -479,7 +479,7 @@ int Ctx::set_heads(const std::vector<std::pair<uint32_t, uint8_t>> &heads /* (id
       (e = hipMemcpyAsync(d_head_ids.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st)))
     return hipfail(e, "set_heads");
   if ((e = hipMemcpyAsync(d_head_pat0.p, pat0.data(), pat0.size() * 4, hipMemcpyHostToDevice, st)) ||
-      (e = hipStreamSynchronize(st)))
+      (e = sync_st()))
     return hipfail(e, "set_heads");
   return HMC_OK;
 }
@@ -497,7 +497,7 @@ int Ctx::bynum_replay(const MineArgs &, int ntot, int mnl, int mxl, int, uint64_
        (e = hipMemcpyAsync(stt.data(), n_start.p, (size_t)ntot * 4, hipMemcpyDeviceToHost, st)) ||
        (e = hipMemcpyAsync(fr.data(), n_freq.p, (size_t)ntot * 8, hipMemcpyDeviceToHost, st)) ||
        (e = hipMemcpyAsync(cnt.data(), n_cnt.p, (size_t)ntot * 4, hipMemcpyDeviceToHost, st)) ||
-       (e = hipStreamSynchronize(st))))
+       (e = sync_st())))
     return hipfail(e, "bynum");
   const unsigned long long n_items = (unsigned long long)mine_args(!have_samples).n_items;
   struct C { int32_t v; int len; };  // v < 0: root of start -v-1 (the empty pattern)
@@ -561,7 +561,7 @@ int Ctx::bynum_replay(const MineArgs &, int ntot, int mnl, int mxl, int, uint64_
   if (ntot > 0 &&
       ((e = hipMemcpyAsync(n_flags.p, fl.data(), (size_t)ntot, hipMemcpyHostToDevice, st)) ||
        (e = hipMemcpyAsync(n_pos.p, pos.data(), (size_t)ntot * 4, hipMemcpyHostToDevice, st)) ||
-       (e = hipStreamSynchronize(st))))
+       (e = sync_st())))
     return hipfail(e, "bynum");
   P = (int)out.size();
   rm_out = rm;
@@ -581,14 +581,14 @@ int Ctx::build_heads_from_nodes(const MineArgs &, int hb, int he) {
     std::vector<uint8_t> fl(n0), alle(n0);
     std::vector<uint32_t> pos(n0);
     if ((e = hipMemcpyAsync(rcb.data(), d_r_child_base.p, 4, hipMemcpyDeviceToHost, st)) ||
-        (e = hipStreamSynchronize(st)))
+        (e = sync_st()))
       return hipfail(e, "heads");
     if (n0 > 0) {
       const long long r0 = (long long)rcb[0] - wbase;  // physical index of root 0's first child
       if ((e = hipMemcpyAsync(fl.data(), n_flags.p + r0, n0, hipMemcpyDeviceToHost, st)) ||
           (e = hipMemcpyAsync(alle.data(), n_allele.p + r0, n0, hipMemcpyDeviceToHost, st)) ||
           (e = hipMemcpyAsync(pos.data(), n_pos.p + r0, (size_t)n0 * 4, hipMemcpyDeviceToHost, st)) ||
-          (e = hipStreamSynchronize(st)))
+          (e = sync_st()))
         return hipfail(e, "heads");
     }
     for (int k = 0; k < n0; ++k)
@@ -605,7 +605,7 @@ int Ctx::build_heads_from_nodes(const MineArgs &, int hb, int he) {
         (e = hipMemcpyAsync(fl.data(), n_flags.p, (size_t)he, hipMemcpyDeviceToHost, st)) ||
         (e = hipMemcpyAsync(alle.data(), n_allele.p, (size_t)he, hipMemcpyDeviceToHost, st)) ||
         (e = hipMemcpyAsync(pos.data(), n_pos.p, (size_t)he * 4, hipMemcpyDeviceToHost, st)) ||
-        (e = hipStreamSynchronize(st)))
+        (e = sync_st()))
       return hipfail(e, "heads");
     std::vector<std::pair<uint32_t, std::vector<uint8_t>>> hs;
     for (int v = hb; v < he; ++v) {
@@ -628,7 +628,7 @@ int Ctx::build_heads_from_nodes(const MineArgs &, int hb, int he) {
     }
     if ((e = d_head_al.ensure(tab.size())) ||
         (e = hipMemcpyAsync(d_head_al.p, tab.data(), tab.size(), hipMemcpyHostToDevice, st)) ||
-        (e = hipStreamSynchronize(st)))
+        (e = sync_st()))
       return hipfail(e, "heads");
   }
   return set_heads(heads);
@@ -679,7 +679,7 @@ int Ctx::mine_level(int level, int n, const int32_t *start, const int32_t *allel
     if ((e = launch_mine_scan(a, level, n, d_lv_start.p, d_lv_al.p, d_lv_sum.p, st))) return hipfail(e, "mine_scan");
     if ((rc = allreduce_sum(d_lv_sum.p, n))) return rc;
   }
-  if ((e = hipMemcpyAsync(freq, d_lv_sum.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) || (e = hipStreamSynchronize(st)))
+  if ((e = hipMemcpyAsync(freq, d_lv_sum.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) || (e = sync_st()))
     return hipfail(e, "mine_level");
   const double denom = genotype ? (double)pan.N : total_weight;  // :178, :190
   for (int c = 0; c < n; ++c) freq[c] = freq[c] / denom;

@@ -69,10 +69,11 @@ if ((e = buf.ensure(vec.size())) ||                                             
   UP(d_rank_of, rk);
   UP(d_r_child_base, rcb);
 #undef UP
-  if ((e = hipStreamSynchronize(st))) return hipfail(e, "upload_panel");
+  if ((e = sync_st())) return hipfail(e, "upload_panel");
   have_panel = true;
   have_model = have_samples = have_estep = have_best = false;
   snap.valid = false;  // a saved table belongs to the panel it was built on
+  win_scale = 1.0;     // window shrinking learnt on another panel does not carry over
   P = 0;
   H = 0;
   return HMC_OK;

@@ -13,7 +13,7 @@ int Ctx::haplocomp(double out[3]) {
         (e = launch_haplocomp_counts(d_geno_im.p, i0, ncmp, L, d_best.p, d_hc_cnt.p, d_hc_bad.p, st)) ||
         (e = hipMemcpyAsync(hc.data(), d_hc_cnt.p, hc.size() * 4, hipMemcpyDeviceToHost, st)) ||
         (e = hipMemcpyAsync(bad.data(), d_hc_bad.p, bad.size() * 4, hipMemcpyDeviceToHost, st)) ||
-        (e = hipStreamSynchronize(st)))
+        (e = sync_st()))
       return hipfail(e, "haplocomp");
   }
   double cnt[6] = {0, 0, 0, 0, 0, 0};  // se_num, se_den, ihp_num, ihp_den, igp_num, igp_den
@@ -46,7 +46,7 @@ int Ctx::init_best() {
   hipError_t e;
   if ((e = d_best.ensure(best_res.size())) ||
       (e = hipMemcpyAsync(d_best.p, best_res.data(), best_res.size(), hipMemcpyHostToDevice, st)) ||
-      (e = hipStreamSynchronize(st)))
+      (e = sync_st()))
     return hipfail(e, "resolutions");
   have_best = best_on_host = true;
   return HMC_OK;
@@ -110,7 +110,7 @@ int Ctx::model_save() {
       (e = dcopy(snap.last, t_last, p)) || (e = dcopy(snap.succ, t_succ, p * A)) ||
       (e = dcopy(snap.head_ids, d_head_ids, std::max<size_t>(n_head, 1))) ||
       (e = dcopy(snap.head_pat0, d_head_pat0, A + 1)) ||
-      (head_len > 1 && (e = dcopy(snap.head_al, d_head_al, p * head_len))) || (e = hipStreamSynchronize(st)))
+      (head_len > 1 && (e = dcopy(snap.head_al, d_head_al, p * head_len))) || (e = sync_st()))
     return hipfail(e, "model_save");
   snap.P = P;
   snap.L = pan.L;
@@ -142,7 +142,7 @@ int Ctx::em_rewind() {
       (e = dcopy(d_head_ids, snap.head_ids, std::max<size_t>(snap.n_head, 1))) ||
       (e = dcopy(d_head_pat0, snap.head_pat0, A + 1)) ||
       (snap.head_len > 1 && (e = dcopy(d_head_al, snap.head_al, p * snap.head_len))) ||
-      (e = hipStreamSynchronize(st)))
+      (e = sync_st()))
     return hipfail(e, "em_rewind");
   P = snap.P;
   head_len = snap.head_len;
@@ -164,6 +164,7 @@ int Ctx::em_rewind() {
   h_cost.clear();
   prev_rneed.clear();
   prev_P = 0;
+  win_scale = 1.0;
   fcap = fcap_user;
   return HMC_OK;
 }

@@ -388,29 +388,28 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
           if (s == EST_OVERFLOW_FRONTIER || s == EST_OVERFLOW_CONTRIB) grow = true;
         }
         if (grow) {
+          // as restart_status: fail only when the capacity that overflowed was
+          // already the largest (F_MAX itself is tried), contributions bounded
+          // like ccap1 (INT32_MAX / 2)
+          bool f_over = false, c_over = false;
           for (int bi : todo) {
-            const int s = h_status[bi];
-            if (s == EST_OVERFLOW_FRONTIER && wfcap < F_MAX) {
-              wfcap = (int)std::min<int64_t>(F_MAX, (int64_t)wfcap * 4);
-              fcap = std::max(fcap, wfcap);
-              break;
-            }
+            f_over = f_over || h_status[bi] == EST_OVERFLOW_FRONTIER;
+            c_over = c_over || h_status[bi] == EST_OVERFLOW_CONTRIB;
           }
-          for (int bi : todo)
-            if (h_status[bi] == EST_OVERFLOW_CONTRIB) {
-              ccap_mult *= 2;
-              break;
-            }
-          for (int bi : todo)
-            if ((h_status[bi] == EST_OVERFLOW_FRONTIER && wfcap >= F_MAX) ||
-                (h_status[bi] == EST_OVERFLOW_CONTRIB && (int64_t)ccap_mult * wfcap >= INT32_MAX))
-              return fail(HMC_EUNSUPPORTED, "frontier exceeds %d states", F_MAX);
+          if (f_over && wfcap >= F_MAX) return fail(HMC_EUNSUPPORTED, "frontier exceeds %d states", F_MAX);
+          if (c_over && (int64_t)ccap_mult * wfcap >= INT32_MAX / 2)
+            return fail(HMC_EUNSUPPORTED, "contributions of one locus exceed %d", INT32_MAX / 2);
+          if (f_over) {
+            wfcap = (int)std::min<int64_t>(F_MAX, (int64_t)wfcap * 4);
+            fcap = std::max(fcap, wfcap);
+          }
+          if (c_over) ccap_mult *= 2;
           if (debug_mem) fprintf(stderr, "[hmc] window %d/%d: capacities %d states x %d, the window again\n", w + 1, nwin, wfcap, ccap_mult);
           if ((e = hipMemcpyAsync(d_ck_cursor.p, &zero64, 8, hipMemcpyHostToDevice, st))) return hipfail(e, "windowed E-step");
           continue;
         }
         if ((e = hipMemcpyAsync(h_re_w.data(), d_re.p, (size_t)n * 8, hipMemcpyDeviceToHost, st)) ||
-            (e = hipStreamSynchronize(st)))
+            (e = sync_st()))
           return hipfail(e, "windowed E-step");
         for (int bi : todo) re_tot[bi] += h_re_w[bi];
       }
@@ -540,7 +539,7 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     hipError_t e2;
     std::vector<int32_t> gs(n);
     if ((e2 = hipMemcpyAsync(gs.data(), d_gc_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
-        (e2 = hipStreamSynchronize(st)))
+        (e2 = sync_st()))
       return hipfail(e2, "trace collection");
     hipEventElapsedTime(&ms, ev[4], ev[5]);
     ms_ck += ms;
@@ -554,7 +553,7 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
       fprintf(stderr, "[hmc] collection for %zu individuals: %.1f ms%s\n", gc_ids.size(), ms, again.empty() ? "" : " (node store full: grows)");
     if (!again.empty()) {
       unsigned long long used = 0;
-      if ((e2 = hipMemcpyAsync(&used, d_node_cursor.p, 8, hipMemcpyDeviceToHost, st)) || (e2 = hipStreamSynchronize(st)))
+      if ((e2 = hipMemcpyAsync(&used, d_node_cursor.p, 8, hipMemcpyDeviceToHost, st)) || (e2 = sync_st()))
         return hipfail(e2, "trace collection");
       used = std::min<unsigned long long>(used, d_nodes.n / 3);
       if ((e2 = hipMemcpyAsync(d_node_cursor.p, &used, 8, hipMemcpyHostToDevice, st)) ||
@@ -616,7 +615,7 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
       hipEventRecord(ev[2], st);
       if ((e = launch_traceback(t, 0, st))) return hipfail(e, "traceback");
       hipEventRecord(ev[3], st);
-      if ((e = hipStreamSynchronize(st))) return hipfail(e, "traceback");
+      if ((e = sync_st())) return hipfail(e, "traceback");
       hipEventElapsedTime(&ms, ev[2], ev[3]);
       ms_tb += ms;
     }
@@ -625,10 +624,8 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
       for (int w = 0; w < nwin; ++w) rec_all[bi] += rw[(size_t)bi * nwin + w];
     }
   }
-  if ((e = hipMemcpyAsync(d_re.p, re_tot.data(), (size_t)n * 8, hipMemcpyHostToDevice, st)) || (e = hipStreamSynchronize(st)))
+  if ((e = hipMemcpyAsync(d_re.p, re_tot.data(), (size_t)n * 8, hipMemcpyHostToDevice, st)) || (e = sync_st()))
     return hipfail(e, "windowed E-step");
-  prev_rneed.swap(rec_all);  // record words per individual (the next E-step's estimates at this scale)
-  prev_P = P;
   // individuals whose forward likelihoods underflow: the classic passes, which
   // rebuild their structure with extend()'s forward test (prune mode)
   if (!underflow.empty()) {
@@ -638,7 +635,15 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     rc = estep_split(underflow);
     window_mode = saved;
     if (rc) return rc;
+    // estep_split left prev_rneed = its own needs (non-zero only for the
+    // underflow individuals): keep every other individual's windowed record
+    // words, or the next E-step would estimate 64 words for them and re-run
+    // nearly everyone's structure pass
+    if (prev_rneed.size() == rec_all.size())
+      for (int bi : underflow) rec_all[bi] = prev_rneed[bi];
   }
+  prev_rneed.swap(rec_all);  // record words per individual (the next E-step's estimates at this scale)
+  prev_P = P;
   return HMC_OK;
 }
 

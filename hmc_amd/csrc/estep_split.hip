@@ -23,8 +23,10 @@
 //
 // If pass 2 meets a forward likelihood of 0 before the last locus (the
 // reference would skip that pair) the individual is flagged EST_NEEDS_EXACT
-// and the host re-runs it on the fused kernel (estep.hip), which evaluates
-// extend()'s test as it goes.  Results are bit-identical to the fused kernel.
+// and the host re-runs only it through pass 1 in prune mode (each new state's
+// forward sum in add order, extend()'s test `forward_likelihood() > 0`,
+// HaploBuilder.cpp:237) and then pass 2 again, in the same store regions.
+// The fused kernel (estep.hip) is a variants-library option only.
 #include "hmc_internal.hpp"
 #include "select.hpp"
 #include "coop_select.hpp"

@@ -357,6 +357,7 @@ hipError_t launch_gather_resolutions(const uint8_t *rows, int L, const int32_t *
                                      const uchar2 *geno_im, int i0, int n, uint8_t *out, hipStream_t st);
 hipError_t launch_haplocomp_counts(const uchar2 *geno_im, int i0, int n, int L, const uint8_t *res, int32_t *cnt,
                                    int32_t *bad, hipStream_t st);
+hipError_t launch_stall(double ms, hipStream_t st);  // hmc_debug_stall (mstep.hip)
 hipError_t launch_scan_i32(const int32_t *in, int32_t *out_excl, int n, int mul, int32_t *total, hipStream_t st);
 
 }  // namespace hmc

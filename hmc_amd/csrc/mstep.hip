@@ -749,4 +749,22 @@ hipError_t launch_mine_succ_level(const MineArgs &a, const PatternTable &t, int 
   return hipGetLastError();
 }
 
+// Test hook of the bounded collective wait (hmc_debug_stall): one wavefront
+// that keeps the context stream busy for `ticks` of the device's
+// constant-rate wall clock, then exits — every launch ends on its own.
+__global__ void __launch_bounds__(64) stall_kernel(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+hipError_t launch_stall(double ms, hipStream_t st) {
+  if (!(ms > 0) || ms > 60000) return hipErrorInvalidValue;
+  int dev = 0, khz = 0;
+  hipError_t e;
+  if ((e = hipGetDevice(&dev)) || (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev))) return e;
+  if (khz <= 0) khz = 100000;
+  hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, st, (long long)(ms * khz));
+  return hipGetLastError();
+}
+
 }  // namespace hmc

@@ -209,8 +209,19 @@ class HaploModel:
         self._check(lib().hmc_set_reduction(self._h, {"ordered": 0, "allreduce": 1}[mode]))
 
     def set_force_collectives(self, on: bool = True):
-        """Test hook: a one-rank context with a communicator runs every collective."""
+        """Test hook: a one-rank context with a communicator runs every collective
+        (the ordered chain's hop as a grouped ncclSend/ncclRecv to itself)."""
         self._check(lib().hmc_set_force_collectives(self._h, int(bool(on))))
+
+    def comm_stats(self) -> dict:
+        """Point-to-point hops of the ordered chain issued so far (hmc_comm_stats)."""
+        s, r, b = C.c_int64(), C.c_int64(), C.c_uint64()
+        self._check(lib().hmc_comm_stats(self._h, C.byref(s), C.byref(r), C.byref(b)))
+        return dict(sends=s.value, recvs=r.value, bytes_received=b.value)
+
+    def set_comm_timeout(self, seconds: float):
+        """Bounded waits of an RCCL context (hmc_set_comm_timeout)."""
+        self._check(lib().hmc_set_comm_timeout(self._h, float(seconds)))
 
     def set_estep_mode(self, mode: int):
         """0 = split E-step (structure pass + value pass, default), 1 = fused kernel."""
@@ -252,12 +263,17 @@ class HaploModel:
     def estep_windows(self) -> dict:
         w, wl, g, ms = C.c_int(), C.c_int(), C.c_int(), C.c_double()
         self._check(lib().hmc_last_estep_windows(self._h, C.byref(w), C.byref(wl), C.byref(g), C.byref(ms)))
-        return dict(windows=w.value, window_loci=wl.value, groups=g.value, collection_ms=ms.value)
+        rs, sc = C.c_int(), C.c_double()
+        self._check(lib().hmc_last_estep_restarts(self._h, C.byref(rs), C.byref(sc)))
+        return dict(windows=w.value, window_loci=wl.value, groups=g.value, collection_ms=ms.value,
+                    restarts=rs.value, window_scale=sc.value)
 
     def set_value_mode(self, mode: str):
         """Value pass of the split E-step: "fast" (value-only k-best lists, the
-        libstdc++ permutations only for individuals with ties) or "exact" (the
-        permutations for everyone; default).  Results are identical."""
+        libstdc++ permutations only for individuals with ties), "exact" (the
+        permutations for everyone) or "auto" (default: fast on multi-allelic
+        panels once the model is smaller than the panel, exact otherwise and
+        after an E-step that re-ran more than 35 %).  Results are identical."""
         self._check(lib().hmc_set_value_mode(self._h, {"fast": 0, "exact": 1, "auto": 2}[mode]))
 
     def set_value_layout(self, mode: int):

@@ -179,6 +179,21 @@ int hmc_last_mine_stats(const hmc_ctx *ctx, int *blocks, int64_t *nodes, double 
  * levels reduced.  0 / 0 on one rank.  Replaces no reference interface
  * (the reference is single-process). */
 int hmc_last_mine_reduction(const hmc_ctx *ctx, double *ms, int *levels);
+/* Point-to-point hops of the ordered chain issued by this context since its
+ * creation: ncclSend calls, ncclRecv calls and bytes received (a forced
+ * one-rank context sends each hop to itself, grouped).  Replaces no reference
+ * interface. */
+int hmc_comm_stats(const hmc_ctx *ctx, int64_t *sends, int64_t *recvs, uint64_t *bytes_received);
+/* Bounded waits of an RCCL context (default 1800 s): every stream sync polls
+ * ncclCommGetAsyncError; on an asynchronous error or after `seconds` without
+ * the stream draining, the communicator is aborted (ncclCommAbort — a
+ * caller-owned communicator too: do not destroy it afterwards) and the call
+ * returns HMC_ERCCL, as does every later collective of the context.  A rank
+ * whose neighbour died therefore ends instead of hanging in ncclRecv. */
+int hmc_set_comm_timeout(hmc_ctx *ctx, double seconds);
+/* Test hook of the bounded wait: keeps the context stream busy for `ms`
+ * (one wavefront, bounded) and syncs it through the same wait. */
+int hmc_debug_stall(hmc_ctx *ctx, double ms);
 /* Pattern table in id order (HaploPattern.h:16-98).  succ[P][max_alleles]
  * holds pattern ids (-1 = none); alleles[P][maxlen] symbols (-1 padding).
  * Any output pointer may be NULL. */
@@ -416,6 +431,11 @@ int hmc_set_estep_windows(hmc_ctx *ctx, int mode, int window_loci);
  * individuals, and device ms of the trace collections (part of the value
  * passes' time). */
 int hmc_last_estep_windows(const hmc_ctx *ctx, int *windows, int *window_loci, int *groups, double *recompute_ms);
+/* Restarts of the last E-step (a frontier or contribution capacity grown, or
+ * a window's traces past the store: windows 0.6x as long, or for a fixed
+ * window length smaller groups) and the window scale now in force (1.0 until
+ * a trace-store overflow; reset by a panel load or hmc_set_shard). */
+int hmc_last_estep_restarts(const hmc_ctx *ctx, int *restarts, double *window_scale);
 /* Individuals the last E-step re-ran with the libstdc++ permutations (mode 0)
  * and the device time of those re-runs (ms, part of values_ms). */
 int hmc_last_estep_order(const hmc_ctx *ctx, int *n_rerun, double *rerun_ms);

@@ -1597,6 +1597,23 @@ double ora_time_resolve_list(void *h, const int *ids, int n) {
   m->hp.clear();
   return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
+// HaploBuilder::initialize (HaploBuilder.cpp:25-33) clears one std::map per
+// pattern (m_best_pair, vector<map<int, int> >, HaploBuilder.h:29) before every
+// individual — O(P) work the restatement's resolve skips (its key table is
+// per-locus).  The bench's CPU baseline adds it back: seconds of one such
+// pass over P empty maps, the best of `reps` passes.
+double ora_time_best_pair_reset(long long P, int reps) {
+  if (P <= 0 || reps <= 0) return 0.0;
+  std::vector<std::map<int, int>> best((size_t)P);
+  double best_s = 1e300;
+  for (int r = 0; r < reps; ++r) {
+    best[(size_t)(r * 7919) % (size_t)P][r] = r;  // one live entry, as after an individual
+    auto t0 = std::chrono::steady_clock::now();
+    for (auto &x : best) x.clear();
+    best_s = std::min(best_s, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+  }
+  return best_s;
+}
 double ora_time_find_patterns_root_list(void *h, const int *roots, int n) {
   Model *m = (Model *)h;
   ora::Params &pr = m->prm;

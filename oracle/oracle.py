@@ -90,6 +90,8 @@ def lib():
         L.ora_time_find_patterns_roots.argtypes = [vp, i, i]
         L.ora_time_resolve_list.restype = d
         L.ora_time_resolve_list.argtypes = [vp, P(i), i]
+        L.ora_time_best_pair_reset.restype = d
+        L.ora_time_best_pair_reset.argtypes = [C.c_longlong, i]
         L.ora_time_find_patterns_root_list.restype = d
         L.ora_time_find_patterns_root_list.argtypes = [vp, P(i), i]
         L.ora_resolve_range.restype = d
@@ -194,6 +196,12 @@ class Oracle:
         """Seconds of HaploBuilder::resolve over the listed individuals."""
         a = np.ascontiguousarray(ids, np.int32)
         return lib().ora_time_resolve_list(self.h, _p(a, C.c_int), len(a))
+
+    @staticmethod
+    def time_best_pair_reset(P: int, reps: int = 3) -> float:
+        """Seconds of HaploBuilder::initialize's per-individual clear of P
+        maps (HaploBuilder.cpp:25-33), which resolve() here does not repeat."""
+        return lib().ora_time_best_pair_reset(int(P), int(reps))
 
     def time_find_patterns_root_list(self, roots) -> float:
         """Seconds of searchPattern + initialize over the listed start loci."""

@@ -10,6 +10,8 @@ import socket
 import subprocess
 import sys
 
+import time
+
 import numpy as np
 import pytest
 
@@ -1047,9 +1049,72 @@ def test_rccl_collectives_one_rank(oracle_mod, how, reduction):
     assert [x["ll"] for x in m.log] == r["ll"].tolist()
     assert np.array_equal(res, r["resolutions"])
     np.testing.assert_array_equal(np.array([x["haplocomp"] for x in m.log]), r["haplocomp"])
+    cs = m.comm_stats()
+    if reduction == "ordered":
+        # every mining level's sums and every E-step's LL / weight went through
+        # a grouped ncclSend + ncclRecv hop (to this rank itself) into a
+        # NaN-poisoned buffer: the run above is bit-exact through that path
+        assert cs["sends"] == cs["recvs"] > 0 and cs["bytes_received"] > 0, cs
+        print(f"ordered chain over RCCL send/recv: {cs}", flush=True)
+    else:
+        assert cs["sends"] == cs["recvs"] == 0, cs
     m.close()
     if rccl is not None:
         assert rccl.hmc_rccl_comm_destroy(comm) == 0  # the caller's communicator outlives the context
+
+
+@pytest.mark.parametrize("name,kw", [("cfg1", {}), ("a3miss5", {}), ("n300", {"model": "MC"})])
+def test_rccl_send_recv_chain_full_em(oracle_mod, name, kw):
+    """The ordered reduction's point-to-point path (ctx.hpp ordered_chain:
+    ncclRecv -> continue -> ncclSend -> ncclBroadcast) on a one-rank RCCL
+    communicator: each hop is a grouped ncclSend/ncclRecv to the rank itself
+    into a NaN-poisoned buffer.  Whole EMs equal the restatement's bit for bit
+    (every LL, every accepted pair, the M0 table)."""
+    p = panel(name)
+    m = hmc_amd.HaploModel(device=0, rank=0, world=1, unique_id=hmc_amd.HaploModel.unique_id())
+    m.set_force_collectives(True)
+    m.set_comm_timeout(600)
+    o0 = oracle_mod.Oracle(p.alleles, p.types, sample_size=10, max_iter=10)
+    if kw.get("model") == "MC":
+        m.model, m.mc_order = "MC", 1
+        o0.set_model("MC", 1)
+    m.max_iteration = 10
+    res = m.run(hmc_amd.GenoData.from_panel(p))
+    r = o0.run()
+    assert [x["ll"] for x in m.log] == r["ll"].tolist()
+    assert np.array_equal(res, r["resolutions"])
+    cs = m.comm_stats()
+    assert cs["sends"] == cs["recvs"] > 0, cs
+    m.close()
+
+
+HMC_ERCCL = -6  # include/hmc_amd.h
+
+
+def test_rccl_bounded_wait_aborts():
+    """A stream that does not drain within the communicator timeout ends the
+    call with HMC_ERCCL (the communicator is aborted, ncclCommAbort) instead
+    of waiting forever; later collectives of the context fail the same way.
+    The stall is a bounded one-wavefront kernel (hmc_debug_stall)."""
+    import ctypes as C
+    m = hmc_amd.HaploModel(device=0, rank=0, world=1, unique_id=hmc_amd.HaploModel.unique_id())
+    m.set_force_collectives(True)
+    L = hmc_amd.lib()
+    m.set_comm_timeout(30)
+    assert L.hmc_debug_stall(m._h, C.c_double(50.0)) == 0  # drains inside the timeout
+    m.set_comm_timeout(0.2)
+    t0 = time.time()
+    rc = L.hmc_debug_stall(m._h, C.c_double(2000.0))
+    dt = time.time() - t0
+    msg = L.hmc_ctx_error(m._h).decode()
+    assert rc == HMC_ERCCL, (rc, msg)
+    assert "timeout" in msg, msg
+    assert dt < 10, dt
+    p = panel("cfg1")
+    with pytest.raises(hmc_amd.HMCError) as ei:
+        m.run(hmc_amd.GenoData.from_panel(p))
+    assert ei.value.code == HMC_ERCCL, ei.value
+    m.close()
 
 
 def test_shard_ranges_balanced_and_tiling():

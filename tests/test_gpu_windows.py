@@ -130,6 +130,56 @@ def test_windowed_equals_classic_cfg2():
     assert runs[0] == runs[1] == runs[2]
 
 
+def _homozygous_lead_panel(N=200, lead=80, L=160, seed=11):
+    """A founder mosaic behind `lead` loci where everyone is homozygous: the
+    window probe (the first >= 64 loci) sees one-state frontiers, so the plan
+    under-sizes the trace ring for the later windows."""
+    q = synth.founder_mosaic(N, L, A=2, seed=seed)
+    a = np.concatenate([np.full((N, 2, lead), ord("1"), np.int32), q.alleles], axis=2)
+    return synth.Panel(alleles=a, types="S" * (lead + L))
+
+
+def test_windowed_fixed_length_trace_overflow_shrinks_group(oracle_mod):
+    """The round-5 hang (gpurun_out/r5f: window_ab.py CFG=3 on `always:1000`)
+    pinned: a FIXED window length whose two windows of traces exceed the trace
+    store.  Before ecc6276 the plan ignored win_scale for a fixed length, so
+    every ESTEP_RESTART re-made the same plan and the E-step never ended; now
+    the plan takes smaller groups until the traces fit (ctx_window.cpp plan
+    loop, `fits`), bounded by win_scale >= 1e-3.  Here a 2 MB trace budget
+    and a probe that sees only homozygous loci force several restarts; the
+    E-step must end in >= 2 groups, bit-exact against the restatement, and
+    the next E-step (a new model, the shrunken scale kept) equal the classic
+    passes'."""
+    p = _homozygous_lead_panel()
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
+    o.find_patterns()
+    pt = o.patterns()
+    m = gpu_model(p)
+    m.set_estep_windows("always", 8)
+    m.set_store_budgets(trace_bytes=2 << 20, record_bytes=64 << 20)
+    m.set_patterns(pt["start"], pt["len"], pt["freq"], pt["tp"], pt["succ"], last_symbols(pt))
+    ll_g, H, re_g = m.resolve_all()
+    w = m.estep_windows()
+    print(f"windows {w}", flush=True)
+    assert w["restarts"] >= 1 and w["window_scale"] < 1.0, w
+    assert w["groups"] >= 2 and w["window_loci"] == 8, w
+    o.reset_counters()
+    assert_estep_equal(m, o, ll_g, o.resolve_all(), H, re_g)
+    # E2 on the GPU's own M1, windows at the scale learnt above vs the classic passes
+    c = gpu_model(p)
+    c.set_estep_windows("never")
+    c.set_patterns(pt["start"], pt["len"], pt["freq"], pt["tp"], pt["succ"], last_symbols(pt))
+    c.resolve_all()
+    out = []
+    for x in (m, c):
+        x.find_patterns()
+        ll, H2, re2 = x.resolve_all()
+        al, wt, tw = x.samples(H2)
+        out.append((float(ll).hex(), H2, re2, al.tobytes(), wt.tobytes(), float(tw).hex()))
+    assert out[0] == out[1]
+    assert m.estep_windows()["groups"] >= 2
+
+
 def _heartbeat(path, stop):
     """A line every 30 s under gpurun_out/ while a multi-minute test runs, so
     that a runner watching its output directory sees progress."""
