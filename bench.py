@@ -53,7 +53,7 @@ from hmc_amd import synth  # noqa: E402
 
 METRIC = "individuals×loci/sec per EM iter, synthetic panel, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s HBM3E (spec)
-PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r05", "r04", "r03")]  # newest profile of the workload first
+PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r06", "r05", "r04", "r03")]  # newest profile of the workload first
 DBL_MAX = sys.float_info.max
 # What bounds estep_values (SQ counters under profiles/): the
 # roofline prices it against HBM as the contract asks, but the kernel moves a
@@ -62,7 +62,9 @@ DBL_MAX = sys.float_info.max
 # The sampled CPU estimate checked against the whole single-thread chain at
 # cfg 2 (bench.py --config 2 --cpu-validate on a GPU box, same run).
 VALIDATION_NOTE = "profiles/r04/cpu_validate_cfg2.json"
-LIMITER = "VALU issue of the segmented k-best selection (SQ_INSTS_VALU x 4 cycles over the SIMDs' issue capacity, DESIGN.md 9), not HBM bandwidth"
+LIMITER = ("VALU issue of the segmented k-best selection: the SIMDs' VALU issue slots measured busy "
+           "(4 x (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) over 32 SIMDs x SQ_BUSY_CYCLES per SE; dual issue calibrated "
+           "by tools/diag/issue_bench.hip, DESIGN.md 9), not HBM bandwidth")
 
 
 def parse():
@@ -376,11 +378,15 @@ def main():
                 "traffic_same_build": pmc["same_build"] if pmc else None,
                 "hbm_frac_measured": hbm_frac_meas if pmc and pmc["same_build"] else None,
                 "valu_issue_frac": sq["valu_issue_frac"] if sq and sq["same_build"] else None,
-                "valu_issue_frac_2cyc": sq["valu_issue_frac_2cyc"] if sq and sq["same_build"] else None,
+                "valu_dual_issue_share": sq["valu_dual_issue_share"] if sq and sq["same_build"] else None,
+                "valu_issue_frac_nominal_4cyc": sq["valu_issue_frac_nominal_4cyc"] if sq and sq["same_build"] else None,
+                "valu_issue_frac_nominal_2cyc": sq["valu_issue_frac_nominal_2cyc"] if sq and sq["same_build"] else None,
                 "lds_bank_conflict_ratio": sq["lds_bank_conflict_ratio"] if sq and sq["same_build"] else None,
                 "valu_issue_source": sq.get("source") if sq else None,
                 "valu_issue_same_build": sq["same_build"] if sq else None,
-                "valu_issue_formula": "SQ_INSTS_VALU * 4 cycles / (1024 SIMDs * 2.4 GHz * kernel time of the SQ pass)",
+                "valu_issue_formula": "4 * (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) / (32 SIMDs per SE * SQ_BUSY_CYCLES): "
+                                      "measured VALU issue-slot occupancy (one instruction per quad-cycle, two when "
+                                      "they dual-issue; profiles/r06/issue/)",
                 "limiter": LIMITER,
                 "alg_bytes_per_launch": 8.0 * r_e_all / world / max(1, n_launch),
                 "avg_launch_ms": val_ms / max(1, n_launch),
@@ -434,12 +440,21 @@ def sq_summary(tag, ident):
     d = _profile_json(f"sq_estep_values_{tag}.json", ident)
     if not d or not d.get("kernels"):
         return None
-    ks = d["kernels"].values()
+    ks = list(d["kernels"].values())
     t = sum(k["kernel_seconds"] for k in ks)
     cap = 1024 * 2.4e9 * t
     valu = sum(k["valu_insts"] for k in ks)
     lds_conf = max(k["lds_bank_conflict_ratio"] for k in ks)
-    return {"valu_issue_frac": 4.0 * valu / cap if cap else None, "valu_issue_frac_2cyc": 2.0 * valu / cap if cap else None,
+    meas, dual = None, None
+    bp = [k.get("busy_pass") for k in ks]
+    if all(b and b.get("SQ_BUSY_CYCLES") for b in bp):  # measured issue over every instantiation the pass launched
+        v1 = sum(b["SQ_INSTS_VALU"] for b in bp)
+        v2 = sum(b["SQ_ACTIVE_INST_VALU2"] or 0.0 for b in bp)
+        meas = 4.0 * (v1 - v2) / (32.0 * sum(b["SQ_BUSY_CYCLES"] for b in bp))
+        dual = 2.0 * v2 / v1 if v1 else None
+    return {"valu_issue_frac": meas, "valu_dual_issue_share": dual,
+            "valu_issue_frac_nominal_4cyc": 4.0 * valu / cap if cap else None,
+            "valu_issue_frac_nominal_2cyc": 2.0 * valu / cap if cap else None,
             "lds_bank_conflict_ratio": lds_conf, "source": d["source"], "same_build": d["same_build"]}
 
 

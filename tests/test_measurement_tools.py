@@ -77,6 +77,45 @@ def test_sq_summary_issue_fraction_json(tmp_path):
     d = json.load(open(out))
     kk = d["kernels"]["hmc::estep_values<false, 4, false, true>"]
     assert kk["launches"] == 2 and abs(kk["kernel_seconds"] - 2e-9) < 1e-18
-    assert abs(kk["valu_issue_frac"] - 4 * 4.8e3 / (1024 * 2.4e9 * 2e-9)) < 1e-9
+    assert abs(kk["valu_issue_frac_nominal"] - 4 * 4.8e3 / (1024 * 2.4e9 * 2e-9)) < 1e-9
+    assert kk["valu_issue_frac"] is None  # no busy pass: nothing measured
     assert abs(kk["lds_bank_conflict_ratio"] - 0.5) < 1e-12
     assert d["library"] == {"sha256_16": "abc"}
+
+
+def test_sq_summary_measured_issue_with_dual_issue(tmp_path):
+    """Measured VALU issue (round 6): one instruction per quad-cycle per SIMD,
+    two when they dual-issue (SQ_ACTIVE_INST_VALU2 quad-cycles), over 32 SIMDs
+    per shader engine x SQ_BUSY_CYCLES (summed over the engines):
+    4 * (VALU - VALU2) / (32 * BUSY); the mix pass gives per-type shares."""
+    k = "void hmc::estep_values<false, 4, false, true>(hmc::ValueArgs)"
+    write_counters(tmp_path / "a.csv", [(1, k, "SQ_WAVE_CYCLES", 100.0), (1, k, "SQ_INSTS_VALU", 1e6)])
+    write_counters(tmp_path / "b.csv", [(1, k, "SQ_LDS_BANK_CONFLICT", 1.0), (1, k, "SQ_ACTIVE_INST_LDS", 2.0)])
+    write_counters(tmp_path / "busy.csv", [(1, k, "SQ_INSTS_VALU", 1000.0), (1, k, "SQ_ACTIVE_INST_VALU2", 100.0),
+                                           (1, k, "SQ_BUSY_CYCLES", 50.0)])
+    write_counters(tmp_path / "mix.csv", [(1, k, "SQ_INSTS_VALU", 1000.0), (1, k, "SQ_INSTS_VALU_INT32", 450.0),
+                                          (1, k, "SQ_INSTS_VALU_ADD_F64", 10.0)])
+    with open(tmp_path / "bench.json", "w") as f:
+        f.write(json.dumps({"library": {"sha256_16": "abc"}}) + "\n")
+    out = tmp_path / "sq.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "sq_summary.py"), str(tmp_path / "a.csv"),
+                    str(tmp_path / "b.csv"), "estep_values", str(out), str(tmp_path / "bench.json"),
+                    str(tmp_path / "busy.csv"), str(tmp_path / "mix.csv")], capture_output=True, text=True, check=True)
+    kk = json.load(open(out))["kernels"]["hmc::estep_values<false, 4, false, true>"]
+    assert kk["valu_issue_frac"] == 4 * (1000 - 100) / (32 * 50.0)
+    assert kk["valu_dual_issue_share"] == 0.2 and kk["valu_cycles_per_inst"] == 3.6
+    assert kk["valu_mix"]["INT32"] == 0.45 and kk["valu_mix"]["ADD_F64"] == 0.01
+    sys.path.insert(0, ROOT)
+    import bench
+    d = json.load(open(out))
+    d["library"] = {"sha256_16": "abc"}
+    os.makedirs(tmp_path / "p", exist_ok=True)
+    with open(tmp_path / "p" / "sq_estep_values_cfgX.json", "w") as f:
+        json.dump(d, f)
+    old = bench.PMC_DIRS
+    try:
+        bench.PMC_DIRS = [str(tmp_path / "p")]
+        sq = bench.sq_summary("cfgX", {"sha256_16": "abc"})
+    finally:
+        bench.PMC_DIRS = old
+    assert sq["same_build"] and sq["valu_issue_frac"] == kk["valu_issue_frac"] and sq["valu_dual_issue_share"] == 0.2

@@ -3,8 +3,8 @@
 #   HBM traffic of the dominant kernel estep_values from two separate PMC
 #   passes (FETCH_SIZE, WRITE_SIZE) over the bench command itself, the
 #   kernel-trace stats of the same command, and SQ counter passes (instruction
-#   mix, LDS waits / bank conflicts, wave cycles) of both E-step passes on a
-#   short run.
+#   mix, LDS waits / bank conflicts, wave cycles, VALU issue busy incl. dual
+#   issue, typed VALU mix) of both E-step passes on a short run.
 # usage: bash tools/profile_round.sh OUTDIR TAG CONFIG
 #   -> OUTDIR/commit/TAG/ (copy to profiles/TAG afterwards); the PMC summary is
 #      profiles/TAG/pmc_estep_values_cfgCONFIG.json, which bench.py reads.
@@ -38,7 +38,9 @@ tail -1 "$OUT/trace.json" > "$DEST/bench_under_rocprof_cfg$CFG.json"
 SHORT="bench.py --config $CFG --no-cpu-baseline --steps 2 --warmup 0"
 [ -n "${SKIP_SQ:-}" ] && { echo "[profile] done (SQ passes skipped)" >&2; exit 0; }
 for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU" \
-         "SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM"; do
+         "SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM" \
+         "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_CYCLES GRBM_GUI_ACTIVE" \
+         "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_TRANS_F64"; do
   N=$(echo "$P" | awk '{print $1}')
   echo "[profile] SQ pass $N" >&2
   timeout -s KILL 300 rocprofv3 --pmc $P --kernel-include-regex "estep_values|estep_structure" --output-format csv -d "$OUT/sq_$N" -o s -- \
@@ -46,5 +48,6 @@ for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
   cp "$(find "$OUT/sq_$N" -name "*counter_collection.csv" | head -n 1)" "$DEST/sq_${N}_cfg$CFG.csv"
 done
 python3 tools/sq_summary.py "$DEST/sq_SQ_WAVES_cfg$CFG.csv" "$DEST/sq_SQ_INSTS_LDS_cfg$CFG.csv" $K \
-  "$DEST/sq_${K}_cfg$CFG.json" "$OUT/sq_SQ_WAVES.json"
+  "$DEST/sq_${K}_cfg$CFG.json" "$OUT/sq_SQ_WAVES.json" "$DEST/sq_SQ_ACTIVE_INST_VALU_cfg$CFG.csv" \
+  "$DEST/sq_SQ_INSTS_VALU_INT32_cfg$CFG.csv"
 echo "[profile] done" >&2
