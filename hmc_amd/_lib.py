@@ -115,6 +115,7 @@ _SIGS = [
     ("hmc_last_exact_walk", _i, [_vp, _P(C.c_int64), _P(C.c_int64), _P(C.c_int64), _P(_i)]),
     ("hmc_last_estep_windows", _i, [_vp, _P(_i), _P(_i), _P(_i), _P(_d)]),
     ("hmc_last_estep_restarts", _i, [_vp, _P(_i), _P(_d)]),
+    ("hmc_last_host_phases", _i, [_vp, _P(_d), _i]),
     ("hmc_model_save", _i, [_vp]),
     ("hmc_em_rewind", _i, [_vp]),
     ("hmc_build_info", _cp, []),

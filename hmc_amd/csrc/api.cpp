@@ -328,6 +328,12 @@ int hmc_last_estep_windows(const hmc_ctx *h, int *windows, int *window_loci, int
   return HMC_OK;
 }
 
+int hmc_last_host_phases(const hmc_ctx *h, double *ms, int n) {
+  if (!h || !ms || n <= 0) return HMC_EARG;
+  for (int k = 0; k < n && k < hmc::Ctx::HP_N; ++k) ms[k] = h->c.hp_ms[k];
+  return hmc::Ctx::HP_N;
+}
+
 int hmc_last_estep_restarts(const hmc_ctx *h, int *restarts, double *window_scale) {
   if (!h) return HMC_EARG;
   if (restarts) *restarts = h->c.n_restarts;

@@ -1020,6 +1020,17 @@ struct Ctx {
   int last_windows = 0, last_window_loci = 0, last_window_groups = 0;  // hmc_last_estep_windows
   int n_restarts = 0;  // restarts of the last E-step (capacity growth, smaller windows): hmc_last_estep_restarts
   double ms_ck = 0;  // device ms of the trace collections (part of ms_s2)
+  // Host wall time of the last EM iteration's phases (hmc_last_host_phases):
+  // the E-step call, its store (re)allocation and end-order table build, the
+  // sample gather after the passes, accept + HaploComp, the M-step call.
+  enum { HP_ESTEP, HP_STORES, HP_GMODEL, HP_SAMPLES, HP_ACCEPT, HP_HAPLOCOMP, HP_MSTEP, HP_SETUP, HP_N };
+  double hp_ms[HP_N] = {};
+  struct HpTimer {
+    double &acc;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit HpTimer(double &a) : acc(a) {}
+    ~HpTimer() { acc += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+  };
   // A probe of the first loci of a sample decides: WIN_DECLINED when the
   // classic passes fit groups of at least two individuals per CU (or the
   // whole shard).
@@ -1139,6 +1150,7 @@ struct Ctx {
   int init_best();
   // HaploModel.cpp:132-133: resolutions = this E-step's best pairs (device copy)
   int accept_resolutions() {
+    HpTimer hpt(hp_ms[HP_ACCEPT]);
     if (!have_estep) return fail(HMC_EARG, "no E-step has run");
     const int n = nloc(), L = pan.L;
     hipError_t e;

@@ -92,6 +92,7 @@ int Ctx::build_head_frontier() {
 
 int Ctx::estep(double *ll_out, int *H_out, uint64_t *re_out) {
   if (!have_model) return fail(HMC_EARG, "no pattern model");
+  auto hp_t0 = std::chrono::steady_clock::now();
   if (head_len > 1) {
     if (h_head_al.size() != h_head_ids.size() * (size_t)head_len || (h_head_ids.empty() && n_head > 0))
       return fail(HMC_EUNSUPPORTED, "head_len > 1 needs the head patterns' alleles (mined tables only)");
@@ -140,8 +141,17 @@ int Ctx::estep(double *ll_out, int *H_out, uint64_t *re_out) {
   // scratch is allocated from what they leave free.  (Past the budget by more
   // than 1/8 only: the budgets move by a few GB with the M-step's buffers,
   // and re-mapping a store of ~100 GB costs seconds.)
-  if (d_trace.n > trace_budget + trace_budget / 8) d_trace.release();
-  if (d_rec.n > rec_budget + rec_budget / 8) d_rec.release();
+  {
+    HpTimer hpt(hp_ms[HP_STORES]);
+    if (d_trace.n > trace_budget + trace_budget / 8) d_trace.release();
+    if (d_rec.n > rec_budget + rec_budget / 8) d_rec.release();
+  }
+  // A store up to 10 % below its new budget stays as it is and becomes the
+  // budget: growing it re-maps the whole store (cfg 4's per-rank E2: 79.3 ->
+  // 80.0 GB of traces cost 2.2 s of a 5.5 s iteration, profiles/r06/cfg4/),
+  // while a few GB less only moves the group cut.
+  if (d_trace.p && d_trace.n < trace_budget && d_trace.n * 10 >= trace_budget * 9) trace_budget = d_trace.n;
+  if (d_rec.p && d_rec.n < rec_budget && d_rec.n * 10 >= rec_budget * 9) rec_budget = d_rec.n;
   h_total.assign(n, 0.0);
   h_ncand.assign(n, 0);
   h_status.assign(n, 0);
@@ -165,6 +175,7 @@ int Ctx::estep(double *ll_out, int *H_out, uint64_t *re_out) {
   std::vector<int32_t> order(n);
   for (int q = 0; q < n; ++q) order[q] = q;
   std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return h_cost[x] > h_cost[y]; });
+  hp_ms[HP_SETUP] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - hp_t0).count();
   if ((e = hipMemcpyAsync(d_cost.p, h_cost.data(), (size_t)n * 4, hipMemcpyHostToDevice, st)))
     return hipfail(e, "estep");
   ms_fwd = ms_tb = 0;
@@ -184,6 +195,7 @@ int Ctx::estep(double *ll_out, int *H_out, uint64_t *re_out) {
   if (last_fast && value_mode == VM_AUTO && (double)n_order_redo > 0.35 * (double)n) fast_off = true;
   // samples in the reference's order: individuals in order, candidates in
   // order, h0 then h1 (HaploModel.cpp:105-106)
+  HpTimer hpt_samples(hp_ms[HP_SAMPLES]);
   std::vector<int32_t> rowmap;
   rowmap.reserve((size_t)2 * S * n);
   for (int i = 0; i < n; ++i)
@@ -236,6 +248,7 @@ int Ctx::estep(double *ll_out, int *H_out, uint64_t *re_out) {
 
 int Ctx::ensure_store(DevBuf<uint32_t> &b, uint64_t words, uint64_t budget, const char *what) {
   if (b.n >= words && b.p) return HMC_OK;
+  HpTimer hpt(hp_ms[HP_STORES]);
   if (words > budget) return fail(HMC_ENOMEM, "%s: one individual needs %llu words (budget %llu)", what,
                                   (unsigned long long)words, (unsigned long long)budget);
   b.release();  // 1.25x headroom: a store of tens of GB is mapped eagerly, re-allocations are slow
@@ -905,6 +918,7 @@ DevModel Ctx::dev_model() const {
 // the structure pass keeps the id-ordered table (same records).
 int Ctx::ensure_gmodel() {
   if (!end_order || gmodel_gen == model_gen || P <= 0) return HMC_OK;
+  HpTimer hpt(hp_ms[HP_GMODEL]);
   const int A = pan.amax;
   const size_t tb = gmodel_sort_bytes(P, pan.L);
   hipError_t e;

@@ -56,16 +56,21 @@ int Ctx::em_iteration(int it, int max_iter, bool force_m, double &old_ll, hmc_it
   using clk = std::chrono::steady_clock;
   int rc;
   if (!have_best && (rc = init_best())) return rc;
+  for (double &x : hp_ms) x = 0.0;
   auto t1 = clk::now();
   double ll = 0;
   int Hs = 0;
   uint64_t re = 0;
   if ((rc = estep(&ll, &Hs, &re))) return rc;
   const double te = std::chrono::duration<double>(clk::now() - t1).count();
+  hp_ms[HP_ESTEP] = te * 1e3;
   if (ll >= old_ll && (rc = accept_resolutions())) return rc;
   rec = hmc_iter_log{};
   double hc[3];
-  if ((rc = haplocomp(hc))) return rc;  // HaploModel.cpp:134-136
+  {
+    HpTimer hpt(hp_ms[HP_HAPLOCOMP]);
+    if ((rc = haplocomp(hc))) return rc;  // HaploModel.cpp:134-136
+  }
   rec.switch_error = hc[0];
   rec.ihp = hc[1];
   rec.igp = hc[2];
@@ -81,6 +86,7 @@ int Ctx::em_iteration(int it, int max_iter, bool force_m, double &old_ll, hmc_it
     uint64_t rm = 0;
     if ((rc = mine(&np, &rm))) return rc;
     rec.t_mstep_s = std::chrono::duration<double>(clk::now() - t2).count();
+    hp_ms[HP_MSTEP] = rec.t_mstep_s * 1e3;
     rec.r_m = rm;
     rec.n_patterns = np;
     old_ll = ll;

@@ -268,6 +268,16 @@ class HaploModel:
         return dict(windows=w.value, window_loci=wl.value, groups=g.value, collection_ms=ms.value,
                     restarts=rs.value, window_scale=sc.value)
 
+    HOST_PHASES = ("estep", "stores", "gmodel", "samples", "accept", "haplocomp", "mstep", "estep_setup")
+
+    def host_phases(self) -> dict:
+        """Host wall ms of the last em_iteration's phases (hmc_last_host_phases)."""
+        buf = (C.c_double * len(self.HOST_PHASES))()
+        n = lib().hmc_last_host_phases(self._h, buf, len(self.HOST_PHASES))
+        if n < 0:
+            self._check(n)
+        return {k: buf[i] for i, k in enumerate(self.HOST_PHASES)}
+
     def set_value_mode(self, mode: str):
         """Value pass of the split E-step: "fast" (value-only k-best lists, the
         libstdc++ permutations only for individuals with ties), "exact" (the

@@ -436,6 +436,14 @@ int hmc_last_estep_windows(const hmc_ctx *ctx, int *windows, int *window_loci, i
  * window length smaller groups) and the window scale now in force (1.0 until
  * a trace-store overflow; reset by a panel load or hmc_set_shard). */
 int hmc_last_estep_restarts(const hmc_ctx *ctx, int *restarts, double *window_scale);
+/* Host wall time (ms) of the last hmc_em_iteration's phases, in this order:
+ * [0] the E-step call, [1] its store (re)allocations and releases, [2] the
+ * end-order table build, [3] the sample gather after the passes, [4] accepting
+ * the resolutions, [5] HaploComp, [6] the M-step call, [7] the E-step's setup
+ * before the passes (buffers, budgets, cost order).  [1]-[3] and [7] are parts
+ * of [0].  Writes min(n, 8) values and returns 8.  Replaces no reference
+ * interface (measurement of the per-rank host gap). */
+int hmc_last_host_phases(const hmc_ctx *ctx, double *ms, int n);
 /* Individuals the last E-step re-ran with the libstdc++ permutations (mode 0)
  * and the device time of those re-runs (ms, part of values_ms). */
 int hmc_last_estep_order(const hmc_ctx *ctx, int *n_rerun, double *rerun_ms);

@@ -52,6 +52,10 @@ for W in worlds:
                   f"(structure {s['structure_ms']:.0f}, values {s['values_ms']:.0f}), "
                   f"M {t['mstep_ms'] if go else 0:.0f} ms ({log['n_patterns']} patterns), wall {wall * 1e3:.0f} ms"
                   + ("" if go else "  [stop]"), flush=True)
+            hp = m.host_phases()
+            print("    host ms: " + ", ".join(f"{k} {v:.0f}" for k, v in hp.items())
+                  + f"; E-step wall minus device passes {hp['estep'] - t['estep_forward_ms'] - t['estep_traceback_ms']:.0f}",
+                  flush=True)
             if not go or it >= 10:
                 break
         print(f"  chain {rep}: {it} iterations, {tot / it * 1e3:.0f} ms per iteration "
