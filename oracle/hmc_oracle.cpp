@@ -306,6 +306,12 @@ struct Params {
   int num_patterns = -1;      // HMC.cpp:38 (findPatternByNum when > 0)
   int mc_order = 1;           // HMC.cpp:41
   bool exact = false;         // --exact-estimate (HMC.cpp:42, HaploModel.h:26)
+  // exact M-step summation: 0 = the device walk's order (xwalk, bit-exact
+  // with exact.hip); 1 = the reference's grouping in double (rwalk: list 0,
+  // then 1, then 2, predecessors in creation order for std::map's pointer
+  // order, every frequency and prefix added in double) — the independent
+  // check at the north star's 1e-6 bar
+  int exact_order = 0;
 };
 
 struct Timing { double m0 = 0, e = 0, m = 0; };
@@ -1094,6 +1100,92 @@ struct Model {
   }
   int P_al(int pat, int locus) const { return P[pat].al[locus - P[pat].start]; }
 
+  // HaploBuilder::estimateFrequency(node, locus, a, last_freq, last_match)
+  // (HaploBuilder.cpp:334-450) as the reference writes it, in double: the
+  // three std::map<HaploPair*, double> lists become dense arrays over the
+  // locus's states, iterated in creation order (the pool allocator's pointer
+  // order, the closest reproducible stand-in); list 0's terms first, then
+  // list 1's, then list 2's (:369-427); the child's frequency one running
+  // sum over list 0, 1, 2 (:429-434); hp->setFrequency / setPrefixFreq in
+  // double in visiting order (:437-441); every child of every node visited
+  // (the reference does not skip zero lists; their terms are +0.0).
+  std::vector<double> racc_f, racc_p;
+  void rwalk(int node, int locus, int ai, double last_freq, int F, const double *L0, const double *L1,
+             const double *L2) {
+    const int hl = head_len();
+    const bool head = locus < hl;
+    const std::vector<Pair> &Z = hp[head ? hl : locus + 1];
+    const int Fc = head ? F : (int)Z.size();
+    std::vector<double> M0(Fc, 0.0), M1(Fc, 0.0), M2(Fc, 0.0);
+    auto alA = [&](int t) { return head ? g.index(locus, P_al(Z[t].pa, locus)) : g.index(locus, Z[t].alA); };
+    auto alB = [&](int t) { return head ? g.index(locus, P_al(Z[t].pb, locus)) : g.index(locus, Z[t].alB); };
+    if (head) {  // :340-367
+      for (int t = 0; t < F; ++t) {
+        const double w = L0[t];
+        if (alA(t) == ai) {
+          if (alB(t) == ai) M0[t] += w;
+          else M1[t] += w * 0.5;
+        } else if (alB(t) == ai) {
+          M2[t] += w * 0.5;
+        }
+      }
+      for (int t = 0; t < F; ++t)
+        if (alA(t) == ai) M1[t] += L1[t];
+      for (int t = 0; t < F; ++t)
+        if (alB(t) == ai) M2[t] += L2[t];
+    } else {  // :369-427
+      const std::vector<Pair> &X = hp[locus];
+      for (int s2 = 0; s2 < F; ++s2) {
+        const double w = L0[s2];
+        if (w == 0.0) continue;  // (its terms are +0.0)
+        for (int r = 0; r < 2; ++r)
+          for (int t : X[s2].fl[r]) {
+            const double tp = Z[t].tp;
+            if (alA(t) == ai) {
+              if (alB(t) == ai) M0[t] += w * tp;
+              else M1[t] += w * tp * 0.5;
+            } else if (alB(t) == ai) {
+              M2[t] += w * tp * 0.5;
+            }
+          }
+      }
+      for (int s2 = 0; s2 < F; ++s2) {
+        const double w = L1[s2];
+        if (w == 0.0) continue;
+        for (int t : X[s2].fl[0])
+          if (alA(t) == ai) M1[t] += w * Z[t].tp;
+        for (int t : X[s2].fl[1])
+          if (alB(t) == ai) M2[t] += w * Z[t].tp;
+      }
+      for (int s2 = 0; s2 < F; ++s2) {
+        const double w = L2[s2];
+        if (w == 0.0) continue;
+        for (int t : X[s2].fl[0])
+          if (alB(t) == ai) M2[t] += w * Z[t].tp;
+        for (int t : X[s2].fl[1])
+          if (alA(t) == ai) M1[t] += w * Z[t].tp;
+      }
+    }
+    double freq = 0;
+    bool any = false;
+    for (const std::vector<double> *M : {&M0, &M1, &M2})
+      for (int t = 0; t < Fc; ++t) {
+        freq += (*M)[t] * Z[t].bwd;
+        any = any || (*M)[t] != 0.0;
+      }
+    freq /= cur_gp;
+    const FNode &nd = fnodes[node];
+    if (nd.data >= 0) {
+      racc_f[nd.data] += freq;
+      racc_p[nd.data] += last_freq;
+    }
+    if (!any) {  // every descendant adds +0.0 (its lists stay zero), prefixes +0.0
+      return;
+    }
+    for (int i = 0; i < (int)nd.ch.size(); ++i)
+      if (nd.ch[i] >= 0) rwalk(nd.ch[i], locus + 1, i, freq, Fc, M0.data(), M1.data(), M2.data());
+  }
+
   // HaploBuilder::estimateFrequency(patterns) (:274-332) for pats[b, e)
   void estimateFreqs(std::vector<Pat> &pats, size_t b, size_t e) {
     const int L = g.L, N = g.N, hl = head_len(), width = g.maxnum();
@@ -1108,6 +1200,9 @@ struct Model {
     }
     xacc_f.assign(pats.size(), 0);
     xacc_p.assign(pats.size(), 0);
+    racc_f.assign(pats.size(), 0.0);
+    racc_p.assign(pats.size(), 0.0);
+    const bool ref_order = prm.exact_order == 1;
     std::vector<Candidate> out;
     std::vector<int> resol;
     for (int gi = 0; gi < N; ++gi) {
@@ -1124,14 +1219,20 @@ struct Model {
         const int F0 = (int)hp[end].size();
         std::vector<double> l0(3 * (size_t)F0, 0.0);
         for (int i = 0; i < F0; ++i) l0[i] = hp[end][i].fwd;
-        xwalk(froot[start], start, 0, F0, l0.data(), 1.0);
+        if (ref_order) {  // :296-308: match_list[0] = forward likelihoods, lists 1 and 2 empty
+          const FNode &rt = fnodes[froot[start]];
+          for (int i = 0; i < (int)rt.ch.size(); ++i)
+            if (rt.ch[i] >= 0) rwalk(rt.ch[i], start, i, 1.0, F0, l0.data(), l0.data() + F0, l0.data() + 2 * F0);
+        } else {
+          xwalk(froot[start], start, 0, F0, l0.data(), 1.0);
+        }
       }
     }
     hp.clear();
     for (size_t k = b; k < e; ++k) {
       Pat &p = pats[k];
-      double freq = std::min((double)xacc_f[k] / XFIX, (double)N);
-      double pre = std::min((double)xacc_p[k] / XFIX, (double)N);
+      double freq = std::min(ref_order ? racc_f[k] : (double)xacc_f[k] / XFIX, (double)N);
+      double pre = std::min(ref_order ? racc_p[k] : (double)xacc_p[k] / XFIX, (double)N);
       freq = std::min(freq, pre);
       p.freq = freq / N;
       p.prefix = pre / N;
@@ -1670,6 +1771,9 @@ void ora_set_model(void *h, int model, int mc_order) {
 }
 // HaploModel::exact_estimate (HMC.cpp:42): M-steps by estimatePatterns
 void ora_set_exact(void *h, int on) { ((Model *)h)->prm.exact = on != 0; }
+// 0: the device walk's summation order (bit-exact check); 1: the reference's
+// grouping in double (rwalk, the independent 1e-6 check)
+void ora_set_exact_order(void *h, int mode) { ((Model *)h)->prm.exact_order = mode; }
 // One exact M-step (PatternManager::estimatePatterns) after an E-step; returns
 // the pattern count; *rx = match-list entries visited by the trie walks.
 int ora_estimate_patterns(void *h, uint64_t *rx) {

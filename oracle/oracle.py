@@ -55,6 +55,7 @@ def lib():
         L.ora_set_threads.argtypes = [i]
         L.ora_set_unphased.argtypes = [vp, i]
         L.ora_set_exact.argtypes = [vp, i]
+        L.ora_set_exact_order.argtypes = [vp, i]
         L.ora_estimate_patterns.restype = i
         L.ora_estimate_patterns.argtypes = [vp, P(u64)]
         L.ora_set_model.argtypes = [vp, i, i]
@@ -222,6 +223,12 @@ class Oracle:
     def set_exact(self, on: bool = True):
         """HaploModel::exact_estimate (--exact-estimate): M-steps by estimatePatterns."""
         lib().ora_set_exact(self.h, 1 if on else 0)
+
+    def set_exact_order(self, mode: str):
+        """Summation order of the exact M-step: "device" (the walk of
+        hmc_amd's exact.hip, bit-exact) or "reference" (HaploBuilder.cpp:334-450's
+        list-0/1/2 grouping in double, predecessors in creation order)."""
+        lib().ora_set_exact_order(self.h, {"device": 0, "reference": 1}[mode])
 
     def estimate_patterns(self):
         """One exact M-step (PatternManager::estimatePatterns) after an E-step;

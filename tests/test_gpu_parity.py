@@ -1278,6 +1278,44 @@ def test_exact_mstep_against_oracle(oracle_mod, name):
     _assert_table_bits(pg, po)
 
 
+RARE = dict(N=80, L=50, A=2, K=40, rho=0.05, seed=12)  # patterns down to min_freq = 0.2 / 2N = 1.25e-3
+
+
+@pytest.mark.parametrize("name", EXACT_PANELS + ["rare"])
+def test_exact_mstep_against_reference_order(oracle_mod, name):
+    """The north star's bar against an independent restatement: the GPU's
+    exact M-step table vs the restatement that sums in the reference's own
+    grouping in double (oracle rwalk: HaploBuilder.cpp:369-434 — list 0's
+    terms, then list 1's, then list 2's, predecessors in creation order for
+    std::map's pointer order; frequencies and prefixes added in double in
+    visiting order, :437-441), not a copy of the device's arithmetic.  Same
+    patterns, order and successors; freq / prefix / tp within 1e-6 relative,
+    including `rare`, whose patterns sit at the min_freq threshold."""
+    if name == "rare":
+        p, mfa = synth.founder_mosaic(**RARE), 0.2
+    else:
+        p, mfa = panel(name), 1.5
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10, min_freq_abs=mfa)
+    o.set_exact_order("reference")
+    o.find_patterns()
+    o.resolve_all()
+    P_o, _ = o.estimate_patterns()
+    po = o.patterns()
+    m = gpu_model(p, min_freq_abs=mfa)
+    m.exact_estimate = True
+    m.find_patterns()
+    m.resolve_all()
+    P_g, _ = m.find_patterns()
+    pg = m.patterns()
+    assert P_g == P_o
+    for k in ("start", "len", "alleles", "succ"):
+        assert np.array_equal(pg[k], po[k]), k
+    for k in ("freq", "prefix", "tp"):
+        rel = np.abs(pg[k] - po[k]) / np.maximum(np.abs(po[k]), 1e-300)
+        print(f"{name} {k}: max rel {rel.max():.2e} over {len(rel)} patterns (min {po[k].min():.3g})", flush=True)
+        assert _rel_close(pg[k], po[k], rtol=1e-6, atol=0.0), (k, rel.max())
+
+
 @pytest.mark.variants
 @pytest.mark.parametrize("name", ["n60"])
 def test_exact_walk_four_items_per_wave(oracle_mod, name):
