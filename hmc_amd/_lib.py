@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("HMC_AMD_LIB") or os.path.join(_HERE, "libhmc_amd.so")
+_DEFAULT_LIB = os.path.join(_HERE, "libhmc_amd.so")
+LIB_PATH = os.environ.get("HMC_AMD_LIB") or _DEFAULT_LIB
 
 HMC_OK = 0
 ERRORS = {-1: "EARG", -2: "EHIP", -3: "EIO", -4: "EUNSUPPORTED", -5: "ENOPATTERN", -6: "ERCCL", -7: "ENOMEM"}
@@ -109,6 +110,7 @@ _SIGS = [
     ("hmc_last_mine_reduction", _i, [_vp, _P(_d), _P(_i)]),
     ("hmc_comm_stats", _i, [_vp, _P(C.c_int64), _P(C.c_int64), _P(C.c_uint64)]),
     ("hmc_set_comm_timeout", _i, [_vp, _d]),
+    ("hmc_set_key_probes", _i, [_vp, _i]),
     ("hmc_debug_stall", _i, [_vp, _d]),
     ("hmc_set_estep_windows", _i, [_vp, _i, _i]),
     ("hmc_set_shard", _i, [_vp, _i, _i]),
@@ -150,8 +152,16 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is not built; run __graft_entry__.build() or make -C hmc_amd/csrc")
         L = C.CDLL(LIB_PATH)
+        # an older build picked with HMC_AMD_LIB (A/B runs) may lack newer
+        # entry points; the in-tree product library must export every one
+        ab = "HMC_AMD_LIB" in os.environ and os.path.abspath(LIB_PATH) != os.path.abspath(_DEFAULT_LIB)
         for name, res, args in _SIGS:
-            f = getattr(L, name)
+            try:
+                f = getattr(L, name)
+            except AttributeError:
+                if ab:
+                    continue
+                raise
             f.restype = res
             f.argtypes = args
         _lib = L

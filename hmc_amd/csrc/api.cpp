@@ -423,6 +423,12 @@ int hmc_last_mine_reduction(const hmc_ctx *h, double *ms, int *levels) {
   return HMC_OK;
 }
 
+int hmc_set_key_probes(hmc_ctx *h, int probes) {
+  if (!h || probes < 1 || probes > 4096) return HMC_EARG;
+  h->c.key_probes = probes;
+  return HMC_OK;
+}
+
 int hmc_comm_stats(const hmc_ctx *h, int64_t *sends, int64_t *recvs, uint64_t *bytes_received) {
   if (!h) return HMC_EARG;
   if (sends) *sends = h->c.p2p_sends;

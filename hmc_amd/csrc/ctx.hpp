@@ -291,6 +291,7 @@ struct Ctx {
   // size (estep_split: 1:20 from 32 individuals per CU, 2:8 from 8, else 3:8);
   // structure-pass individuals per CU, 0 = by group size (12 / 8 / 4)
   int vp_nw = 0, vp_ipc = 0, s1_ipc = 0, s1_nw = 0;
+  int key_probes = 16;  // structure pass: LDS probes of the key table before its HBM tier (hmc_set_key_probes)
   // diagnostics only (stderr logging, never a change of what runs): read once
   // at context creation from HMC_DEBUG_MEM / HMC_DIAG_MINE
   bool debug_mem = false, diag_mine = false;
@@ -1058,7 +1059,9 @@ struct Ctx {
   int exact_ipw = 1;
   static void s1_tier(int budget, int amax, int nw, int &fc, int &hc, int &cc, bool v2 = false) {
     for (int f = 2048; f >= 16; f -= 16) {
-      const int h = next_pow2(2 * f), c = 2 * f;
+      // 4-wave blocks keep their lane masks out of the slots (estep_split.hip
+      // k1_lid), so their 20-byte slots take a table of 4x the states: load <= 0.25
+      const int h = next_pow2((!v2 && nw == 4 ? 4 : 2) * f), c = 2 * f;
       const size_t b = v2 ? estep_s1v2_lds_bytes(f, h, c, amax, nw) : estep_s1_lds_bytes(f, h, c, amax, nw);
       if ((int)b <= budget) { fc = f; hc = h; cc = c; return; }
     }

@@ -94,6 +94,7 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     s1.hcap = hcap1;
     s1.ccap = ccap1;
     s1_tier(160 * 1024 / bpc1 - 256, pan.amax, nw1, s1.lds_fc, s1.lds_hc, s1.lds_cc);
+    s1.probe_lds = key_probes;
     s1.rec = d_rec.p;
     s1.rec_cap = d_rec.n;
     s1.rec_cursor = d_rec_cursor.p;

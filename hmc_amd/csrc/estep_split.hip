@@ -79,11 +79,40 @@ struct IdFront {
   __device__ uint32_t *at(int k, int t) const { return t < fc ? l + k * fc + t : g + (size_t)k * gs + (t - fc); }
 };
 
+// The frontiers of estep_structure: LO, HI and NL alternate between the two
+// (the previous frontier's are read, the new one's written); SLOT, NS and CB
+// belong to the new frontier only while its locus is built (key slots,
+// predecessor-length sums, first contributions), so one set serves both and
+// a state takes 36 bytes of LDS instead of 48 — at two 4-wave blocks per CU
+// the LDS tier holds 528 states instead of 432 (cfg 3's E1: 468 on average).
+struct IdFront1 {
+  uint32_t *l, *g, *ls, *gsh;
+  int fc, gs;
+  __device__ uint32_t *at(int k, int t) const {
+    if (k < F_SLOT) return t < fc ? l + k * fc + t : g + (size_t)k * gs + (t - fc);
+    return t < fc ? ls + (k - F_SLOT) * fc + t : gsh + (size_t)(k - F_SLOT) * gs + (t - fc);
+  }
+};
+
 // m_best_pair: slots < hc in LDS, the rest in the HBM table.  Per slot the
 // key, one 64-bit lane mask per wavefront of the block (the contributions of
 // the current chunk that carry the key), the count of contributions so far
 // and the state the key created.
 __host__ __device__ inline int k1_slot_bytes(int nw) { return 16 + 8 * nw; }
+// estep_structure with up to 4 waves per block keeps no lane masks in the
+// slots: the first contribution of a chunk to claim a slot writes
+// (chunk tag << 10 | its thread index) into the slot's tag word, and the chunk's
+// lane masks for that key go to an LDS array indexed by that thread index
+// ([NT][NW] words, zeroed again by the key's first contribution).  A slot is
+// then 20 bytes instead of 16 + 8 NW (48 at 4 waves): at two 4-wave blocks
+// per CU the LDS table holds 2 048 keys instead of 1 024 for the same LDS, so
+// the probe sequences stay short and few keys reach the HBM tier (cfg 3's E1:
+// 20 of 700 contributions per locus did, and a wave with one such lane waits
+// for two global round trips per chunk).  16-wave blocks (cfg 4's small E1
+// groups) keep the masks in the slots: their [NT][NW] array would be 128 KB.
+__host__ __device__ inline bool k1_lid(int nw) { return nw <= 4; }
+__host__ __device__ inline int k1v_slot_bytes(int nw) { return k1_lid(nw) ? 20 : k1_slot_bytes(nw); }
+constexpr int LID_BITS = 10;  // thread index (NT <= 1024) in a tag word; the chunk tag above it
 struct K1Keys {
   unsigned char *l, *g;
   int hc, hcap, nw;
@@ -102,6 +131,10 @@ struct K1Keys {
     return s < (uint32_t)hc ? (uint32_t *)(l + (size_t)hc * (12 + 8 * nw)) + s
                             : (uint32_t *)(g + (size_t)hcap * (12 + 8 * nw)) + (s - hc);
   }
+  __device__ uint32_t *tag(uint32_t s) const {  // estep_structure's local-id layout (nw = 0) only
+    return s < (uint32_t)hc ? (uint32_t *)(l + (size_t)hc * (16 + 8 * nw)) + s
+                            : (uint32_t *)(g + (size_t)hcap * (16 + 8 * nw)) + (s - hc);
+  }
 };
 
 // The locus's contributions in extendAll order: (pred | reversed), state, rank.
@@ -115,7 +148,7 @@ struct CTier {
 };
 
 struct K1Plan {
-  int o_pairs, o_bucket, o_red, o_front[2], o_keys, o_contrib, bytes;
+  int o_pairs, o_bucket, o_red, o_front[2], o_fsh, o_keys, o_lanes, o_contrib, bytes;
 };
 
 // npm: allele pairs of a fully missing locus, amax (amax + 1) / 2
@@ -126,9 +159,11 @@ __host__ __device__ inline K1Plan k1_plan(int fc, int hc, int cc, int npm, int n
   p.o_pairs = take((npm + 2) * 4 + 3 * npm);
   p.o_bucket = take(NBUCKET * 4);
   p.o_red = take((2 * nw + 4) * 8);
-  p.o_front[0] = take(F_NARR * fc * 4);
-  p.o_front[1] = take(F_NARR * fc * 4);
-  p.o_keys = take(hc * k1_slot_bytes(nw));
+  p.o_front[0] = take(F_SLOT * fc * 4);  // LO, HI, NL of one frontier
+  p.o_front[1] = take(F_SLOT * fc * 4);
+  p.o_fsh = take((F_NARR - F_SLOT) * fc * 4);  // SLOT, NS, CB of the one being built
+  p.o_keys = take(hc * k1v_slot_bytes(nw));
+  p.o_lanes = take(k1_lid(nw) ? 64 * nw * nw * 8 : 0);
   p.o_contrib = take(3 * cc * 4);
   p.bytes = o;
   return p;
@@ -268,7 +303,7 @@ __device__ inline unsigned long long rec_alloc(const StructArgs &a, const Blk<NW
 __host__ __device__ inline size_t k1_front_words(int fcap) { return al256((size_t)fcap * 4) / 4; }
 
 size_t estep_s1_scratch_bytes(int fcap, int hcap, int ccap, int nw, bool prune) {
-  return 2 * al256(F_NARR * k1_front_words(fcap) * 4) + al256((size_t)hcap * k1_slot_bytes(nw)) +
+  return 2 * al256(F_NARR * k1_front_words(fcap) * 4) + al256((size_t)hcap * k1v_slot_bytes(nw)) +
          al256((size_t)ccap * 12) + (prune ? 2 * al256((size_t)fcap * 8) : 0);
 }
 size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax, int nw) {
@@ -279,7 +314,7 @@ size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax, int nw) {
 // the structure pass (each stamp drains the wave's memory counters), plus
 // counters; summed over individuals into a.stamps[16].
 #ifdef HMC_STAMPS
-#define S1_T0 unsigned long long s1t = __builtin_amdgcn_s_memtime(), s1acc[16] = {};
+#define S1_T0 unsigned long long s1t = __builtin_amdgcn_s_memtime(), s1acc[20] = {};
 #define S1_ST(k)                                                   \
   do {                                                             \
     __builtin_amdgcn_s_waitcnt(0);                                 \
@@ -290,7 +325,7 @@ size_t estep_s1_lds_bytes(int fc, int hc, int cc, int amax, int nw) {
 #define S1_CNT(k, v) s1acc[k] += (unsigned long long)(v)
 #define S1_FLUSH                                                   \
   if (a.stamps && tid == 0)                                        \
-    for (int k = 0; k < 16; ++k) atomicAdd(&a.stamps[k], s1acc[k]);
+    for (int k = 0; k < 20; ++k) atomicAdd(&a.stamps[k], s1acc[k]);
 #else
 #define S1_T0
 #define S1_ST(k) do { } while (0)
@@ -332,12 +367,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
 
   char *sp = a.scratch + (size_t)blockIdx.x * a.scratch_stride;
   const int gs = (int)k1_front_words(a.fcap);
-  const IdFront FA{(uint32_t *)(smem + plan.o_front[0]), (uint32_t *)sp, a.lds_fc, gs};
+  // HBM tiers: the first region's arrays 0-2 (LO, HI, NL) and 3-5 (the shared
+  // SLOT, NS, CB), the second region's arrays 0-2
+  uint32_t *const gsh = (uint32_t *)sp + (size_t)F_SLOT * gs;
+  uint32_t *const lsh = (uint32_t *)(smem + plan.o_fsh);
+  const IdFront1 FA{(uint32_t *)(smem + plan.o_front[0]), (uint32_t *)sp, lsh, gsh, a.lds_fc, gs};
   sp += al256(F_NARR * (size_t)gs * 4);
-  const IdFront FB{(uint32_t *)(smem + plan.o_front[1]), (uint32_t *)sp, a.lds_fc, gs};
+  const IdFront1 FB{(uint32_t *)(smem + plan.o_front[1]), (uint32_t *)sp, lsh, gsh, a.lds_fc, gs};
   sp += al256(F_NARR * (size_t)gs * 4);
-  const K1Keys K{smem + plan.o_keys, (unsigned char *)sp, a.lds_hc, a.hcap, NW};
-  sp += al256((size_t)a.hcap * k1_slot_bytes(NW));
+  constexpr bool LID = NW <= 4;  // k1_lid: lane masks by local id, not per slot
+  const K1Keys K{smem + plan.o_keys, (unsigned char *)sp, a.lds_hc, a.hcap, LID ? 0 : NW};
+  sp += al256((size_t)a.hcap * k1v_slot_bytes(NW));
+  unsigned long long *const lanes = (unsigned long long *)(smem + plan.o_lanes);  // LID: [NT][NW]
   const CTier CT{(uint32_t *)(smem + plan.o_contrib), (uint32_t *)sp, a.lds_cc, a.ccap};
   sp += al256((size_t)a.ccap * 12);
   // prune: forward likelihoods of the previous and the current frontier (HBM)
@@ -354,9 +395,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
   auto reset_tables = [&]() {
     for (int h = tid; h < K.hc + a.hcap; h += NT) {
       *K.key(h) = KEY_EMPTY;
-      for (int w = 0; w < NW; ++w) K.lanes(h)[w] = 0ull;
+      if constexpr (LID) *K.tag(h) = 0u;
+      else
+        for (int w = 0; w < NW; ++w) K.lanes(h)[w] = 0ull;
       *K.cnt(h) = 0;
     }
+    if constexpr (LID)
+      for (int w = tid; w < NT * NW; w += NT) lanes[w] = 0ull;
     __threadfence();
     B.sync();
   };
@@ -382,7 +427,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     unsigned long long rend = a.rec_base ? (a.rec_size ? rcur + a.rec_size[bi] : ~0ull) : 0;
     bool counting = false;
     unsigned long long rneed = 0, tneed = 0;  // exact record / trace words (block-uniform)
-    IdFront X = FA, Y = FB;
+    IdFront1 X = FA, Y = FB;
 
     // ---- initHeadList (HaploBuilder.cpp:153-224) ----------------------------
     // head_len == 1 on the device; longer heads from the host's list.  A locus
@@ -525,6 +570,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
       const int npairs = pr_off[npm + 1];
       const int C = pr_off[npairs];
       if (C > a.ccap) { status = EST_OVERFLOW_CONTRIB; break; }
+      // (LID: chunk tags must stay below 2^(32 - LID_BITS); the host then fails loudly)
+      if (NW <= 4 && (long long)C >= ((1ll << (32 - LID_BITS)) - 1) * NT) { status = EST_OVERFLOW_CONTRIB; break; }
       S1_ST(0);
       S1_CNT(8, C);
       S1_CNT(9, Fp);
@@ -556,6 +603,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
             }
           }
         }
+        S1_ST(14);
         uint32_t sa = g_sa[0], sb = g_sb[0], s = g_s[0];
 #pragma unroll
         for (int q = 1; q < GB; ++q)
@@ -575,12 +623,31 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
           lo = rev ? sb : sa;
           hi = rev ? sa : sb;
         }
+        // this key's lane masks for the chunk: in the slot, or (LID) in the
+        // lanes row of the slot's first claimant in this chunk
+        unsigned long long *lw = nullptr;
+        bool lw_lds = true;
         if (valid) {
           slot = k1_key_slot(K, ((unsigned long long)lo << 32) | hi, key_hash(lo, hi), a.probe_lds);
-          atomicOr(K.lanes(slot) + wv, 1ull << lane);
+          if constexpr (LID) {
+            const uint32_t ctag = (uint32_t)(c0 / NT) + 1u;  // < 2^22: C <= ccap (EST_OVERFLOW_CONTRIB above)
+            uint32_t *tg = K.tag(slot);
+            uint32_t w = slot < (uint32_t)K.hc ? *tg : ld_acq(tg);
+            while ((w >> LID_BITS) != ctag) {
+              const uint32_t mine = ctag << LID_BITS | (uint32_t)tid;
+              const uint32_t prev = atomicCAS(tg, w, mine);
+              w = prev == w ? mine : prev;
+            }
+            lw = lanes + (size_t)(w & ((1u << LID_BITS) - 1u)) * NW;
+          } else {
+            lw = K.lanes(slot);
+            lw_lds = slot < (uint32_t)K.hc;
+          }
+          atomicOr(lw + wv, 1ull << lane);
         }
         S1_CNT(10, 1);
         S1_CNT(11, __popcll(__ballot(valid && slot >= (uint32_t)K.hc)));
+        S1_ST(15);
         B.sync();
         // this contribution's rank among the chunk's ones with the same key
         // (waves before it, then lanes below it) and the chunk's count
@@ -589,21 +656,23 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         if (valid) {
 #pragma unroll 4
           for (int w = 0; w < NW; ++w) {
-            const uint64_t m = slot < (uint32_t)K.hc ? K.lanes(slot)[w] : ld_acq(K.lanes(slot) + w);
+            const uint64_t m = lw_lds ? lw[w] : ld_acq(lw + w);
             li += w < wv ? __popcll(m) : (w == wv ? __popcll(m & lt) : 0);
             gsz += __popcll(m);
           }
           cnt0 = kcnt(slot);
         }
         B.sync();
+        S1_ST(16);
         if (valid && li == 0) {
           *K.cnt(slot) = cnt0 + (uint32_t)gsz;
 #pragma unroll 4
-          for (int w = 0; w < NW; ++w) K.lanes(slot)[w] = 0ull;
+          for (int w = 0; w < NW; ++w) lw[w] = 0ull;
         }
         const bool is_new = valid && cnt0 == 0 && li == 0;
         int nnew = 0;
         const int rk_new = B.scan(is_new ? 1 : 0, &nnew);
+        S1_ST(17);
         if (Fn + nnew > a.fcap) { status = EST_OVERFLOW_FRONTIER; break; }
         uint32_t st = 0;
         if (is_new) {
@@ -623,6 +692,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
           *CT.at(C_ST, c) = valid ? st : NONE;
           *CT.at(C_RK, c) = cnt0 + (uint32_t)li;
         }
+        S1_ST(7);
       }
       if (status != EST_OK) break;
       if (Fn == 0) { status = EST_UNRESOLVED; break; }
@@ -745,10 +815,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
           const uint32_t sl = *Y.at(F_SLOT, t);
           *K.key(sl) = KEY_EMPTY;
           *K.cnt(sl) = 0;
+          if constexpr (LID) *K.tag(sl) = 0u;
         }
       }
       B.sync();
-      const IdFront T = X;
+      const IdFront1 T = X;
       X = Y;
       Y = T;
       double *const ft = fwx;

@@ -219,6 +219,10 @@ class HaploModel:
         self._check(lib().hmc_comm_stats(self._h, C.byref(s), C.byref(r), C.byref(b)))
         return dict(sends=s.value, recvs=r.value, bytes_received=b.value)
 
+    def set_key_probes(self, probes: int):
+        """Structure pass: LDS probes of the key table before its HBM tier (results unchanged)."""
+        self._check(lib().hmc_set_key_probes(self._h, int(probes)))
+
     def set_comm_timeout(self, seconds: float):
         """Bounded waits of an RCCL context (hmc_set_comm_timeout)."""
         self._check(lib().hmc_set_comm_timeout(self._h, float(seconds)))

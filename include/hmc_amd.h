@@ -184,6 +184,9 @@ int hmc_last_mine_reduction(const hmc_ctx *ctx, double *ms, int *levels);
  * one-rank context sends each hop to itself, grouped).  Replaces no reference
  * interface. */
 int hmc_comm_stats(const hmc_ctx *ctx, int64_t *sends, int64_t *recvs, uint64_t *bytes_received);
+/* Structure pass (tuning, results unchanged): LDS probes of the key table
+ * (m_best_pair) before a key goes to its HBM tier; default 16. */
+int hmc_set_key_probes(hmc_ctx *ctx, int probes);
 /* Bounded waits of an RCCL context (default 1800 s): every stream sync polls
  * ncclCommGetAsyncError; on an asynchronous error or after `seconds` without
  * the stream draining, the communicator is aborted (ncclCommAbort — a

@@ -19,6 +19,9 @@ cfg = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 vmode = os.environ.get("HMC_VALUE_MODE", "exact")
 m = hmc_amd.HaploModel()
 m.set_value_mode(vmode)
+if os.environ.get("HMC_KEY_PROBES"):
+    m.set_key_probes(int(os.environ["HMC_KEY_PROBES"]))
+    tag += f"/probes{os.environ['HMC_KEY_PROBES']}"
 m.load(hmc_amd.GenoData.from_panel(synth.config_panel(cfg)))
 t0 = time.perf_counter()
 P, _ = m.find_patterns()

@@ -24,7 +24,7 @@ for it in range(iters):
     m.resolve_all()
     st = (C.c_uint64 * 40)()
     hmc_amd.lib().hmc_get_stamps(m._h, st)
-    s1 = st[20:36]
+    s1 = st[20:40]
     s = m.estep_split_stats()
     nl = max(1, s1[13])
     tot = sum(s1[:7])
@@ -32,6 +32,9 @@ for it in range(iters):
           f"(lane-0 cycles, summed over all passes):")
     for k in range(7):
         print(f"   {names[k]:20s} {s1[k] / nl:9.0f}  {100 * s1[k] / max(tot, 1):5.1f}%")
+    sub = [("gathers", 14), ("keys+lanes", 15), ("rank sync", 16), ("new-state scan", 17), ("states+records", 7)]
+    nch = max(1, s1[10])
+    print("   per chunk of contributions: " + ", ".join(f"{nm} {s1[k] / nch:.0f}" for nm, k in sub))
     print(f"   C {s1[8] / nl:.1f}  F {s1[9] / nl:.1f}  chunks {s1[10] / nl:.2f}  HBM-tier keys {s1[11] / nl:.1f}  "
           f"HBM-tier states {s1[12] / nl:.1f}  loci walked {s1[13]}", flush=True)
     m.find_patterns()
