@@ -111,6 +111,7 @@ _SIGS = [
     ("hmc_comm_stats", _i, [_vp, _P(C.c_int64), _P(C.c_int64), _P(C.c_uint64)]),
     ("hmc_set_comm_timeout", _i, [_vp, _d]),
     ("hmc_set_key_probes", _i, [_vp, _i]),
+    ("hmc_set_structure_tier", _i, [_vp, _i, _i]),
     ("hmc_debug_stall", _i, [_vp, _d]),
     ("hmc_set_estep_windows", _i, [_vp, _i, _i]),
     ("hmc_set_shard", _i, [_vp, _i, _i]),

@@ -423,6 +423,13 @@ int hmc_last_mine_reduction(const hmc_ctx *h, double *ms, int *levels) {
   return HMC_OK;
 }
 
+int hmc_set_structure_tier(hmc_ctx *h, int key_mult10, int contrib_mult10) {
+  if (!h || key_mult10 < 0 || contrib_mult10 < 0 || key_mult10 > 160 || contrib_mult10 > 160) return HMC_EARG;
+  h->c.s1_kmul = key_mult10;
+  h->c.s1_cmul = contrib_mult10;
+  return HMC_OK;
+}
+
 int hmc_set_key_probes(hmc_ctx *h, int probes) {
   if (!h || probes < 1 || probes > 4096) return HMC_EARG;
   h->c.key_probes = probes;

@@ -1057,11 +1057,17 @@ struct Ctx {
   // wavefront (default); 4 four items per wavefront, 2 breadth-first lane
   // units (both variants)
   int exact_ipw = 1;
-  static void s1_tier(int budget, int amax, int nw, int &fc, int &hc, int &cc, bool v2 = false) {
+  // LDS split of a structure-pass block: states per frontier (fc), key slots
+  // (hc, a power of two) and contributions (cc) per locus.  Key slots and
+  // contributions as multiples of the states: s1_kmul / s1_cmul (tenths),
+  // hmc_set_structure_tier; 0 = the defaults below.
+  int s1_kmul = 0, s1_cmul = 0;
+  void s1_tier(int budget, int amax, int nw, int &fc, int &hc, int &cc, bool v2 = false) const {
+    // 4-wave blocks keep their lane masks out of the slots (estep_split.hip
+    // k1_lid), so their 20-byte slots take a table of 4x the states: load <= 0.25
+    const int km = s1_kmul > 0 ? s1_kmul : (!v2 && nw == 4 ? 40 : 20), cm = s1_cmul > 0 ? s1_cmul : 20;
     for (int f = 2048; f >= 16; f -= 16) {
-      // 4-wave blocks keep their lane masks out of the slots (estep_split.hip
-      // k1_lid), so their 20-byte slots take a table of 4x the states: load <= 0.25
-      const int h = next_pow2((!v2 && nw == 4 ? 4 : 2) * f), c = 2 * f;
+      const int h = next_pow2(std::max(16, km * f / 10)), c = std::max(16, cm * f / 10);
       const size_t b = v2 ? estep_s1v2_lds_bytes(f, h, c, amax, nw) : estep_s1_lds_bytes(f, h, c, amax, nw);
       if ((int)b <= budget) { fc = f; hc = h; cc = c; return; }
     }

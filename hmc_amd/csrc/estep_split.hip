@@ -711,6 +711,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         if (t < Fn) *Y.at(F_CB, t) = (uint32_t)(Cv + ex);
         Cv += tot;
       }
+      S1_ST(18);
       const unsigned long long words =
           4 + 4ull * Fn + 1 + (unsigned long long)Cv + Fn + (a.exact ? (unsigned long long)C + npairs : 0ull);
       rneed += (words + 1) & ~1ull;
@@ -722,6 +723,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
       uint32_t *Rhd = R + 4 + 2 * Fn, *Rcb = Rhd + Fn, *Rct = Rcb + Fn + 1, *Rch = Rct + Cv;
       if (tid < NBUCKET) bucket[tid] = 0;
       B.sync();
+      S1_ST(19);
       // per state: k-best list length min(S, sum of predecessor lengths) (the
       // adds keep S once they overflow, HaploPair.cpp:85-88), tp product, last
       // alleles; states whose lists overflow get a chain entry

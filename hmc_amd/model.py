@@ -223,6 +223,10 @@ class HaploModel:
         """Structure pass: LDS probes of the key table before its HBM tier (results unchanged)."""
         self._check(lib().hmc_set_key_probes(self._h, int(probes)))
 
+    def set_structure_tier(self, key_mult10: int = 0, contrib_mult10: int = 0):
+        """Structure pass LDS split (tenths of the frontier states; 0 = default; results unchanged)."""
+        self._check(lib().hmc_set_structure_tier(self._h, int(key_mult10), int(contrib_mult10)))
+
     def set_comm_timeout(self, seconds: float):
         """Bounded waits of an RCCL context (hmc_set_comm_timeout)."""
         self._check(lib().hmc_set_comm_timeout(self._h, float(seconds)))

@@ -187,6 +187,10 @@ int hmc_comm_stats(const hmc_ctx *ctx, int64_t *sends, int64_t *recvs, uint64_t 
 /* Structure pass (tuning, results unchanged): LDS probes of the key table
  * (m_best_pair) before a key goes to its HBM tier; default 16. */
 int hmc_set_key_probes(hmc_ctx *ctx, int probes);
+/* Structure pass (tuning, results unchanged): the block's LDS split — key
+ * slots and contributions per frontier state, in tenths (0 = defaults: 40 and
+ * 20 at 4 waves per individual, 20 and 20 otherwise). */
+int hmc_set_structure_tier(hmc_ctx *ctx, int key_mult10, int contrib_mult10);
 /* Bounded waits of an RCCL context (default 1800 s): every stream sync polls
  * ncclCommGetAsyncError; on an asynchronous error or after `seconds` without
  * the stream draining, the communicator is aborted (ncclCommAbort — a

@@ -19,6 +19,10 @@ cfg = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 vmode = os.environ.get("HMC_VALUE_MODE", "exact")
 m = hmc_amd.HaploModel()
 m.set_value_mode(vmode)
+if os.environ.get("HMC_S1_TIER"):  # "key_mult10,contrib_mult10"
+    km, cm = (int(x) for x in os.environ["HMC_S1_TIER"].split(","))
+    m.set_structure_tier(km, cm)
+    tag += f"/tier{km},{cm}"
 if os.environ.get("HMC_KEY_PROBES"):
     m.set_key_probes(int(os.environ["HMC_KEY_PROBES"]))
     tag += f"/probes{os.environ['HMC_KEY_PROBES']}"

@@ -19,7 +19,9 @@ p = synth.config_panel(cfg)
 m = hmc_amd.HaploModel()
 m.load(hmc_amd.GenoData.from_panel(p))
 m.find_patterns()
-names = ["pairs", "contributions+keys", "scan/states", "chains/order", "clear", "head", "epilogue"]
+names = {0: "pairs", 14: "chunk: gathers", 15: "chunk: keys+lanes", 16: "chunk: rank sync",
+         17: "chunk: new-state scan", 7: "chunk: states+records", 1: "after the chunks", 18: "counts scan",
+         19: "record alloc", 2: "per-state loop", 3: "chains/order", 4: "clear", 5: "head", 6: "epilogue"}
 for it in range(iters):
     m.resolve_all()
     st = (C.c_uint64 * 40)()
@@ -27,14 +29,11 @@ for it in range(iters):
     s1 = st[20:40]
     s = m.estep_split_stats()
     nl = max(1, s1[13])
-    tot = sum(s1[:7])
+    tot = sum(s1[:8]) + sum(s1[14:20])
     print(f"E{it + 1}: structure {s['structure_ms']:.1f} ms in {s['structure_passes']} passes; per individual-locus "
           f"(lane-0 cycles, summed over all passes):")
-    for k in range(7):
-        print(f"   {names[k]:20s} {s1[k] / nl:9.0f}  {100 * s1[k] / max(tot, 1):5.1f}%")
-    sub = [("gathers", 14), ("keys+lanes", 15), ("rank sync", 16), ("new-state scan", 17), ("states+records", 7)]
-    nch = max(1, s1[10])
-    print("   per chunk of contributions: " + ", ".join(f"{nm} {s1[k] / nch:.0f}" for nm, k in sub))
+    for k, nm in names.items():
+        print(f"   {nm:24s} {s1[k] / nl:9.0f}  {100 * s1[k] / max(tot, 1):5.1f}%")
     print(f"   C {s1[8] / nl:.1f}  F {s1[9] / nl:.1f}  chunks {s1[10] / nl:.2f}  HBM-tier keys {s1[11] / nl:.1f}  "
           f"HBM-tier states {s1[12] / nl:.1f}  loci walked {s1[13]}", flush=True)
     m.find_patterns()
