@@ -221,8 +221,11 @@ __device__ inline void walk_terms(bool ma, bool mb, bool rev, double w0, double 
 // union of reached states in state order (zero entries add +0.0).  Scratch
 // invariant: every dense entry not in a touched list is 0.0 (the host zeroes
 // the scratch before the launch and every item clears what it wrote).
+#ifndef HMC_XWALK_WPE
+#define HMC_XWALK_WPE 4  // resident waves per SIMD the walk's registers allow (tuning builds vary it)
+#endif
 template <int GL>
-__global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WPE))) void exact_walk(ExactArgs a) {
   extern __shared__ unsigned long long lds64[];  // per group: per depth descend mask, written-slot mask; ints; marks
   constexpr int NG = WAVE / GL;  // items walked at once by the wavefront, GL lanes each
   const int lane = threadIdx.x, g = lane / GL, gl = lane % GL;
@@ -294,7 +297,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
       const double *fw = (const double *)(a.x + xo[e0]);
       double *S0 = slot(0, 0);
       for (int t = gl; t < F0; t += GL) {
-        S0[t] = fw[t];
+        S0[3 * t] = fw[t];
         touched[t] = (uint32_t)t;
       }
       if (gl == 0) {
@@ -326,7 +329,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
         const int locus = start + d;  // the children's allele is at this locus
         const double last_freq = d == 0 ? 1.0 : cfreq[(size_t)d * W + sslot[d]];  // prefix freq (HaploBuilder.cpp:305)
         const int Fpd = sF[d], Fc = sF[d + 1];  // this depth's states, the children's
-        const double *P0 = slot(d, sslot[d]), *P1 = P0 + Fpd, *P2 = P1 + Fpd;
+        const double *P0 = slot(d, sslot[d]), *P1 = P0 + 1, *P2 = P0 + 2;  // [F][3]: n0 n1 n2 of a state together
         const uint32_t *Tp = tch(d);
         uint32_t *Tc = tch(d + 1);
         {  // the previous sibling's children at depth d+1 back to zero
@@ -336,9 +339,9 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
             const uint32_t t = Tc[j];
             for (unsigned long long m = wm; m; m &= m - 1) {
               double *C0 = slot(d + 1, __builtin_ctzll(m));
-              C0[t] = 0.0;
-              C0[Fc + t] = 0.0;
-              C0[2 * Fc + t] = 0.0;
+              C0[3 * t] = 0.0;
+              C0[3 * t + 1] = 0.0;
+              C0[3 * t + 2] = 0.0;
             }
           }
         }
@@ -357,7 +360,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
               xa = a.head_al[(size_t)plo[t] * hl + locus];
               xb = a.head_al[(size_t)phi[t] * hl + locus];
             }
-            const double w0 = P0[t], w1 = P1[t], w2 = P2[t];
+            const double w0 = P0[3 * t], w1 = P1[3 * t], w2 = P2[3 * t];
             for (unsigned long long m = cm; m; m &= m - 1) {
               const uint32_t i = (uint32_t)__builtin_ctzll(m);
               const bool ma = xa == i, mb = xb == i;
@@ -371,9 +374,9 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
               if (ma) n1 += w1;
               if (mb) n2 += w2;
               double *C0 = slot(d + 1, (int)i);
-              C0[t] = n0;
-              C0[Fc + t] = n1;
-              C0[2 * Fc + t] = n2;
+              C0[3 * t] = n0;
+              C0[3 * t + 1] = n1;
+              C0[3 * t + 2] = n2;
             }
             Tc[t] = (uint32_t)t;
           }
@@ -387,7 +390,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
           const int Fp = (int)a.rec[roff[locus]];  // states the links leave from
           for (int j = gl; j < np; j += GL) {
             const uint32_t s = Tp[j];
-            if (P0[s] == 0.0 && P1[s] == 0.0 && P2[s] == 0.0) continue;
+            if (P0[3 * s] == 0.0 && P1[3 * s] == 0.0 && P2[3 * s] == 0.0) continue;
             uint32_t off = 0;
             for (int p = 0; p < R.NP; ++p) {
               const uint32_t no = R.npo[p];
@@ -441,21 +444,21 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
               const uint32_t w = R.ct[r];
               const uint32_t s = cw_state(w);
               const bool rev = cw_rev(w);
-              const double w0 = P0[s], w1 = P1[s], w2 = P2[s];
+              const double w0 = P0[3 * s], w1 = P1[3 * s], w2 = P2[3 * s];
               if (ca) walk_terms(true, xb == xa, rev, w0, w1, w2, tp, a0, a1, a2);
               if (cb) walk_terms(false, true, rev, w0, w1, w2, tp, b0, b1, b2);
             }
             if (ca) {
               double *C0 = slot(d + 1, (int)xa);
-              C0[t] = a0;
-              C0[Fc + t] = a1;
-              C0[2 * Fc + t] = a2;
+              C0[3 * t] = a0;
+              C0[3 * t + 1] = a1;
+              C0[3 * t + 2] = a2;
             }
             if (cb) {
               double *C0 = slot(d + 1, (int)xb);
-              C0[t] = b0;
-              C0[Fc + t] = b1;
-              C0[2 * Fc + t] = b2;
+              C0[3 * t] = b0;
+              C0[3 * t + 1] = b1;
+              C0[3 * t + 2] = b2;
             }
           }
         }
@@ -472,7 +475,7 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
           bool any = false;
           for (int j = gl; j < ntc; j += GL) {
             const uint32_t t = Tc[j];
-            const double n0 = C0[t], n1 = C0[Fc + t], n2 = C0[2 * Fc + t];
+            const double n0 = C0[3 * t], n1 = C0[3 * t + 1], n2 = C0[3 * t + 2];
             const double v = ((n0 + n1) + n2) * bw[t];
             if constexpr (NG == 1) {
               part[0] += v;
@@ -534,9 +537,9 @@ __global__ __launch_bounds__(64) void exact_walk(ExactArgs a) {
         const uint32_t t = T[j];
         for (unsigned long long m = wm; m; m &= m - 1) {
           double *D0 = slot(dd, __builtin_ctzll(m));
-          D0[t] = 0.0;
-          D0[Fd + t] = 0.0;
-          D0[2 * Fd + t] = 0.0;
+          D0[3 * t] = 0.0;
+          D0[3 * t + 1] = 0.0;
+          D0[3 * t + 2] = 0.0;
         }
       }
     }
