@@ -177,7 +177,7 @@ __device__ inline uint32_t k1_key_slot(const K1Keys &K, unsigned long long key, 
   for (int p = 0; p < probes; ++p) {
     const unsigned long long prev = atomicCAS(&lk[h], KEY_EMPTY, key);
     if (prev == KEY_EMPTY || prev == key) return h;
-    h = (h + 1) & (uint32_t)(K.hc - 1);
+    h = (h + (uint32_t)p + 1u) & (uint32_t)(K.hc - 1);  // triangular steps: no primary clusters
   }
   const uint32_t gmask = (uint32_t)K.hcap - 1u;
   uint32_t g = (h0 * 0x9E3779B1u) & gmask;
