@@ -1653,6 +1653,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE))) voi
       K2_ST(1);
       K2_CNT(8, NCH);
       K2_CNT(9, F);
+      K2_CNT(7, F > Y.fc ? F - Y.fc : 0);  // states written to the frontier's HBM tier
       if (bs->flag) {
         status = EST_NEEDS_EXACT;
         break;

@@ -19,7 +19,8 @@ m.load(hmc_amd.GenoData.from_panel(p))
 m.find_patterns()
 names = ["record hdr", "phase A", "phase B", "trace", "final sync", "final select"]
 for it in range(int(os.environ.get("ITERS", "3"))):
-    m.resolve_all()
+    ll, H, re = m.resolve_all()
+    print(f"  R_E {re}", flush=True)
     st = (C.c_uint64 * 40)()
     hmc_amd.lib().hmc_get_stamps(m._h, st)
     s = m.estep_split_stats()
@@ -30,6 +31,8 @@ for it in range(int(os.environ.get("ITERS", "3"))):
           f"mean per individual-locus cycles (thread 0):")
     for k in range(6):
         print(f"   {names[k]:14s} {st[k] / nl:9.0f}  {100 * st[k] / max(tot, 1):5.1f}%")
+    print(f"   states past the LDS tier (frontier HBM-tier writes) {st[7] / nl:.1f} per locus of {st[9] / nl:.1f}; "
+          f"loci {st[11]}; R_E {m.last_re if hasattr(m, 'last_re') else 'see log'}")
     print(f"   chains/locus {st[8] / nl:.1f}  states/locus {st[9] / nl:.1f}  "
           f"wave-0 chain steps/locus {st[10] / nl:.2f}  critical-path steps/locus {st[12] / nl:.2f}  "
           f"phase-B cycles per critical step {st[2] / max(st[12], 1):.0f}")
