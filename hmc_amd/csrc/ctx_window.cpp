@@ -276,7 +276,11 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     const bool small_heavy = heavy && (per_cu < 4 || (vp_nw == 0 && fmean > 1000.0));
     const int sh_ipc = per_cu < 4 ? per_cu : 1;
     const int vnw = vp_nw > 0 ? vp_nw : (small_heavy ? 16 / sh_ipc : (heavy ? 4 : (k_ >= 32 * dev_cu ? 1 : (k_ >= 8 * dev_cu ? 2 : 3))));
-    const int vipc = vp_ipc > 0 ? vp_ipc : (small_heavy ? sh_ipc : (vnw == 1 ? 16 : (vnw >= 8 ? 2 : (vnw >= 4 ? 4 : 8))));
+    // (heavy groups of five or more per CU: 4 x 5 on the 5-wave build — cfg 3's
+    // E1 windows 1 917-1 921 -> 1 891 ms, profiles/r06/ab/value_shapes_e1_cfg3.log)
+    const int vipc = vp_ipc > 0 ? vp_ipc
+                                : (small_heavy ? sh_ipc
+                                               : (vnw == 1 ? 16 : (vnw >= 8 ? 2 : (vnw >= 4 ? (per_cu >= 5 ? 5 : 4) : 8))));
     const bool pair = S <= 16 && (value_pair == 2 || (value_pair == 1 && heavy));
     const int G2 = std::max(1, std::min(waves > 0 ? waves : dev_cu * vipc, n));
     const int vwpe = vnw * vipc > 16 && vnw * vipc <= 20 ? 5 : 4;
