@@ -19,10 +19,11 @@ cfg = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 vmode = os.environ.get("HMC_VALUE_MODE", "exact")
 m = hmc_amd.HaploModel()
 m.set_value_mode(vmode)
-if os.environ.get("HMC_VALUE_SHAPE"):  # "waves_per_individual,individuals_per_cu" of the value pass
-    vw, vi = (int(x) for x in os.environ["HMC_VALUE_SHAPE"].split(","))
-    m.set_pass_shapes(0, 0, vw, vi)
-    tag += f"/vshape{vw}x{vi}"
+if os.environ.get("HMC_VALUE_SHAPE") or os.environ.get("HMC_STRUCT_SHAPE"):  # "waves,individuals_per_cu"
+    vw, vi = (int(x) for x in os.environ.get("HMC_VALUE_SHAPE", "0,0").split(","))
+    sw, si = (int(x) for x in os.environ.get("HMC_STRUCT_SHAPE", "0,0").split(","))
+    m.set_pass_shapes(sw, si, vw, vi)
+    tag += f"/vshape{vw}x{vi}/sshape{sw}x{si}"
 if os.environ.get("HMC_VALUE_LAYOUT"):  # 0 one link per lane, 1 two for heavy groups, 2 two everywhere
     m.set_value_layout(int(os.environ["HMC_VALUE_LAYOUT"]))
     tag += f"/layout{os.environ['HMC_VALUE_LAYOUT']}"
