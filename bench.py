@@ -332,12 +332,16 @@ def main():
     hbm_frac_meas = None
     if pmc and pmc.get("hbm_bytes_per_launch") and val_ms > 0 and n_launch:
         hbm_frac_meas = pmc["hbm_bytes_per_launch"] / (val_ms * 1e-3 / n_launch) / 1e9 / HBM_PEAK_GBS
-    bound = "hbm"
-    if sq and sq.get("valu_issue_frac") is not None:
+    # (only counters of the library this process loaded count as evidence;
+    # without them the line prices against HBM and says the bound is unmeasured)
+    bound, bound_basis = "hbm", "no same-build counters: priced against HBM, limiter unmeasured"
+    if sq and sq["same_build"] and sq.get("valu_issue_frac") is not None:
         hbm_f = hbm_frac_meas or achieved / HBM_PEAK_GBS
         bound = "valu-issue" if sq["valu_issue_frac"] > hbm_f else "hbm"
         if max(sq["valu_issue_frac"], hbm_f) < 0.5:  # neither roof near: the waves wait (SQ_WAIT_ANY)
             bound = "latency"
+        bound_basis = (f"measured VALU issue occupancy {sq['valu_issue_frac']:.2f} vs HBM fraction {hbm_f:.2f} "
+                       f"({'PMC' if hbm_frac_meas else 'algorithmic bytes'}), same build")
 
     if rank == 0:
         line = {
@@ -370,7 +374,7 @@ def main():
                       "ms_per_iteration": chain_s / chain_iters * 1e3 if chain_iters else None},
             "value_steady": steady,
             "roofline": {
-                "bound": bound, "kernel": "estep_values",
+                "bound": bound, "bound_basis": bound_basis, "kernel": "estep_values",
                 "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                 "traffic": pmc.get("hbm_bytes_per_launch") if pmc and pmc["same_build"] else None,
                 "traffic_over_alg": pmc.get("traffic_over_alg") if pmc and pmc["same_build"] else None,
