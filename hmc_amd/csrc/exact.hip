@@ -63,12 +63,15 @@ struct RecView {  // one locus record of the structure pass
   int F, C, NCH, CF, NP;  // states, stored contributions, chains, contributions in extendAll order, allele pairs
   const double *tpv;
   const uint32_t *hdr, *cb, *ct, *out, *npo;
-  __device__ RecView(const uint32_t *R, bool head) {
-    F = (int)R[0];
-    C = (int)R[1];
-    NCH = (int)R[2];
-    CF = (int)(R[3] >> 10);
-    NP = (int)(R[3] & 1023u);
+  __device__ RecView(const uint32_t *R, bool head) { set(R, (int)R[0], (int)R[1], (int)R[2], R[3], head); }
+  // from header words the caller already holds (exact_walk's per-depth cache)
+  __device__ RecView(const uint32_t *R, int f, int c, int nch, uint32_t cfnp, bool head) { set(R, f, c, nch, cfnp, head); }
+  __device__ void set(const uint32_t *R, int f, int c, int nch, uint32_t cfnp, bool head) {
+    F = f;
+    C = c;
+    NCH = nch;
+    CF = (int)(cfnp >> 10);
+    NP = (int)(cfnp & 1023u);
     tpv = (const double *)(R + 4);
     hdr = R + 4 + 2 * F;
     cb = hdr + F;
@@ -226,7 +229,7 @@ __device__ inline void walk_terms(bool ma, bool mb, bool rev, double w0, double 
 #endif
 template <int GL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WPE))) void exact_walk(ExactArgs a) {
-  extern __shared__ unsigned long long lds64[];  // per group: per depth descend mask, written-slot mask; ints; marks
+  extern __shared__ unsigned long long lds64[];  // per group: exact_walk_lds_bytes
   constexpr int NG = WAVE / GL;  // items walked at once by the wavefront, GL lanes each
   const int lane = threadIdx.x, g = lane / GL, gl = lane % GL;
   // this group's lanes of a wave ballot
@@ -238,10 +241,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
   const int D = maxd + 2;
   unsigned long long *stk64 = lds64 + (size_t)g * (exact_walk_lds_bytes(maxd, a.fmax) / 8);
   unsigned long long *sdesc = stk64, *smask = stk64 + D;
-  int *snode = (int *)(stk64 + 2 * D), *snext = snode + D, *sslot = snext + D, *tcnt = sslot + D;
+  // per depth, read once per item: the record's offset, the x-store offset of its locus
+  unsigned long long *droff = stk64 + 2 * D, *dxo = stk64 + 3 * D;
+  int *snode = (int *)(stk64 + 4 * D), *snext = snode + D, *sslot = snext + D, *tcnt = sslot + D;
   int *sF = tcnt + D, *soff = sF + D;        // per depth: the states of its locus, their first entry in the item's layout
-  uint32_t *marks = (uint32_t *)(soff + D);  // [fmax/32 + 1] reached-state bitmap
+  int *dC = soff + D, *dNCH = dC + D;        // per depth: the record's header words (RecView)
+  uint32_t *dCFNP = (uint32_t *)(dNCH + D), *dnpo0 = dCFNP + D;  // ... and its first allele pair's out-degree
+  // per depth: the first GL entries of the touched list (u16 states; the rest,
+  // and every entry when a locus has more than 65 536 states, in the scratch)
+  uint16_t *tl16 = (uint16_t *)(dnpo0 + D);
+  uint32_t *marks = (uint32_t *)(tl16 + (size_t)D * WAVE);  // [fmax/32 + 1] reached-state bitmap
   const int nwords = (a.fmax + 31) >> 5;
+  const int tlc = a.fmax <= 65536 ? GL : 0;
   // The item's lists: per depth d, W slots of three lists over the F_d states
   // of d's locus (slot i of depth d at 3 (W soff[d] + i F_d)); the wave's
   // region holds the largest such span of any item (ExactArgs::span)
@@ -249,7 +260,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
   double *cfreq = lists + (size_t)3 * W * a.span;                          // [maxd+2][W]
   uint32_t *touched = (uint32_t *)(cfreq + (size_t)(maxd + 2) * W);       // [span]: per depth at soff[d]
   auto slot = [&](int d, int i) { return lists + (size_t)3 * ((size_t)W * soff[d] + (size_t)i * sF[d]); };
-  auto tch = [&](int d) { return touched + soff[d]; };
+  // entry j of depth d's touched list
+  auto tget = [&](int d, int j) -> uint32_t { return j < tlc ? (uint32_t)tl16[d * WAVE + j] : touched[soff[d] + j]; };
+  auto tput = [&](int d, int j, uint32_t t) {
+    if (j < tlc) tl16[d * WAVE + j] = (uint16_t)t;
+    else touched[soff[d] + j] = t;
+  };
   for (int d = gl; d < D; d += GL) {
     tcnt[d] = 0;
     smask[d] = 0ull;
@@ -269,12 +285,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
     const unsigned long long *xo = a.x_off + (size_t)bi * (L + 1);
     const uint32_t *Rh = a.rec + roff[hl];
     const int Fh = (int)Rh[0];
-    {  // the item's layout: depth d's states are those of record max(start + d, head_len)
+    {  // the item's layout: depth d's states are those of record max(start + d, head_len);
+       // each depth's record header and offsets are read here once
       int carry = 0;
       for (int d0 = 0; d0 < D; d0 += GL) {
         const int dd = d0 + gl;
         const int r = start + dd > hl ? start + dd : hl;
-        const int f = dd < D && r <= L ? (int)a.rec[roff[r]] : 0;
+        const bool has = dd < D && r <= L;
+        int f = 0;
+        if (has) {
+          const unsigned long long ro = roff[r];
+          const uint32_t *R = a.rec + ro;
+          const uint32_t hx = R[0], hy = R[1], hz = R[2], hw = R[3];  // F, C, NCH, CF << 10 | NP
+          f = (int)hx;
+          droff[dd] = ro;
+          dxo[dd] = xo[r];
+          dC[dd] = (int)hy;
+          dNCH[dd] = (int)hz;
+          dCFNP[dd] = hw;
+          // out-degree of the first allele pair (npo[0]) of a non-head record
+          dnpo0[dd] = r > hl && (hw & 1023u) > 0u ? R[4 + 4 * (size_t)f + 1 + hy + hz + (hw >> 10)] : 0u;
+        }
         int incl = f;
 #pragma unroll
         for (int o = 1; o < GL; o <<= 1) {
@@ -292,13 +323,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
     __threadfence_block();
     // depth 0: every state after max(start, head_len) loci, weight = forward likelihood
     {
-      const int e0 = start > hl ? start : hl;
-      const int F0 = (int)a.rec[roff[e0]];
-      const double *fw = (const double *)(a.x + xo[e0]);
+      const int F0 = sF[0];
+      const double *fw = (const double *)(a.x + dxo[0]);
       double *S0 = slot(0, 0);
       for (int t = gl; t < F0; t += GL) {
         S0[3 * t] = fw[t];
-        touched[t] = (uint32_t)t;
+        tput(0, t, (uint32_t)t);
       }
       if (gl == 0) {
         tcnt[0] = F0;
@@ -317,26 +347,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
       const int node = snode[d];
       if (snext[d] < 0) {  // ---- all children of this node, into depth d+1 ----
         unsigned long long cm = 0ull;  // alleles with a child
-        if (d < maxd)
-          for (int i0 = 0; i0 < W; i0 += GL) {
-            const int i = i0 + gl;
-            cm |= gballot(i < W && a.tr_child[(size_t)node * W + i] >= 0) << i0;
+        // (one item per wave: lane i holds child i and its pattern, read here once)
+        int chv = -1, patv = -1;
+        if (d < maxd) {
+          if constexpr (GL == WAVE) {
+            chv = gl < W ? a.tr_child[(size_t)node * W + gl] : -1;
+            cm = gballot(chv >= 0);
+            patv = chv >= 0 ? a.tr_data[chv] : -1;
+          } else {
+            for (int i0 = 0; i0 < W; i0 += GL) {
+              const int i = i0 + gl;
+              cm |= gballot(i < W && a.tr_child[(size_t)node * W + i] >= 0) << i0;
+            }
           }
+        }
         if (cm == 0ull) {  // node done
           --d;
           continue;
         }
         const int locus = start + d;  // the children's allele is at this locus
         const double last_freq = d == 0 ? 1.0 : cfreq[(size_t)d * W + sslot[d]];  // prefix freq (HaploBuilder.cpp:305)
-        const int Fpd = sF[d], Fc = sF[d + 1];  // this depth's states, the children's
         const double *P0 = slot(d, sslot[d]), *P1 = P0 + 1, *P2 = P0 + 2;  // [F][3]: n0 n1 n2 of a state together
-        const uint32_t *Tp = tch(d);
-        uint32_t *Tc = tch(d + 1);
         {  // the previous sibling's children at depth d+1 back to zero
           const int nc = tcnt[d + 1];
           const unsigned long long wm = smask[d + 1];
           for (int j = gl; j < nc; j += GL) {
-            const uint32_t t = Tc[j];
+            const uint32_t t = tget(d + 1, j);
             for (unsigned long long m = wm; m; m &= m - 1) {
               double *C0 = slot(d + 1, __builtin_ctzll(m));
               C0[3 * t] = 0.0;
@@ -347,6 +383,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
         }
         int ntc = 0;
         const double *bw;
+        // one reached state per lane (ntc <= GL, not the head): its children's
+        // three weights stay in registers for the frequencies (4)
+        bool regs = false;
+        uint32_t rxa = 0, rxb = 0;
+        bool rca = false, rcb = false;
+        double ra0 = 0.0, ra1 = 0.0, ra2 = 0.0, rb0 = 0.0, rb1 = 0.0, rb2 = 0.0, rbw = 0.0;
         if (locus < hl) {  // head pairs: their patterns' alleles (HaploBuilder.cpp:340-367), same states
           const RecView R(Rh, true);
           const uint32_t *plo = R.cb + Fh + 1, *phi = plo + Fh;
@@ -378,22 +420,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
               C0[3 * t + 1] = n1;
               C0[3 * t + 2] = n2;
             }
-            Tc[t] = (uint32_t)t;
+            tput(d + 1, t, (uint32_t)t);
           }
           ntc = Fh;
         } else {  // along the forward links into the states after `locus` (:369-427)
-          const RecView R(a.rec + roff[locus + 1], false);
-          bw = (const double *)(a.x + xo[locus + 1]) + R.F;
+          // depth d's record is `locus`, depth d+1's `locus + 1` (both >= head_len)
+          const RecView R(a.rec + droff[d + 1], sF[d + 1], dC[d + 1], dNCH[d + 1], dCFNP[d + 1], false);
+          const uint32_t npo0 = dnpo0[d + 1];
+          bw = (const double *)(a.x + dxo[d + 1]) + R.F;
           // (1) mark the states the parent's non-zero states link to and whose
           //     pair carries the allele of some child on either side
           const int np = tcnt[d];
-          const int Fp = (int)a.rec[roff[locus]];  // states the links leave from
+          const int Fp = sF[d];  // states the links leave from
           for (int j = gl; j < np; j += GL) {
-            const uint32_t s = Tp[j];
+            const uint32_t s = tget(d, j);
             if (P0[3 * s] == 0.0 && P1[3 * s] == 0.0 && P2[3 * s] == 0.0) continue;
             uint32_t off = 0;
             for (int p = 0; p < R.NP; ++p) {
-              const uint32_t no = R.npo[p];
+              const uint32_t no = p == 0 ? npo0 : R.npo[p];
               for (uint32_t o = 0; o < no; ++o) {
                 const uint32_t w = R.out[off + s * no + o];
                 if (w != NONE) {
@@ -424,29 +468,44 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
             while (bits) {
               const int b = __builtin_ctz(bits);
               bits &= bits - 1u;
-              Tc[at++] = (uint32_t)(w * 32 + b);
+              tput(d + 1, at++, (uint32_t)(w * 32 + b));
             }
             if (w < nw) marks[w] = 0u;
             ntc += __shfl(incl, g * GL + GL - 1);
           }
           __builtin_amdgcn_wave_barrier();
           __threadfence_block();
+          regs = GL == WAVE && ntc <= GL;
           // (3) each reached state gathers over its incoming contributions, for
           //     the children of its a allele and of its b allele in one pass
+          //     (contributions two at a time: both words, then both weight sets,
+          //     then the terms in record order)
           for (int j = gl; j < ntc; j += GL) {
-            const uint32_t t = Tc[j];
+            const uint32_t t = tget(d + 1, j);
             const uint32_t hd = R.hdr[t];
             const uint32_t xa = hd & 0xFFu, xb = (hd >> 8) & 0xFFu;
             const bool ca = (cm >> xa) & 1ull, cb = xb != xa && ((cm >> xb) & 1ull);
             double a0 = 0.0, a1 = 0.0, a2 = 0.0, b0 = 0.0, b1 = 0.0, b2 = 0.0;
             const double tp = R.tpv[t];
-            for (uint32_t r = R.cb[t]; r < R.cb[t + 1]; ++r) {
-              const uint32_t w = R.ct[r];
-              const uint32_t s = cw_state(w);
-              const bool rev = cw_rev(w);
-              const double w0 = P0[3 * s], w1 = P1[3 * s], w2 = P2[3 * s];
-              if (ca) walk_terms(true, xb == xa, rev, w0, w1, w2, tp, a0, a1, a2);
-              if (cb) walk_terms(false, true, rev, w0, w1, w2, tp, b0, b1, b2);
+            const uint32_t r0 = R.cb[t], r1 = R.cb[t + 1];
+            if (regs) rbw = bw[t];
+            for (uint32_t r = r0; r < r1; r += 2) {
+              const bool two = r + 1 < r1;
+              const uint32_t wA = R.ct[r], wB = two ? R.ct[r + 1] : 0u;
+              const uint32_t sA = cw_state(wA), sB = cw_state(wB);
+              const double u0 = P0[3 * sA], u1 = P1[3 * sA], u2 = P2[3 * sA];
+              double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+              if (two) {
+                v0 = P0[3 * sB];
+                v1 = P1[3 * sB];
+                v2 = P2[3 * sB];
+              }
+              if (ca) walk_terms(true, xb == xa, cw_rev(wA), u0, u1, u2, tp, a0, a1, a2);
+              if (cb) walk_terms(false, true, cw_rev(wA), u0, u1, u2, tp, b0, b1, b2);
+              if (two) {
+                if (ca) walk_terms(true, xb == xa, cw_rev(wB), v0, v1, v2, tp, a0, a1, a2);
+                if (cb) walk_terms(false, true, cw_rev(wB), v0, v1, v2, tp, b0, b1, b2);
+              }
             }
             if (ca) {
               double *C0 = slot(d + 1, (int)xa);
@@ -460,6 +519,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
               C0[3 * t + 1] = b1;
               C0[3 * t + 2] = b2;
             }
+            rxa = xa;
+            rxb = xb;
+            rca = ca;
+            rcb = cb;
+            ra0 = a0;
+            ra1 = a1;
+            ra2 = a2;
+            rb0 = b0;
+            rb1 = b1;
+            rb2 = b2;
           }
         }
         __builtin_amdgcn_wave_barrier();
@@ -468,28 +537,43 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
         unsigned long long desc = 0ull;
         for (unsigned long long m = cm; m; m &= m - 1) {
           const int i = __builtin_ctzll(m);
-          const double *C0 = slot(d + 1, i);
           double part[NG];  // virtual lane gl + GL k of a 64-lane sum (group_sum_fixed)
 #pragma unroll
           for (int k = 0; k < NG; ++k) part[k] = 0.0;
           bool any = false;
-          for (int j = gl; j < ntc; j += GL) {
-            const uint32_t t = Tc[j];
-            const double n0 = C0[3 * t], n1 = C0[3 * t + 1], n2 = C0[3 * t + 2];
-            const double v = ((n0 + n1) + n2) * bw[t];
-            if constexpr (NG == 1) {
-              part[0] += v;
-            } else {
-              const int k = (j / GL) & (NG - 1);
-#pragma unroll
-              for (int u = 0; u < NG; ++u)
-                if (u == k) part[u] += v;
+          if (regs) {  // this lane's state (if any) from (3): the same terms the scratch holds
+            if (gl < ntc) {
+              const bool isa = rca && rxa == (uint32_t)i, isb = rcb && rxb == (uint32_t)i;
+              const double n0 = isa ? ra0 : (isb ? rb0 : 0.0), n1 = isa ? ra1 : (isb ? rb1 : 0.0),
+                           n2 = isa ? ra2 : (isb ? rb2 : 0.0);
+              part[0] += ((n0 + n1) + n2) * rbw;
+              any = (n0 != 0.0) | (n1 != 0.0) | (n2 != 0.0);
             }
-            any |= (n0 != 0.0) | (n1 != 0.0) | (n2 != 0.0);
+          } else {
+            const double *C0 = slot(d + 1, i);
+            for (int j = gl; j < ntc; j += GL) {
+              const uint32_t t = tget(d + 1, j);
+              const double n0 = C0[3 * t], n1 = C0[3 * t + 1], n2 = C0[3 * t + 2];
+              const double v = ((n0 + n1) + n2) * bw[t];
+              if constexpr (NG == 1) {
+                part[0] += v;
+              } else {
+                const int k = (j / GL) & (NG - 1);
+#pragma unroll
+                for (int u = 0; u < NG; ++u)
+                  if (u == k) part[u] += v;
+              }
+              any |= (n0 != 0.0) | (n1 != 0.0) | (n2 != 0.0);
+            }
           }
           const double freq = group_sum_fixed<GL>(part) / pg;
-          const int child = a.tr_child[(size_t)node * W + i];
-          const int pat = a.tr_data[child];
+          int pat;
+          if constexpr (GL == WAVE) {
+            pat = __shfl(patv, i);
+          } else {
+            const int child = a.tr_child[(size_t)node * W + i];
+            pat = a.tr_data[child];
+          }
           if (gl == 0) {
             cfreq[(size_t)(d + 1) * W + i] = freq;
             if (pat >= 0) {
@@ -531,10 +615,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
     for (int dd = 0; dd <= maxd; ++dd) {
       const int nc = tcnt[dd];
       const unsigned long long wm = smask[dd];
-      const uint32_t *T = tch(dd);
-      const int Fd = sF[dd];
       for (int j = gl; j < nc; j += GL) {
-        const uint32_t t = T[j];
+        const uint32_t t = tget(dd, j);
         for (unsigned long long m = wm; m; m &= m - 1) {
           double *D0 = slot(dd, __builtin_ctzll(m));
           D0[3 * t] = 0.0;
