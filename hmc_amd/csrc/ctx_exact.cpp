@@ -246,11 +246,11 @@ int Ctx::exact_walk_group(ExactArgs &x, int k, int dev_cu) {
   if (exact_ipw == 2) return exact_walk_bfs(x, k, dev_cu);  // (variants)
   const int L = pan.L;
   hipError_t e;
-  if (exact_walk_lds_bytes(tr_maxd, x.fmax) > EXACT_WALK_LDS_MAX)
+  if (exact_walk_lds_bytes(tr_maxd, x.fmax, x.width) > EXACT_WALK_LDS_MAX)
     return fail(HMC_EUNSUPPORTED, "exact M-step: a frontier of %d states (trie depth %d) exceeds the walk's LDS bitmap",
                 x.fmax, tr_maxd);
   // (variants) items per wavefront: 4 (16 lanes each) when their LDS fits, else 1
-  const int ipw = exact_ipw == 4 && exact_walk_lds_bytes(tr_maxd, x.fmax) * 4 <= EXACT_WALK_LDS_MAX ? 4 : 1;
+  const int ipw = exact_ipw == 4 && exact_walk_lds_bytes(tr_maxd, x.fmax, x.width) * 4 <= EXACT_WALK_LDS_MAX ? 4 : 1;
   {  // the largest list span of any item of the group (the per-wave scratch)
     unsigned span = 0;
     if ((e = d_xspan.ensure(1))) return hipfail(e, "exact_span");

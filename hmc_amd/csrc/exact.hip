@@ -239,17 +239,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
   };
   const int L = a.L, hl = a.head_len, W = a.width, maxd = a.max_depth;
   const int D = maxd + 2;
-  unsigned long long *stk64 = lds64 + (size_t)g * (exact_walk_lds_bytes(maxd, a.fmax) / 8);
+  unsigned long long *stk64 = lds64 + (size_t)g * (exact_walk_lds_bytes(maxd, a.fmax, a.width) / 8);
   unsigned long long *sdesc = stk64, *smask = stk64 + D;
   // per depth, read once per item: the record's offset, the x-store offset of its locus
   unsigned long long *droff = stk64 + 2 * D, *dxo = stk64 + 3 * D;
-  int *snode = (int *)(stk64 + 4 * D), *snext = snode + D, *sslot = snext + D, *tcnt = sslot + D;
+  // narrow tries (width <= XWALK_CACHE_W): per depth and slot, the non-zero
+  // entries of the slot's lists among the first GL touched states (bit j), and the child ids
+  const int wc = exact_walk_cache_w(W);
+  unsigned long long *nzm = stk64 + 4 * D;
+  int *snode = (int *)(nzm + (size_t)D * wc), *snext = snode + D, *sslot = snext + D, *tcnt = sslot + D;
   int *sF = tcnt + D, *soff = sF + D;        // per depth: the states of its locus, their first entry in the item's layout
   int *dC = soff + D, *dNCH = dC + D;        // per depth: the record's header words (RecView)
   uint32_t *dCFNP = (uint32_t *)(dNCH + D), *dnpo0 = dCFNP + D;  // ... and its first allele pair's out-degree
+  int *dnzv = (int *)(dnpo0 + D);            // per depth: nzm holds its slots' masks
+  int *schild = dnzv + D;                    // [D][wc]: the children of the node at depth d
   // per depth: the first GL entries of the touched list (u16 states; the rest,
   // and every entry when a locus has more than 65 536 states, in the scratch)
-  uint16_t *tl16 = (uint16_t *)(dnpo0 + D);
+  uint16_t *tl16 = (uint16_t *)(schild + (size_t)D * wc);
   uint32_t *marks = (uint32_t *)(tl16 + (size_t)D * WAVE);  // [fmax/32 + 1] reached-state bitmap
   const int nwords = (a.fmax + 31) >> 5;
   const int tlc = a.fmax <= 65536 ? GL : 0;
@@ -354,6 +360,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
             chv = gl < W ? a.tr_child[(size_t)node * W + gl] : -1;
             cm = gballot(chv >= 0);
             patv = chv >= 0 ? a.tr_data[chv] : -1;
+            if (gl < wc) schild[d * wc + gl] = chv;
           } else {
             for (int i0 = 0; i0 < W; i0 += GL) {
               const int i = i0 + gl;
@@ -432,20 +439,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
           //     pair carries the allele of some child on either side
           const int np = tcnt[d];
           const int Fp = sF[d];  // states the links leave from
+          // the parent's non-zero entries among its first GL states, when its
+          // parent computed them in registers (otherwise the lists are read)
+          const bool nzk = wc > 0 && d > 0 && dnzv[d] != 0;
+          const unsigned long long nzb = nzk ? nzm[d * wc + sslot[d]] : ~0ull;
           for (int j = gl; j < np; j += GL) {
             const uint32_t s = tget(d, j);
-            if (P0[3 * s] == 0.0 && P1[3 * s] == 0.0 && P2[3 * s] == 0.0) continue;
+            if (nzk && j < GL) {
+              if (!((nzb >> j) & 1ull)) continue;
+            } else if (P0[3 * s] == 0.0 && P1[3 * s] == 0.0 && P2[3 * s] == 0.0) {
+              continue;
+            }
             uint32_t off = 0;
             for (int p = 0; p < R.NP; ++p) {
               const uint32_t no = p == 0 ? npo0 : R.npo[p];
-              for (uint32_t o = 0; o < no; ++o) {
-                const uint32_t w = R.out[off + s * no + o];
-                if (w != NONE) {
-                  const uint32_t t = cw_state(w);
-                  const uint32_t hd = R.hdr[t];
-                  if (((cm >> (hd & 0xFFu)) & 1ull) || ((cm >> ((hd >> 8) & 0xFFu)) & 1ull))
+              // four links at a time: their words, then their pairs' alleles, then the marks
+              for (uint32_t o = 0; o < no; o += 4) {
+                uint32_t wv[4], hv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) wv[u] = o + u < no ? R.out[off + s * no + o + u] : NONE;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) hv[u] = wv[u] != NONE ? R.hdr[cw_state(wv[u])] : 0u;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                  if (wv[u] != NONE && (((cm >> (hv[u] & 0xFFu)) & 1ull) || ((cm >> ((hv[u] >> 8) & 0xFFu)) & 1ull))) {
+                    const uint32_t t = cw_state(wv[u]);
                     atomicOr(&marks[t >> 5], 1u << (t & 31u));
-                }
+                  }
               }
               off += (uint32_t)Fp * no;
             }
@@ -581,9 +601,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
               atomicAdd(&a.acc_prefix[pat], (unsigned long long)__double2ll_rn(last_freq * EXACT_FIXED_SCALE));
             }
           }
-          if (gballot(any) != 0ull && d + 1 <= maxd) desc |= 1ull << i;
+          const unsigned long long anym = gballot(any);
+          if (anym != 0ull && d + 1 <= maxd) desc |= 1ull << i;
+          if (gl == 0 && i < wc) nzm[(d + 1) * wc + i] = anym;  // (bit j = touched entry j when regs)
         }
         if (gl == 0) {
+          if (wc > 0) dnzv[d + 1] = regs ? 1 : 0;
           tcnt[d + 1] = ntc;
           smask[d + 1] = cm;
           sdesc[d] = desc;
@@ -599,7 +622,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
         continue;
       }
       const int i = __builtin_ctzll(left);
-      const int child = a.tr_child[(size_t)node * W + i];
+      const int child = GL == WAVE && wc > 0 ? schild[d * wc + i] : a.tr_child[(size_t)node * W + i];
       __builtin_amdgcn_wave_barrier();
       if (gl == 0) {
         snext[d] = i + 1;
@@ -918,7 +941,7 @@ hipError_t launch_exact_span(const ExactArgs &a, int grid, hipStream_t st) {
 hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st, int items_per_wave) {
   if (a.n_order <= 0) return hipSuccess;
   if (a.width < 1 || a.width > 64 || (items_per_wave != 1 && items_per_wave != 4)) return hipErrorInvalidValue;
-  const size_t lds = exact_walk_lds_bytes(a.max_depth, a.fmax) * (size_t)items_per_wave;
+  const size_t lds = exact_walk_lds_bytes(a.max_depth, a.fmax, a.width) * (size_t)items_per_wave;
   if (lds > EXACT_WALK_LDS_MAX) return hipErrorInvalidValue;  // the host reports it (exact_walk_group)
 #ifdef HMC_VARIANTS
   void (*k)(ExactArgs) = items_per_wave == 4 ? exact_walk<16> : exact_walk<WAVE>;

@@ -77,11 +77,16 @@ hipError_t launch_exact_span(const ExactArgs &a, int grid, hipStream_t st);
 // items_per_wave 1 (64 lanes per item) or 4 (16 lanes each); scratch: grid x items x stride
 hipError_t launch_exact_walk(const ExactArgs &a, int grid, hipStream_t st, int items_per_wave = 1);
 size_t exact_walk_scratch_doubles(int max_depth, long long span, int width);
-// LDS of one walked item: per depth two masks, two record offsets, ten ints
-// and 64 cached touched states (u16), the reached-state bitmap (8-byte multiple)
-__host__ __device__ inline size_t exact_walk_lds_bytes(int max_depth, int fmax) {
-  const size_t D = (size_t)max_depth + 2;
-  return (D * 32 + D * 40 + D * 128 + (size_t)((fmax + 31) / 32 + 1) * 4 + 7) & ~(size_t)7;
+// Tries of at most this many alleles per node keep, per depth and slot, the
+// child ids and the non-zero masks of the walk in LDS (wider ones read them)
+constexpr int XWALK_CACHE_W = 8;
+__host__ __device__ inline int exact_walk_cache_w(int width) { return width <= XWALK_CACHE_W ? width : 0; }
+// LDS of one walked item: per depth two masks, two record offsets, eleven ints
+// and 64 cached touched states (u16), per depth and cached slot a non-zero mask
+// and a child id, the reached-state bitmap (8-byte multiple)
+__host__ __device__ inline size_t exact_walk_lds_bytes(int max_depth, int fmax, int width) {
+  const size_t D = (size_t)max_depth + 2, wc = (size_t)exact_walk_cache_w(width);
+  return (D * 32 + D * wc * 8 + D * 44 + D * wc * 4 + D * 128 + (size_t)((fmax + 31) / 32 + 1) * 4 + 7) & ~(size_t)7;
 }
 constexpr size_t EXACT_WALK_LDS_MAX = 160 * 1024;  // gfx950 LDS per workgroup
 
