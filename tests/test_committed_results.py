@@ -75,7 +75,8 @@ def test_headline_counters_from_the_same_build(rel):
 def test_headline_launch_time_agrees_with_kernel_trace(rel):
     d = _line(rel)
     r = d["roofline"]
-    stats = os.path.join(os.path.dirname(os.path.join(ROOT, r["traffic_source"])), "kernel_stats_cfg3.csv")
+    tag = d["config"]["workload"].split(":")[0]  # "cfg3", "cfg5", ...
+    stats = os.path.join(os.path.dirname(os.path.join(ROOT, r["traffic_source"])), f"kernel_stats_{tag}.csv")
     with open(stats) as f:
         rows = [row for row in csv.DictReader(f) if "estep_values" in row["Name"]]
     calls = sum(int(row["Calls"]) for row in rows)
