@@ -14,7 +14,8 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADLINES = ["profiles/r06/bench/bench_cfg3_r06.json", "profiles/r06/bench/bench_cfg5_r06.json"]
+HEADLINES = ["profiles/r06/bench/bench_cfg3_r06.json", "profiles/r06/bench/bench_cfg5_r06.json",
+             "profiles/r06/bench/bench_cfg2_r06.json"]
 
 REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
             "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"]
