@@ -268,13 +268,16 @@ int Ctx::estep_windowed(const std::vector<int32_t> &order) {
     const int wl = bound[w + 1] - bound[w];
     const bool heavy = rsum / ((double)k_ * wl) > 1500.0;
     const int per_cu = (k_ + dev_cu - 1) / dev_cu;
-    // heavy groups whose mean frontier passes 1 000 states take a whole CU per
-    // individual (cfg 4's E1, ~1 600 states per locus: values 14.3 -> 13.4-13.7
-    // s; cfg 3's E1, ~430: 4 x 4 stays — 16 x 1 there: 270-300 instead of ~215
-    // ms per window, E1 values 2.10 -> 2.75 s)
+    // heavy groups whose mean frontier passes 1 000 states take half a CU per
+    // individual, 8 x 2 (cfg 4's E1, ~1 600 states per locus: 4 x 4 -> 16 x 1,
+    // values 14.3 -> 13.4-13.7 s in round 5; 16 x 1 -> 8 x 2 in round 6, 12.48
+    // -> 11.96 s at the same 80-loci windows,
+    // profiles/r06/cfg4/cfg4_rank0_value_shapes_fixed80.log; cfg 3's E1, ~430:
+    // 4 x 4 stays — 16 x 1 there: 270-300 instead of ~215 ms per window, E1
+    // values 2.10 -> 2.75 s)
     const double fmean = (tsum / std::max(1.0, (double)k_ * wl) - 2.0) / (1.0 + S);
     const bool small_heavy = heavy && (per_cu < 4 || (vp_nw == 0 && fmean > 1000.0));
-    const int sh_ipc = per_cu < 4 ? per_cu : 1;
+    const int sh_ipc = per_cu < 4 ? per_cu : 2;
     const int vnw = vp_nw > 0 ? vp_nw : (small_heavy ? 16 / sh_ipc : (heavy ? 4 : (k_ >= 32 * dev_cu ? 1 : (k_ >= 8 * dev_cu ? 2 : 3))));
     // (heavy groups of five or more per CU: 4 x 5 on the 5-wave build — cfg 3's
     // E1 windows 1 917-1 921 -> 1 891 ms, profiles/r06/ab/value_shapes_e1_cfg3.log)

@@ -781,7 +781,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
             const uint32_t ns = *X.at(F_NL, (int)cw_state(w));
             Rct[*Y.at(F_CB, (int)st) + *CT.at(C_RK, c)] = w | ns << 24;
           }
-          if (a.exact) Rout[c] = st == NONE ? NONE : (st | (w & CW_REV));
+          if (a.exact)
+            Rout[c] = st == NONE ? NONE
+                                 : (st | (w & CW_REV) |
+                                    xpair_index(LAST[*Y.at(F_LO, (int)st)], LAST[*Y.at(F_HI, (int)st)]) << XPAIR_SHIFT);
         }
       }
       if (a.exact && !counting)
@@ -1276,7 +1279,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
             const uint32_t ns = *X.at(F_NL, (int)cw_state(w));
             Rct[cb + rank] = w | ns << 24;
           }
-          if (a.exact) Rout[c] = stt == NONE ? NONE : (stt | (w & CW_REV));
+          if (a.exact)
+            Rout[c] = stt == NONE ? NONE
+                                  : (stt | (w & CW_REV) |
+                                     xpair_index(a.mod.last[*Y.at(F_LO, (int)stt)], a.mod.last[*Y.at(F_HI, (int)stt)])
+                                         << XPAIR_SHIFT);
         }
         if (a.exact)
           for (int p = tid; p < npairs; p += NT) Rout[C + p] = simple ? (uint32_t)o1 : pr_o[p];

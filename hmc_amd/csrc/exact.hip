@@ -259,6 +259,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
   uint32_t *marks = (uint32_t *)(tl16 + (size_t)D * WAVE);  // [fmax/32 + 1] reached-state bitmap
   const int nwords = (a.fmax + 31) >> 5;
   const int tlc = a.fmax <= 65536 ? GL : 0;
+  // one item per wave and at most 64 unordered allele pairs (width <= 10):
+  // lane p holds pair p's alleles, and a node's pairs that carry an allele of
+  // one of its children form one ballot, tested against the links' pair bits
+  const bool pmk = GL == WAVE && W * (W + 1) / 2 <= WAVE;
+  int px = 0;
+  while ((px + 1) * (px + 2) / 2 <= lane) ++px;
+  const int py = lane - px * (px + 1) / 2;
+  const bool pin = lane < W * (W + 1) / 2;
   // The item's lists: per depth d, W slots of three lists over the F_d states
   // of d's locus (slot i of depth d at 3 (W soff[d] + i F_d)); the wave's
   // region holds the largest such span of any item (ExactArgs::span)
@@ -439,6 +447,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
           //     pair carries the allele of some child on either side
           const int np = tcnt[d];
           const int Fp = sF[d];  // states the links leave from
+          const unsigned long long pm = pmk ? __ballot(pin && (((cm >> px) & 1ull) || ((cm >> py) & 1ull))) : 0ull;
           // the parent's non-zero entries among its first GL states, when its
           // parent computed them in registers (otherwise the lists are read)
           const bool nzk = wc > 0 && d > 0 && dnzv[d] != 0;
@@ -459,10 +468,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HMC_XWALK_WP
 #pragma unroll
                 for (int u = 0; u < 4; ++u) wv[u] = o + u < no ? R.out[off + s * no + o + u] : NONE;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) hv[u] = wv[u] != NONE ? R.hdr[cw_state(wv[u])] : 0u;
+                for (int u = 0; u < 4; ++u) hv[u] = !pmk && wv[u] != NONE ? R.hdr[cw_state(wv[u])] : 0u;
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                  if (wv[u] != NONE && (((cm >> (hv[u] & 0xFFu)) & 1ull) || ((cm >> ((hv[u] >> 8) & 0xFFu)) & 1ull))) {
+                  if (wv[u] != NONE && (pmk ? ((pm >> cw_xpair(wv[u])) & 1ull) != 0ull
+                                            : (((cm >> (hv[u] & 0xFFu)) & 1ull) || ((cm >> ((hv[u] >> 8) & 0xFFu)) & 1ull)))) {
                     const uint32_t t = cw_state(wv[u]);
                     atomicOr(&marks[t >> 5], 1u << (t & 31u));
                   }

@@ -40,6 +40,16 @@ __host__ __device__ inline uint32_t cw_pack(uint32_t s, bool rev) { return s | (
 __host__ __device__ inline uint32_t cw_state(uint32_t w) { return w & F_MASK; }
 __host__ __device__ inline bool cw_rev(uint32_t w) { return (w >> F_BITS) & 1u; }
 __host__ __device__ inline uint32_t cw_ns(uint32_t w) { return w >> 24; }
+// Exact-mode forward-link words (the records' extendAll list) carry in bits
+// 22..31 the target state's unordered allele pair max(a,b)(max(a,b)+1)/2 +
+// min(a,b) (< 990: at most 44 alleles per locus in exact mode), so the trie
+// walk tests a target's alleles without reading its header.
+constexpr int XPAIR_SHIFT = F_BITS + 1;
+__host__ __device__ inline uint32_t xpair_index(uint32_t a, uint32_t b) {
+  const uint32_t x = a > b ? a : b, y = a > b ? b : a;
+  return x * (x + 1) / 2 + y;
+}
+__host__ __device__ inline uint32_t cw_xpair(uint32_t w) { return w >> XPAIR_SHIFT; }
 
 // Per-state trace header word: last allele of pattern a / b, link count.
 __host__ __device__ inline uint32_t hdr_pack(uint32_t al_a, uint32_t al_b, uint32_t n) {

@@ -4,7 +4,8 @@ M0), then the E-step over rank r's balanced shard only (hmc_set_shard) —
 exactly the E1 work of rank r in `bench.py --gpus 8 --config 4`.  Prints the
 E-step's device ms (structure / values / trace collection), its windows, and
 that a repeat is bit-identical.  SHAPES = "s_nw:s_ipc:v_nw:v_ipc,..." runs
-the E-step once per pass-shape set (0 = automatic).
+the E-step once per pass-shape set (0 = automatic); WINDOW = loci per window
+fixes the window length for every run (0 / unset: planned from the stores).
 
     python tools/cfg4_rank.py [RANK [WORLD [CFG]]]
 """
@@ -34,6 +35,8 @@ i0, i1 = balanced_shard(p.alleles, rank, world)
 del p
 m.set_shard(i0, i1)
 print(f"rank {rank} of {world}: individuals [{i0}, {i1}) = {i1 - i0}", flush=True)
+if os.environ.get("WINDOW"):  # fixed window length (loci), the same for every run of the sweep
+    m.set_estep_windows("always", int(os.environ["WINDOW"]))
 ref = None
 for rep, sh in enumerate(shapes):
     m.set_pass_shapes(*sh)
@@ -47,7 +50,8 @@ for rep, sh in enumerate(shapes):
     print(f"E1 run {rep} shapes {sh}: wall {wall:.2f} s; device: structure {s['structure_ms']:.0f} ms "
           f"({s['structure_passes']} passes), values {s['values_ms']:.0f} ms ({s['value_passes']}; trace collection "
           f"{w['collection_ms']:.0f} of it), traceback {t['estep_traceback_ms']:.0f} ms, fallback {s['fallback_ms']:.0f} ms "
-          f"({s['n_fallback']}); windows {w['windows']} of {w['window_loci']} loci in {w['groups']} group(s); "
+          f"({s['n_fallback']}); windows {w['windows']} of {w['window_loci']} loci in {w['groups']} group(s), "
+          f"{w['restarts']} restart(s), window scale {w['window_scale']:.3g}; "
           f"frontier {fr}; LL {ll!r} H {H} R_E {re}", flush=True)
     if ref is None:
         ref = (float(ll).hex(), H, re)
