@@ -1278,6 +1278,33 @@ def test_exact_mstep_against_oracle(oracle_mod, name):
     _assert_table_bits(pg, po)
 
 
+def test_exact_mstep_wide_trie(oracle_mod):
+    """The exact walk's wide-trie paths: microsatellite loci with up to 20
+    alleles (trie width 20 > 10), so marking reads each target's header
+    instead of the allele-pair ballot and no per-depth child or non-zero-mask
+    cache is kept (exact.hip, exact_walk_cache_w) — the table still equals the
+    restatement's bit for bit."""
+    rng = np.random.default_rng(20)
+    base = synth.founder_mosaic(40, 30, A=2, seed=11)
+    a = np.where(base.alleles < 0, -1, base.alleles - ord("1") + 1).astype(np.int32)
+    for k in (4, 11, 19, 26):
+        a[:, :, k] = rng.integers(1, 21, size=(40, 2))
+    p = synth.Panel(alleles=a, types="M" * 30)
+    o = oracle_mod.Oracle(p.alleles, p.types, sample_size=10)
+    o.find_patterns()
+    o.resolve_all()
+    P_o, _ = o.estimate_patterns()
+    po = o.patterns()
+    m = gpu_model(p)
+    m.exact_estimate = True
+    m.find_patterns()
+    m.resolve_all()
+    P_g, _ = m.find_patterns()
+    assert m.amax > 10
+    assert P_g == P_o
+    _assert_table_bits(m.patterns(), po)
+
+
 RARE = dict(N=80, L=50, A=2, K=40, rho=0.05, seed=12)  # patterns down to min_freq = 0.2 / 2N = 1.25e-3
 
 
